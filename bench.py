@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 ImageNet-1K (224x224, 1000 classes) training throughput.
+
+Metric (BASELINE.json): images/sec for the whole job, ResNet-50 ImageNet-1K, at 1/2/4/8
+MI355X, bf16, synthetic data + random-init weights, weak scaling (fixed per-GPU batch).
+
+  python bench.py --gpus N --steps K --warmup W        # N=1 runs in-process
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Implementations (``--impl``):
+  native  the framework's flagship path: NHWC bf16 ResNet program on the hand-written HIP
+          kernels (dbx.ops), graph-captured step, flat-bucket DDP on RCCL (default)
+  torch   reference-equivalent stock PyTorch-ROCm: eager nn.Module, autocast bf16,
+          torch DDP on RCCL, torch.optim.SGD — the measured "reference" column of BASELINE.md
+
+Every timed step does the full work: input normalisation from uint8, forward, loss,
+backward, gradient all-reduce (N>1) and the SGD-momentum update.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+# Reference-equivalent stock PyTorch ResNet-50 throughput measured on ONE MI355X with
+# `python bench.py --impl torch`. None until measured.
+BASELINE_IMG_PER_SEC_PER_GPU = None
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--batch", type=int, default=256, help="per-GPU batch (weak scaling)")
+    p.add_argument("--impl", default="native", choices=["native", "torch"])
+    p.add_argument("--model", default="resnet50")
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--num-classes", type=int, default=1000)
+    p.add_argument("--channels-last", type=int, default=1, help="torch impl only")
+    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--json-out", default=None)
+    return p.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    from dbx_distributed_pytorch_examples_amd.train.bench_steps import build_step
+
+    info = ddist.init_distributed()
+    if info.world_size != args.gpus and info.rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
+    torch.manual_seed(1234 + info.rank)
+    step, meta = build_step(args, info)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ddist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ddist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    elapsed = ddist.all_reduce_max(elapsed)
+
+    n = info.world_size
+    imgs = args.batch * n * args.steps
+    value = imgs / elapsed
+    base = BASELINE_IMG_PER_SEC_PER_GPU
+    out = {
+        "metric": "images/sec (whole node) ResNet-50 ImageNet-1K",
+        "value": round(value, 2),
+        "unit": "images/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(value / (base * n), 4) if base else None),
+        "dtype": "bf16",
+        "data": "synthetic (uint8 NHWC 224x224 images + random labels, on-device; random-init weights)",
+        "config": {
+            "model": f"{args.model} ImageNet-1K {args.image_size}x{args.image_size} {args.num_classes} classes",
+            "global_batch": args.batch * n,
+            "per_gpu_batch": args.batch,
+            "seq_len": None,
+            "parallelism": f"dp{n}",
+            "impl": args.impl,
+            "optimizer": "SGD momentum 0.9 nesterov=False wd 5e-5",
+            **meta,
+        },
+    }
+    if info.rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    ddist.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,28 @@
+// Argument structs shared by the kernel translation units and the pybind11 bindings.
+#pragma once
+typedef __bf16 bf16;
+namespace dbx {
+struct IGemmArgs {
+  const bf16* x;          // A source, NHWC [N][IH][IW][IC]
+  const bf16* w;          // B, [OC][KTOT] with KTOT = R*S*IC (STEM: 8*32)
+  bf16* y;                // out, [M][OC]
+  const float* in_scale;  // prologue affine per input channel (nullable)
+  const float* in_shift;
+  float* stats;           // [nshard][2][OC] (sum, sumsq) or null
+  int N, IH, IW, IC, OH, OW, OC, R, S, stride, pad;
+  int M, nshard, relu_in;
+  // tap subset iterated by the K loop: r = r0 + tstep*tr (tr < nr), s = s0 + tstep*ts (ts < ns)
+  int nr, ns, r0, s0, tstep;
+  // DGRAD: A gather ih = i + dh0 - tr ; output pixel (i*osub + oph, j*osub + opw) of [FH][FW]
+  int dh0, dw0, osub, oph, opw, FH, FW;
+};
+struct WgradArgs {
+  const bf16* dy;        // [M][OC]
+  const bf16* x;         // NHWC input [N][IH][IW][IC] (STEM: IC = 4)
+  float* ws;             // [nsplit][OC][KTOT] fp32 partials
+  const float* in_scale; // prologue on X (BN-apply of previous layer) or null
+  const float* in_shift;
+  int N, IH, IW, IC, OH, OW, OC, R, S, stride, pad;
+  int M, KTOT, nsplit, m_per_split, relu_in;
+};
+}  // namespace dbx

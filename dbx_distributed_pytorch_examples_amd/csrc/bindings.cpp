@@ -1,0 +1,189 @@
+// pybind11 bindings for the HIP kernels: a thin C ABI (raw device pointers + hipStream_t as
+// integers). Deliberately independent of the libtorch C++ API so the extension builds in seconds
+// with hipcc and never mixes ABIs with the bundled torch; the Python side (ops/_ext.py) checks
+// dtype/shape/contiguity and passes tensor.data_ptr() + the current torch stream.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+#include "abi.h"
+
+extern "C" {
+int dbx_conv_igemm(int mode, int bm, int bn, const dbx::IGemmArgs* a, int pro, int stats, int accum, hipStream_t st);
+int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, hipStream_t st);
+int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
+int dbx_bn_finalize(const float*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
+                    float*, float*, float*, hipStream_t);
+int dbx_bn_eval_coeff(int, const float*, const float*, float, const float*, const float*, float*, float*, hipStream_t);
+int dbx_channel_stats(const bf16*, long long, int, float*, int, hipStream_t);
+int dbx_bn_apply(const bf16*, const float*, const float*, const bf16*, const float*, const float*, bf16*, long long, int,
+                 int, int, hipStream_t);
+int dbx_bn_bwd_reduce(const bf16*, const bf16*, const bf16*, const float*, const float*, const float*, const float*,
+                      long long, int, float*, int, int, hipStream_t);
+int dbx_bn_bwd_coeff(const float*, int, int, float, const float*, const float*, const float*, float*, float*, float*,
+                     int, hipStream_t);
+int dbx_bn_bwd_apply(const bf16*, const bf16*, const bf16*, const float*, const float*, const float*, bf16*, bf16*,
+                     long long, int, int, hipStream_t);
+int dbx_maxpool_fwd(const bf16*, const float*, const float*, bf16*, unsigned char*, int, int, int, int, int, int, int,
+                    int, int, int, hipStream_t);
+int dbx_maxpool_bwd(const bf16*, const unsigned char*, bf16*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int dbx_avgpool_fwd(const bf16*, bf16*, int, int, int, hipStream_t);
+int dbx_avgpool_bwd(const bf16*, bf16*, int, int, int, hipStream_t);
+int dbx_softmax_ce(const void*, int, const long long*, void*, float*, float*, int, int, float, float, hipStream_t);
+int dbx_sgd(float*, const float*, float*, bf16*, long long, const float*, float, float, float, float, int, int,
+            const float*, float, hipStream_t);
+int dbx_adam(float*, const float*, float*, float*, bf16*, long long, const float*, float, float, float, float, float, int,
+             float, float, const float*, float, hipStream_t);
+int dbx_sumsq(const float*, long long, float*, hipStream_t);
+int dbx_clip_factor(const float*, float, float*, hipStream_t);
+int dbx_normalize_u8(const unsigned char*, bf16*, const unsigned char*, int, int, int, int, float, float, float, float,
+                     float, float, hipStream_t);
+int dbx_weight_prep(const float*, bf16*, const void*, int, hipStream_t);
+int dbx_cast_f32_bf16(const float*, bf16*, long long, hipStream_t);
+int dbx_cast_bf16_f32(const bf16*, float*, long long, float, int, hipStream_t);
+}
+
+template <typename T>
+static inline T P(uintptr_t v) { return reinterpret_cast<T>(v); }
+static inline hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
+static void check(int rc, const char* what) {
+  if (rc != 0) {
+    std::string msg = std::string("dbx kernel launch failed: ") + what + " rc=" + std::to_string(rc);
+    if (rc > 0) msg += std::string(" (") + hipGetErrorString((hipError_t)rc) + ")";
+    throw std::runtime_error(msg);
+  }
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "dbx_distributed_pytorch_examples_amd native HIP kernels (gfx950)";
+  m.def("conv_igemm", [](int mode, int bm, int bn, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t in_scale,
+                         uintptr_t in_shift, int relu_in, uintptr_t stats, int nshard, int N, int IH, int IW, int IC,
+                         int OH, int OW, int OC, int R, int S_, int stride, int pad, int accum, int nr, int ns, int r0,
+                         int s0, int tstep, int dh0, int dw0, int osub, int oph, int opw, int FH, int FW,
+                         uintptr_t st) {
+    dbx::IGemmArgs a{P<const bf16*>(x), P<const bf16*>(w), P<bf16*>(y), P<const float*>(in_scale),
+                     P<const float*>(in_shift), P<float*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
+                     N * OH * OW, nshard > 0 ? nshard : 1, relu_in, nr, ns, r0, s0, tstep, dh0, dw0, osub, oph, opw,
+                     FH, FW};
+    check(dbx_conv_igemm(mode, bm, bn, &a, in_scale != 0, stats != 0, accum, S(st)), "conv_igemm");
+  });
+  m.def("conv_wgrad", [](int mode, int bm, int bn, uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t in_scale,
+                         uintptr_t in_shift, int relu_in, int N, int IH, int IW, int IC, int OH, int OW, int OC, int R,
+                         int S_, int stride, int pad, int KTOT, int nsplit, int m_per_split, uintptr_t st) {
+    dbx::WgradArgs a{P<const bf16*>(dy), P<const bf16*>(x), P<float*>(ws), P<const float*>(in_scale),
+                     P<const float*>(in_shift), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad, N * OH * OW, KTOT,
+                     nsplit, m_per_split, relu_in};
+    check(dbx_conv_wgrad(mode, bm, bn, &a, in_scale != 0, S(st)), "conv_wgrad");
+  });
+  m.def("wgrad_reduce", [](uintptr_t ws, uintptr_t dw, long long n, int nsplit, float scale, int acc, uintptr_t st) {
+    check(dbx_wgrad_reduce(P<const float*>(ws), P<float*>(dw), n, nsplit, scale, acc, S(st)), "wgrad_reduce");
+  });
+  m.def("bn_finalize", [](uintptr_t stats, int nshard, int C, float count, uintptr_t gamma, uintptr_t beta, float eps,
+                          float momentum, uintptr_t rm, uintptr_t rv, uintptr_t scale, uintptr_t shift, uintptr_t smean,
+                          uintptr_t sinv, uintptr_t st) {
+    check(dbx_bn_finalize(P<const float*>(stats), nshard, C, count, P<const float*>(gamma), P<const float*>(beta), eps,
+                          momentum, P<float*>(rm), P<float*>(rv), P<float*>(scale), P<float*>(shift), P<float*>(smean),
+                          P<float*>(sinv), S(st)),
+          "bn_finalize");
+  });
+  m.def("bn_eval_coeff", [](int C, uintptr_t gamma, uintptr_t beta, float eps, uintptr_t rm, uintptr_t rv,
+                            uintptr_t scale, uintptr_t shift, uintptr_t st) {
+    check(dbx_bn_eval_coeff(C, P<const float*>(gamma), P<const float*>(beta), eps, P<const float*>(rm),
+                            P<const float*>(rv), P<float*>(scale), P<float*>(shift), S(st)),
+          "bn_eval_coeff");
+  });
+  m.def("channel_stats", [](uintptr_t y, long long M, int C, uintptr_t stats, int nshard, uintptr_t st) {
+    check(dbx_channel_stats(P<const bf16*>(y), M, C, P<float*>(stats), nshard, S(st)), "channel_stats");
+  });
+  m.def("bn_apply", [](uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t res, uintptr_t rsc, uintptr_t rsh,
+                       uintptr_t out, long long n, int C, int res_mode, int relu, uintptr_t st) {
+    check(dbx_bn_apply(P<const bf16*>(y), P<const float*>(sc), P<const float*>(sh), P<const bf16*>(res),
+                       P<const float*>(rsc), P<const float*>(rsh), P<bf16*>(out), n, C, res_mode, relu, S(st)),
+          "bn_apply");
+  });
+  m.def("bn_bwd_reduce", [](uintptr_t dout, uintptr_t mref, uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t mean,
+                            uintptr_t invstd, long long M, int C, uintptr_t stats, int nshard, int mask_mode,
+                            uintptr_t st) {
+    check(dbx_bn_bwd_reduce(P<const bf16*>(dout), P<const bf16*>(mref), P<const bf16*>(y), P<const float*>(sc),
+                            P<const float*>(sh), P<const float*>(mean), P<const float*>(invstd), M, C,
+                            P<float*>(stats), nshard, mask_mode, S(st)),
+          "bn_bwd_reduce");
+  });
+  m.def("bn_bwd_coeff", [](uintptr_t stats, int nshard, int C, float count, uintptr_t gamma, uintptr_t mean,
+                           uintptr_t invstd, uintptr_t coeff, uintptr_t dgamma, uintptr_t dbeta, int acc, uintptr_t st) {
+    check(dbx_bn_bwd_coeff(P<const float*>(stats), nshard, C, count, P<const float*>(gamma), P<const float*>(mean),
+                           P<const float*>(invstd), P<float*>(coeff), P<float*>(dgamma), P<float*>(dbeta), acc, S(st)),
+          "bn_bwd_coeff");
+  });
+  m.def("bn_bwd_apply", [](uintptr_t dout, uintptr_t mref, uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t coeff,
+                           uintptr_t dy, uintptr_t gout, long long n, int C, int mask_mode, uintptr_t st) {
+    check(dbx_bn_bwd_apply(P<const bf16*>(dout), P<const bf16*>(mref), P<const bf16*>(y), P<const float*>(sc),
+                           P<const float*>(sh), P<const float*>(coeff), P<bf16*>(dy), P<bf16*>(gout), n, C, mask_mode,
+                           S(st)),
+          "bn_bwd_apply");
+  });
+  m.def("maxpool_fwd", [](uintptr_t x, uintptr_t sc, uintptr_t sh, uintptr_t out, uintptr_t arg, int N, int H, int W,
+                          int C, int Pp, int Q, int K, int stride, int pad, int relu, uintptr_t st) {
+    check(dbx_maxpool_fwd(P<const bf16*>(x), P<const float*>(sc), P<const float*>(sh), P<bf16*>(out),
+                          P<unsigned char*>(arg), N, H, W, C, Pp, Q, K, stride, pad, relu, S(st)),
+          "maxpool_fwd");
+  });
+  m.def("maxpool_bwd", [](uintptr_t dout, uintptr_t arg, uintptr_t dx, int N, int H, int W, int C, int Pp, int Q, int K,
+                          int stride, int pad, uintptr_t st) {
+    check(dbx_maxpool_bwd(P<const bf16*>(dout), P<const unsigned char*>(arg), P<bf16*>(dx), N, H, W, C, Pp, Q, K,
+                          stride, pad, S(st)),
+          "maxpool_bwd");
+  });
+  m.def("avgpool_fwd", [](uintptr_t x, uintptr_t out, int N, int HW, int C, uintptr_t st) {
+    check(dbx_avgpool_fwd(P<const bf16*>(x), P<bf16*>(out), N, HW, C, S(st)), "avgpool_fwd");
+  });
+  m.def("avgpool_bwd", [](uintptr_t dout, uintptr_t dx, int N, int HW, int C, uintptr_t st) {
+    check(dbx_avgpool_bwd(P<const bf16*>(dout), P<bf16*>(dx), N, HW, C, S(st)), "avgpool_bwd");
+  });
+  m.def("softmax_ce", [](uintptr_t logits, int is_bf16, uintptr_t labels, uintptr_t dlogits, uintptr_t loss_out,
+                         uintptr_t stats, int B, int C, float smoothing, float gscale, uintptr_t st) {
+    check(dbx_softmax_ce(P<const void*>(logits), is_bf16, P<const long long*>(labels), P<void*>(dlogits),
+                         P<float*>(loss_out), P<float*>(stats), B, C, smoothing, gscale, S(st)),
+          "softmax_ce");
+  });
+  m.def("sgd", [](uintptr_t p, uintptr_t g, uintptr_t v, uintptr_t p16, long long n, uintptr_t hyper, float lr,
+                  float mom, float damp, float wd, int nesterov, int first, uintptr_t gsp, float gs, uintptr_t st) {
+    check(dbx_sgd(P<float*>(p), P<const float*>(g), P<float*>(v), P<bf16*>(p16), n, P<const float*>(hyper), lr, mom,
+                  damp, wd, nesterov, first, P<const float*>(gsp), gs, S(st)),
+          "sgd");
+  });
+  m.def("adam", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t p16, long long n, uintptr_t hyper,
+                   float lr, float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2, uintptr_t gsp,
+                   float gs, uintptr_t st) {
+    check(dbx_adam(P<float*>(p), P<const float*>(g), P<float*>(mm), P<float*>(v), P<bf16*>(p16), n,
+                   P<const float*>(hyper), lr, b1, b2, eps, wd, decoupled, bc1, bc2, P<const float*>(gsp), gs, S(st)),
+          "adam");
+  });
+  m.def("sumsq", [](uintptr_t x, long long n, uintptr_t out, uintptr_t st) {
+    check(dbx_sumsq(P<const float*>(x), n, P<float*>(out), S(st)), "sumsq");
+  });
+  m.def("clip_factor", [](uintptr_t sumsq, float max_norm, uintptr_t out, uintptr_t st) {
+    check(dbx_clip_factor(P<const float*>(sumsq), max_norm, P<float*>(out), S(st)), "clip_factor");
+  });
+  m.def("normalize_u8", [](uintptr_t in, uintptr_t out, uintptr_t flip, int N, int H, int W, int Cin, float m0, float m1,
+                           float m2, float s0, float s1, float s2, uintptr_t st) {
+    check(dbx_normalize_u8(P<const unsigned char*>(in), P<bf16*>(out), P<const unsigned char*>(flip), N, H, W, Cin, m0,
+                           m1, m2, s0, s1, s2, S(st)),
+          "normalize_u8");
+  });
+  m.def("weight_prep", [](uintptr_t master, uintptr_t wbuf, uintptr_t desc, int nlayers, uintptr_t st) {
+    check(dbx_weight_prep(P<const float*>(master), P<bf16*>(wbuf), P<const void*>(desc), nlayers, S(st)),
+          "weight_prep");
+  });
+  m.def("cast_f32_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t st) {
+    check(dbx_cast_f32_bf16(P<const float*>(x), P<bf16*>(y), n, S(st)), "cast_f32_bf16");
+  });
+  m.def("cast_bf16_f32", [](uintptr_t x, uintptr_t y, long long n, float scale, int acc, uintptr_t st) {
+    check(dbx_cast_bf16_f32(P<const bf16*>(x), P<float*>(y), n, scale, acc, S(st)), "cast_bf16_f32");
+  });
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,615 @@
+// NHWC bf16 implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16).
+//
+// Replaces the cuDNN/MIOpen conv kernels the reference reaches through torchvision
+// (SURVEY.md §2.4 K1-K5). One kernel family, three problem mappings:
+//
+//   FWD    Y[m=(n,oh,ow)][k]  = sum_{r,s,c} X[n][oh*st-pad+r][ow*st-pad+s][c] * W[k][r][s][c]
+//   DGRAD  dX[m=(n,h,w)][c]   = sum_{r,s,k} dY[n][(h+pad-r)/st][(w+pad-s)/st][k] * Wt[c][r][s][k]
+//          (transposed gather: a tap contributes only where (h+pad-r) % st == 0)
+//   STEM   the 7x7 C=3 stem with the image padded to 4 channels: a "tap" is one filter row r
+//          and its 8 pixels x 4 channels (64 contiguous bytes of an input row); K = 8 x 32.
+//
+// GEMM view: M = output pixels, N = output channels, K = taps x input channels. Both operands are
+// K-contiguous (NHWC activations, KRSC weights), so every lane loads 16 contiguous bytes and the
+// MFMA fragments come straight out of LDS with ds_read_b128 (XOR-swizzled: conflict-free).
+//
+// Fusions (the reason this exists rather than MIOpen — the reference profile spends more time
+// in BatchNorm/ReLU/add passes than in the convolutions, profiles/r1_torch_reference):
+//   * prologue: BN-apply (+ReLU) of the PREVIOUS layer on the A operand while staging it
+//     (y_prev * scale[c] + shift[c], max 0), so BN outputs are never materialised;
+//   * epilogue: per-output-channel sum / sum-of-squares for THIS layer's BN, from the fp32
+//     accumulators, written as per-tile-row partials into sharded fp32 slabs (atomics);
+//   * epilogue: accumulate into the existing output (dX of a block = dgrad(conv1) + dgrad(ds)).
+//
+// Tiles: BM x BN x 64, 256 threads = 2x2 waves, double-buffered LDS with register staging
+// (the prologue needs the data in registers anyway), one barrier per K block, XCD-aware
+// tile order (A-sharing tiles adjacent -> same XCD L2).
+#include "common.h"
+#include "abi.h"
+
+namespace dbx {
+
+enum ConvMode { FWD = 0, DGRAD = 1, STEM = 2 };
+
+
+template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM>
+__global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
+  constexpr int BK = 64;
+  constexpr int A_CH = BM * BK / 8 / 256;  // 16-byte chunks per thread (A)
+  constexpr int B_CH = BN * BK / 8 / 256;
+  constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 MFMA tiles per wave (2x2 waves)
+  constexpr int LDS_AB = 2 * (BM + BN) * BK;  // bf16 elements
+  constexpr int LDS_C = BM * (BN + 8);
+  constexpr int LDS_ELEMS = (LDS_AB > LDS_C + 4 * BN * 2) ? LDS_AB : (LDS_C + 4 * BN * 2);
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
+  bf16* sA = lds;                  // [2][BM][BK]
+  bf16* sB = lds + 2 * BM * BK;    // [2][BN][BK]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
+  const int ntn = a.OC / BN, ntm = (a.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, ntn * ntm);
+  const int tm = bid / ntn, tn = bid - tm * ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- per-thread A rows: decompose output pixel once ------------------------------
+  const int ach = tid & 7;
+  const bf16* abase[A_CH];
+  int ahb[A_CH], awb[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    const int ohw = a.OH * a.OW;
+    int n = m / ohw;
+    const int pq = m - n * ohw;
+    const int oh = pq / a.OW, ow = pq - (pq / a.OW) * a.OW;
+    if (m >= a.M) { n = 0; }
+    abase[i] = a.x + (size_t)n * a.IH * a.IW * a.IC;
+    if (MODE == DGRAD) { ahb[i] = oh + a.dh0; awb[i] = ow + a.dw0; }
+    else { ahb[i] = oh * a.stride - a.pad; awb[i] = ow * a.stride - a.pad; }
+    if (m >= a.M) ahb[i] = -(1 << 28);
+  }
+  const int KTOT = (MODE == STEM) ? 256 : a.R * a.S * a.IC;  // weight row length
+  const int cpt = (MODE == STEM) ? 1 : a.IC / BK;              // K blocks per tap
+  const int KB = (MODE == STEM) ? 4 : a.nr * a.ns * cpt;
+
+  u32x4 ra[A_CH], rb[B_CH];
+  const u32x4 zero4 = {0u, 0u, 0u, 0u};
+
+  auto load_a = [&](int kb) {
+    if constexpr (MODE == STEM) {
+      // k block kb covers filter rows r = 2kb, 2kb+1; chunk ach: r = 2kb + (ach>>2), pixels
+      // s = 2*(ach&3), +1, 4 channels (8 bytes) each.
+      const int r = 2 * kb + (ach >> 2);
+      const int s0 = 2 * (ach & 3);
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int ih = ahb[i] + r;
+        const bool rv = (r < a.R) && ih >= 0 && ih < a.IH;
+        unsigned int w4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int s = s0 + p, iw = awb[i] + s;
+          if (rv && s < a.S && iw >= 0 && iw < a.IW) {
+            const uint2 v = *reinterpret_cast<const uint2*>(abase[i] + ((size_t)ih * a.IW + iw) * 4);
+            w4[2 * p] = v.x; w4[2 * p + 1] = v.y;
+          }
+        }
+        ra[i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
+      }
+    } else {
+      const int tap = kb / cpt;
+      const int c0 = (kb - tap * cpt) * BK + ach * 8;
+      const int tr = tap / a.ns, ts = tap - (tap / a.ns) * a.ns;
+      const int r = a.r0 + a.tstep * tr, s = a.s0 + a.tstep * ts;
+      f32x4 ps0, ps1, ph0, ph1;  // prologue affine of this thread's 8 channels (same for all its rows)
+      if constexpr (PRO) {
+        ps0 = *reinterpret_cast<const f32x4*>(a.in_scale + c0);
+        ps1 = *reinterpret_cast<const f32x4*>(a.in_scale + c0 + 4);
+        ph0 = *reinterpret_cast<const f32x4*>(a.in_shift + c0);
+        ph1 = *reinterpret_cast<const f32x4*>(a.in_shift + c0 + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        int ih, iw;
+        bool v;
+        if constexpr (MODE == DGRAD) {
+          ih = ahb[i] - tr; iw = awb[i] - ts;
+          v = ih >= 0 && iw >= 0 && ih < a.IH && iw < a.IW;
+        } else {
+          ih = ahb[i] + r; iw = awb[i] + s;
+          v = ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
+        }
+        if (v) {
+          ra[i] = *reinterpret_cast<const u32x4*>(abase[i] + ((size_t)ih * a.IW + iw) * a.IC + c0);
+          if constexpr (PRO) {
+            float f[8];
+            unpack8(ra[i], f);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              f[j] = f[j] * ps0[j] + ph0[j];
+              f[j + 4] = f[j + 4] * ps1[j] + ph1[j];
+            }
+            if (a.relu_in) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+            }
+            ra[i] = pack8(f);
+          }
+        } else {
+          ra[i] = zero4;
+        }
+      }
+    }
+  };
+  auto load_b = [&](int kb) {
+    int koff;
+    if constexpr (MODE == STEM) {
+      koff = kb * BK + ach * 8;
+    } else {
+      const int tap = kb / cpt;
+      const int tr = tap / a.ns, ts = tap - (tap / a.ns) * a.ns;
+      koff = ((a.r0 + a.tstep * tr) * a.S + a.s0 + a.tstep * ts) * a.IC + (kb - tap * cpt) * BK + ach * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      rb[i] = *reinterpret_cast<const u32x4*>(a.w + (size_t)n * KTOT + koff);
+    }
+  };
+  auto store_ab = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<u32x4*>(sA + buf * BM * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<u32x4*>(sB + buf * BN * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_a(0);
+  load_b(0);
+  store_ab(0);
+  __syncthreads();
+
+  for (int kb = 0; kb < KB; ++kb) {
+    const int buf = kb & 1;
+    if (kb + 1 < KB) { load_a(kb + 1); load_b(kb + 1); }
+    const bf16* cA = sA + buf * BM * BK;
+    const bf16* cB = sB + buf * BN * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+      const int ch = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (BM / 2) + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(cA + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (BN / 2) + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(cB + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kb + 1 < KB) store_ab(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ------------------------------------------------------------------------
+  // acc[i][j][r]: row = wm*BM/2 + i*16 + (lane>>4)*4 + r, col = wn*BN/2 + j*16 + (lane&15)
+  bf16* sC = lds;  // [BM][BN+8]
+  float* sStat = reinterpret_cast<float*>(lds + LDS_C);  // [2 wm][2][BN]
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * (BN / 2) + j * 16 + (lane & 15);
+        sC[row * (BN + 8) + col] = (bf16)acc[i][j][r];
+      }
+  if constexpr (STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = (float)(bf16)acc[i][j][r];
+          s += v; q += v * v;
+        }
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        const int col = wn * (BN / 2) + j * 16 + lane;
+        sStat[(wm * 2 + 0) * BN + col] = s;
+        sStat[(wm * 2 + 1) * BN + col] = q;
+      }
+    }
+  }
+  __syncthreads();
+  if constexpr (STATS) {
+    if (tid < BN) {
+      const float s = sStat[0 * BN + tid] + sStat[2 * BN + tid];
+      const float q = sStat[1 * BN + tid] + sStat[3 * BN + tid];
+      float* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
+      atomicAdd(st + n0 + tid, s);
+      atomicAdd(st + a.OC + n0 + tid, q);
+    }
+  }
+  constexpr int CPR = BN / 8;  // 16B chunks per output row
+#pragma unroll
+  for (int it = 0; it < BM * CPR / 256; ++it) {
+    const int idx = tid + it * 256;
+    const int row = idx / CPR, cc = idx - row * CPR;
+    const int m = m0 + row;
+    if (m < a.M) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(sC + row * (BN + 8) + cc * 8);
+      size_t pix = (size_t)m;
+      if (MODE == DGRAD && a.osub > 1) {
+        const int ohw = a.OH * a.OW;
+        const int n = m / ohw, pq = m - (m / ohw) * ohw;
+        const int i = pq / a.OW, j = pq - (pq / a.OW) * a.OW;
+        pix = ((size_t)n * a.FH + i * a.osub + a.oph) * a.FW + j * a.osub + a.opw;
+      }
+      bf16* dst = a.y + pix * a.OC + n0 + cc * 8;
+      if constexpr (ACCUM) {
+        float f[8], g[8];
+        unpack8(v, f);
+        unpack8(*reinterpret_cast<const u32x4*>(dst), g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += g[j];
+        v = pack8(f);
+      }
+      *reinterpret_cast<u32x4*>(dst) = v;
+    }
+  }
+}
+
+// ======================================================================================
+// Weight gradient: dW[k][kk] = sum_m dY[m][k] * Xcol[m][kk]   (kk = (r, s, c), KRSC order)
+// Both operands arrive pixel-major (reduction dim outermost), so tiles are staged as
+// [64 pixels][128 cols] row-major (16B/lane copies) and the MFMA fragments are read
+// column-wise with ds_read_b64_tr_b16 (gfx950 hardware-transposed LDS read). The reduction over
+// M = N*OH*OW (up to 3.2M pixels) is split over blocks; each block writes an fp32 partial slab
+// and wgrad_reduce sums the slabs in a fixed order (deterministic).
+// ======================================================================================
+
+__device__ __forceinline__ int tr_swz(int row, int ch, int nch) {
+  // conflict-free for the transposed reads (see tools/lds_banks.py): 16 chunks per 256B row
+  if (nch == 16) return ch ^ ((((row & 3) | ((row >> 1) & 4)) << 1) & 15);
+  return ch ^ ((((row & 3) << 1) ^ (((row >> 3) & 1) << 1)) & 7);
+}
+
+template <int BM, int BN, int MODE, bool PRO>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
+  constexpr int BKM = 64;                    // pixels per K block
+  constexpr int NCA = BM / 8, NCB = BN / 8;  // 16B chunks per tile row
+  constexpr int A_CH = BKM * NCA / 256, B_CH = BKM * NCB / 256;
+  constexpr int TM = BM / 32, TN = BN / 32;
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * BKM * (BM + BN)];
+  bf16* sA = lds;                   // [2][BKM][BM]
+  bf16* sB = lds + 2 * BKM * BM;    // [2][BKM][BN]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
+  const int ntm = a.OC / BM, ntn = a.KTOT / BN;
+  const int ntile = ntm * ntn;
+  // blockIdx.x = split * ntile + tile : consecutive blocks of a split share its dY rows
+  const int split = blockIdx.x / ntile;
+  const int tile = blockIdx.x - split * ntile;
+  const int tm = tile / ntn, tn = tile - (tile / ntn) * ntn;
+  const int k0 = tm * BM, kk0 = tn * BN;
+  const int mbeg = split * a.m_per_split;
+  const int mend = min(a.M, mbeg + a.m_per_split);
+  const int nkb = (mend - mbeg + BKM - 1) / BKM;
+
+  // A (dY) loader: thread -> (pixel row ra_row = tid / (256/A_CH... )
+  // each thread owns one pixel row and A_CH chunks of it (chunk = c0 + j*stride)
+  constexpr int ATPR = NCA / A_CH;   // threads per pixel row for A
+  constexpr int BTPR = NCB / B_CH;   // threads per pixel row for B
+  const int a_row = tid / ATPR, a_c = tid % ATPR;
+  const int b_row = tid / BTPR, b_c = tid % BTPR;
+
+  // B column chunks: tap and channel per chunk (fixed over the K loop)
+  int b_tap_h[B_CH], b_tap_w[B_CH], b_ch[B_CH];
+#pragma unroll
+  for (int j = 0; j < B_CH; ++j) {
+    const int cc = b_c + j * BTPR;
+    const int kk = kk0 + cc * 8;
+    if constexpr (MODE == STEM) {  // kk = r*32 + s*4 + c  (8 pixels x 4 ch per filter row)
+      b_tap_h[j] = kk >> 5; b_tap_w[j] = (kk >> 2) & 7; b_ch[j] = 0;
+    } else {
+      const int tap = kk / a.IC;
+      b_ch[j] = kk - tap * a.IC;
+      b_tap_h[j] = tap / a.S; b_tap_w[j] = tap - (tap / a.S) * a.S;
+    }
+  }
+  u32x4 ra[A_CH], rb[B_CH];
+  const u32x4 zero4 = {0u, 0u, 0u, 0u};
+  float psc[PRO ? B_CH : 1][8], psh[PRO ? B_CH : 1][8];  // prologue affine per B chunk (fixed)
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < B_CH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { psc[j][e] = a.in_scale[b_ch[j] + e]; psh[j][e] = a.in_shift[b_ch[j] + e]; }
+  }
+
+  auto load = [&](int kb) {
+    const int ma = mbeg + kb * BKM + a_row;
+#pragma unroll
+    for (int j = 0; j < A_CH; ++j) {
+      const int cc = a_c + j * ATPR;
+      ra[j] = (ma < mend) ? *reinterpret_cast<const u32x4*>(a.dy + (size_t)ma * a.OC + k0 + cc * 8) : zero4;
+    }
+    const int mb = mbeg + kb * BKM + b_row;
+    const bool mv = mb < mend;
+    const int ohw = a.OH * a.OW;
+    const int n = mv ? mb / ohw : 0;
+    const int pq = mb - n * ohw;
+    const int oh = pq / a.OW, ow = pq - (pq / a.OW) * a.OW;
+    const bf16* base = a.x + (size_t)n * a.IH * a.IW * a.IC;
+#pragma unroll
+    for (int j = 0; j < B_CH; ++j) {
+      const int ih = oh * a.stride - a.pad + b_tap_h[j];
+      if constexpr (MODE == STEM) {
+        // 16B chunk = 2 pixels (s, s+1) x 4 channels
+        unsigned int w4[4] = {0u, 0u, 0u, 0u};
+        const bool rv = mv && b_tap_h[j] < a.R && ih >= 0 && ih < a.IH;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int s = b_tap_w[j] + p, iw = ow * a.stride - a.pad + s;
+          if (rv && s < a.S && iw >= 0 && iw < a.IW) {
+            const uint2 v = *reinterpret_cast<const uint2*>(base + ((size_t)ih * a.IW + iw) * 4);
+            w4[2 * p] = v.x; w4[2 * p + 1] = v.y;
+          }
+        }
+        rb[j] = u32x4{w4[0], w4[1], w4[2], w4[3]};
+      } else {
+        const int iw = ow * a.stride - a.pad + b_tap_w[j];
+        const bool v = mv && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
+        if (v) {
+          rb[j] = *reinterpret_cast<const u32x4*>(base + ((size_t)ih * a.IW + iw) * a.IC + b_ch[j]);
+          if constexpr (PRO) {
+            float f[8];
+            unpack8(rb[j], f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              f[e] = f[e] * psc[j][e] + psh[j][e];
+              if (a.relu_in) f[e] = fmaxf(f[e], 0.f);
+            }
+            rb[j] = pack8(f);
+          }
+        } else {
+          rb[j] = zero4;
+        }
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < A_CH; ++j) {
+      const int cc = a_c + j * ATPR;
+      *reinterpret_cast<u32x4*>(sA + buf * BKM * BM + a_row * BM + (tr_swz(a_row, cc, NCA) << 3)) = ra[j];
+    }
+#pragma unroll
+    for (int j = 0; j < B_CH; ++j) {
+      const int cc = b_c + j * BTPR;
+      *reinterpret_cast<u32x4*>(sB + buf * BKM * BN + b_row * BN + (tr_swz(b_row, cc, NCB) << 3)) = rb[j];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nkb > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int buf = kb & 1;
+    if (kb + 1 < nkb) load(kb + 1);
+    const bf16* cA = sA + buf * BKM * BM;
+    const bf16* cB = sB + buf * BKM * BN;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * (BM / 2) + i * 16 + 4 * p;
+        s16x4 lo, hi;
+        {
+          const int row = ks * 32 + 8 * g + q;
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (DBX_LDS s16x4*)(cA + row * BM + (tr_swz(row, col >> 3, NCA) << 3) + (col & 7)));
+          const int row2 = row + 4;
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (DBX_LDS s16x4*)(cA + row2 * BM + (tr_swz(row2, col >> 3, NCA) << 3) + (col & 7)));
+        }
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / 2) + j * 16 + 4 * p;
+        s16x4 lo, hi;
+        {
+          const int row = ks * 32 + 8 * g + q;
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (DBX_LDS s16x4*)(cB + row * BN + (tr_swz(row, col >> 3, NCB) << 3) + (col & 7)));
+          const int row2 = row + 4;
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (DBX_LDS s16x4*)(cB + row2 * BN + (tr_swz(row2, col >> 3, NCB) << 3) + (col & 7)));
+        }
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kb + 1 < nkb) store(buf ^ 1);
+    __syncthreads();
+  }
+  // partial slab write: ws[split][k][kk]
+  float* out = a.ws + (size_t)split * a.OC * a.KTOT;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        const int kk = kk0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        out[(size_t)k * a.KTOT + kk] = acc[i][j][r];
+      }
+}
+
+// Deterministic 2-level split-K reduction. Level 1 (G > 1): thread (i, g) sums the fixed split
+// range of group g into ws2[g][i]; level 2 sums the G group partials in order, scales, and writes
+// (or accumulates into) the fp32 gradient. Both levels are wide (n4 x G threads), so a 1024-split
+// reduction of a tiny 64x64 weight no longer serialises 1024 dependent loads in one thread.
+__global__ void wgrad_reduce_l1_kernel(const float* __restrict__ ws, float* __restrict__ ws2, int n4, int nsplit,
+                                       int spg) {
+  const f32x4* w4 = reinterpret_cast<const f32x4*>(ws);
+  f32x4* o4 = reinterpret_cast<f32x4*>(ws2);
+  const int g = blockIdx.y;
+  const int s0 = g * spg, s1 = min(nsplit, s0 + spg);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = s0; k < s1; ++k) s += w4[(size_t)k * n4 + i];
+    o4[(size_t)g * n4 + i] = s;
+  }
+}
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
+                                    int n4, int nsplit, float scale, int accumulate) {
+  const f32x4* w4 = reinterpret_cast<const f32x4*>(ws);
+  f32x4* o4 = reinterpret_cast<f32x4*>(dw);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    f32x4 s = w4[i];
+    for (int k = 1; k < nsplit; ++k) s += w4[(size_t)k * n4 + i];
+    s *= scale;
+    if (accumulate) s += o4[i];
+    o4[i] = s;
+  }
+}
+
+}  // namespace dbx
+
+// ======================================================================================
+// host launchers (C ABI; raw pointers + stream, called from bindings.cpp)
+// ======================================================================================
+using namespace dbx;
+
+template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM>
+static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
+  const int nwg = (a.OC / BN) * ((a.M + BM - 1) / BM);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, MODE, PRO, STATS, ACCUM>), dim3(nwg), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int MODE>
+static int dispatch_flags(const IGemmArgs& a, bool pro, bool stats, bool accum, hipStream_t st) {
+  if (pro) {
+    if (stats) return accum ? launch_igemm_t<BM, BN, MODE, true, true, true>(a, st) : launch_igemm_t<BM, BN, MODE, true, true, false>(a, st);
+    return accum ? launch_igemm_t<BM, BN, MODE, true, false, true>(a, st) : launch_igemm_t<BM, BN, MODE, true, false, false>(a, st);
+  }
+  if (stats) return accum ? launch_igemm_t<BM, BN, MODE, false, true, true>(a, st) : launch_igemm_t<BM, BN, MODE, false, true, false>(a, st);
+  return accum ? launch_igemm_t<BM, BN, MODE, false, false, true>(a, st) : launch_igemm_t<BM, BN, MODE, false, false, false>(a, st);
+}
+
+extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
+                              int accum, hipStream_t st) {
+  const IGemmArgs& a = *args;
+  if (a.OC % bn != 0) return -1;
+  if (mode == STEM) {
+    if (pro || accum) return -2;
+    if (bm == 128 && bn == 64) return dispatch_flags<128, 64, STEM>(a, false, stats, false, st);
+    return -3;
+  }
+  if (a.IC % 64 != 0) return -4;
+  if (mode == FWD) {
+    if (bm == 128 && bn == 128) return dispatch_flags<128, 128, FWD>(a, pro, stats, accum, st);
+    if (bm == 128 && bn == 64) return dispatch_flags<128, 64, FWD>(a, pro, stats, accum, st);
+    if (bm == 64 && bn == 64) return dispatch_flags<64, 64, FWD>(a, pro, stats, accum, st);
+    return -3;
+  }
+  if (mode == DGRAD) {
+    if (pro) return -2;
+    if (bm == 128 && bn == 128) return dispatch_flags<128, 128, DGRAD>(a, false, stats, accum, st);
+    if (bm == 128 && bn == 64) return dispatch_flags<128, 64, DGRAD>(a, false, stats, accum, st);
+    if (bm == 64 && bn == 64) return dispatch_flags<64, 64, DGRAD>(a, false, stats, accum, st);
+    return -3;
+  }
+  return -5;
+}
+
+extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, int pro, hipStream_t st) {
+  const WgradArgs& a = *args;
+  if (a.OC % bm != 0 || a.KTOT % bn != 0) return -1;
+  const int nblk = (a.OC / bm) * (a.KTOT / bn) * a.nsplit;
+  if (mode == STEM) {
+    if (bm == 64 && bn == 128) hipLaunchKernelGGL((wgrad_kernel<64, 128, STEM, false>), dim3(nblk), dim3(256), 0, st, a);
+    else return -3;
+    return (int)hipGetLastError();
+  }
+  if (a.IC % bn != 0 && !(bn == 128 && a.IC == 64 && false)) {
+    // a column tile must stay inside one tap
+    if (a.IC % bn != 0) return -4;
+  }
+#define WG(BM_, BN_)                                                                                   \
+  if (bm == BM_ && bn == BN_) {                                                                        \
+    if (pro) hipLaunchKernelGGL((wgrad_kernel<BM_, BN_, FWD, true>), dim3(nblk), dim3(256), 0, st, a); \
+    else hipLaunchKernelGGL((wgrad_kernel<BM_, BN_, FWD, false>), dim3(nblk), dim3(256), 0, st, a);    \
+    return (int)hipGetLastError();                                                                     \
+  }
+  WG(128, 128)
+  WG(128, 64)
+  WG(64, 128)
+  WG(64, 64)
+#undef WG
+  return -3;
+}
+
+extern "C" int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale,
+                                int accumulate, hipStream_t st) {
+  if (n % 4) return -1;
+  const int n4 = (int)(n / 4);
+  const int gx = (n4 + 255) / 256;
+  if (nsplit > 8 && (long long)gx * 4 < 1024) {
+    // level 1 into the tail of the workspace (after the nsplit slabs)
+    int G = 1024 / gx;
+    if (G > nsplit / 4) G = nsplit / 4;
+    if (G > 64) G = 64;
+    if (G < 2) G = 2;
+    const int spg = (nsplit + G - 1) / G;
+    G = (nsplit + spg - 1) / spg;
+    float* ws2 = const_cast<float*>(ws) + (size_t)nsplit * n;
+    hipLaunchKernelGGL(wgrad_reduce_l1_kernel, dim3(gx, G), dim3(256), 0, st, ws, ws2, n4, nsplit, spg);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(gx), dim3(256), 0, st, ws2, dw, n4, G, scale, accumulate);
+  } else {
+    const int grid = gx > 4096 ? 4096 : gx;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, st, ws, dw, n4, nsplit, scale, accumulate);
+  }
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,723 @@
+// Memory-bound CNN ops for the NHWC bf16 ResNet programs (gfx950).
+//
+// The reference executes these as separate MIOpen/ATen passes (BatchNorm fwd/bwd, ReLU,
+// residual add, maxpool, softmax-CE, foreach optimizer: SURVEY.md §2.4 K6-K17, K20). Here each
+// op is one vectorised (16 B/lane) pass, and the passes are fused where the ResNet dataflow
+// allows it:
+//   * BN statistics come from the conv epilogue (conv_igemm.hip); bn_finalize turns the sharded
+//     partial sums into scale/shift + running stats in one tiny launch;
+//   * BN-apply + residual (identity or BN'd downsample branch) + ReLU = ONE pass (bn_apply);
+//   * BN backward = one reduce pass (sum g, sum g*xhat with the ReLU mask recomputed from the
+//     saved pre-BN tensor or the block output) + one apply pass that writes dy (and optionally
+//     the masked gradient for the residual branch) using 3 per-channel coefficients;
+//   * maxpool consumes the stem's raw conv output with BN-apply+ReLU in its prologue;
+//   * softmax-cross-entropy, label smoothing, argmax/correct-count and dlogits in one kernel;
+//   * SGD-momentum / Adam(W) over the flat fp32 master buffer, writing the bf16 compute copy.
+#include "common.h"
+
+namespace dbx {
+
+// ----------------------------------------------------------------------------------------
+// BN finalize: stats[nshard][2][C] -> scale/shift (+ saved mean/invstd, running stats)
+// ----------------------------------------------------------------------------------------
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, int nshard, int C, float count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float eps, float momentum, float* running_mean, float* running_var,
+                                   float* scale, float* shift, float* save_mean, float* save_invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < nshard; ++k) {
+    s += stats[(size_t)k * 2 * C + c];
+    q += stats[(size_t)k * 2 * C + C + c];
+  }
+  const double mean = s / count;
+  double var = q / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * invstd;
+  shift[c] = b - (float)mean * g * invstd;
+  if (save_mean) save_mean[c] = (float)mean;
+  if (save_invstd) save_invstd[c] = invstd;
+  if (running_mean && momentum > 0.f) {
+    const double unbiased = count > 1.f ? var * count / (count - 1.0) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  }
+}
+
+// eval-mode BN: scale/shift from running stats
+__global__ void bn_eval_coeff_kernel(int C, const float* gamma, const float* beta, float eps,
+                                     const float* rm, const float* rv, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = rsqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * inv;
+  shift[c] = b - rm[c] * g * inv;
+}
+
+// Channel sums of a bf16 [M][C] tensor (stats pass for layers whose producer cannot emit them)
+__global__ void channel_stats_kernel(const bf16* __restrict__ y, long long M, int C, float* stats, int nshard) {
+  const int tpr = C / 8, rpb = 256 / tpr;
+  const int tid = threadIdx.x;
+  const int cg = tid % tpr, r0 = tid / tpr;
+  float s[8] = {0}, q[8] = {0};
+  if (r0 < rpb) {
+    for (long long m = (long long)blockIdx.x * rpb + r0; m < M; m += (long long)gridDim.x * rpb) {
+      float f[8];
+      unpack8(*reinterpret_cast<const u32x4*>(y + m * C + cg * 8), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
+    }
+  }
+  __shared__ float red[2][256 * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[0][tid * 8 + j] = s[j]; red[1][tid * 8 + j] = q[j]; }
+  __syncthreads();
+  float* st = stats + (size_t)(blockIdx.x % nshard) * 2 * C;
+  for (int c = tid; c < C; c += 256) {
+    const int g = c / 8, j = c % 8;
+    float ss = 0.f, qq = 0.f;
+    for (int r = 0; r < rpb; ++r) { ss += red[0][(r * tpr + g) * 8 + j]; qq += red[1][(r * tpr + g) * 8 + j]; }
+    atomicAdd(st + c, ss);
+    atomicAdd(st + C + c, qq);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// BN apply (+ residual) (+ ReLU):  out = act(y*sc + sh + res_term)
+//   RES 0: none   RES 1: + res (bf16 activation)   RES 2: + res*rsc + rsh (raw downsample conv)
+// ----------------------------------------------------------------------------------------
+// Thread mapping for all per-channel elementwise passes: a thread owns ONE 8-channel group
+// (tpr = C/8 threads per row, rpb = 256/tpr rows per block iteration) and walks rows, so its
+// per-channel coefficients are loaded once into registers instead of once per element.
+struct RowMap {
+  int cg, r0, rpb;
+  __device__ RowMap(int C) {
+    const int tpr = C >> 3;
+    rpb = 256 / tpr;
+    cg = threadIdx.x % tpr;
+    r0 = threadIdx.x / tpr;
+  }
+};
+__device__ __forceinline__ void load8f(const float* p, float* v) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+
+template <int RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ sc,
+                                const float* __restrict__ sh, const bf16* __restrict__ res,
+                                const float* __restrict__ rsc, const float* __restrict__ rsh,
+                                bf16* __restrict__ out, long long M, int C) {
+  const RowMap rm(C);
+  if (rm.r0 >= rm.rpb) return;
+  const int c0 = rm.cg * 8;
+  float s[8], h[8], a[8], b[8];
+  load8f(sc + c0, s);
+  load8f(sh + c0, h);
+  if (RES == 2) { load8f(rsc + c0, a); load8f(rsh + c0, b); }
+  for (long long m = (long long)blockIdx.x * rm.rpb + rm.r0; m < M; m += (long long)gridDim.x * rm.rpb) {
+    const long long e = m * C + c0;
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(y + e), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * s[j] + h[j];
+    if (RES) {
+      float r[8];
+      unpack8(*reinterpret_cast<const u32x4*>(res + e), r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += (RES == 2) ? r[j] * a[j] + b[j] : r[j];
+    }
+    if (RELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    *reinterpret_cast<u32x4*>(out + e) = pack8(f);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// BN backward.
+//   g = dout * mask,  MASK 0: none, 1: (mref > 0) with mref the block output,
+//                     2: (y*sc + sh > 0) recomputed from the pre-BN tensor
+//   reduce: sum g, sum g*xhat (xhat = (y-mean)*invstd) -> stats[nshard][2][C]
+//   coeff:  dy = k1*g + k2*y + k3 ; dgamma = sum g*xhat ; dbeta = sum g
+// ----------------------------------------------------------------------------------------
+template <int MASK>
+__device__ __forceinline__ void load_g(const bf16* dout, const bf16* mref, const bf16* y, const float* sc,
+                                       const float* sh, long long e, float* g, float* yv) {
+  unpack8(*reinterpret_cast<const u32x4*>(dout + e), g);
+  unpack8(*reinterpret_cast<const u32x4*>(y + e), yv);
+  if (MASK == 1) {
+    float mr[8];
+    unpack8(*reinterpret_cast<const u32x4*>(mref + e), mr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = mr[j] > 0.f ? g[j] : 0.f;
+  } else if (MASK == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = (yv[j] * sc[j] + sh[j]) > 0.f ? g[j] : 0.f;
+  }
+}
+
+template <int MASK>
+__global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ mref,
+                                     const bf16* __restrict__ y, const float* __restrict__ sc,
+                                     const float* __restrict__ sh, const float* __restrict__ mean,
+                                     const float* __restrict__ invstd, long long M, int C, float* stats,
+                                     int nshard) {
+  const int tpr = C / 8, rpb = 256 / tpr;
+  const int tid = threadIdx.x;
+  const int cg = tid % tpr, r0 = tid / tpr;
+  const int c0 = cg * 8;
+  float s[8] = {0}, q[8] = {0};
+  if (r0 < rpb) {
+    float mu[8], is[8], scr[8] = {0}, shr[8] = {0};
+    load8f(mean + c0, mu);
+    load8f(invstd + c0, is);
+    if (MASK == 2) { load8f(sc + c0, scr); load8f(sh + c0, shr); }
+    for (long long m = (long long)blockIdx.x * rpb + r0; m < M; m += (long long)gridDim.x * rpb) {
+      float g[8], yv[8];
+      load_g<MASK>(dout, mref, y, scr, shr, m * C + c0, g, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += g[j]; q[j] += g[j] * (yv[j] - mu[j]) * is[j]; }
+    }
+  }
+  __shared__ float red[2][256 * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[0][tid * 8 + j] = s[j]; red[1][tid * 8 + j] = q[j]; }
+  __syncthreads();
+  float* st = stats + (size_t)(blockIdx.x % nshard) * 2 * C;
+  for (int c = tid; c < C; c += 256) {
+    const int g = c / 8, j = c % 8;
+    float ss = 0.f, qq = 0.f;
+    for (int r = 0; r < rpb; ++r) { ss += red[0][(r * tpr + g) * 8 + j]; qq += red[1][(r * tpr + g) * 8 + j]; }
+    atomicAdd(st + c, ss);
+    atomicAdd(st + C + c, qq);
+  }
+}
+
+// per-channel backward coefficients + parameter grads (fp32, written into the flat grad buffer)
+__global__ void bn_bwd_coeff_kernel(const float* __restrict__ stats, int nshard, int C, float count,
+                                    const float* __restrict__ gamma, const float* __restrict__ mean,
+                                    const float* __restrict__ invstd, float* coeff /*[3][C]*/,
+                                    float* dgamma, float* dbeta, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f, q = 0.f;
+  for (int k = 0; k < nshard; ++k) { s += stats[(size_t)k * 2 * C + c]; q += stats[(size_t)k * 2 * C + C + c]; }
+  const float g = gamma ? gamma[c] : 1.f, is = invstd[c], mu = mean[c];
+  const float sg = s / count, sgx = q / count;
+  const float k1 = g * is;
+  const float k2 = -g * is * is * sgx;
+  const float k3 = -g * is * sg + g * is * is * sgx * mu;
+  coeff[c] = k1; coeff[C + c] = k2; coeff[2 * C + c] = k3;
+  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + q;
+  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + s;
+}
+
+template <int MASK, bool WRITE_G>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ mref,
+                                    const bf16* __restrict__ y, const float* __restrict__ sc,
+                                    const float* __restrict__ sh, const float* __restrict__ coeff,
+                                    bf16* __restrict__ dy, bf16* __restrict__ gout, long long M, int C) {
+  const RowMap rm(C);
+  if (rm.r0 >= rm.rpb) return;
+  const int c0 = rm.cg * 8;
+  float k1[8], k2[8], k3[8], scr[8] = {0}, shr[8] = {0};
+  load8f(coeff + c0, k1);
+  load8f(coeff + C + c0, k2);
+  load8f(coeff + 2 * C + c0, k3);
+  if (MASK == 2) { load8f(sc + c0, scr); load8f(sh + c0, shr); }
+  for (long long m = (long long)blockIdx.x * rm.rpb + rm.r0; m < M; m += (long long)gridDim.x * rm.rpb) {
+    const long long e = m * C + c0;
+    float g[8], yv[8];
+    load_g<MASK>(dout, mref, y, scr, shr, e, g, yv);
+    if (WRITE_G) *reinterpret_cast<u32x4*>(gout + e) = pack8(g);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = k1[j] * g[j] + k2[j] * yv[j] + k3[j];
+    *reinterpret_cast<u32x4*>(dy + e) = pack8(o);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// MaxPool 3x3 s2 p1 (NHWC) with BN-apply + ReLU prologue; argmax (0..8) saved as uint8.
+// ----------------------------------------------------------------------------------------
+__global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ sc,
+                                   const float* __restrict__ sh, bf16* __restrict__ out,
+                                   unsigned char* __restrict__ arg, int N, int H, int W, int C, int P,
+                                   int Q, int K, int stride, int pad, int relu) {
+  const int cpt = C / 8;
+  const long long total = (long long)N * P * Q * cpt;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % cpt);
+    long long pix = i / cpt;
+    const int q = (int)(pix % Q); pix /= Q;
+    const int p = (int)(pix % P);
+    const int n = (int)(pix / P);
+    const int c0 = cg * 8;
+    float best[8];
+    unsigned char bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int r = 0; r < K; ++r) {
+      const int h = p * stride - pad + r;
+      if (h < 0 || h >= H) continue;
+      for (int s = 0; s < K; ++s) {
+        const int w = q * stride - pad + s;
+        if (w < 0 || w >= W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const u32x4*>(x + (((size_t)n * H + h) * W + w) * C + c0), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float v = sc ? f[j] * sc[c0 + j] + sh[c0 + j] : f[j];
+          if (relu) v = fmaxf(v, 0.f);
+          if (v > best[j]) { best[j] = v; bi[j] = (unsigned char)(r * K + s); }
+        }
+      }
+    }
+    const size_t o = (((size_t)n * P + p) * Q + q) * C + c0;
+    *reinterpret_cast<u32x4*>(out + o) = pack8(best);
+    *reinterpret_cast<uint2*>(arg + o) = *reinterpret_cast<uint2*>(bi);
+  }
+}
+
+// gather form of the backward (no atomics): dx[n,h,w,c] = sum over windows whose argmax is (h,w)
+__global__ void maxpool_bwd_kernel(const bf16* __restrict__ dout, const unsigned char* __restrict__ arg,
+                                   bf16* __restrict__ dx, int N, int H, int W, int C, int P, int Q, int K,
+                                   int stride, int pad) {
+  const int cpt = C / 8;
+  const long long total = (long long)N * H * W * cpt;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % cpt);
+    long long pix = i / cpt;
+    const int w = (int)(pix % W); pix /= W;
+    const int h = (int)(pix % H);
+    const int n = (int)(pix / H);
+    const int c0 = cg * 8;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // outputs p with p*stride - pad <= h <= p*stride - pad + K - 1
+    const int p_lo = max(0, (h + pad - K + stride) / stride), p_hi = min(P - 1, (h + pad) / stride);
+    const int q_lo = max(0, (w + pad - K + stride) / stride), q_hi = min(Q - 1, (w + pad) / stride);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int r = h - (p * stride - pad);
+      if (r < 0 || r >= K) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int s = w - (q * stride - pad);
+        if (s < 0 || s >= K) continue;
+        const size_t o = (((size_t)n * P + p) * Q + q) * C + c0;
+        float g[8];
+        unpack8(*reinterpret_cast<const u32x4*>(dout + o), g);
+        const uint2 av = *reinterpret_cast<const uint2*>(arg + o);
+        const unsigned char* a8 = reinterpret_cast<const unsigned char*>(&av);
+        const unsigned char me = (unsigned char)(r * K + s);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += (a8[j] == me) ? g[j] : 0.f;
+      }
+    }
+    *reinterpret_cast<u32x4*>(dx + (((size_t)n * H + h) * W + w) * C + c0) = pack8(acc);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Global average pool [N][HW][C] -> [N][C] (bf16 out, fp32 accumulate) and its backward
+// ----------------------------------------------------------------------------------------
+__global__ void avgpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ out, int N, int HW, int C) {
+  const int n = blockIdx.y;
+  const int c0 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (c0 >= C) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < HW; ++i) {
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + ((size_t)n * HW + i) * C + c0), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f[j];
+  }
+  const float inv = 1.f / HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  *reinterpret_cast<u32x4*>(out + (size_t)n * C + c0) = pack8(acc);
+}
+
+__global__ void avgpool_bwd_kernel(const bf16* __restrict__ dout, bf16* __restrict__ dx, int N, int HW, int C) {
+  const long long total = (long long)N * HW * C / 8;
+  const float inv = 1.f / HW;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long e = i * 8;
+    const int c0 = (int)(e % C);
+    const long long n = e / ((long long)HW * C);
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(dout + n * C + c0), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= inv;
+    *reinterpret_cast<u32x4*>(dx + e) = pack8(f);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Softmax cross-entropy (+label smoothing) fused with dlogits, argmax-correct count.
+// One 256-thread block per row; logits fp32 or bf16; dlogits = (p - target)/B * gscale.
+// out_stats[0] += sum loss, out_stats[1] += correct   (device accumulators: no host sync)
+// ----------------------------------------------------------------------------------------
+template <typename T>
+__global__ void softmax_ce_kernel(const T* __restrict__ logits, const long long* __restrict__ labels,
+                                  T* __restrict__ dlogits, float* __restrict__ loss_out, float* stats,
+                                  int B, int C, float smoothing, float gscale) {
+  const int row = blockIdx.x;
+  const T* x = logits + (size_t)row * C;
+  const int tid = threadIdx.x;
+  __shared__ float red[8];
+  __shared__ int redi[8];
+  float mx = -INFINITY;
+  int amx = 0;
+  for (int c = tid; c < C; c += 256) {
+    const float v = (float)x[c];
+    if (v > mx) { mx = v; amx = c; }
+  }
+  // argmax-aware max reduction
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(amx, o, 64);
+    if (om > mx || (om == mx && oa < amx)) { mx = om; amx = oa; }
+  }
+  const int wid = tid >> 6, lane = tid & 63;
+  if (lane == 0) { red[wid] = mx; redi[wid] = amx; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (red[w] > red[0] || (red[w] == red[0] && redi[w] < redi[0])) { red[0] = red[w]; redi[0] = redi[w]; }
+  }
+  __syncthreads();
+  mx = red[0];
+  amx = redi[0];
+  __syncthreads();
+  float se = 0.f, sx = 0.f;
+  for (int c = tid; c < C; c += 256) {
+    const float v = (float)x[c];
+    se += __expf(v - mx);
+    sx += v;
+  }
+  se = wave_sum(se);
+  sx = wave_sum(sx);
+  if (lane == 0) { red[wid] = se; red[4 + wid] = sx; }
+  __syncthreads();
+  se = red[0] + red[1] + red[2] + red[3];
+  sx = red[4] + red[5] + red[6] + red[7];
+  const float lse = mx + __logf(se);
+  const long long lab = labels[row];
+  const float xl = (float)x[lab];
+  // loss = -(1-eps)*log p_lab - eps/C * sum_c log p_c
+  const float loss = (1.f - smoothing) * (lse - xl) + smoothing * (lse - sx / C);
+  if (tid == 0) {
+    if (loss_out) loss_out[row] = loss;
+    if (stats) {
+      atomicAdd(stats, loss);
+      atomicAdd(stats + 1, (amx == lab) ? 1.f : 0.f);
+    }
+  }
+  if (dlogits) {
+    const float inv = gscale / B;
+    for (int c = tid; c < C; c += 256) {
+      const float p = __expf((float)x[c] - lse);
+      const float t = (c == lab ? (1.f - smoothing) : 0.f) + smoothing / C;
+      dlogits[(size_t)row * C + c] = (T)((p - t) * inv);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Fused optimizers over the flat fp32 master buffer (+ optional bf16 compute copy).
+//   SGD (PyTorch semantics): d = g + wd*p; v = mom*v + (1-damp)*d (v = d at step 1);
+//                            d = nesterov ? d + mom*v : v; p -= lr*d
+//   Adam/AdamW: m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr * mhat/(sqrt(vhat)+eps)
+//   grad_scale multiplies g first (DDP averaging / loss scaling / clipping factor), read
+//   from device memory so it can be produced by a previous kernel (global-norm clip).
+// ----------------------------------------------------------------------------------------
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ v,
+                           bf16* __restrict__ p16, long long n, const float* __restrict__ hyper, float lr, float mom,
+                           float damp, float wd, int nesterov, int first, const float* __restrict__ gscale_ptr,
+                           float gscale) {
+  // hyper (device, nullable): [lr] so a captured graph follows the LR schedule on replay
+  if (hyper) lr = hyper[0];
+  const float gs = gscale_ptr ? gscale * gscale_ptr[0] : gscale;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i * 4 < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long e = i * 4;
+    if (e + 4 <= n) {
+      f32x4 pp = *reinterpret_cast<f32x4*>(p + e);
+      f32x4 gg = *reinterpret_cast<const f32x4*>(g + e) * gs;
+      gg += wd * pp;
+      f32x4 d = gg;
+      if (mom != 0.f) {
+        f32x4 vv = first ? gg : (*reinterpret_cast<f32x4*>(v + e) * mom + (1.f - damp) * gg);
+        *reinterpret_cast<f32x4*>(v + e) = vv;
+        d = nesterov ? gg + mom * vv : vv;
+      }
+      pp -= lr * d;
+      *reinterpret_cast<f32x4*>(p + e) = pp;
+      if (p16) {
+        bf16x4 b = {(bf16)pp[0], (bf16)pp[1], (bf16)pp[2], (bf16)pp[3]};
+        *reinterpret_cast<bf16x4*>(p16 + e) = b;
+      }
+    } else {
+      for (long long k = e; k < n; ++k) {
+        float gg = g[k] * gs + wd * p[k];
+        float d = gg;
+        if (mom != 0.f) {
+          const float vv = first ? gg : v[k] * mom + (1.f - damp) * gg;
+          v[k] = vv;
+          d = nesterov ? gg + mom * vv : vv;
+        }
+        p[k] -= lr * d;
+        if (p16) p16[k] = (bf16)p[k];
+      }
+    }
+  }
+}
+
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, bf16* __restrict__ p16, long long n, const float* __restrict__ hyper,
+                            float lr, float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
+                            const float* __restrict__ gscale_ptr, float gscale) {
+  // hyper (device, nullable): [lr, 1-b1^t, 1-b2^t] so graph replays track the step count
+  if (hyper) { lr = hyper[0]; bc1 = hyper[1]; bc2 = hyper[2]; }
+  const float gs = gscale_ptr ? gscale * gscale_ptr[0] : gscale;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+    float gg = g[k] * gs;
+    float pp = p[k];
+    if (decoupled) pp -= lr * wd * pp;
+    else gg += wd * pp;
+    const float mm = b1 * m[k] + (1.f - b1) * gg;
+    const float vv = b2 * v[k] + (1.f - b2) * gg * gg;
+    m[k] = mm; v[k] = vv;
+    pp -= lr * (mm / bc1) / (sqrtf(vv / bc2) + eps);
+    p[k] = pp;
+    if (p16) p16[k] = (bf16)pp;
+  }
+}
+
+// sum of squares over a flat fp32 buffer (global-norm clipping), one atomic per block
+__global__ void sumsq_kernel(const float* __restrict__ x, long long n, float* out) {
+  float s = 0.f;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) s += x[k] * x[k];
+  s = wave_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+// clip factor = min(1, max_norm / (sqrt(sumsq) + 1e-6)) written to out[0]
+__global__ void clip_factor_kernel(const float* sumsq, float max_norm, float* out) {
+  const float nrm = sqrtf(sumsq[0]);
+  out[0] = fminf(1.f, max_norm / (nrm + 1e-6f));
+  out[1] = nrm;
+}
+
+// ----------------------------------------------------------------------------------------
+// Input: uint8 NHWC [N][H][W][3] -> bf16 NHWC4 normalised ((x/255 - mean)/std, ch3 = 0),
+// optional per-sample horizontal flip (flags[n] != 0).
+// ----------------------------------------------------------------------------------------
+__global__ void normalize_u8_kernel(const unsigned char* __restrict__ in, bf16* __restrict__ out,
+                                    const unsigned char* __restrict__ flip, int N, int H, int W, int Cin,
+                                    float m0, float m1, float m2, float s0, float s1, float s2) {
+  const long long total = (long long)N * H * W;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int w = (int)(i % W);
+    const long long nh = i / W;
+    const int n = (int)(nh / H);
+    const int ws = (flip && flip[n]) ? (W - 1 - w) : w;
+    const unsigned char* src = in + ((nh * W) + ws) * Cin;
+    float f0, f1, f2;
+    if (Cin == 1) { f0 = f1 = f2 = src[0] * (1.f / 255.f); }
+    else { f0 = src[0] * (1.f / 255.f); f1 = src[1] * (1.f / 255.f); f2 = src[2] * (1.f / 255.f); }
+    bf16x4 o = {(bf16)((f0 - m0) / s0), (bf16)((f1 - m1) / s1), (bf16)((f2 - m2) / s2), (bf16)0.f};
+    *reinterpret_cast<bf16x4*>(out + i * 4) = o;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Weight prep: fp32 KRSC master -> bf16 KRSC (fwd) and bf16 CRSK (dgrad) ; batched over layers
+// ----------------------------------------------------------------------------------------
+struct WDesc { long long src, fwd, tr; int K, RS, C, pad; };
+__global__ void weight_prep_kernel(const float* __restrict__ master, bf16* __restrict__ wbuf,
+                                   const WDesc* __restrict__ desc, int nlayers) {
+  const WDesc d = desc[blockIdx.y];
+  const long long n = (long long)d.K * d.RS * d.C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = master[d.src + i];
+    const bf16 b = (bf16)v;
+    if (d.fwd >= 0) wbuf[d.fwd + i] = b;
+    if (d.tr >= 0) {
+      // i = (k*RS + t)*C + c  ->  tr index (c*RS + t)*K + k
+      const int c = (int)(i % d.C);
+      const long long kt = i / d.C;
+      const int t = (int)(kt % d.RS);
+      const int k = (int)(kt / d.RS);
+      wbuf[d.tr + ((long long)c * d.RS + t) * d.K + k] = b;
+    }
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) y[i] = (bf16)x[i];
+}
+__global__ void cast_bf16_f32_kernel(const bf16* __restrict__ x, float* __restrict__ y, long long n, float scale, int accumulate) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = (accumulate ? y[i] : 0.f) + scale * (float)x[i];
+}
+
+}  // namespace dbx
+
+// ======================================================================================
+// C ABI launchers
+// ======================================================================================
+using namespace dbx;
+
+static inline int grid_for(long long n, int block = 256, int cap = 8192) {
+  long long g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+#define RET_LAST return (int)hipGetLastError()
+
+extern "C" int dbx_bn_finalize(const float* stats, int nshard, int C, float count, const float* gamma,
+                               const float* beta, float eps, float momentum, float* rm, float* rv,
+                               float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, stats, nshard, C, count, gamma,
+                     beta, eps, momentum, rm, rv, scale, shift, save_mean, save_invstd);
+  RET_LAST;
+}
+extern "C" int dbx_bn_eval_coeff(int C, const float* gamma, const float* beta, float eps, const float* rm,
+                                 const float* rv, float* scale, float* shift, hipStream_t st) {
+  hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, eps, rm, rv, scale, shift);
+  RET_LAST;
+}
+extern "C" int dbx_channel_stats(const bf16* y, long long M, int C, float* stats, int nshard, hipStream_t st) {
+  if (C % 8 || C / 8 > 256) return -1;
+  const int rpb = 256 / (C / 8);
+  hipLaunchKernelGGL(channel_stats_kernel, dim3(grid_for(M, rpb, 2048)), dim3(256), 0, st, y, M, C, stats, nshard);
+  RET_LAST;
+}
+extern "C" int dbx_bn_apply(const bf16* y, const float* sc, const float* sh, const bf16* res, const float* rsc,
+                            const float* rsh, bf16* out, long long n, int C, int res_mode, int relu, hipStream_t st) {
+  if (n % C || C % 8 || C / 8 > 256) return -1;
+  const long long M = n / C;
+  const dim3 g(grid_for(M, 256 / (C / 8), 4096)), b(256);
+#define BA(R, A) hipLaunchKernelGGL((bn_apply_kernel<R, A>), g, b, 0, st, y, sc, sh, res, rsc, rsh, out, M, C)
+  if (res_mode == 0) { if (relu) BA(0, true); else BA(0, false); }
+  else if (res_mode == 1) { if (relu) BA(1, true); else BA(1, false); }
+  else { if (relu) BA(2, true); else BA(2, false); }
+#undef BA
+  RET_LAST;
+}
+extern "C" int dbx_bn_bwd_reduce(const bf16* dout, const bf16* mref, const bf16* y, const float* sc, const float* sh,
+                                 const float* mean, const float* invstd, long long M, int C, float* stats,
+                                 int nshard, int mask_mode, hipStream_t st) {
+  if (C % 8 || C / 8 > 256) return -1;
+  const int rpb = 256 / (C / 8);
+  const dim3 g(grid_for(M, rpb, 2048)), b(256);
+  if (mask_mode == 0) hipLaunchKernelGGL((bn_bwd_reduce_kernel<0>), g, b, 0, st, dout, mref, y, sc, sh, mean, invstd, M, C, stats, nshard);
+  else if (mask_mode == 1) hipLaunchKernelGGL((bn_bwd_reduce_kernel<1>), g, b, 0, st, dout, mref, y, sc, sh, mean, invstd, M, C, stats, nshard);
+  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<2>), g, b, 0, st, dout, mref, y, sc, sh, mean, invstd, M, C, stats, nshard);
+  RET_LAST;
+}
+extern "C" int dbx_bn_bwd_coeff(const float* stats, int nshard, int C, float count, const float* gamma,
+                                const float* mean, const float* invstd, float* coeff, float* dgamma, float* dbeta,
+                                int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_coeff_kernel, dim3((C + 255) / 256), dim3(256), 0, st, stats, nshard, C, count, gamma,
+                     mean, invstd, coeff, dgamma, dbeta, accumulate);
+  RET_LAST;
+}
+extern "C" int dbx_bn_bwd_apply(const bf16* dout, const bf16* mref, const bf16* y, const float* sc, const float* sh,
+                                const float* coeff, bf16* dy, bf16* gout, long long n, int C, int mask_mode,
+                                hipStream_t st) {
+  if (n % C || C % 8 || C / 8 > 256) return -1;
+  const long long M = n / C;
+  const dim3 g(grid_for(M, 256 / (C / 8), 4096)), b(256);
+#define BB(MK, WG) hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, WG>), g, b, 0, st, dout, mref, y, sc, sh, coeff, dy, gout, M, C)
+  if (mask_mode == 0) { if (gout) BB(0, true); else BB(0, false); }
+  else if (mask_mode == 1) { if (gout) BB(1, true); else BB(1, false); }
+  else { if (gout) BB(2, true); else BB(2, false); }
+#undef BB
+  RET_LAST;
+}
+extern "C" int dbx_maxpool_fwd(const bf16* x, const float* sc, const float* sh, bf16* out, unsigned char* arg, int N,
+                               int H, int W, int C, int P, int Q, int K, int stride, int pad, int relu, hipStream_t st) {
+  if (C % 8) return -1;
+  const long long total = (long long)N * P * Q * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, x, sc, sh, out, arg, N, H, W, C, P, Q,
+                     K, stride, pad, relu);
+  RET_LAST;
+}
+extern "C" int dbx_maxpool_bwd(const bf16* dout, const unsigned char* arg, bf16* dx, int N, int H, int W, int C, int P,
+                               int Q, int K, int stride, int pad, hipStream_t st) {
+  if (C % 8) return -1;
+  const long long total = (long long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, dout, arg, dx, N, H, W, C, P, Q, K,
+                     stride, pad);
+  RET_LAST;
+}
+extern "C" int dbx_avgpool_fwd(const bf16* x, bf16* out, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((C / 8 + 63) / 64, N), dim3(64), 0, st, x, out, N, HW, C);
+  RET_LAST;
+}
+extern "C" int dbx_avgpool_bwd(const bf16* dout, bf16* dx, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long long)N * HW * C / 8)), dim3(256), 0, st, dout, dx, N, HW, C);
+  RET_LAST;
+}
+extern "C" int dbx_softmax_ce(const void* logits, int is_bf16, const long long* labels, void* dlogits, float* loss_out,
+                              float* stats, int B, int C, float smoothing, float gscale, hipStream_t st) {
+  if (is_bf16)
+    hipLaunchKernelGGL(softmax_ce_kernel<bf16>, dim3(B), dim3(256), 0, st, (const bf16*)logits, labels, (bf16*)dlogits,
+                       loss_out, stats, B, C, smoothing, gscale);
+  else
+    hipLaunchKernelGGL(softmax_ce_kernel<float>, dim3(B), dim3(256), 0, st, (const float*)logits, labels,
+                       (float*)dlogits, loss_out, stats, B, C, smoothing, gscale);
+  RET_LAST;
+}
+extern "C" int dbx_sgd(float* p, const float* g, float* v, bf16* p16, long long n, const float* hyper, float lr,
+                       float mom, float damp, float wd, int nesterov, int first, const float* gscale_ptr, float gscale,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p, g, v, p16, n, hyper, lr, mom, damp,
+                     wd, nesterov, first, gscale_ptr, gscale);
+  RET_LAST;
+}
+extern "C" int dbx_adam(float* p, const float* g, float* m, float* v, bf16* p16, long long n, const float* hyper,
+                        float lr, float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
+                        const float* gscale_ptr, float gscale, hipStream_t st) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, p16, n, hyper, lr, b1, b2, eps, wd,
+                     decoupled, bc1, bc2, gscale_ptr, gscale);
+  RET_LAST;
+}
+extern "C" int dbx_sumsq(const float* x, long long n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, x, n, out);
+  RET_LAST;
+}
+extern "C" int dbx_clip_factor(const float* sumsq, float max_norm, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(clip_factor_kernel, dim3(1), dim3(1), 0, st, sumsq, max_norm, out);
+  RET_LAST;
+}
+extern "C" int dbx_normalize_u8(const unsigned char* in, bf16* out, const unsigned char* flip, int N, int H, int W,
+                                int Cin, float m0, float m1, float m2, float s0, float s1, float s2, hipStream_t st) {
+  hipLaunchKernelGGL(normalize_u8_kernel, dim3(grid_for((long long)N * H * W)), dim3(256), 0, st, in, out, flip, N, H, W,
+                     Cin, m0, m1, m2, s0, s1, s2);
+  RET_LAST;
+}
+extern "C" int dbx_weight_prep(const float* master, bf16* wbuf, const void* desc_dev, int nlayers, hipStream_t st) {
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(64, nlayers), dim3(256), 0, st, master, wbuf, (const WDesc*)desc_dev, nlayers);
+  RET_LAST;
+}
+extern "C" int dbx_cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, y, n);
+  RET_LAST;
+}
+extern "C" int dbx_cast_bf16_f32(const bf16* x, float* y, long long n, float scale, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, y, n, scale, accumulate);
+  RET_LAST;
+}

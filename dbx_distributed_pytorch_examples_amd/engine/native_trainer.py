@@ -1,0 +1,257 @@
+"""Native training step: ResNetProgram + fused optimizer + flat-bucket DDP, replayed as HIP graphs.
+
+One ``NativeTrainer.step()`` = input normalisation (uint8 -> bf16 NHWC4), forward, softmax-CE,
+backward, gradient all-reduce (world > 1) and the optimizer update (SGD-momentum / Adam /
+AdamW over the flat fp32 master, then the bf16 weight copies are re-derived next step).
+
+Graphs. With world_size == 1 the whole step is ONE captured graph. With world_size > 1 the
+step is captured as segments cut where gradient buckets become final (head+layer4 | layer3 |
+layer2 | layer1+stem | optimizer); between segment replays the trainer issues the bucket's
+RCCL all-reduce on a dedicated comm stream, so the all-reduce of layer4's 15M-parameter bucket
+runs under layer3..1's backward (the reference's DDP overlap, SURVEY.md §2.5 M3, without
+capturing collectives inside a graph). The optimizer segment waits on the comm stream.
+
+Bucket sizing for xGMI: each segment range is split into chunks of ``bucket_cap_mb`` (default
+64 MiB: 8 GPUs x 7 point-to-point links want few, large messages; the 25 MiB NVSwitch-era
+default of torch DDP only adds launch latency here).
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops import kernels as K
+from .program import ResNetProgram
+
+
+@dataclass
+class OptimConfig:
+    name: str = "sgd"            # sgd | adam | adamw
+    lr: float = 0.1
+    momentum: float = 0.9
+    dampening: float = 0.0
+    nesterov: bool = False
+    weight_decay: float = 5e-5
+    betas: Tuple[float, float] = (0.9, 0.999)
+    eps: float = 1e-8
+    grad_clip: float = 0.0       # global-norm clip (DeepSpeed "gradient_clipping")
+
+
+class NativeTrainer:
+    def __init__(self, model: nn.Module, batch: int, image_hw: Tuple[int, int], device: torch.device,
+                 optim: OptimConfig = OptimConfig(), label_smoothing: float = 0.0, use_graphs: bool = True,
+                 bucket_cap_mb: float = 64.0, allreduce_dtype: torch.dtype = torch.float32,
+                 process_group=None):
+        self.dev = device
+        self.prog = ResNetProgram(model, batch, image_hw, device)
+        self.prog.build_backward()
+        self.opt = optim
+        self.smoothing = label_smoothing
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        n = self.prog.n_params
+        self.mom = torch.zeros(n, device=device)
+        self.mom2 = torch.zeros(n, device=device) if optim.name in ("adam", "adamw") else None
+        self.hyper = torch.zeros(4, device=device)      # lr, bc1, bc2 (device-side, graph-safe)
+        self.clip_work = torch.zeros(4, device=device)
+        self.step_count = 0
+        self.use_graphs = use_graphs and device.type == "cuda"
+        self.graphs: List[Optional[torch.cuda.CUDAGraph]] = []
+        self.bucket_cap = int(bucket_cap_mb * (1 << 20) // 4)
+        self.ar_dtype = allreduce_dtype
+        self.comm_stream = (torch.cuda.Stream(device=device, priority=-1)
+                            if self.world > 1 and device.type == "cuda" else None)
+        self.flip = None
+        self._build_phases()
+        # broadcast initial parameters from rank 0 (DDP constructor semantics, M2)
+        if self.world > 1:
+            dist.broadcast(self.prog.master, 0, group=process_group)
+            for bn in self.prog.bns:
+                dist.broadcast(bn.mod.running_mean, 0, group=process_group)
+                dist.broadcast(bn.mod.running_var, 0, group=process_group)
+        self._ar_bufs = {}
+
+    # ----------------------------------------------------------------------------------
+    def _build_phases(self):
+        p = self.prog
+        segs = p._segments
+        ranges = p.segment_param_ranges()
+        # contiguous [lo, hi) of every backward segment's gradients
+        self.seg_ranges = []
+        for rs in ranges:
+            if not rs:
+                self.seg_ranges.append(None)
+                continue
+            lo = min(r[1] for r in rs)
+            hi = max(r[1] + (r[2] + 15) // 16 * 16 for r in rs)
+            self.seg_ranges.append((lo, hi))
+
+        def fwd_phase():
+            p.prepare_weights()
+            p.load_input_u8(self.flip)
+            for bn in p.bns:
+                bn.mod.num_batches_tracked.add_(1)
+            p.forward(smoothing=self.smoothing)
+
+        phases: List[Tuple[str, Callable, Optional[Tuple[int, int]]]] = []
+        # phase 0 = forward + first backward segment
+        first_name, first_fn = segs[0]
+        phases.append(("fwd+" + first_name, lambda: (fwd_phase(), first_fn()), self.seg_ranges[0]))
+        for (name, fn), rg in zip(segs[1:], self.seg_ranges[1:]):
+            phases.append((name, fn, rg))
+        phases.append(("optimizer", self._optimizer_phase, None))
+        self.phases = phases
+
+    def _optimizer_phase(self):
+        p, o = self.prog, self.opt
+        gsp = None
+        if o.grad_clip and o.grad_clip > 0:
+            # clip on the averaged gradient: factor computed on device (no host sync)
+            K.global_norm_clip_factor(p.grad, o.grad_clip * self.world, self.clip_work)
+            gsp = self.clip_work[2:3]
+        gscale = 1.0 / self.world
+        if o.name == "sgd":
+            K.sgd_step(p.master, p.grad, self.mom, None, lr=o.lr, momentum=o.momentum, dampening=o.dampening,
+                       weight_decay=o.weight_decay, nesterov=o.nesterov, first=False, grad_scale_ptr=gsp,
+                       grad_scale=gscale, hyper=self.hyper)
+        else:
+            K.adam_step(p.master, p.grad, self.mom, self.mom2, None, lr=o.lr, beta1=o.betas[0], beta2=o.betas[1],
+                        eps=o.eps, weight_decay=o.weight_decay, decoupled=(o.name == "adamw"), step=1,
+                        grad_scale_ptr=gsp, grad_scale=gscale, hyper=self.hyper)
+
+    # ----------------------------------------------------------------------------------
+    def _allreduce_range(self, lo: int, hi: int):
+        g = self.prog.grad
+        pos = lo
+        while pos < hi:
+            end = min(hi, pos + self.bucket_cap)
+            chunk = g[pos:end]
+            if self.ar_dtype == torch.float32:
+                dist.all_reduce(chunk, group=self.pg)
+            else:
+                buf = chunk.to(self.ar_dtype)
+                dist.all_reduce(buf, group=self.pg)
+                chunk.copy_(buf)
+            pos = end
+
+    def _set_hyper(self):
+        o = self.opt
+        self.step_count += 1
+        t = self.step_count
+        if o.name == "sgd":
+            vals = [o.lr, 1.0, 1.0, 0.0]
+        else:
+            vals = [o.lr, 1.0 - o.betas[0] ** t, 1.0 - o.betas[1] ** t, 0.0]
+        self._hyper_host = torch.tensor(vals, dtype=torch.float32).pin_memory() if self.dev.type == "cuda" else torch.tensor(vals)
+        self.hyper.copy_(self._hyper_host, non_blocking=True)
+
+    def set_lr(self, lr: float):
+        self.opt.lr = float(lr)
+
+    def _run_phases_eager(self):
+        if self.dev.type != "cuda":  # CPU (reference ops; gloo all-reduce, synchronous)
+            for name, fn, rg in self.phases:
+                fn()
+                if rg is not None and self.world > 1:
+                    self._allreduce_range(*rg)
+            return
+        cur = torch.cuda.current_stream(self.dev)
+        for name, fn, rg in self.phases:
+            if name == "optimizer" and self.world > 1:
+                cur.wait_stream(self.comm_stream)
+            fn()
+            if rg is not None and self.world > 1:
+                self.comm_stream.wait_stream(cur)
+                with torch.cuda.stream(self.comm_stream):
+                    self._allreduce_range(*rg)
+
+    def _capture(self):
+        """Capture each phase (or the whole step when world == 1) into HIP graphs."""
+        torch.cuda.synchronize(self.dev)
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        pool = torch.cuda.graph_pool_handle()
+        self.graphs = []
+        with torch.cuda.stream(s):
+            if self.world == 1:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool, stream=s):
+                    for _, fn, _ in self.phases:
+                        fn()
+                self.graphs = [g]
+            else:
+                for _, fn, _ in self.phases:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool, stream=s):
+                        fn()
+                    self.graphs.append(g)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize(self.dev)
+
+    def _replay(self):
+        cur = torch.cuda.current_stream(self.dev)
+        if self.world == 1:
+            self.graphs[0].replay()
+            return
+        for (name, _, rg), g in zip(self.phases, self.graphs):
+            if name == "optimizer":
+                cur.wait_stream(self.comm_stream)
+            g.replay()
+            if rg is not None:
+                self.comm_stream.wait_stream(cur)
+                with torch.cuda.stream(self.comm_stream):
+                    self._allreduce_range(*rg)
+
+    # ----------------------------------------------------------------------------------
+    def step(self, images_u8: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
+             flip: Optional[torch.Tensor] = None):
+        """One training step. ``images_u8`` [N,H,W,C] uint8 and ``labels`` [N] int64 are copied
+        into the program's static input buffers (pass None to reuse what is already there)."""
+        p = self.prog
+        p.training = True
+        if images_u8 is not None:
+            p.img_u8.copy_(images_u8, non_blocking=True)
+        if labels is not None:
+            p.labels.copy_(labels, non_blocking=True)
+        self._set_hyper()
+        if not self.use_graphs:
+            self._run_phases_eager()
+            return
+        if not self.graphs:
+            # two eager warm-up steps (allocator / library handles), then capture. The warm-up
+            # steps are real steps: they update weights like any other.
+            if not hasattr(self, "_warm"):
+                self._warm = 0
+            if self._warm < 2:
+                self._warm += 1
+                self._run_phases_eager()
+                return
+            # stream capture records without executing: no state to snapshot
+            self._capture()
+        self._replay()
+
+    # ----------------------------------------------------------------------------------
+    @torch.no_grad()
+    def evaluate_batch(self, images_u8: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """Eval-mode forward (running BN stats); returns logits (bf16) and accumulates metrics."""
+        p = self.prog
+        p.training = False
+        p.img_u8.copy_(images_u8)
+        p.labels.copy_(labels)
+        p.prepare_weights()
+        p.load_input_u8(None)
+        out = p.forward(smoothing=0.0, compute_grad=False)
+        p.training = True
+        return out
+
+    def read_metrics(self, reset: bool = True) -> Tuple[float, float]:
+        m = self.prog.metrics[:2].tolist()
+        if reset:
+            self.prog.metrics.zero_()
+        return m[0], m[1]

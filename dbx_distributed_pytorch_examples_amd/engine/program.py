@@ -1,0 +1,516 @@
+"""ResNet programs: a static NHWC-bf16 forward/backward schedule over the HIP kernels.
+
+The reference trains torchvision ResNets through autograd + cuDNN (SURVEY.md §3.3 hot loop).
+On MI355X we instead *compile* the module tree once into a fixed op list over a preallocated
+activation arena, because that is what lets the hot path be fused and graph-captured:
+
+* the BN of every conv is split into (stats in the conv epilogue) + (apply in the consumer's
+  prologue), so no BN/ReLU output is ever materialised inside a block; the block tail
+  (BN + residual [+ BN of the downsample branch] + ReLU) is one pass;
+* backward is written out explicitly: BN-backward reductions with recomputed ReLU masks,
+  dgrad with the residual gradient accumulated in its epilogue, split-K wgrad whose reduce
+  writes fp32 straight into the flat gradient buffer (= the DDP buckets);
+* every tensor has a fixed address, so the whole step (weight cast -> fwd -> loss -> bwd ->
+  optimizer) replays as a HIP graph (``engine.step``), segmented at the points where gradient
+  buckets become ready so RCCL all-reduces overlap the remaining backward.
+
+Parameters live in ONE flat fp32 master buffer (conv weights in KRSC order); the module's
+``nn.Parameter`` s are re-pointed at views of it (conv weights as channels_last views), so
+``model.state_dict()`` / ``load_state_dict`` / checkpoint files keep torchvision layouts.
+
+Supported module trees: ``models.ResNet`` (BasicBlock / Bottleneck, any in_channels <= 4) and
+``models.CifarResNet18``; everything else trains through the autograd path (engine.autograd_step).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..models.resnet import BasicBlock, Bottleneck, CifarBlock, CifarResNet18, ResNet
+from ..ops import kernels as K
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def supports(model: nn.Module) -> bool:
+    if not isinstance(model, (ResNet, CifarResNet18)):
+        return False
+    if model.conv1.in_channels > 4:
+        return False
+    return True
+
+
+# ======================================================================================
+# specs
+# ======================================================================================
+@dataclass
+class ConvL:
+    name: str
+    mod: nn.Conv2d
+    IC: int
+    OC: int
+    R: int
+    S: int
+    stride: int
+    pad: int
+    IH: int
+    IW: int
+    OH: int
+    OW: int
+    stem: bool = False
+    off: int = 0          # master offset (KRSC fp32)
+    w16: Optional[torch.Tensor] = None   # [OC, KTOT] bf16 forward weights
+    wt16: Optional[torch.Tensor] = None  # [IC, R*S*OC] bf16 dgrad weights
+    grad: Optional[torch.Tensor] = None  # fp32 [OC, R*S*IC] view into the flat grad buffer
+
+    @property
+    def numel(self) -> int:
+        return self.OC * self.IC * self.R * self.S
+
+
+@dataclass
+class BNL:
+    name: str
+    mod: nn.BatchNorm2d
+    C: int
+    off_w: int = 0
+    off_b: int = 0
+    # per-step device state (views into one fp32 arena)
+    scale: Optional[torch.Tensor] = None
+    shift: Optional[torch.Tensor] = None
+    mean: Optional[torch.Tensor] = None
+    invstd: Optional[torch.Tensor] = None
+    coeff: Optional[torch.Tensor] = None
+    stats: Optional[torch.Tensor] = None
+    bstats: Optional[torch.Tensor] = None
+    gamma: Optional[torch.Tensor] = None
+    beta: Optional[torch.Tensor] = None
+    dgamma: Optional[torch.Tensor] = None
+    dbeta: Optional[torch.Tensor] = None
+
+
+@dataclass
+class BlockL:
+    kind: str                      # "bottleneck" | "basic"
+    convs: List[ConvL]
+    bns: List[BNL]
+    ds_conv: Optional[ConvL]
+    ds_bn: Optional[BNL]
+    in_shape: Tuple[int, int, int]   # H, W, C of the block input
+    out_shape: Tuple[int, int, int]
+    # activations
+    ys: List[torch.Tensor] = field(default_factory=list)   # raw conv outputs
+    yd: Optional[torch.Tensor] = None
+    out: Optional[torch.Tensor] = None
+    # gradients
+    dys: List[torch.Tensor] = field(default_factory=list)  # BN-input grads (per conv)
+    das: List[torch.Tensor] = field(default_factory=list)  # grads wrt intermediate activations
+    dyd: Optional[torch.Tensor] = None
+    dx: Optional[torch.Tensor] = None                       # grad wrt block input
+
+
+class ResNetProgram:
+    """Compile a ResNet nn.Module into a fixed-shape NHWC program for (batch, H, W)."""
+
+    def __init__(self, model: nn.Module, batch: int, image_hw: Tuple[int, int], device: torch.device,
+                 bn_momentum: Optional[float] = None):
+        if not supports(model):
+            raise TypeError(f"ResNetProgram does not support {type(model).__name__}")
+        self.model = model
+        self.N = batch
+        self.H, self.W = image_hw
+        self.dev = device
+        self.in_ch = model.conv1.in_channels
+        self._build_layers()
+        self._alloc_params()
+        self._alloc_activations()
+        self.training = True
+
+    # ----------------------------------------------------------------------------------
+    # construction
+    # ----------------------------------------------------------------------------------
+    def _conv(self, name, mod: nn.Conv2d, ih, iw, stem=False) -> ConvL:
+        R, S = mod.kernel_size
+        st, pad = mod.stride[0], mod.padding[0]
+        if mod.bias is not None or mod.groups != 1 or mod.dilation != (1, 1) or mod.stride[0] != mod.stride[1]:
+            raise TypeError(f"{name}: unsupported conv configuration")
+        oh, ow = K.conv_out_hw(ih, iw, R, S, st, pad)
+        return ConvL(name, mod, mod.in_channels, mod.out_channels, R, S, st, pad, ih, iw, oh, ow, stem)
+
+    def _build_layers(self):
+        m = self.model
+        self.stem = self._conv("conv1", m.conv1, self.H, self.W, stem=True)
+        self.stem_bn = BNL("bn1", m.bn1, m.bn1.num_features)
+        mp = m.maxpool
+        self.pool_k, self.pool_s, self.pool_p = mp.kernel_size, mp.stride, mp.padding
+        ph = (self.stem.OH + 2 * self.pool_p - self.pool_k) // self.pool_s + 1
+        pw = (self.stem.OW + 2 * self.pool_p - self.pool_k) // self.pool_s + 1
+        self.pool_hw = (ph, pw)
+        h, w, c = ph, pw, self.stem.OC
+        self.blocks: List[BlockL] = []
+        for li in range(1, 5):
+            layer = getattr(m, f"layer{li}")
+            for bi, blk in enumerate(layer):
+                pre = f"layer{li}.{bi}"
+                if isinstance(blk, Bottleneck):
+                    c1 = self._conv(f"{pre}.conv1", blk.conv1, h, w)
+                    c2 = self._conv(f"{pre}.conv2", blk.conv2, c1.OH, c1.OW)
+                    c3 = self._conv(f"{pre}.conv3", blk.conv3, c2.OH, c2.OW)
+                    convs = [c1, c2, c3]
+                    bns = [BNL(f"{pre}.bn1", blk.bn1, blk.bn1.num_features),
+                           BNL(f"{pre}.bn2", blk.bn2, blk.bn2.num_features),
+                           BNL(f"{pre}.bn3", blk.bn3, blk.bn3.num_features)]
+                    kind = "bottleneck"
+                    ds = blk.downsample
+                elif isinstance(blk, (BasicBlock, CifarBlock)):
+                    c1 = self._conv(f"{pre}.conv1", blk.conv1, h, w)
+                    c2 = self._conv(f"{pre}.conv2", blk.conv2, c1.OH, c1.OW)
+                    convs = [c1, c2]
+                    bns = [BNL(f"{pre}.bn1", blk.bn1, blk.bn1.num_features),
+                           BNL(f"{pre}.bn2", blk.bn2, blk.bn2.num_features)]
+                    kind = "basic"
+                    ds = blk.downsample if isinstance(blk, BasicBlock) else (
+                        blk.skip_connection if len(blk.skip_connection) > 0 else None)
+                else:
+                    raise TypeError(f"unsupported block {type(blk).__name__}")
+                dsc = dsb = None
+                if ds is not None:
+                    dsc = self._conv(f"{pre}.downsample.0", ds[0], h, w)
+                    dsb = BNL(f"{pre}.downsample.1", ds[1], ds[1].num_features)
+                last = convs[-1]
+                blk_l = BlockL(kind, convs, bns, dsc, dsb, (h, w, c), (last.OH, last.OW, last.OC))
+                self.blocks.append(blk_l)
+                h, w, c = last.OH, last.OW, last.OC
+        self.feat_hw = (h, w)
+        self.feat_c = c
+        self.fc: nn.Linear = m.fc
+        self.num_classes = m.fc.out_features
+        self.convs: List[ConvL] = [self.stem] + [cv for b in self.blocks for cv in (b.convs + ([b.ds_conv] if b.ds_conv else []))]
+        self.bns: List[BNL] = [self.stem_bn] + [bn for b in self.blocks for bn in (b.bns + ([b.ds_bn] if b.ds_bn else []))]
+        for cv in self.convs[1:]:
+            if cv.IC % 64 or cv.OC % 64:
+                raise TypeError(f"{cv.name}: channels must be multiples of 64 for the HIP conv kernels")
+
+    def _alloc_params(self):
+        """Flat fp32 master / grad buffers; re-point module parameters at views of master."""
+        dev = self.dev
+        entries: List[Tuple[str, object, str, int]] = []  # (kind, obj, attr, numel)
+        # Flat order = backward-segment order reversed (stem, layer1..4, fc): every backward
+        # segment's gradients form ONE contiguous range -> one bucket, no gather/scatter.
+        groups = [("conv1.", "bn1.")] + [(f"layer{i}.",) for i in range(1, 5)]
+        for pre in groups:
+            for cv in self.convs:
+                if cv.name.startswith(pre) or (cv.stem and "conv1." in pre):
+                    entries.append(("conv", cv, "weight", cv.numel))
+            for bn in self.bns:
+                if bn.name.startswith(pre) or (bn is self.stem_bn and "bn1." in pre):
+                    entries.append(("bn_w", bn, "weight", bn.C))
+                    entries.append(("bn_b", bn, "bias", bn.C))
+        entries.append(("fc_w", self.fc, "weight", self.fc.weight.numel()))
+        entries.append(("fc_b", self.fc, "bias", self.fc.bias.numel()))
+        assert len(entries) == len(self.convs) + 2 * len(self.bns) + 2, "parameter grouping lost a tensor"
+        # 16-element alignment of every tensor (vectorised kernels, 64-B bucket edges)
+        total = 0
+        offs = []
+        for e in entries:
+            offs.append(total)
+            total += (e[3] + 15) // 16 * 16
+        self.n_params = total
+        self.master = torch.zeros(total, device=dev, dtype=torch.float32)
+        self.grad = torch.zeros(total, device=dev, dtype=torch.float32)
+        self.param_ranges: List[Tuple[str, int, int]] = []  # (param name, off, numel) for bucketing
+        with torch.no_grad():
+            for (kind, obj, attr, n), off in zip(entries, offs):
+                if kind == "conv":
+                    cv: ConvL = obj
+                    cv.off = off
+                    src = cv.mod.weight.detach().to(dev, torch.float32)  # [K, C, R, S]
+                    flat = self.master[off:off + n]
+                    flat.copy_(src.permute(0, 2, 3, 1).reshape(-1))
+                    view = flat.view(cv.OC, cv.R, cv.S, cv.IC).permute(0, 3, 1, 2)  # channels_last view
+                    cv.mod.weight = nn.Parameter(view, requires_grad=cv.mod.weight.requires_grad)
+                    cv.grad = self.grad[off:off + n].view(cv.OC, cv.R * cv.S * cv.IC)
+                    self.param_ranges.append((cv.name + ".weight", off, n))
+                elif kind in ("bn_w", "bn_b"):
+                    bn: BNL = obj
+                    mod = bn.mod
+                    p = getattr(mod, attr)
+                    flat = self.master[off:off + n]
+                    flat.copy_(p.detach().to(dev, torch.float32))
+                    setattr(mod, attr, nn.Parameter(flat, requires_grad=p.requires_grad))
+                    if kind == "bn_w":
+                        bn.off_w, bn.gamma, bn.dgamma = off, flat, self.grad[off:off + n]
+                    else:
+                        bn.off_b, bn.beta, bn.dbeta = off, flat, self.grad[off:off + n]
+                    self.param_ranges.append((f"{bn.name}.{attr}", off, n))
+                    # running stats stay module buffers (moved to device, updated in place)
+                    mod.running_mean.data = mod.running_mean.data.to(dev, torch.float32)
+                    mod.running_var.data = mod.running_var.data.to(dev, torch.float32)
+                    mod.num_batches_tracked.data = mod.num_batches_tracked.data.to(dev)
+                else:
+                    p = getattr(self.fc, attr)
+                    flat = self.master[off:off + n]
+                    flat.copy_(p.detach().reshape(-1).to(dev, torch.float32))
+                    view = flat.view(p.shape)
+                    setattr(self.fc, attr, nn.Parameter(view, requires_grad=p.requires_grad))
+                    if attr == "weight":
+                        self.fc_w_off, self.fc_w_grad = off, self.grad[off:off + n].view(p.shape)
+                    else:
+                        self.fc_b_off, self.fc_b_grad = off, self.grad[off:off + n]
+                    self.param_ranges.append((f"fc.{attr}", off, n))
+        # bf16 compute copies: KRSC fwd + CRSK dgrad per conv, fc weight
+        n16 = 0
+        descs = []
+        for cv in self.convs:
+            if cv.stem:
+                continue
+            fwd_off = n16
+            n16 += cv.numel
+            tr_off = n16
+            n16 += cv.numel
+            descs.append((cv.off, fwd_off, tr_off, cv.OC, cv.R * cv.S, cv.IC))
+            cv._w16_off, cv._wt16_off = fwd_off, tr_off
+        fc_off = n16
+        n16 += self.fc.weight.numel()
+        descs.append((self.fc_w_off, fc_off, -1, self.num_classes, 1, self.fc.in_features))
+        self.w16buf = torch.zeros(n16 + 16, device=dev, dtype=torch.bfloat16)
+        for cv in self.convs:
+            if cv.stem:
+                cv.w16 = torch.zeros(cv.OC, 256, device=dev, dtype=torch.bfloat16)
+                continue
+            cv.w16 = self.w16buf[cv._w16_off:cv._w16_off + cv.numel].view(cv.OC, -1)
+            cv.wt16 = self.w16buf[cv._wt16_off:cv._wt16_off + cv.numel].view(cv.IC, -1)
+        self.fc_w16 = self.w16buf[fc_off:fc_off + self.fc.weight.numel()].view(self.num_classes, -1)
+        # WDesc {long long src, fwd, tr; int K, RS, C, pad} = 40 bytes
+        raw = []
+        for (src, f, t, k, rs, c) in descs:
+            raw.append(torch.tensor([src, f, t], dtype=torch.int64).view(torch.int32))
+            raw.append(torch.tensor([k, rs, c, 0], dtype=torch.int32))
+        self.wdesc = torch.cat(raw).to(dev)
+        self.n_wdesc = len(descs)
+        self.fc_b16 = torch.zeros(self.num_classes, device=dev, dtype=torch.bfloat16)
+        self.stem_grad_tmp = torch.zeros(self.stem.OC, 256, device=dev, dtype=torch.float32)
+
+    def _alloc_activations(self):
+        N, dev, bf = self.N, self.dev, torch.bfloat16
+        E = lambda *s: torch.empty(*s, device=dev, dtype=bf)  # noqa: E731
+        st = self.stem
+        self.x4 = torch.zeros(N, self.H, self.W, 4, device=dev, dtype=bf)
+        self.y0 = E(N, st.OH, st.OW, st.OC)
+        ph, pw = self.pool_hw
+        self.p0 = E(N, ph, pw, st.OC)
+        self.parg = torch.empty(N, ph, pw, st.OC, device=dev, dtype=torch.uint8)
+        self.dp0 = E(N, ph, pw, st.OC)
+        self.da0 = E(N, st.OH, st.OW, st.OC)
+        self.dy0 = E(N, st.OH, st.OW, st.OC)
+        wsmax = 0
+        for b in self.blocks:
+            b.ys = [E(N, cv.OH, cv.OW, cv.OC) for cv in b.convs]
+            b.dys = [E(N, cv.OH, cv.OW, cv.OC) for cv in b.convs]
+            b.das = [E(N, cv.OH, cv.OW, cv.OC) for cv in b.convs[:-1]]
+            h, w, c = b.in_shape
+            b.dx = E(N, h, w, c)
+            if b.ds_conv is not None:
+                b.yd = E(N, b.ds_conv.OH, b.ds_conv.OW, b.ds_conv.OC)
+                b.dyd = E(N, b.ds_conv.OH, b.ds_conv.OW, b.ds_conv.OC)
+            oh, ow, oc = b.out_shape
+            b.out = E(N, oh, ow, oc)
+        for cv in self.convs:
+            ktot = 256 if cv.stem else cv.R * cv.S * cv.IC
+            wsmax = max(wsmax, cv.OC * ktot)
+        # split-K wgrad workspace: up to 64 splits of the largest layer, >= 64 MiB
+        self.ws = torch.empty(max(64 * wsmax, 16 << 20), device=dev, dtype=torch.float32)
+        fh, fw = self.feat_hw
+        self.dfeat = self.blocks[-1].out  # placeholder name; real grad buffer below
+        self.dlast = E(N, fh, fw, self.feat_c)
+        self.pooled = E(N, self.feat_c)
+        self.dpooled = E(N, self.feat_c)
+        self.logits = E(N, self.num_classes)
+        self.dlogits = E(N, self.num_classes)
+        self.labels = torch.zeros(N, device=dev, dtype=torch.int64)
+        self.img_u8 = torch.zeros(N, self.H, self.W, 3 if self.in_ch != 1 else 1, device=dev, dtype=torch.uint8)
+        self.metrics = torch.zeros(4, device=dev, dtype=torch.float32)  # loss sum, correct, -, -
+        # BN state arena
+        tot = 0
+        for bn in self.bns:
+            tot += 7 * bn.C + 2 * 2 * K.NSHARD * bn.C
+        self.bn_arena = torch.zeros(tot, device=dev, dtype=torch.float32)
+        o = 0
+        self.stats_lo = None
+        # stats slabs first (contiguous: zeroed by ONE memset per step)
+        for bn in self.bns:
+            bn.stats = self.bn_arena[o:o + 2 * K.NSHARD * bn.C]
+            o += 2 * K.NSHARD * bn.C
+            bn.bstats = self.bn_arena[o:o + 2 * K.NSHARD * bn.C]
+            o += 2 * K.NSHARD * bn.C
+        self.stats_region = self.bn_arena[:o]
+        for bn in self.bns:
+            bn.scale = self.bn_arena[o:o + bn.C]; o += bn.C
+            bn.shift = self.bn_arena[o:o + bn.C]; o += bn.C
+            bn.mean = self.bn_arena[o:o + bn.C]; o += bn.C
+            bn.invstd = self.bn_arena[o:o + bn.C]; o += bn.C
+            bn.coeff = self.bn_arena[o:o + 3 * bn.C]; o += 3 * bn.C
+        self.mean_t = torch.tensor(IMAGENET_MEAN)
+        self.std_t = torch.tensor(IMAGENET_STD)
+
+    # ----------------------------------------------------------------------------------
+    # per-step pieces
+    # ----------------------------------------------------------------------------------
+    def prepare_weights(self):
+        """fp32 master -> bf16 compute copies (KRSC fwd, CRSK dgrad, fc, stem 8x8x4)."""
+        K.weight_prep(self.master, self.w16buf, self.wdesc, self.n_wdesc)
+        st = self.stem
+        w = self.master[st.off:st.off + st.numel].view(st.OC, st.R, st.S, st.IC)
+        stem16 = st.w16.view(st.OC, 8, 8, 4)
+        stem16[:, :st.R, :st.S, :st.IC].copy_(w)
+        self.fc_b16.copy_(self.fc.bias.detach())
+
+    def load_input_u8(self, flip: Optional[torch.Tensor] = None):
+        mean = IMAGENET_MEAN if self.in_ch == 3 else (0.5, 0.5, 0.5)
+        std = IMAGENET_STD if self.in_ch == 3 else (0.5, 0.5, 0.5)
+        K.normalize_u8(self.img_u8, self.x4, mean, std, flip)
+
+    def _bn_fwd(self, bn: BNL, count: int):
+        mod = bn.mod
+        if self.training:
+            mom = mod.momentum if mod.momentum is not None else 0.1
+            K.bn_finalize(bn.stats, count, bn.gamma, bn.beta, mod.eps, mom if mod.track_running_stats else 0.0,
+                          mod.running_mean, mod.running_var, bn.scale, bn.shift, bn.mean, bn.invstd)
+        else:
+            K.bn_eval_coeff(bn.gamma, bn.beta, mod.eps, mod.running_mean, mod.running_var, bn.scale, bn.shift)
+
+    def forward(self, smoothing: float = 0.0, compute_grad: bool = True, grad_scale: float = 1.0):
+        """Full forward incl. loss. Assumes x4 / labels filled and prepare_weights() done."""
+        tr = self.training
+        if tr:
+            self.stats_region.zero_()
+        N = self.N
+        st, sbn = self.stem, self.stem_bn
+        K.conv_stem_fwd(self.x4, st.w16, self.y0, R=st.R, S=st.S, stride=st.stride, pad=st.pad,
+                        stats=sbn.stats if tr else None)
+        self._bn_fwd(sbn, N * st.OH * st.OW)
+        K.maxpool_fwd(self.y0, self.p0, self.parg, K=self.pool_k, stride=self.pool_s, pad=self.pool_p,
+                      scale=sbn.scale, shift=sbn.shift, relu=True)
+        x = self.p0
+        for b in self.blocks:
+            prev_bn = None
+            for i, cv in enumerate(b.convs):
+                src = x if i == 0 else b.ys[i - 1]
+                K.conv_fwd(src, cv.w16, b.ys[i], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                           stats=b.bns[i].stats if tr else None,
+                           in_scale=prev_bn.scale if prev_bn else None, in_shift=prev_bn.shift if prev_bn else None,
+                           relu_in=True)
+                self._bn_fwd(b.bns[i], N * cv.OH * cv.OW)
+                prev_bn = b.bns[i]
+            last = b.bns[-1]
+            if b.ds_conv is not None:
+                dc = b.ds_conv
+                K.conv_fwd(x, dc.w16, b.yd, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad,
+                           stats=b.ds_bn.stats if tr else None)
+                self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
+                K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=b.yd, res_scale=b.ds_bn.scale,
+                           res_shift=b.ds_bn.shift, relu=True)
+            else:
+                K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=x, relu=True)
+            x = b.out
+        K.avgpool_fwd(x, self.pooled)
+        torch.addmm(self.fc_b16, self.pooled, self.fc_w16.t(), out=self.logits)
+        K.softmax_ce(self.logits, self.labels, self.dlogits if compute_grad else None, None, self.metrics,
+                     smoothing=smoothing, grad_scale=grad_scale)
+        return self.logits
+
+    def backward_segments(self):
+        """Yield closures, one per backward segment; after segment k all params whose
+        names appear in ``segment_params[k]`` have final gradients (bucket-ready points)."""
+        return self._segments
+
+    def build_backward(self):
+        segs = []
+        # head + layer4 blocks, each stage its own segment (reverse order)
+        stages: Dict[int, List[int]] = {}
+        bi = 0
+        for li in range(1, 5):
+            n = len(getattr(self.model, f"layer{li}"))
+            stages[li] = list(range(bi, bi + n))
+            bi += n
+        segs.append(("head", self._bwd_head))
+        for li in (4, 3, 2, 1):
+            idx = list(reversed(stages[li]))
+            segs.append((f"layer{li}", (lambda idx=idx: [self._bwd_block(i) for i in idx])))
+        segs.append(("stem", self._bwd_stem))
+        self._segments = segs
+        return segs
+
+    def _bwd_head(self):
+        # fc: dW = dlogits^T @ pooled (fp32 accumulate), db = sum dlogits, dpooled = dlogits @ W
+        torch.mm(self.dlogits.t().float(), self.pooled.float(), out=self.fc_w_grad)
+        torch.sum(self.dlogits.float(), 0, out=self.fc_b_grad)
+        torch.mm(self.dlogits, self.fc_w16, out=self.dpooled)
+        K.avgpool_bwd(self.dpooled, self.dlast)
+
+    def _bn_bwd(self, bn: BNL, dout, y, dy, count, mask_mode, mref=None, gout=None):
+        K.bn_bwd_reduce(dout, y, bn.mean, bn.invstd, bn.bstats, mask_mode=mask_mode, mref=mref,
+                        scale=bn.scale, shift=bn.shift)
+        K.bn_bwd_coeff(bn.bstats, count, bn.gamma, bn.mean, bn.invstd, bn.coeff, bn.dgamma, bn.dbeta)
+        K.bn_bwd_apply(dout, y, bn.coeff, dy, mask_mode=mask_mode, mref=mref, scale=bn.scale, shift=bn.shift,
+                       gout=gout)
+
+    def _bwd_block(self, i: int):
+        b = self.blocks[i]
+        N = self.N
+        dout = self.dlast if i == len(self.blocks) - 1 else self.blocks[i + 1].dx
+        x = self.p0 if i == 0 else self.blocks[i - 1].out
+        nconv = len(b.convs)
+        lc = b.convs[-1]
+        cnt_last = N * lc.OH * lc.OW
+        # block tail: out = relu(bn_last(y_last) + shortcut)
+        self._bn_bwd(b.bns[-1], dout, b.ys[-1], b.dys[-1], cnt_last, K.MASK_OUT, mref=b.out,
+                     gout=(b.dx if b.ds_conv is None else None))
+        if b.ds_conv is not None:
+            dc = b.ds_conv
+            self._bn_bwd(b.ds_bn, dout, b.yd, b.dyd, N * dc.OH * dc.OW, K.MASK_OUT, mref=b.out)
+        # convs from last to first
+        for j in range(nconv - 1, -1, -1):
+            cv = b.convs[j]
+            src = x if j == 0 else b.ys[j - 1]
+            pbn = None if j == 0 else b.bns[j - 1]
+            K.conv_wgrad(b.dys[j], src, cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                         in_scale=pbn.scale if pbn else None, in_shift=pbn.shift if pbn else None, relu_in=True)
+            if j > 0:
+                K.conv_dgrad(b.dys[j], cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad)
+                pc = b.convs[j - 1]
+                self._bn_bwd(pbn, b.das[j - 1], b.ys[j - 1], b.dys[j - 1], N * pc.OH * pc.OW, K.MASK_Y)
+            else:
+                if b.ds_conv is not None:
+                    dc = b.ds_conv
+                    K.conv_wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
+                    K.conv_dgrad(b.dyd, dc.wt16, b.dx, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
+                K.conv_dgrad(b.dys[0], cv.wt16, b.dx, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad, accumulate=True)
+
+    def _bwd_stem(self):
+        st, sbn = self.stem, self.stem_bn
+        K.maxpool_bwd(self.blocks[0].dx, self.parg, self.da0, K=self.pool_k, stride=self.pool_s, pad=self.pool_p)
+        self._bn_bwd(sbn, self.da0, self.y0, self.dy0, self.N * st.OH * st.OW, K.MASK_Y)
+        K.conv_wgrad(self.dy0, self.x4, self.stem_grad_tmp, self.ws, R=st.R, S=st.S, stride=st.stride,
+                     pad=st.pad, stem=True)
+        g = self.grad[st.off:st.off + st.numel].view(st.OC, st.R, st.S, st.IC)
+        g.copy_(self.stem_grad_tmp.view(st.OC, 8, 8, 4)[:, :st.R, :st.S, :st.IC])
+
+    def backward(self):
+        for _, fn in self._segments:
+            fn()
+
+    # parameter-name groups per backward segment (for bucket assembly)
+    def segment_param_ranges(self) -> List[List[Tuple[str, int, int]]]:
+        groups = []
+        by_prefix = {"head": ["fc."], "layer4": ["layer4."], "layer3": ["layer3."], "layer2": ["layer2."],
+                     "layer1": ["layer1."], "stem": ["conv1.", "bn1."]}
+        for name, _ in self._segments:
+            pre = by_prefix[name]
+            groups.append([r for r in self.param_ranges if any(r[0].startswith(p) for p in pre)])
+        return groups

@@ -1,0 +1,396 @@
+"""Python front-ends of the HIP kernels (``csrc/*.hip``).
+
+Every wrapper validates dtype / contiguity / shape on the host before launching (a mismatch
+would otherwise be an out-of-bounds GPU access), launches on the current torch stream (so the
+calls are captured by ``torch.cuda.graph``), and never synchronises. Layout conventions:
+
+* activations: NHWC bf16, contiguous, ``[N, H, W, C]`` (C % 8 == 0; conv inputs C % 64 == 0,
+  except the stem which takes the NHWC4 image);
+* conv weights: KRSC bf16 ``[OC, R*S*IC]`` for forward, CRSK ``[IC, R*S*OC]`` for dgrad,
+  the stem as ``[64, 8*8*4]`` (7x7x3 zero-padded to 8x8x4);
+* BN statistics: fp32 ``[nshard, 2, C]`` slabs accumulated by conv epilogues.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import reference as _ref
+from ._ext import C, stream_ptr, use_native
+
+FWD, DGRAD, STEM = 0, 1, 2
+
+
+def _dispatch(fn):
+    """Run the HIP kernel for GPU tensors, the PyTorch reference (ops/reference.py) otherwise."""
+    ref = getattr(_ref, fn.__name__)
+
+    def wrapper(*args, **kw):
+        t = args[0]
+        if isinstance(t, torch.Tensor) and not use_native(t):
+            return ref(*args, **kw)
+        return fn(*args, **kw)
+
+    wrapper.__name__ = fn.__name__
+    wrapper.__doc__ = fn.__doc__
+    wrapper.__wrapped__ = fn
+    return wrapper
+NSHARD = 32  # BN-statistics shards (spreads the epilogue atomics over 32 copies)
+
+
+def _p(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(t: torch.Tensor, dtype, name: str, numel: Optional[int] = None):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a GPU tensor")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name}: expected {numel} elements, got {t.numel()} (shape {tuple(t.shape)})")
+
+
+def conv_out_hw(h: int, w: int, r: int, s: int, stride: int, pad: int) -> Tuple[int, int]:
+    return (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
+
+
+def pick_tile(M: int, OC: int) -> Tuple[int, int]:
+    """Tile heuristic: biggest tile that still puts >= ~2 workgroups on each of the 256 CUs."""
+    if OC % 128 == 0 and ((M + 127) // 128) * (OC // 128) >= 512:
+        return 128, 128
+    if ((M + 127) // 128) * (OC // 64) >= 384:
+        return 128, 64
+    return 64, 64
+
+
+# --------------------------------------------------------------------------------------
+# convolutions
+# --------------------------------------------------------------------------------------
+@_dispatch
+def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None,
+             relu_in=True, tile=None):
+    N, IH, IW, IC = x.shape
+    OH, OW = conv_out_hw(IH, IW, R, S, stride, pad)
+    OC = w16.shape[0]
+    _chk(x, torch.bfloat16, "x")
+    _chk(w16, torch.bfloat16, "w16", OC * R * S * IC)
+    _chk(out, torch.bfloat16, "out", N * OH * OW * OC)
+    if IC % 64 or OC % 64:
+        raise ValueError(f"conv_fwd needs IC,OC % 64 == 0 (got {IC},{OC})")
+    if stats is not None:
+        _chk(stats, torch.float32, "stats", NSHARD * 2 * OC)
+    if in_scale is not None:
+        _chk(in_scale, torch.float32, "in_scale", IC)
+        _chk(in_shift, torch.float32, "in_shift", IC)
+    bm, bn = tile or pick_tile(N * OH * OW, OC)
+    C().conv_igemm(FWD, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
+                   int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
+                   R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, stream_ptr())
+    return out
+
+
+def dgrad_phases(H: int, W: int, R: int, S: int, stride: int, pad: int):
+    """Parity decomposition of a strided dgrad into stride-1 sub-problems.
+
+    Output pixel h receives tap r only where (h + pad - r) % stride == 0, so for each output
+    phase (ph, pw) only taps r = r0 + stride*t contribute and the gather is dense:
+    ih = i + (ph + pad - r0) // stride - t over the phase's sub-grid i (h = i*stride + ph).
+    Returns [(ph, pw, OHs, OWs, r0, nr, s0, ns, dh0, dw0)] (classes with no taps included, nr=0).
+    """
+    out = []
+    for ph in range(stride):
+        for pw in range(stride):
+            ohs = (H - ph + stride - 1) // stride
+            ows = (W - pw + stride - 1) // stride
+            r0 = (ph + pad) % stride
+            s0 = (pw + pad) % stride
+            nr = max(0, (R - r0 + stride - 1) // stride)
+            ns = max(0, (S - s0 + stride - 1) // stride)
+            out.append((ph, pw, ohs, ows, r0, nr, s0, ns, (ph + pad - r0) // stride, (pw + pad - s0) // stride))
+    return out
+
+
+@_dispatch
+def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None):
+    """dX = conv_transpose(dY, W): dy [N,P,Q,K], wt16 [C, R*S*K] (CRSK), dx [N,H,W,C].
+
+    Stride > 1 runs one dense launch per output phase (``dgrad_phases``): no MFMA work on the
+    (stride^2 - 1)/stride^2 taps that a masked gather would multiply by zero.
+    """
+    N, P, Q, K = dy.shape
+    _, H, W, Cc = dx.shape
+    _chk(dy, torch.bfloat16, "dy")
+    _chk(wt16, torch.bfloat16, "wt16", Cc * R * S * K)
+    _chk(dx, torch.bfloat16, "dx")
+    if (H + 2 * pad - R) // stride + 1 != P or (W + 2 * pad - S) // stride + 1 != Q:
+        raise ValueError("conv_dgrad: dy / dx shapes inconsistent with the conv geometry")
+    if K % 64 or Cc % 64:
+        raise ValueError("conv_dgrad needs channels % 64 == 0")
+    phases = dgrad_phases(H, W, R, S, stride, pad)
+    if not accumulate and any(ph[5] == 0 or ph[7] == 0 for ph in phases):
+        dx.zero_()  # phases without taps receive no contribution
+        accumulate = True
+    for (ph, pw, ohs, ows, r0, nr, s0, ns, dh0, dw0) in phases:
+        if nr == 0 or ns == 0 or ohs == 0 or ows == 0:
+            continue
+        bm, bn = tile or pick_tile(N * ohs * ows, Cc)
+        C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
+                       N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
+                       nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W, stream_ptr())
+    return dx
+
+
+@_dispatch
+def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
+    """Stem conv on the NHWC4 image: w16s [OC, 256] = (8 rows x 8 pixels x 4 channels)."""
+    N, IH, IW, C4 = x4.shape
+    if C4 != 4:
+        raise ValueError("stem expects NHWC4 input")
+    OH, OW = conv_out_hw(IH, IW, R, S, stride, pad)
+    OC = w16s.shape[0]
+    _chk(x4, torch.bfloat16, "x4")
+    _chk(w16s, torch.bfloat16, "w16s", OC * 256)
+    _chk(out, torch.bfloat16, "out", N * OH * OW * OC)
+    if stats is not None:
+        _chk(stats, torch.float32, "stats", NSHARD * 2 * OC)
+    if R > 8 or S > 8:
+        raise ValueError("stem kernel supports R,S <= 8")
+    C().conv_igemm(STEM, 128, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
+                   N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
+                   stream_ptr())
+    return out
+
+
+def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int) -> Tuple[int, int]:
+    """Split the pixel reduction so that ~1024 workgroups stream (>= 8 K-blocks each); the
+    workspace holds nsplit slabs + up to 64 level-1 partial slabs of the reduction."""
+    tiles = (OC // bm) * (KTOT // bn)
+    target = max(1, 1024 // tiles)
+    ms = max(512, ((M + target - 1) // target + 63) // 64 * 64)
+    nsplit = (M + ms - 1) // ms
+    while (nsplit + min(64, nsplit)) * OC * KTOT > max_ws_elems and nsplit > 1:
+        ms *= 2
+        nsplit = (M + ms - 1) // ms
+    return nsplit, ms
+
+
+@_dispatch
+def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True,
+               scale=1.0, accumulate=False, stem=False, tile=None):
+    """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace."""
+    N, OH, OW, OC = dy.shape
+    _, IH, IW, IC = x.shape
+    KTOT = 256 if stem else R * S * IC
+    _chk(dy, torch.bfloat16, "dy")
+    _chk(x, torch.bfloat16, "x")
+    _chk(dw, torch.float32, "dw", OC * KTOT)
+    _chk(ws, torch.float32, "ws")
+    if conv_out_hw(IH, IW, R, S, stride, pad) != (OH, OW):
+        raise ValueError("conv_wgrad: shapes inconsistent with the conv geometry")
+    if stem:
+        bm, bn = 64, 128
+    else:
+        if OC % 64 or IC % 64:
+            raise ValueError("conv_wgrad needs channels % 64 == 0")
+        if tile:
+            bm, bn = tile
+        else:
+            bm = 128 if OC % 128 == 0 else 64
+            bn = 128 if IC % 128 == 0 else 64
+    if in_scale is not None:
+        _chk(in_scale, torch.float32, "in_scale", IC)
+        _chk(in_shift, torch.float32, "in_shift", IC)
+    M = N * OH * OW
+    nsplit, ms = wgrad_splits(M, OC, KTOT, bm, bn, ws.numel())
+    if (nsplit + (min(64, nsplit) if nsplit > 8 else 0)) * OC * KTOT > ws.numel():
+        raise ValueError("wgrad workspace too small")
+    C().conv_wgrad(STEM if stem else FWD, bm, bn, dy.data_ptr(), x.data_ptr(), ws.data_ptr(), _p(in_scale),
+                   _p(in_shift), int(relu_in), N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, KTOT, nsplit, ms,
+                   stream_ptr())
+    C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsplit, float(scale), int(accumulate), stream_ptr())
+    return dw
+
+
+# --------------------------------------------------------------------------------------
+# batch norm / elementwise
+# --------------------------------------------------------------------------------------
+@_dispatch
+def bn_finalize(stats, count, gamma, beta, eps, momentum, running_mean, running_var, scale, shift,
+                save_mean, save_invstd):
+    Cc = scale.numel()
+    C().bn_finalize(stats.data_ptr(), NSHARD, Cc, float(count), _p(gamma), _p(beta), float(eps), float(momentum),
+                    _p(running_mean), _p(running_var), scale.data_ptr(), shift.data_ptr(), _p(save_mean),
+                    _p(save_invstd), stream_ptr())
+
+
+@_dispatch
+def bn_eval_coeff(gamma, beta, eps, running_mean, running_var, scale, shift):
+    C().bn_eval_coeff(scale.numel(), _p(gamma), _p(beta), float(eps), running_mean.data_ptr(),
+                      running_var.data_ptr(), scale.data_ptr(), shift.data_ptr(), stream_ptr())
+
+
+@_dispatch
+def channel_stats(y, stats):
+    Cc = y.shape[-1]
+    _chk(y, torch.bfloat16, "y")
+    _chk(stats, torch.float32, "stats", NSHARD * 2 * Cc)
+    C().channel_stats(y.data_ptr(), y.numel() // Cc, Cc, stats.data_ptr(), NSHARD, stream_ptr())
+
+
+@_dispatch
+def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True):
+    Cc = y.shape[-1]
+    _chk(y, torch.bfloat16, "y")
+    _chk(out, torch.bfloat16, "out", y.numel())
+    mode = 0
+    if res is not None:
+        _chk(res, torch.bfloat16, "res", y.numel())
+        mode = 2 if res_scale is not None else 1
+    C().bn_apply(y.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(res), _p(res_scale), _p(res_shift),
+                 out.data_ptr(), y.numel(), Cc, mode, int(relu), stream_ptr())
+    return out
+
+
+MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
+
+
+@_dispatch
+def bn_bwd_reduce(dout, y, mean, invstd, stats, *, mask_mode, mref=None, scale=None, shift=None):
+    Cc = y.shape[-1]
+    _chk(dout, torch.bfloat16, "dout", y.numel())
+    _chk(y, torch.bfloat16, "y")
+    _chk(stats, torch.float32, "stats", NSHARD * 2 * Cc)
+    if mask_mode == MASK_OUT:
+        _chk(mref, torch.bfloat16, "mref", y.numel())
+    C().bn_bwd_reduce(dout.data_ptr(), _p(mref), y.data_ptr(), _p(scale), _p(shift), mean.data_ptr(),
+                      invstd.data_ptr(), y.numel() // Cc, Cc, stats.data_ptr(), NSHARD, mask_mode, stream_ptr())
+
+
+@_dispatch
+def bn_bwd_coeff(stats, count, gamma, mean, invstd, coeff, dgamma=None, dbeta=None, accumulate=False):
+    Cc = mean.numel()
+    C().bn_bwd_coeff(stats.data_ptr(), NSHARD, Cc, float(count), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
+                     coeff.data_ptr(), _p(dgamma), _p(dbeta), int(accumulate), stream_ptr())
+
+
+@_dispatch
+def bn_bwd_apply(dout, y, coeff, dy, *, mask_mode, mref=None, scale=None, shift=None, gout=None):
+    Cc = y.shape[-1]
+    _chk(dy, torch.bfloat16, "dy", y.numel())
+    if gout is not None:
+        _chk(gout, torch.bfloat16, "gout", y.numel())
+    C().bn_bwd_apply(dout.data_ptr(), _p(mref), y.data_ptr(), _p(scale), _p(shift), coeff.data_ptr(),
+                     dy.data_ptr(), _p(gout), y.numel(), Cc, mask_mode, stream_ptr())
+
+
+@_dispatch
+def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True):
+    N, H, W, Cc = x.shape
+    _, P, Q, _ = out.shape
+    _chk(x, torch.bfloat16, "x")
+    _chk(out, torch.bfloat16, "out")
+    _chk(arg, torch.uint8, "arg", out.numel())
+    C().maxpool_fwd(x.data_ptr(), _p(scale), _p(shift), out.data_ptr(), arg.data_ptr(), N, H, W, Cc, P, Q, K,
+                    stride, pad, int(relu), stream_ptr())
+
+
+@_dispatch
+def maxpool_bwd(dout, arg, dx, *, K=3, stride=2, pad=1):
+    N, H, W, Cc = dx.shape
+    _, P, Q, _ = dout.shape
+    _chk(dout, torch.bfloat16, "dout")
+    _chk(arg, torch.uint8, "arg", dout.numel())
+    _chk(dx, torch.bfloat16, "dx")
+    C().maxpool_bwd(dout.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, H, W, Cc, P, Q, K, stride, pad, stream_ptr())
+
+
+@_dispatch
+def avgpool_fwd(x, out):
+    N, H, W, Cc = x.shape
+    _chk(x, torch.bfloat16, "x")
+    _chk(out, torch.bfloat16, "out", N * Cc)
+    C().avgpool_fwd(x.data_ptr(), out.data_ptr(), N, H * W, Cc, stream_ptr())
+
+
+@_dispatch
+def avgpool_bwd(dout, dx):
+    N, H, W, Cc = dx.shape
+    _chk(dout, torch.bfloat16, "dout", N * Cc)
+    _chk(dx, torch.bfloat16, "dx")
+    C().avgpool_bwd(dout.data_ptr(), dx.data_ptr(), N, H * W, Cc, stream_ptr())
+
+
+@_dispatch
+def softmax_ce(logits, labels, dlogits=None, loss_out=None, stats=None, smoothing=0.0, grad_scale=1.0):
+    B, Cc = logits.shape
+    if logits.dtype not in (torch.float32, torch.bfloat16) or not logits.is_contiguous():
+        raise TypeError("logits must be contiguous fp32/bf16")
+    _chk(labels, torch.int64, "labels", B)
+    if dlogits is not None:
+        _chk(dlogits, logits.dtype, "dlogits", B * Cc)
+    C().softmax_ce(logits.data_ptr(), int(logits.dtype == torch.bfloat16), labels.data_ptr(), _p(dlogits),
+                   _p(loss_out), _p(stats), B, Cc, float(smoothing), float(grad_scale), stream_ptr())
+
+
+@_dispatch
+def sgd_step(p, g, v, p16=None, *, lr, momentum, dampening=0.0, weight_decay=0.0, nesterov=False, first=False,
+             grad_scale_ptr=None, grad_scale=1.0, hyper=None):
+    """PyTorch-SGD semantics. ``hyper`` (fp32[1] device tensor) overrides ``lr`` at run time."""
+    n = p.numel()
+    _chk(p, torch.float32, "p")
+    _chk(g, torch.float32, "g", n)
+    _chk(v, torch.float32, "v", n)
+    if p16 is not None:
+        _chk(p16, torch.bfloat16, "p16", n)
+    C().sgd(p.data_ptr(), g.data_ptr(), v.data_ptr(), _p(p16), n, _p(hyper), float(lr), float(momentum), float(dampening),
+            float(weight_decay), int(nesterov), int(first), _p(grad_scale_ptr), float(grad_scale), stream_ptr())
+
+
+@_dispatch
+def adam_step(p, g, m, v, p16=None, *, lr, beta1, beta2, eps, weight_decay, decoupled, step,
+              grad_scale_ptr=None, grad_scale=1.0, hyper=None):
+    """Adam / AdamW. ``hyper`` (fp32[3] device: lr, 1-b1^t, 1-b2^t) overrides lr/step at run time."""
+    n = p.numel()
+    for t, nm in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
+        _chk(t, torch.float32, nm, n)
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    C().adam(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _p(p16), n, _p(hyper), float(lr), float(beta1),
+             float(beta2), float(eps), float(weight_decay), int(decoupled), float(bc1), float(bc2),
+             _p(grad_scale_ptr), float(grad_scale), stream_ptr())
+
+
+@_dispatch
+def global_norm_clip_factor(g, max_norm, work):
+    """work: fp32[4] scratch; returns work[2:4] = (factor, norm) on device (no host sync)."""
+    work.zero_()
+    C().sumsq(g.data_ptr(), g.numel(), work.data_ptr(), stream_ptr())
+    C().clip_factor(work.data_ptr(), float(max_norm), work[2:].data_ptr(), stream_ptr())
+    return work[2:3]
+
+
+@_dispatch
+def normalize_u8(img, out, mean, std, flip=None):
+    N, H, W, Cin = img.shape
+    _chk(img, torch.uint8, "img")
+    _chk(out, torch.bfloat16, "out", N * H * W * 4)
+    if flip is not None:
+        _chk(flip, torch.uint8, "flip", N)
+    C().normalize_u8(img.data_ptr(), out.data_ptr(), _p(flip), N, H, W, Cin, float(mean[0]), float(mean[1]),
+                     float(mean[2]), float(std[0]), float(std[1]), float(std[2]), stream_ptr())
+
+
+@_dispatch
+def weight_prep(master, wbuf, desc_dev, nlayers):
+    C().weight_prep(master.data_ptr(), wbuf.data_ptr(), desc_dev.data_ptr(), nlayers, stream_ptr())
+
+
+@_dispatch
+def cast_f32_bf16(x, y):
+    _chk(x, torch.float32, "x")
+    _chk(y, torch.bfloat16, "y", x.numel())
+    C().cast_f32_bf16(x.data_ptr(), y.data_ptr(), x.numel(), stream_ptr())

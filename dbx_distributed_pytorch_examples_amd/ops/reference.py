@@ -1,0 +1,324 @@
+"""PyTorch reference implementations of every HIP kernel, with identical signatures.
+
+``ops.kernels`` dispatches here for CPU tensors, which makes the whole native program
+(``engine.program``) runnable — and testable, including the DDP bucket path over gloo — on a
+host without a GPU. They are the semantic definition the HIP kernels are tested against
+(tests/test_kernels_gpu.py compares the kernels to plain fp32 torch ops of the same math).
+Numerics mirror the kernels: bf16 storage, fp32 accumulation, prologue output rounded to bf16.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+NSHARD = 32
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1)
+
+
+def _act_in(x, in_scale, in_shift, relu_in):
+    xf = x.float()
+    if in_scale is not None:
+        xf = xf * in_scale + in_shift
+        if relu_in:
+            xf = torch.relu(xf)
+        xf = xf.bfloat16().float()
+    return xf
+
+
+def _add_stats(stats, y):
+    C = y.shape[-1]
+    yf = y.float().reshape(-1, C)
+    st = stats.view(NSHARD, 2, C)
+    st[0, 0] += yf.sum(0)
+    st[0, 1] += (yf * yf).sum(0)
+
+
+def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None, relu_in=True, tile=None):
+    OC = w16.shape[0]
+    IC = x.shape[-1]
+    xf = _act_in(x, in_scale, in_shift, relu_in)
+    w = w16.float().view(OC, R, S, IC).permute(0, 3, 1, 2)
+    y = _nhwc(F.conv2d(_nchw(xf), w, stride=stride, padding=pad)).bfloat16()
+    out.copy_(y.reshape(out.shape))
+    if stats is not None:
+        _add_stats(stats, out)
+    return out
+
+
+def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None):
+    N, P, Q, Kc = dy.shape
+    _, H, W, Cc = dx.shape
+    w = wt16.float().view(Cc, R, S, Kc).permute(3, 0, 1, 2)  # [K, C, R, S]
+    g = torch.nn.grad.conv2d_input((N, Cc, H, W), w, _nchw(dy.float()), stride=stride, padding=pad)
+    g = _nhwc(g)
+    if accumulate:
+        g = g + dx.float()
+    dx.copy_(g.bfloat16())
+    return dx
+
+
+def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
+    OC = w16s.shape[0]
+    w = w16s.float().view(OC, 8, 8, 4)[:, :R, :S, :].permute(0, 3, 1, 2)
+    y = _nhwc(F.conv2d(_nchw(x4.float()), w, stride=stride, padding=pad)).bfloat16()
+    out.copy_(y)
+    if stats is not None:
+        _add_stats(stats, out)
+    return out
+
+
+def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True, scale=1.0,
+               accumulate=False, stem=False, tile=None):
+    N, OH, OW, OC = dy.shape
+    IC = x.shape[-1]
+    xf = _act_in(x, in_scale, in_shift, relu_in)
+    g = torch.nn.grad.conv2d_weight(_nchw(xf), (OC, IC, R, S), _nchw(dy.float()), stride=stride, padding=pad)
+    g = g.permute(0, 2, 3, 1) * scale  # KRSC
+    if stem:
+        full = torch.zeros(OC, 8, 8, 4, dtype=torch.float32, device=dy.device)
+        full[:, :R, :S, :IC] = g
+        g = full
+    g = g.reshape(dw.shape)
+    if accumulate:
+        g = g + dw
+    dw.copy_(g)
+    return dw
+
+
+def bn_finalize(stats, count, gamma, beta, eps, momentum, running_mean, running_var, scale, shift, save_mean,
+                save_invstd):
+    C = scale.numel()
+    st = stats.view(NSHARD, 2, C).double().sum(0)
+    mean = st[0] / count
+    var = (st[1] / count - mean * mean).clamp_min(0)
+    invstd = 1.0 / torch.sqrt(var + eps)
+    g = gamma.double() if gamma is not None else torch.ones_like(mean)
+    b = beta.double() if beta is not None else torch.zeros_like(mean)
+    scale.copy_((g * invstd).float())
+    shift.copy_((b - mean * g * invstd).float())
+    if save_mean is not None:
+        save_mean.copy_(mean.float())
+    if save_invstd is not None:
+        save_invstd.copy_(invstd.float())
+    if running_mean is not None and momentum > 0:
+        unb = var * count / (count - 1) if count > 1 else var
+        running_mean.mul_(1 - momentum).add_(momentum * mean.float())
+        running_var.mul_(1 - momentum).add_(momentum * unb.float())
+
+
+def bn_eval_coeff(gamma, beta, eps, running_mean, running_var, scale, shift):
+    inv = torch.rsqrt(running_var + eps)
+    g = gamma if gamma is not None else torch.ones_like(inv)
+    b = beta if beta is not None else torch.zeros_like(inv)
+    scale.copy_(g * inv)
+    shift.copy_(b - running_mean * g * inv)
+
+
+def channel_stats(y, stats):
+    _add_stats(stats, y)
+
+
+def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True):
+    f = y.float() * scale + shift
+    if res is not None:
+        r = res.float()
+        if res_scale is not None:
+            r = r * res_scale + res_shift
+        f = f + r
+    if relu:
+        f = torch.relu(f)
+    out.copy_(f.bfloat16())
+    return out
+
+
+MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
+
+
+def _g(dout, y, mask_mode, mref, scale, shift):
+    g = dout.float()
+    if mask_mode == MASK_OUT:
+        g = g * (mref.float() > 0)
+    elif mask_mode == MASK_Y:
+        g = g * ((y.float() * scale + shift) > 0)
+    return g
+
+
+def bn_bwd_reduce(dout, y, mean, invstd, stats, *, mask_mode, mref=None, scale=None, shift=None):
+    C = y.shape[-1]
+    g = _g(dout, y, mask_mode, mref, scale, shift).reshape(-1, C)
+    xhat = ((y.float() - mean) * invstd).reshape(-1, C)
+    st = stats.view(NSHARD, 2, C)
+    st[0, 0] += g.sum(0)
+    st[0, 1] += (g * xhat).sum(0)
+
+
+def bn_bwd_coeff(stats, count, gamma, mean, invstd, coeff, dgamma=None, dbeta=None, accumulate=False):
+    C = mean.numel()
+    st = stats.view(NSHARD, 2, C).sum(0)
+    s, q = st[0], st[1]
+    g = gamma if gamma is not None else torch.ones_like(mean)
+    sg, sgx = s / count, q / count
+    k1 = g * invstd
+    k2 = -g * invstd * invstd * sgx
+    k3 = -g * invstd * sg + g * invstd * invstd * sgx * mean
+    coeff.view(3, C).copy_(torch.stack([k1, k2, k3]))
+    if dgamma is not None:
+        dgamma.copy_(q + (dgamma if accumulate else 0))
+    if dbeta is not None:
+        dbeta.copy_(s + (dbeta if accumulate else 0))
+
+
+def bn_bwd_apply(dout, y, coeff, dy, *, mask_mode, mref=None, scale=None, shift=None, gout=None):
+    C = y.shape[-1]
+    g = _g(dout, y, mask_mode, mref, scale, shift)
+    if gout is not None:
+        gout.copy_(g.bfloat16())
+    k = coeff.view(3, C)
+    dy.copy_((k[0] * g + k[1] * y.float() + k[2]).bfloat16())
+
+
+def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True):
+    f = x.float()
+    if scale is not None:
+        f = f * scale + shift
+    if relu:
+        f = torch.relu(f)
+    N, H, W, C = f.shape
+    _, P, Q, _ = out.shape
+    fp = F.pad(_nchw(f), (pad, pad, pad, pad), value=-math.inf)
+    best = torch.full((N, C, P, Q), -math.inf, dtype=torch.float32, device=x.device)
+    bidx = torch.zeros((N, C, P, Q), dtype=torch.uint8, device=x.device)
+    for r in range(K):
+        for s in range(K):
+            win = fp[:, :, r:r + stride * (P - 1) + 1:stride, s:s + stride * (Q - 1) + 1:stride]
+            upd = win > best
+            best = torch.where(upd, win, best)
+            bidx = torch.where(upd, torch.full_like(bidx, r * K + s), bidx)
+    out.copy_(_nhwc(best).bfloat16())
+    arg.copy_(_nhwc(bidx))
+
+
+def maxpool_bwd(dout, arg, dx, *, K=3, stride=2, pad=1):
+    N, H, W, C = dx.shape
+    _, P, Q, _ = dout.shape
+    acc = torch.zeros(N, C, H + 2 * pad, W + 2 * pad, dtype=torch.float32, device=dx.device)
+    g = _nchw(dout.float())
+    a = _nchw(arg)
+    for r in range(K):
+        for s in range(K):
+            contrib = torch.where(a == r * K + s, g, torch.zeros_like(g))
+            acc[:, :, r:r + stride * (P - 1) + 1:stride, s:s + stride * (Q - 1) + 1:stride] += contrib
+    dx.copy_(_nhwc(acc[:, :, pad:pad + H, pad:pad + W]).bfloat16())
+
+
+def avgpool_fwd(x, out):
+    out.copy_(x.float().mean((1, 2)).bfloat16())
+
+
+def avgpool_bwd(dout, dx):
+    N, H, W, C = dx.shape
+    dx.copy_((dout.float() / (H * W))[:, None, None, :].expand(N, H, W, C).bfloat16())
+
+
+def softmax_ce(logits, labels, dlogits=None, loss_out=None, stats=None, smoothing=0.0, grad_scale=1.0):
+    B, C = logits.shape
+    lf = logits.float()
+    lse = torch.logsumexp(lf, 1)
+    xl = lf.gather(1, labels[:, None]).squeeze(1)
+    loss = (1 - smoothing) * (lse - xl) + smoothing * (lse - lf.mean(1))
+    if loss_out is not None:
+        loss_out.copy_(loss)
+    if stats is not None:
+        stats[0] += loss.sum()
+        stats[1] += (lf.argmax(1) == labels).sum().float()
+    if dlogits is not None:
+        p = torch.softmax(lf, 1)
+        t = torch.full_like(p, smoothing / C)
+        t.scatter_add_(1, labels[:, None], torch.full((B, 1), 1 - smoothing, device=p.device))
+        dlogits.copy_(((p - t) * grad_scale / B).to(dlogits.dtype))
+
+
+def sgd_step(p, g, v, p16=None, *, lr, momentum, dampening=0.0, weight_decay=0.0, nesterov=False, first=False,
+             grad_scale_ptr=None, grad_scale=1.0, hyper=None):
+    if hyper is not None:
+        lr = float(hyper[0])
+    gs = grad_scale * (float(grad_scale_ptr[0]) if grad_scale_ptr is not None else 1.0)
+    d = g * gs + weight_decay * p
+    if momentum != 0:
+        if first:
+            v.copy_(d)
+        else:
+            v.mul_(momentum).add_(d, alpha=1 - dampening)
+        d = d + momentum * v if nesterov else v
+    p.sub_(lr * d)
+    if p16 is not None:
+        p16.copy_(p.bfloat16())
+
+
+def adam_step(p, g, m, v, p16=None, *, lr, beta1, beta2, eps, weight_decay, decoupled, step, grad_scale_ptr=None,
+              grad_scale=1.0, hyper=None):
+    bc1, bc2 = 1 - beta1 ** step, 1 - beta2 ** step
+    if hyper is not None:
+        lr, bc1, bc2 = float(hyper[0]), float(hyper[1]), float(hyper[2])
+    gs = grad_scale * (float(grad_scale_ptr[0]) if grad_scale_ptr is not None else 1.0)
+    gg = g * gs
+    if decoupled:
+        p.mul_(1 - lr * weight_decay)
+    else:
+        gg = gg + weight_decay * p
+    m.mul_(beta1).add_(gg, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(gg, gg, value=1 - beta2)
+    p.sub_(lr * (m / bc1) / (torch.sqrt(v / bc2) + eps))
+    if p16 is not None:
+        p16.copy_(p.bfloat16())
+
+
+def global_norm_clip_factor(g, max_norm, work):
+    work.zero_()
+    work[0] = (g.float() ** 2).sum()
+    nrm = torch.sqrt(work[0])
+    work[2] = torch.clamp(max_norm / (nrm + 1e-6), max=1.0)
+    work[3] = nrm
+    return work[2:3]
+
+
+def normalize_u8(img, out, mean, std, flip=None):
+    N, H, W, Cin = img.shape
+    f = img.float() / 255.0
+    if Cin == 1:
+        f = f.expand(N, H, W, 3)
+    if flip is not None:
+        fl = flip.bool()[:, None, None, None]
+        f = torch.where(fl, f.flip(2), f)
+    m = torch.tensor(mean, device=img.device)
+    s = torch.tensor(std, device=img.device)
+    o = torch.zeros(N, H, W, 4, device=img.device)
+    o[..., :3] = (f - m) / s
+    out.copy_(o.bfloat16())
+
+
+def weight_prep(master, wbuf, desc_dev, nlayers):
+    d = desc_dev.view(-1, 10)
+    for i in range(nlayers):
+        row = d[i]
+        src, fwd, tr = (int(x) for x in row[:6].view(torch.int64))
+        k, rs, c = int(row[6]), int(row[7]), int(row[8])
+        n = k * rs * c
+        w = master[src:src + n]
+        if fwd >= 0:
+            wbuf[fwd:fwd + n].copy_(w.bfloat16())
+        if tr >= 0:
+            wbuf[tr:tr + n].copy_(w.view(k, rs, c).permute(2, 1, 0).reshape(-1).bfloat16())
+
+
+def cast_f32_bf16(x, y):
+    y.copy_(x.bfloat16())

@@ -1,0 +1,389 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Shapes come from the ResNet conv tables in SURVEY.md §2.4 / Appendix A at small batch.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def K():
+    from dbx_distributed_pytorch_examples_amd.ops import kernels
+    return kernels
+
+
+def relerr(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+CONV_CASES = [
+    # N, H, W, IC, OC, R, stride, pad
+    (2, 14, 14, 64, 64, 3, 1, 1),
+    (2, 14, 14, 64, 256, 1, 1, 0),
+    (2, 14, 14, 256, 64, 1, 1, 0),
+    (2, 14, 14, 128, 128, 3, 2, 1),
+    (2, 14, 14, 256, 512, 1, 2, 0),
+    (3, 7, 7, 512, 512, 3, 1, 1),
+    (4, 9, 9, 64, 128, 3, 2, 1),
+    (1, 5, 5, 128, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("prologue", [False, True])
+def test_conv_fwd(case, prologue):
+    k = K()
+    N, H, W, IC, OC, R, st, pad = case
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, IC, device=dev).bfloat16()
+    w = (torch.randn(OC, R, R, IC, device=dev) / math.sqrt(IC * R * R)).bfloat16()
+    OH, OW = k.conv_out_hw(H, W, R, R, st, pad)
+    out = torch.empty(N, OH, OW, OC, device=dev, dtype=torch.bfloat16)
+    stats = torch.zeros(k.NSHARD * 2 * OC, device=dev)
+    sc = sh = None
+    xe = x.float()
+    if prologue:
+        sc = torch.rand(IC, device=dev) + 0.5
+        sh = torch.randn(IC, device=dev) * 0.1
+        xe = torch.relu(x.float() * sc + sh).bfloat16().float()
+    for tile in [None, (128, 128), (128, 64), (64, 64)]:
+        if tile and OC % tile[1]:
+            continue
+        stats.zero_()
+        k.conv_fwd(x, w.view(OC, -1), out, R=R, S=R, stride=st, pad=pad, stats=stats, in_scale=sc, in_shift=sh,
+                   relu_in=True, tile=tile)
+        ref = nhwc(F.conv2d(nchw(xe), w.float().permute(0, 3, 1, 2), stride=st, padding=pad))
+        assert relerr(out, ref) < 1e-2, (tile, relerr(out, ref))
+        s = stats.view(k.NSHARD, 2, OC).sum(0)
+        o32 = out.float().view(-1, OC)
+        assert relerr(s[0], o32.sum(0)) < 1e-3
+        assert relerr(s[1], (o32 * o32).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_dgrad(case):
+    k = K()
+    N, H, W, IC, OC, R, st, pad = case
+    torch.manual_seed(1)
+    w = (torch.randn(OC, R, R, IC, device=dev) / math.sqrt(IC * R * R)).bfloat16()
+    OH, OW = k.conv_out_hw(H, W, R, R, st, pad)
+    dy = torch.randn(N, OH, OW, OC, device=dev).bfloat16()
+    wt = w.permute(3, 1, 2, 0).contiguous()  # [IC][R][S][OC]
+    dx = torch.empty(N, H, W, IC, device=dev, dtype=torch.bfloat16)
+    k.conv_dgrad(dy, wt.view(IC, -1), dx, R=R, S=R, stride=st, pad=pad)
+    ref = torch.nn.grad.conv2d_input((N, IC, H, W), w.float().permute(0, 3, 1, 2), nchw(dy.float()),
+                                     stride=st, padding=pad)
+    assert relerr(dx, nhwc(ref)) < 1e-2
+    # accumulate mode
+    base = torch.randn_like(dx)
+    dx2 = base.clone()
+    k.conv_dgrad(dy, wt.view(IC, -1), dx2, R=R, S=R, stride=st, pad=pad, accumulate=True)
+    assert relerr(dx2, nhwc(ref) + base.float()) < 1e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("prologue", [False, True])
+def test_conv_wgrad(case, prologue):
+    k = K()
+    N, H, W, IC, OC, R, st, pad = case
+    torch.manual_seed(2)
+    x = torch.randn(N, H, W, IC, device=dev).bfloat16()
+    OH, OW = k.conv_out_hw(H, W, R, R, st, pad)
+    dy = torch.randn(N, OH, OW, OC, device=dev).bfloat16()
+    dw = torch.empty(OC, R * R * IC, device=dev)
+    ws = torch.empty(64 * 1024 * 1024, device=dev)
+    xe = x.float()
+    sc = sh = None
+    if prologue:
+        sc = torch.rand(IC, device=dev) + 0.5
+        sh = torch.randn(IC, device=dev) * 0.1
+        xe = torch.relu(x.float() * sc + sh).bfloat16().float()
+    k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, in_scale=sc, in_shift=sh)
+    ref = torch.nn.grad.conv2d_weight(nchw(xe), (OC, IC, R, R), nchw(dy.float()), stride=st, padding=pad)
+    assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_stem_fwd_wgrad():
+    k = K()
+    N, H, W = 2, 32, 32
+    torch.manual_seed(3)
+    img = torch.randn(N, H, W, 3, device=dev)
+    x4 = torch.zeros(N, H, W, 4, device=dev)
+    x4[..., :3] = img
+    x4 = x4.bfloat16()
+    w = (torch.randn(64, 7, 7, 3, device=dev) * 0.05)
+    ws_ = torch.zeros(64, 8, 8, 4, device=dev)
+    ws_[:, :7, :7, :3] = w
+    w16s = ws_.bfloat16().view(64, 256)
+    OH, OW = k.conv_out_hw(H, W, 7, 7, 2, 3)
+    out = torch.empty(N, OH, OW, 64, device=dev, dtype=torch.bfloat16)
+    stats = torch.zeros(k.NSHARD * 2 * 64, device=dev)
+    k.conv_stem_fwd(x4, w16s, out, stats=stats)
+    xr = nchw(x4[..., :3].float())
+    wr = ws_.bfloat16().float()[:, :7, :7, :3].permute(0, 3, 1, 2)
+    ref = nhwc(F.conv2d(xr, wr, stride=2, padding=3))
+    assert relerr(out, ref) < 1e-2
+    dy = torch.randn(N, OH, OW, 64, device=dev).bfloat16()
+    dw = torch.empty(64, 256, device=dev)
+    wsp = torch.empty(16 * 1024 * 1024, device=dev)
+    k.conv_wgrad(dy, x4, dw, wsp, R=7, S=7, stride=2, pad=3, stem=True)
+    refw = torch.nn.grad.conv2d_weight(xr, (64, 3, 7, 7), nchw(dy.float()), stride=2, padding=3)
+    got = dw.view(64, 8, 8, 4)
+    assert relerr(got[:, :7, :7, :3], refw.permute(0, 2, 3, 1)) < 1e-2
+    assert got[:, 7].abs().max().item() == 0 and got[:, :, 7].abs().max().item() == 0
+
+
+def _bn_ref_setup(M=4096, Cc=128):
+    torch.manual_seed(4)
+    y = (torch.randn(M, Cc, device=dev) * 2 + 0.5).bfloat16()
+    return y
+
+
+def test_bn_finalize_apply():
+    k = K()
+    M, Cc = 4096, 128
+    y = _bn_ref_setup(M, Cc)
+    stats = torch.zeros(k.NSHARD * 2 * Cc, device=dev)
+    k.channel_stats(y, stats)
+    gamma = torch.rand(Cc, device=dev) + 0.5
+    beta = torch.randn(Cc, device=dev)
+    rm = torch.zeros(Cc, device=dev)
+    rv = torch.ones(Cc, device=dev)
+    scale, shift, sm, si = (torch.empty(Cc, device=dev) for _ in range(4))
+    k.bn_finalize(stats, M, gamma, beta, 1e-5, 0.1, rm, rv, scale, shift, sm, si)
+    yf = y.float()
+    mean = yf.mean(0)
+    var = yf.var(0, unbiased=False)
+    assert relerr(sm, mean) < 1e-4
+    assert relerr(si, 1 / torch.sqrt(var + 1e-5)) < 1e-4
+    assert relerr(rm, 0.1 * mean) < 1e-4
+    assert relerr(rv, 0.9 + 0.1 * yf.var(0, unbiased=True)) < 1e-4
+    out = torch.empty_like(y)
+    res = torch.randn_like(yf).bfloat16()
+    k.bn_apply(y, scale, shift, out, res=res, relu=True)
+    ref = torch.relu((yf - mean) / torch.sqrt(var + 1e-5) * gamma + beta + res.float())
+    assert relerr(out, ref) < 1e-2
+    rsc = torch.rand(Cc, device=dev)
+    rsh = torch.randn(Cc, device=dev)
+    k.bn_apply(y, scale, shift, out, res=res, res_scale=rsc, res_shift=rsh, relu=False)
+    ref = (yf - mean) / torch.sqrt(var + 1e-5) * gamma + beta + res.float() * rsc + rsh
+    assert relerr(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("mask_mode", [0, 1, 2])
+def test_bn_backward(mask_mode):
+    k = K()
+    M, Cc = 4096, 64
+    y = _bn_ref_setup(M, Cc)
+    gamma = torch.rand(Cc, device=dev) + 0.5
+    beta = torch.randn(Cc, device=dev)
+    yf = y.float().requires_grad_(True)
+    bn = torch.nn.functional.batch_norm(yf, None, None, gamma, beta, training=True, eps=1e-5)
+    dout = torch.randn(M, Cc, device=dev).bfloat16()
+    mref = None
+    if mask_mode == 0:
+        target = bn
+    elif mask_mode == 1:
+        mref = torch.randn(M, Cc, device=dev).bfloat16()
+        target = bn * (mref.float() > 0)
+    else:
+        target = torch.relu(bn)
+    gam = gamma.clone().requires_grad_(True)
+    bet = beta.clone().requires_grad_(True)
+    yf2 = y.float().requires_grad_(True)
+    bn2 = torch.nn.functional.batch_norm(yf2, None, None, gam, bet, training=True, eps=1e-5)
+    if mask_mode == 1:
+        t2 = bn2 * (mref.float() > 0)
+    elif mask_mode == 2:
+        t2 = torch.relu(bn2)
+    else:
+        t2 = bn2
+    t2.backward(dout.float())
+    mean = y.float().mean(0)
+    invstd = 1 / torch.sqrt(y.float().var(0, unbiased=False) + 1e-5)
+    scale = gamma * invstd
+    shift = beta - mean * scale
+    stats = torch.zeros(k.NSHARD * 2 * Cc, device=dev)
+    k.bn_bwd_reduce(dout, y, mean, invstd, stats, mask_mode=mask_mode, mref=mref, scale=scale, shift=shift)
+    coeff = torch.empty(3 * Cc, device=dev)
+    dg = torch.empty(Cc, device=dev)
+    db = torch.empty(Cc, device=dev)
+    k.bn_bwd_coeff(stats, M, gamma, mean, invstd, coeff, dg, db)
+    dy = torch.empty_like(y)
+    gout = torch.empty_like(y)
+    k.bn_bwd_apply(dout, y, coeff, dy, mask_mode=mask_mode, mref=mref, scale=scale, shift=shift, gout=gout)
+    assert relerr(dy, yf2.grad) < 2e-2
+    assert relerr(dg, gam.grad) < 1e-3
+    assert relerr(db, bet.grad) < 1e-3
+
+
+def test_maxpool():
+    k = K()
+    N, H, W, Cc = 2, 16, 16, 64
+    torch.manual_seed(5)
+    x = torch.randn(N, H, W, Cc, device=dev).bfloat16()
+    sc = torch.rand(Cc, device=dev) + 0.5
+    sh = torch.randn(Cc, device=dev) * 0.1
+    out = torch.empty(N, 8, 8, Cc, device=dev, dtype=torch.bfloat16)
+    arg = torch.empty(N, 8, 8, Cc, device=dev, dtype=torch.uint8)
+    k.maxpool_fwd(x, out, arg, scale=sc, shift=sh, relu=True)
+    act = torch.relu(x.float() * sc + sh).requires_grad_(True)
+    ref = F.max_pool2d(nchw(act), 3, 2, 1)
+    assert relerr(out, nhwc(ref)) < 1e-2
+    dout = torch.randn(N, 8, 8, Cc, device=dev).bfloat16()
+    ref.backward(nchw(dout.float()))
+    dx = torch.empty_like(x)
+    k.maxpool_bwd(dout, arg, dx)
+    # ties (relu zeros) may route differently; compare on positive activations only
+    m = (act.detach() > 0)
+    assert relerr(dx.float() * m, act.grad * m) < 2e-2
+
+
+def test_avgpool():
+    k = K()
+    x = torch.randn(4, 7, 7, 256, device=dev).bfloat16()
+    out = torch.empty(4, 256, device=dev, dtype=torch.bfloat16)
+    k.avgpool_fwd(x, out)
+    assert relerr(out, x.float().mean((1, 2))) < 1e-2
+    d = torch.randn(4, 256, device=dev).bfloat16()
+    dx = torch.empty_like(x)
+    k.avgpool_bwd(d, dx)
+    assert relerr(dx, (d.float() / 49)[:, None, None, :].expand(4, 7, 7, 256)) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_softmax_ce(dtype, smoothing):
+    k = K()
+    B, Cc = 64, 1000
+    torch.manual_seed(6)
+    logits = (torch.randn(B, Cc, device=dev) * 3).to(dtype)
+    labels = torch.randint(0, Cc, (B,), device=dev)
+    lf = logits.float().requires_grad_(True)
+    loss = F.cross_entropy(lf, labels, label_smoothing=smoothing)
+    loss.backward()
+    dl = torch.empty_like(logits)
+    lo = torch.empty(B, device=dev)
+    st = torch.zeros(2, device=dev)
+    k.softmax_ce(logits, labels, dl, lo, st, smoothing=smoothing)
+    assert abs(lo.mean().item() - loss.item()) < 1e-3 * max(1, loss.item())
+    assert abs(st[0].item() / B - loss.item()) < 1e-3 * max(1, loss.item())
+    assert st[1].item() == (logits.float().argmax(1) == labels).sum().item()
+    assert relerr(dl, lf.grad) < 1e-2
+
+
+def test_sgd_adam():
+    k = K()
+    n = 100003
+    torch.manual_seed(7)
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    ref = torch.nn.Parameter(p.clone())
+    opt = torch.optim.SGD([ref], lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    v = torch.zeros(n, device=dev)
+    p16 = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    for step in range(3):
+        ref.grad = g.clone()
+        opt.step()
+        k.sgd_step(p, g, v, p16, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True, first=(step == 0))
+    assert relerr(p, ref.detach()) < 1e-5
+    assert relerr(p16, ref.detach()) < 1e-2
+    p = torch.randn(n, device=dev)
+    ref = torch.nn.Parameter(p.clone())
+    opt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    for step in range(1, 4):
+        ref.grad = g.clone()
+        opt.step()
+        k.adam_step(p, g, m, v, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, decoupled=True,
+                    step=step)
+    assert relerr(p, ref.detach()) < 1e-5
+
+
+def test_clip_factor():
+    k = K()
+    g = torch.randn(1 << 20, device=dev)
+    work = torch.zeros(4, device=dev)
+    f = k.global_norm_clip_factor(g, 1.0, work)
+    nrm = g.norm().item()
+    assert abs(work[3].item() - nrm) / nrm < 1e-4
+    assert abs(f.item() - min(1.0, 1.0 / (nrm + 1e-6))) < 1e-6
+
+
+def test_normalize_u8():
+    k = K()
+    img = torch.randint(0, 256, (3, 8, 8, 3), device=dev, dtype=torch.uint8)
+    out = torch.empty(3, 8, 8, 4, device=dev, dtype=torch.bfloat16)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    flip = torch.tensor([0, 1, 0], device=dev, dtype=torch.uint8)
+    k.normalize_u8(img, out, mean, std, flip)
+    ref = (img.float() / 255 - torch.tensor(mean, device=dev)) / torch.tensor(std, device=dev)
+    ref[1] = ref[1].flip(1)
+    assert relerr(out[..., :3], ref) < 1e-2
+    assert out[..., 3].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("shape", [(16, 56, 56, 64, 64, 1, 1, 0), (8, 28, 28, 128, 128, 3, 1, 1),
+                                   (8, 28, 28, 256, 512, 1, 2, 0)])
+def test_conv_wgrad_split(shape):
+    """Large pixel counts -> many split-K slabs and the 2-level reduction."""
+    k = K()
+    N, H, W, IC, OC, R, st, pad = shape
+    torch.manual_seed(8)
+    x = torch.randn(N, H, W, IC, device=dev).bfloat16()
+    OH, OW = k.conv_out_hw(H, W, R, R, st, pad)
+    dy = torch.randn(N, OH, OW, OC, device=dev).bfloat16()
+    dw = torch.empty(OC, R * R * IC, device=dev)
+    ws = torch.empty(64 * 1024 * 1024, device=dev)
+    nsplit, _ = k.wgrad_splits(N * OH * OW, OC, R * R * IC, 64, 64, ws.numel())
+    assert nsplit > 1
+    k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad)
+    ref = torch.nn.grad.conv2d_weight(nchw(x.float()), (OC, IC, R, R), nchw(dy.float()), stride=st, padding=pad)
+    assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_stem_wgrad_split():
+    k = K()
+    N, H, W = 8, 64, 64
+    torch.manual_seed(9)
+    x4 = torch.zeros(N, H, W, 4, device=dev)
+    x4[..., :3] = torch.randn(N, H, W, 3, device=dev)
+    x4 = x4.bfloat16()
+    dy = torch.randn(N, 32, 32, 64, device=dev).bfloat16()
+    dw = torch.empty(64, 256, device=dev)
+    wsp = torch.empty(16 * 1024 * 1024, device=dev)
+    k.conv_wgrad(dy, x4, dw, wsp, R=7, S=7, stride=2, pad=3, stem=True)
+    refw = torch.nn.grad.conv2d_weight(nchw(x4[..., :3].float()), (64, 3, 7, 7), nchw(dy.float()), stride=2, padding=3)
+    assert relerr(dw.view(64, 8, 8, 4)[:, :7, :7, :3], refw.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_conv_dgrad_stride2_tiles():
+    """Parity-decomposed stride-2 dgrad on every tile config."""
+    k = K()
+    N, H, W, IC, OC, R, st, pad = 4, 14, 14, 128, 256, 3, 2, 1
+    w = (torch.randn(OC, R, R, IC, device=dev) / math.sqrt(IC * R * R)).bfloat16()
+    dy = torch.randn(N, 7, 7, OC, device=dev).bfloat16()
+    wt = w.permute(3, 1, 2, 0).contiguous().view(IC, -1)
+    ref = nhwc(torch.nn.grad.conv2d_input((N, IC, H, W), w.float().permute(0, 3, 1, 2), nchw(dy.float()),
+                                          stride=st, padding=pad))
+    for tile in [(128, 128), (128, 64), (64, 64)]:
+        dx = torch.full((N, H, W, IC), 7.0, device=dev, dtype=torch.bfloat16)
+        k.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad, tile=tile)
+        assert relerr(dx, ref) < 1e-2, tile

@@ -1,0 +1,100 @@
+"""The native ResNet program on CPU (reference ops): same schedule / buffers / bucketing as the
+GPU path, checked against fp32 autograd and for state-dict compatibility."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+from dbx_distributed_pytorch_examples_amd.engine.program import ResNetProgram, supports
+from dbx_distributed_pytorch_examples_amd.models import build_model
+
+CPU = torch.device("cpu")
+
+
+def _damp(model, arch):
+    for n, m in model.named_modules():
+        if n.endswith("bn3") or (n.endswith("bn2") and "layer" in n and arch != "resnet50"):
+            torch.nn.init.constant_(m.weight, 0.2)
+
+
+def _cos(a, b):
+    a, b = a.float().flatten(), b.float().flatten()
+    return (a @ b / (a.norm() * b.norm() + 1e-20)).item()
+
+
+@pytest.mark.parametrize("arch,size,batch", [("resnet18", 32, 8), ("cifar_resnet18", 32, 4), ("resnet50", 64, 8)])
+def test_program_grads_match_autograd(arch, size, batch):
+    torch.manual_seed(0)
+    model = build_model(arch, num_classes=10)
+    _damp(model, arch)
+    ref = copy.deepcopy(model).train()
+    tr = NativeTrainer(model, batch, (size, size), CPU, optim=OptimConfig(lr=0.0, momentum=0.0, weight_decay=0.0),
+                       use_graphs=False)
+    p = tr.prog
+    g = torch.Generator().manual_seed(1)
+    img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g)
+    lab = torch.randint(0, 10, (batch,), generator=g)
+    tr.step(img, lab)
+    x = p.x4[..., :3].float().permute(0, 3, 1, 2).contiguous()
+    loss = F.cross_entropy(ref(x), lab)
+    loss.backward()
+    assert abs(p.metrics[0].item() / batch - loss.item()) < 2e-2 * loss.item()
+    nr = dict(ref.named_parameters())
+    for name, prm in model.named_parameters():
+        off = (prm.data_ptr() - p.master.data_ptr()) // 4
+        gf = p.grad[off:off + prm.numel()]
+        gn = gf.view(prm.shape[0], prm.shape[2], prm.shape[3], prm.shape[1]).permute(0, 3, 1, 2) \
+            if prm.dim() == 4 else gf.view(prm.shape)
+        assert _cos(gn, nr[name].grad) > (0.9 if prm.dim() > 1 else 0.75), name
+        assert 0.7 < gn.norm() / (nr[name].grad.norm() + 1e-12) < 1.4, name
+
+
+def test_params_are_views_and_state_dict_roundtrip():
+    torch.manual_seed(0)
+    model = build_model("resnet18", num_classes=10)
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    prog = ResNetProgram(model, 2, (32, 32), CPU)
+    sd1 = model.state_dict()
+    assert set(sd0) == set(sd1)
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k].contiguous()), k
+    # writing master is visible through the module (views), and load_state_dict writes master
+    prog.master.add_(1.0)
+    assert torch.allclose(model.conv1.weight.detach(), sd0["conv1.weight"] + 1.0)
+    model.load_state_dict(sd0)
+    assert torch.allclose(prog.master[prog.stem.off:prog.stem.off + 4],
+                          sd0["conv1.weight"].permute(0, 2, 3, 1).reshape(-1)[:4])
+
+
+def test_supports():
+    assert supports(build_model("resnet50"))
+    assert supports(build_model("resnet18_1ch"))
+    assert not supports(build_model("mnist_net"))
+
+
+def test_native_training_reduces_loss_cpu():
+    torch.manual_seed(0)
+    model = build_model("resnet18", num_classes=4)
+    tr = NativeTrainer(model, 8, (32, 32), CPU, optim=OptimConfig(lr=0.05, momentum=0.9), use_graphs=False)
+    g = torch.Generator().manual_seed(3)
+    img = torch.randint(0, 256, (8, 32, 32, 3), dtype=torch.uint8, generator=g)
+    lab = torch.randint(0, 4, (8,), generator=g)
+    losses = []
+    for _ in range(8):
+        tr.step(img, lab)
+        losses.append(tr.read_metrics()[0] / 8)
+    assert losses[-1] < losses[0] * 0.7, losses
+
+
+def test_segment_ranges_cover_all_params():
+    model = build_model("resnet50", num_classes=10)
+    tr = NativeTrainer(model, 2, (64, 64), CPU, use_graphs=False)
+    covered = torch.zeros(tr.prog.n_params, dtype=torch.bool)
+    for rg in tr.seg_ranges:
+        lo, hi = rg
+        assert not covered[lo:hi].any(), "segment ranges overlap"
+        covered[lo:hi] = True
+    for name, off, n in tr.prog.param_ranges:
+        assert covered[off:off + n].all(), name

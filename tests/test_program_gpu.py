@@ -1,0 +1,98 @@
+"""End-to-end numerics of the native ResNet program vs a PyTorch fp32 autograd reference.
+
+The native path runs bf16 activations / fp32 accumulation, so per-tensor gradients are compared
+by cosine similarity and relative norm error against fp32 autograd on the same (bf16-rounded)
+input, same weights, same labels.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda")
+
+
+def _cos(a, b):
+    a = a.float().flatten()
+    b = b.float().flatten()
+    return (a @ b / (a.norm() * b.norm() + 1e-20)).item()
+
+
+@pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 8), ("resnet18", 32, 16), ("cifar_resnet18", 32, 8)])
+def test_program_matches_autograd(arch, size, batch):
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+
+    torch.manual_seed(0)
+    model = build_model(arch, num_classes=10 if "cifar" in arch else 100)
+    # Damp the residual branches (last BN gamma = 0.2): a random-init ResNet-50 at kaiming init
+    # is in the gradient-explosion regime where bf16-vs-fp32 rounding alone decorrelates the
+    # backward (cos ~0.2 even with the CPU reference ops); damped, it is well conditioned.
+    for n_, m_ in model.named_modules():
+        if n_.endswith("bn3") or (n_.endswith("bn2") and "layer" in n_ and arch != "resnet50"):
+            torch.nn.init.constant_(m_.weight, 0.2)
+    ref = copy.deepcopy(model).to(dev).train()
+    tr = NativeTrainer(model, batch, (size, size), dev, optim=OptimConfig(lr=0.0, momentum=0.0, weight_decay=0.0),
+                       use_graphs=False)
+    p = tr.prog
+    g = torch.Generator().manual_seed(1)
+    img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).to(dev)
+    lab = torch.randint(0, p.num_classes, (batch,), generator=g).to(dev)
+    tr.step(img, lab)
+    torch.cuda.synchronize()
+    loss_native = p.metrics[0].item() / batch
+    x = p.x4[..., :3].float().permute(0, 3, 1, 2).contiguous()
+    out = ref(x)
+    loss = F.cross_entropy(out, lab)
+    loss.backward()
+    assert abs(loss_native - loss.item()) / loss.item() < 3e-2, (loss_native, loss.item())
+    # gradients (lr = 0: master params unchanged, grads left in the flat buffer)
+    named_ref = dict(ref.named_parameters())
+    worst = 1.0
+    for name, prm in model.named_parameters():
+        rg = named_ref[name].grad
+        off_ranges = [r for r in p.param_ranges]
+        # locate the flat-grad view of this parameter through its storage offset in master
+        off = (prm.data_ptr() - p.master.data_ptr()) // 4
+        n = prm.numel()
+        gflat = p.grad[off:off + n]
+        if prm.dim() == 4:
+            gn = gflat.view(prm.shape[0], prm.shape[2], prm.shape[3], prm.shape[1]).permute(0, 3, 1, 2)
+        else:
+            gn = gflat.view(prm.shape)
+        c = _cos(gn, rg)
+        worst = min(worst, c)
+        assert c > (0.9 if prm.dim() > 1 else 0.75), (name, c)
+    # BN running stats updated like torch
+    for (n1, b1), (n2, b2) in zip(model.named_buffers(), ref.named_buffers()):
+        if "running_mean" in n1:
+            assert _cos(b1, b2) > 0.99 or b2.abs().max() < 1e-3, n1
+
+
+def test_program_trains_and_graph_replay():
+    """Loss decreases on a fixed batch; graph replay == eager numerics."""
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+
+    torch.manual_seed(0)
+    size, batch = 32, 32
+    m1 = build_model("resnet18", num_classes=10)
+    m2 = copy.deepcopy(m1)
+    t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05), use_graphs=True)
+    t2 = NativeTrainer(m2, batch, (size, size), dev, optim=OptimConfig(lr=0.05), use_graphs=False)
+    g = torch.Generator().manual_seed(2)
+    img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).to(dev)
+    lab = torch.randint(0, 10, (batch,), generator=g).to(dev)
+    losses = []
+    for i in range(12):
+        t1.step(img, lab)
+        t2.step(img, lab)
+        l1, _ = t1.read_metrics()
+        l2, _ = t2.read_metrics()
+        losses.append(l1 / batch)
+        # BN statistics use fp32 atomics (order-nondeterministic): compare to a tolerance
+        assert abs(l1 - l2) <= 2e-2 * max(1.0, abs(l2)), (i, l1, l2)
+    assert losses[-1] < 0.5 * losses[0], losses
+    assert _cos(t1.prog.master, t2.prog.master) > 0.9999
