@@ -1,0 +1,282 @@
+"""Typed configuration: one dataclass tree, loadable from YAML/JSON/dicts with ``a.b=c`` overrides.
+
+Replaces the reference's scattered configuration:
+
+* ``local_config.yaml`` keys (`/root/reference/UPDATE_local_config.yaml:1-7`, read by
+  `setup/00_setup.py:7-23`): ``catalog, schema, num_nodes, secret_scope, secret_key,
+  cifar_cache, tiny_imagenet_cache, imagenet1k_cache, coco_cache`` -> :class:`LocalConfig`
+  (Unity-Catalog volumes become local directories under ``volume_root``);
+* per-file hyper-parameter constants (§2.3) -> :class:`TrainConfig`;
+* DeepSpeed JSON dicts (`02_deepspeed/deepspeed_config.py`) -> :func:`from_deepspeed`;
+* Composer duration strings ``"2ep"`` / ``"100ba"`` (`03_composer/01_cifar_composer_resnet.ipynb:287`)
+  -> :func:`parse_duration`.
+"""
+from __future__ import annotations
+
+import copy
+import dataclasses
+import json
+import os
+import re
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
+
+import yaml
+
+
+@dataclass
+class LocalConfig:
+    """The reference's local_config.yaml (template `UPDATE_local_config.yaml:1-7` + `coco_cache`)."""
+    catalog: str = ""
+    schema: str = ""
+    num_nodes: int = 1
+    secret_scope: str = ""
+    secret_key: str = ""
+    cifar_cache: str = "cifar"
+    tiny_imagenet_cache: str = "tiny_imagenet"
+    imagenet1k_cache: str = "imagenet_1k"
+    coco_cache: str = "ms_coco"
+    volume_root: str = os.environ.get("DBX_VOLUME_ROOT", os.path.expanduser("~/.dbx_amd/volumes"))
+
+    def volume(self, name: str) -> str:
+        """Map a UC volume path (``/Volumes/<cat>/<schema>/<vol>``) or bare name to a local dir."""
+        v = getattr(self, name, name)
+        if v.startswith("/Volumes/"):
+            v = v[len("/Volumes/"):]
+        path = v if os.path.isabs(v) else os.path.join(self.volume_root, self.catalog or "main",
+                                                        self.schema or "default", v)
+        return path
+
+
+@dataclass
+class OptimizerConfig:
+    name: str = "sgd"                  # sgd | adam | adamw
+    lr: float = 0.1
+    momentum: float = 0.9
+    nesterov: bool = False
+    weight_decay: float = 5e-5
+    betas: Tuple[float, float] = (0.9, 0.999)
+    eps: float = 1e-8
+    grad_clip: float = 0.0
+
+
+@dataclass
+class SchedulerConfig:
+    name: str = "none"                 # none | cosine | warmup_linear | warmup_cosine | step | warmup_lr
+    warmup_steps: int = 0
+    warmup_min_lr: float = 0.0
+    total_steps: int = 0
+    t_max_epochs: int = 0              # CosineAnnealingLR(T_max=epochs), per-epoch stepping
+    step_size: int = 30
+    gamma: float = 0.1
+
+
+@dataclass
+class ZeroConfig:
+    stage: int = 0                     # 0 = plain DDP, 1 = sharded optimizer state, 2 = + sharded grads
+    reduce_bucket_size: int = 500_000_000
+    allgather_bucket_size: int = 500_000_000
+    overlap_comm: bool = True
+    contiguous_gradients: bool = True
+    reduce_scatter: bool = True
+    offload_optimizer: bool = False    # accepted for config parity; documented non-goal (288 GB HBM)
+    offload_param: bool = False
+
+
+@dataclass
+class DataConfig:
+    dataset: str = "synthetic"         # synthetic | cifar10 | mnist | fashion_mnist | tiny_imagenet | imagenet | mds | folder | hf
+    root: str = ""
+    image_size: int = 224
+    num_classes: int = 1000
+    train_samples: int = 0             # synthetic: samples per epoch (0 = 50 batches)
+    augment: bool = True
+    num_workers: int = 4
+    mds_remote: str = ""
+    mds_local: str = ""
+    shuffle: bool = True
+    label_smoothing: float = 0.0
+    cutmix_alpha: float = 0.0
+
+
+@dataclass
+class TrainConfig:
+    model: str = "resnet50"
+    num_classes: int = 1000
+    batch_size: int = 256              # per GPU (micro batch)
+    grad_accum: int = 1
+    epochs: int = 1
+    max_steps: int = 0                 # 0 = full epochs
+    duration: str = ""                 # composer style: "2ep" / "100ba"
+    seed: int = 42
+    precision: str = "bf16"
+    engine: str = "auto"               # auto | native | autograd
+    graphs: bool = True
+    bucket_cap_mb: float = 64.0
+    allreduce_dtype: str = "fp32"
+    log_every: int = 100
+    eval_every: int = 1
+    patience: int = 0                  # early stopping (02_tiny_imagenet_deepspeed_resnet.py:289-297)
+    checkpoint_dir: str = ""
+    checkpoint_every: int = 1
+    resume: str = ""                   # path or "latest"
+    experiment: str = "dbx_amd"
+    run_name: str = ""
+    optim: OptimizerConfig = field(default_factory=OptimizerConfig)
+    sched: SchedulerConfig = field(default_factory=SchedulerConfig)
+    zero: ZeroConfig = field(default_factory=ZeroConfig)
+    data: DataConfig = field(default_factory=DataConfig)
+    local: LocalConfig = field(default_factory=LocalConfig)
+
+
+# ----------------------------------------------------------------------------------------
+def _coerce(cur: Any, val: Any) -> Any:
+    if isinstance(cur, bool):
+        if isinstance(val, str):
+            return val.lower() in ("1", "true", "yes", "on")
+        return bool(val)
+    if isinstance(cur, int) and not isinstance(cur, bool):
+        return int(float(val)) if isinstance(val, str) else int(val)
+    if isinstance(cur, float):
+        return float(val)
+    if isinstance(cur, tuple):
+        if isinstance(val, str):
+            val = [float(x) for x in val.strip("()[]").split(",")]
+        return tuple(type(c)(v) for c, v in zip(cur, val))
+    return val
+
+
+def update_dataclass(obj: Any, d: Dict[str, Any], strict: bool = True) -> Any:
+    for k, v in d.items():
+        if not hasattr(obj, k):
+            if strict:
+                raise KeyError(f"unknown config key {k!r} for {type(obj).__name__}")
+            continue
+        cur = getattr(obj, k)
+        if dataclasses.is_dataclass(cur) and isinstance(v, dict):
+            update_dataclass(cur, v, strict)
+        else:
+            setattr(obj, k, _coerce(cur, v) if cur is not None else v)
+    return obj
+
+
+def apply_overrides(cfg: Any, overrides: Sequence[str]) -> Any:
+    """CLI overrides ``a.b=c`` (values parsed as YAML scalars)."""
+    for ov in overrides:
+        if "=" not in ov:
+            raise ValueError(f"override {ov!r} is not key=value")
+        key, val = ov.split("=", 1)
+        parts = key.split(".")
+        obj = cfg
+        for p in parts[:-1]:
+            obj = getattr(obj, p)
+        if not hasattr(obj, parts[-1]):
+            raise KeyError(f"unknown config key {key!r}")
+        cur = getattr(obj, parts[-1])
+        parsed = yaml.safe_load(val)
+        setattr(obj, parts[-1], _coerce(cur, parsed) if cur is not None else parsed)
+    return cfg
+
+
+def load_config(path: Optional[str] = None, overrides: Sequence[str] = (), base: Optional[TrainConfig] = None
+                ) -> TrainConfig:
+    cfg = copy.deepcopy(base) if base is not None else TrainConfig()
+    if path:
+        with open(path) as f:
+            d = json.load(f) if path.endswith(".json") else yaml.safe_load(f)
+        d = d or {}
+        if "train_micro_batch_size_per_gpu" in d or "zero_optimization" in d:
+            cfg = from_deepspeed(d, cfg)
+        elif set(d) & set(f.name for f in dataclasses.fields(LocalConfig)) and not set(d) & {"model", "optim"}:
+            update_dataclass(cfg.local, d, strict=False)
+        else:
+            update_dataclass(cfg, d)
+    return apply_overrides(cfg, overrides)
+
+
+def load_local_config(path: str = "../local_config.yaml") -> LocalConfig:
+    """``setup/00_setup.py:9-23`` equivalent; missing file -> defaults."""
+    lc = LocalConfig()
+    if os.path.exists(path):
+        with open(path) as f:
+            update_dataclass(lc, yaml.safe_load(f) or {}, strict=False)
+    return lc
+
+
+def to_dict(cfg: Any) -> Dict[str, Any]:
+    return dataclasses.asdict(cfg)
+
+
+# ----------------------------------------------------------------------------------------
+_DUR = re.compile(r"^\s*(\d+(?:\.\d+)?)\s*(ep|ba|sp)\s*$")
+
+
+def parse_duration(s: Union[str, int], steps_per_epoch: int, batch_size: int = 1) -> int:
+    """Composer duration -> number of optimizer steps: ``"2ep"``, ``"100ba"``, ``"5000sp"`` (samples)."""
+    if isinstance(s, int):
+        return s * steps_per_epoch
+    m = _DUR.match(s)
+    if not m:
+        raise ValueError(f"bad duration {s!r} (expected e.g. '2ep', '100ba', '5000sp')")
+    v, unit = float(m.group(1)), m.group(2)
+    if unit == "ep":
+        return int(round(v * steps_per_epoch))
+    if unit == "ba":
+        return int(v)
+    return int(v) // max(1, batch_size)
+
+
+def from_deepspeed(ds: Dict[str, Any], base: Optional[TrainConfig] = None) -> TrainConfig:
+    """Map the DeepSpeed config schema subset used by `02_deepspeed/deepspeed_config.py:5-105`."""
+    cfg = copy.deepcopy(base) if base is not None else TrainConfig()
+    if "train_micro_batch_size_per_gpu" in ds:
+        cfg.batch_size = int(ds["train_micro_batch_size_per_gpu"])
+    if "gradient_accumulation_steps" in ds:
+        cfg.grad_accum = int(ds["gradient_accumulation_steps"])
+    if "gradient_clipping" in ds:
+        cfg.optim.grad_clip = float(ds["gradient_clipping"])
+    if ds.get("bf16", {}).get("enabled"):
+        cfg.precision = "bf16"
+    elif ds.get("fp16", {}).get("enabled"):
+        cfg.precision = "bf16"  # MI355X path computes in bf16; fp16 loss-scaling not needed
+    opt = ds.get("optimizer")
+    if opt:
+        t = opt.get("type", "AdamW").lower()
+        cfg.optim.name = {"adamw": "adamw", "adam": "adam", "sgd": "sgd"}.get(t, "adamw")
+        p = opt.get("params", {})
+        if "lr" in p:
+            cfg.optim.lr = float(p["lr"])
+        if "betas" in p:
+            cfg.optim.betas = tuple(float(b) for b in p["betas"])
+        if "eps" in p:
+            cfg.optim.eps = float(p["eps"])
+        if "weight_decay" in p:
+            cfg.optim.weight_decay = float(p["weight_decay"])
+        if "momentum" in p:
+            cfg.optim.momentum = float(p["momentum"])
+    sch = ds.get("scheduler")
+    if sch:
+        t = sch.get("type", "")
+        p = sch.get("params", {})
+        if t == "WarmupLR":
+            cfg.sched.name = "warmup_lr"
+            cfg.sched.warmup_steps = int(p.get("warmup_num_steps", 0))
+            cfg.sched.warmup_min_lr = float(p.get("warmup_min_lr", 0.0))
+            if "warmup_max_lr" in p:
+                cfg.optim.lr = float(p["warmup_max_lr"])
+        elif t in ("WarmupDecayLR", "WarmupCosineLR"):
+            cfg.sched.name = "warmup_linear" if t == "WarmupDecayLR" else "warmup_cosine"
+            cfg.sched.warmup_steps = int(p.get("warmup_num_steps", 0))
+            cfg.sched.total_steps = int(p.get("total_num_steps", 0))
+    z = ds.get("zero_optimization")
+    if z:
+        cfg.zero.stage = int(z.get("stage", 0))
+        for k in ("reduce_bucket_size", "allgather_bucket_size"):
+            if k in z:
+                setattr(cfg.zero, k, int(float(z[k])))
+        for k in ("overlap_comm", "contiguous_gradients", "reduce_scatter"):
+            if k in z:
+                setattr(cfg.zero, k, bool(z[k]))
+        cfg.zero.offload_optimizer = bool(z.get("offload_optimizer", {}).get("device", "none") not in ("none", None))
+        cfg.zero.offload_param = bool(z.get("offload_param", {}).get("device", "none") not in ("none", None))
+    return cfg

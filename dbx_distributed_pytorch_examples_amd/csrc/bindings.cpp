@@ -43,6 +43,8 @@ int dbx_clip_factor(const float*, float, float*, hipStream_t);
 int dbx_normalize_u8(const unsigned char*, bf16*, const unsigned char*, int, int, int, int, float, float, float, float,
                      float, float, hipStream_t);
 int dbx_weight_prep(const float*, bf16*, const void*, int, hipStream_t);
+int dbx_augment_u8(const unsigned char*, bf16*, const float*, const unsigned char*, int, int, int, int, int, int, float,
+                   float, float, float, float, float, hipStream_t);
 int dbx_cast_f32_bf16(const float*, bf16*, long long, hipStream_t);
 int dbx_cast_bf16_f32(const bf16*, float*, long long, float, int, hipStream_t);
 }
@@ -58,7 +60,10 @@ static void check(int rc, const char* what) {
   }
 }
 
+void register_runtime(py::module& m);  // csrc/runtime/mds_loader.cpp
+
 PYBIND11_MODULE(_C, m) {
+  register_runtime(m);
   m.doc() = "dbx_distributed_pytorch_examples_amd native HIP kernels (gfx950)";
   m.def("conv_igemm", [](int mode, int bm, int bn, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t in_scale,
                          uintptr_t in_shift, int relu_in, uintptr_t stats, int nshard, int N, int IH, int IW, int IC,
@@ -174,6 +179,12 @@ PYBIND11_MODULE(_C, m) {
     check(dbx_normalize_u8(P<const unsigned char*>(in), P<bf16*>(out), P<const unsigned char*>(flip), N, H, W, Cin, m0,
                            m1, m2, s0, s1, s2, S(st)),
           "normalize_u8");
+  });
+  m.def("augment_u8", [](uintptr_t in, uintptr_t out, uintptr_t boxes, uintptr_t flip, int N, int Hin, int Win, int Cin,
+                         int Ho, int Wo, float m0, float m1, float m2, float s0, float s1, float s2, uintptr_t st) {
+    check(dbx_augment_u8(P<const unsigned char*>(in), P<bf16*>(out), P<const float*>(boxes),
+                         P<const unsigned char*>(flip), N, Hin, Win, Cin, Ho, Wo, m0, m1, m2, s0, s1, s2, S(st)),
+          "augment_u8");
   });
   m.def("weight_prep", [](uintptr_t master, uintptr_t wbuf, uintptr_t desc, int nlayers, uintptr_t st) {
     check(dbx_weight_prep(P<const float*>(master), P<bf16*>(wbuf), P<const void*>(desc), nlayers, S(st)),

@@ -20,19 +20,38 @@ namespace dbx {
 // ----------------------------------------------------------------------------------------
 // BN finalize: stats[nshard][2][C] -> scale/shift (+ saved mean/invstd, running stats)
 // ----------------------------------------------------------------------------------------
+// One block per 8 channels: thread (k, j) loads shard k of channel c0+j, LDS tree over the shards
+// (the 32 shard loads are issued in parallel instead of as a dependent chain).
+__device__ __forceinline__ void shard_sums(const float* stats, int nshard, int C, int c0, float& s_out, float& q_out,
+                                           bool& active, int& c) {
+  __shared__ float rs[8][33], rq[8][33];
+  const int j = threadIdx.x & 7, k = threadIdx.x >> 3;  // k in 0..31
+  c = c0 + j;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    for (int kk = k; kk < nshard; kk += 32) { s += stats[(size_t)kk * 2 * C + c]; q += stats[(size_t)kk * 2 * C + C + c]; }
+  }
+  rs[j][k] = s; rq[j][k] = q;
+  __syncthreads();
+  active = (k == 0) && (c < C);
+  if (active) {
+    float ss = 0.f, qq = 0.f;
+    for (int t = 0; t < 32; ++t) { ss += rs[j][t]; qq += rq[j][t]; }
+    s_out = ss; q_out = qq;
+  }
+}
+
 __global__ void bn_finalize_kernel(const float* __restrict__ stats, int nshard, int C, float count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float eps, float momentum, float* running_mean, float* running_var,
                                    float* scale, float* shift, float* save_mean, float* save_invstd) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int k = 0; k < nshard; ++k) {
-    s += stats[(size_t)k * 2 * C + c];
-    q += stats[(size_t)k * 2 * C + C + c];
-  }
-  const double mean = s / count;
-  double var = q / count - mean * mean;
+  float s = 0.f, q = 0.f;
+  bool active;
+  int c;
+  shard_sums(stats, nshard, C, blockIdx.x * 8, s, q, active, c);
+  if (!active) return;
+  const double mean = (double)s / count;
+  double var = (double)q / count - mean * mean;
   if (var < 0.0) var = 0.0;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
@@ -204,10 +223,11 @@ __global__ void bn_bwd_coeff_kernel(const float* __restrict__ stats, int nshard,
                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, float* coeff /*[3][C]*/,
                                     float* dgamma, float* dbeta, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
   float s = 0.f, q = 0.f;
-  for (int k = 0; k < nshard; ++k) { s += stats[(size_t)k * 2 * C + c]; q += stats[(size_t)k * 2 * C + C + c]; }
+  bool active;
+  int c;
+  shard_sums(stats, nshard, C, blockIdx.x * 8, s, q, active, c);
+  if (!active) return;
   const float g = gamma ? gamma[c] : 1.f, is = invstd[c], mu = mean[c];
   const float sg = s / count, sgx = q / count;
   const float k1 = g * is;
@@ -246,40 +266,46 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
 // ----------------------------------------------------------------------------------------
 // MaxPool 3x3 s2 p1 (NHWC) with BN-apply + ReLU prologue; argmax (0..8) saved as uint8.
 // ----------------------------------------------------------------------------------------
-__global__ void maxpool_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ sc,
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ sc,
                                    const float* __restrict__ sh, bf16* __restrict__ out,
                                    unsigned char* __restrict__ arg, int N, int H, int W, int C, int P,
                                    int Q, int K, int stride, int pad, int relu) {
-  const int cpt = C / 8;
-  const long long total = (long long)N * P * Q * cpt;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % cpt);
-    long long pix = i / cpt;
-    const int q = (int)(pix % Q); pix /= Q;
-    const int p = (int)(pix % P);
-    const int n = (int)(pix / P);
-    const int c0 = cg * 8;
+  const RowMap rm(C);
+  if (rm.r0 >= rm.rpb) return;
+  const int c0 = rm.cg * 8;
+  float s[8], h[8];
+  if (sc) { load8f(sc + c0, s); load8f(sh + c0, h); }
+  else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[j] = 1.f; h[j] = 0.f; }
+  }
+  const long long M = (long long)N * P * Q;
+  for (long long pix = (long long)blockIdx.x * rm.rpb + rm.r0; pix < M; pix += (long long)gridDim.x * rm.rpb) {
+    const int q = (int)(pix % Q);
+    const long long t = pix / Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
     float best[8];
     unsigned char bi[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
     for (int r = 0; r < K; ++r) {
-      const int h = p * stride - pad + r;
-      if (h < 0 || h >= H) continue;
-      for (int s = 0; s < K; ++s) {
-        const int w = q * stride - pad + s;
+      const int hh = p * stride - pad + r;
+      if (hh < 0 || hh >= H) continue;
+      for (int ss = 0; ss < K; ++ss) {
+        const int w = q * stride - pad + ss;
         if (w < 0 || w >= W) continue;
         float f[8];
-        unpack8(*reinterpret_cast<const u32x4*>(x + (((size_t)n * H + h) * W + w) * C + c0), f);
+        unpack8(*reinterpret_cast<const u32x4*>(x + (((size_t)n * H + hh) * W + w) * C + c0), f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float v = sc ? f[j] * sc[c0 + j] + sh[c0 + j] : f[j];
+          float v = f[j] * s[j] + h[j];
           if (relu) v = fmaxf(v, 0.f);
-          if (v > best[j]) { best[j] = v; bi[j] = (unsigned char)(r * K + s); }
+          if (v > best[j]) { best[j] = v; bi[j] = (unsigned char)(r * K + ss); }
         }
       }
     }
-    const size_t o = (((size_t)n * P + p) * Q + q) * C + c0;
+    const size_t o = (size_t)pix * C + c0;
     *reinterpret_cast<u32x4*>(out + o) = pack8(best);
     *reinterpret_cast<uint2*>(arg + o) = *reinterpret_cast<uint2*>(bi);
   }
@@ -539,6 +565,47 @@ __global__ void normalize_u8_kernel(const unsigned char* __restrict__ in, bf16* 
 }
 
 // ----------------------------------------------------------------------------------------
+// GPU input augmentation: uint8 NHWC [N][Hin][Win][Cin] -> bf16 NHWC4
+// [N][Ho][Wo][4]: per-sample crop box (y0, x0, h, w in source pixels, float) resized to Ho x Wo
+// with bilinear sampling (pixel-centre convention, edge clamp), optional horizontal flip,
+// (x/255 - mean)/std, channel 3 = 0. Covers RandomResizedCrop / RandomCrop(pad) / Resize /
+// CenterCrop + RandomHorizontalFlip + Normalize of the reference's CPU transform chains.
+// ----------------------------------------------------------------------------------------
+__global__ void augment_u8_kernel(const unsigned char* __restrict__ in, bf16* __restrict__ out,
+                                  const float* __restrict__ boxes, const unsigned char* __restrict__ flip,
+                                  int N, int Hin, int Win, int Cin, int Ho, int Wo, float m0, float m1, float m2,
+                                  float s0, float s1, float s2) {
+  const long long total = (long long)N * Ho * Wo;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int ox = (int)(i % Wo);
+    const long long t = i / Wo;
+    const int oy = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const float by = boxes[4 * n], bx = boxes[4 * n + 1], bh = boxes[4 * n + 2], bw = boxes[4 * n + 3];
+    const int oxx = (flip && flip[n]) ? (Wo - 1 - ox) : ox;
+    // source coordinate of the output pixel centre
+    float sy = by + (oy + 0.5f) * bh / Ho - 0.5f;
+    float sx = bx + (oxx + 0.5f) * bw / Wo - 0.5f;
+    sy = fminf(fmaxf(sy, 0.f), (float)(Hin - 1));
+    sx = fminf(fmaxf(sx, 0.f), (float)(Win - 1));
+    const int y0 = (int)sy, x0 = (int)sx;
+    const int y1 = min(y0 + 1, Hin - 1), x1 = min(x0 + 1, Win - 1);
+    const float wy = sy - y0, wx = sx - x0;
+    const unsigned char* base = in + (size_t)n * Hin * Win * Cin;
+    float v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int cc = Cin == 1 ? 0 : c;
+      const float a = base[((size_t)y0 * Win + x0) * Cin + cc], b = base[((size_t)y0 * Win + x1) * Cin + cc];
+      const float d = base[((size_t)y1 * Win + x0) * Cin + cc], e = base[((size_t)y1 * Win + x1) * Cin + cc];
+      v[c] = ((a * (1.f - wx) + b * wx) * (1.f - wy) + (d * (1.f - wx) + e * wx) * wy) * (1.f / 255.f);
+    }
+    bf16x4 o = {(bf16)((v[0] - m0) / s0), (bf16)((v[1] - m1) / s1), (bf16)((v[2] - m2) / s2), (bf16)0.f};
+    *reinterpret_cast<bf16x4*>(out + i * 4) = o;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // Weight prep: fp32 KRSC master -> bf16 KRSC (fwd) and bf16 CRSK (dgrad) ; batched over layers
 // ----------------------------------------------------------------------------------------
 struct WDesc { long long src, fwd, tr; int K, RS, C, pad; };
@@ -587,7 +654,7 @@ static inline int grid_for(long long n, int block = 256, int cap = 8192) {
 extern "C" int dbx_bn_finalize(const float* stats, int nshard, int C, float count, const float* gamma,
                                const float* beta, float eps, float momentum, float* rm, float* rv,
                                float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, stats, nshard, C, count, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 7) / 8), dim3(256), 0, st, stats, nshard, C, count, gamma,
                      beta, eps, momentum, rm, rv, scale, shift, save_mean, save_invstd);
   RET_LAST;
 }
@@ -628,7 +695,7 @@ extern "C" int dbx_bn_bwd_reduce(const bf16* dout, const bf16* mref, const bf16*
 extern "C" int dbx_bn_bwd_coeff(const float* stats, int nshard, int C, float count, const float* gamma,
                                 const float* mean, const float* invstd, float* coeff, float* dgamma, float* dbeta,
                                 int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_coeff_kernel, dim3((C + 255) / 256), dim3(256), 0, st, stats, nshard, C, count, gamma,
+  hipLaunchKernelGGL(bn_bwd_coeff_kernel, dim3((C + 7) / 8), dim3(256), 0, st, stats, nshard, C, count, gamma,
                      mean, invstd, coeff, dgamma, dbeta, accumulate);
   RET_LAST;
 }
@@ -648,9 +715,9 @@ extern "C" int dbx_bn_bwd_apply(const bf16* dout, const bf16* mref, const bf16* 
 extern "C" int dbx_maxpool_fwd(const bf16* x, const float* sc, const float* sh, bf16* out, unsigned char* arg, int N,
                                int H, int W, int C, int P, int Q, int K, int stride, int pad, int relu, hipStream_t st) {
   if (C % 8) return -1;
-  const long long total = (long long)N * P * Q * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, x, sc, sh, out, arg, N, H, W, C, P, Q,
-                     K, stride, pad, relu);
+  if (C / 8 > 256) return -1;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * P * Q, 256 / (C / 8), 4096)), dim3(256), 0, st,
+                     x, sc, sh, out, arg, N, H, W, C, P, Q, K, stride, pad, relu);
   RET_LAST;
 }
 extern "C" int dbx_maxpool_bwd(const bf16* dout, const unsigned char* arg, bf16* dx, int N, int H, int W, int C, int P,
@@ -707,6 +774,13 @@ extern "C" int dbx_normalize_u8(const unsigned char* in, bf16* out, const unsign
                                 int Cin, float m0, float m1, float m2, float s0, float s1, float s2, hipStream_t st) {
   hipLaunchKernelGGL(normalize_u8_kernel, dim3(grid_for((long long)N * H * W)), dim3(256), 0, st, in, out, flip, N, H, W,
                      Cin, m0, m1, m2, s0, s1, s2);
+  RET_LAST;
+}
+extern "C" int dbx_augment_u8(const unsigned char* in, bf16* out, const float* boxes, const unsigned char* flip, int N,
+                              int Hin, int Win, int Cin, int Ho, int Wo, float m0, float m1, float m2, float s0, float s1,
+                              float s2, hipStream_t st) {
+  hipLaunchKernelGGL(augment_u8_kernel, dim3(grid_for((long long)N * Ho * Wo)), dim3(256), 0, st, in, out, boxes, flip, N,
+                     Hin, Win, Cin, Ho, Wo, m0, m1, m2, s0, s1, s2);
   RET_LAST;
 }
 extern "C" int dbx_weight_prep(const float* master, bf16* wbuf, const void* desc_dev, int nlayers, hipStream_t st) {

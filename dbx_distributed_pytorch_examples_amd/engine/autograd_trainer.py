@@ -1,0 +1,179 @@
+"""Generic training step for any ``nn.Module`` (models the native ResNet program does not cover:
+the MNIST ``Net``, frozen-backbone heads, Composer-style models, user modules) and for CPU hosts.
+
+Stock autograd + our flat-bucket DDP (``parallel.ddp``) + bf16 autocast on the GPU
+(channels_last memory format), torch optimizers (or the flat ZeRO optimizer). Loss: the model's
+own ``loss(outputs, batch)`` if it has one (Composer convention), NLL for log-probability outputs
+(the reference MNIST ``Net`` ends in ``log_softmax``, `01_basic_torch_distributor.py:91,99`), else
+cross-entropy with optional label smoothing; optional CutMix on the batch (Composer algorithm).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..parallel.ddp import DistributedDataParallel, unwrap
+
+
+def build_torch_optimizer(params, o):
+    if o.name == "sgd":
+        return torch.optim.SGD(params, lr=o.lr, momentum=o.momentum, nesterov=o.nesterov, weight_decay=o.weight_decay)
+    if o.name == "adam":
+        return torch.optim.Adam(params, lr=o.lr, betas=tuple(o.betas), eps=o.eps, weight_decay=o.weight_decay)
+    if o.name == "adamw":
+        return torch.optim.AdamW(params, lr=o.lr, betas=tuple(o.betas), eps=o.eps, weight_decay=o.weight_decay)
+    raise ValueError(f"unknown optimizer {o.name!r}")
+
+
+def cutmix(x: torch.Tensor, y: torch.Tensor, num_classes: int, alpha: float, gen: Optional[torch.Generator] = None):
+    """CutMix (Composer ``CutMix(alpha)``, `03_composer/01_cifar_composer_resnet.ipynb:430`): paste a
+    box from a permuted batch, mix one-hot targets by the pasted area."""
+    lam = torch.distributions.Beta(alpha, alpha).sample().item() if alpha > 0 else 1.0
+    B, _, H, W = x.shape
+    perm = torch.randperm(B, device=x.device)
+    rh, rw = int(H * math.sqrt(1 - lam)), int(W * math.sqrt(1 - lam))
+    cy, cx = torch.randint(0, H, (1,)).item(), torch.randint(0, W, (1,)).item()
+    y0, y1 = max(cy - rh // 2, 0), min(cy + rh // 2, H)
+    x0, x1 = max(cx - rw // 2, 0), min(cx + rw // 2, W)
+    x = x.clone()
+    x[:, :, y0:y1, x0:x1] = x[perm, :, y0:y1, x0:x1]
+    lam = 1 - (y1 - y0) * (x1 - x0) / (H * W)
+    t = F.one_hot(y, num_classes).float()
+    return x, lam * t + (1 - lam) * t[perm]
+
+
+def soft_cross_entropy(logits: torch.Tensor, target: torch.Tensor, smoothing: float = 0.0) -> torch.Tensor:
+    if smoothing:
+        target = target * (1 - smoothing) + smoothing / target.shape[1]
+    return -(target * F.log_softmax(logits.float(), 1)).sum(1).mean()
+
+
+class AutogradTrainer:
+    def __init__(self, model: nn.Module, device: torch.device, optim, label_smoothing: float = 0.0,
+                 bucket_cap_mb: float = 64.0, channels_last: bool = True, zero_stage: int = 0,
+                 cutmix_alpha: float = 0.0, grad_accum: int = 1, allreduce_dtype=torch.float32):
+        self.dev = device
+        self.model = model.to(device)
+        if device.type == "cuda" and channels_last:
+            self.model = self.model.to(memory_format=torch.channels_last)
+        self.ddp = DistributedDataParallel(self.model, bucket_cap_mb=bucket_cap_mb, allreduce_dtype=allreduce_dtype)
+        self.world = self.ddp.world
+        self.o = optim
+        self.smoothing = label_smoothing
+        self.cutmix_alpha = cutmix_alpha
+        self.grad_accum = max(1, grad_accum)
+        self.num_classes = getattr(unwrap(model), "num_classes", None)
+        self.zero = None
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        if zero_stage and params:
+            from ..parallel.zero import ZeroShardedOptimizer
+            # ZeRO over the DDP flat gradient buffer: master = flat copy of params in the same order
+            self._zero_master = torch.zeros_like(self.ddp.flat.buffer)
+            for p, off in zip(self.ddp._params, self.ddp.flat.offsets):
+                self._zero_master[off:off + p.numel()].copy_(p.detach().reshape(-1))
+            self.zero = ZeroShardedOptimizer(self._zero_master, self.ddp.flat.buffer, optim, stage=zero_stage,
+                                             grad_scale=1.0)  # DDP already averaged
+            self.opt = None
+        else:
+            self.opt = build_torch_optimizer(params, optim) if params else None
+        self.micro = 0
+        self.loss_sum = torch.zeros((), device=device)
+        self.correct = torch.zeros((), device=device)
+        self.count = 0
+
+    def set_lr(self, lr: float):
+        self.o.lr = lr
+        if self.opt is not None:
+            for g in self.opt.param_groups:
+                g["lr"] = lr
+
+    def _loss(self, out, x, y, target=None):
+        m = unwrap(self.model)
+        if hasattr(m, "loss") and callable(m.loss) and target is None:
+            return m.loss(out, (x, y), label_smoothing=self.smoothing) if "label_smoothing" in m.loss.__code__.co_varnames \
+                else m.loss(out, (x, y))
+        if target is not None:
+            return soft_cross_entropy(out, target, self.smoothing)
+        if getattr(m, "outputs_log_probs", False) or isinstance(m, _log_prob_types()):
+            return F.nll_loss(out.float(), y)
+        return F.cross_entropy(out.float(), y, label_smoothing=self.smoothing)
+
+    def step(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        self.model.train()
+        x = x.to(self.dev, non_blocking=True)
+        y = y.to(self.dev, non_blocking=True)
+        if self.dev.type == "cuda" and x.dim() == 4:
+            x = x.contiguous(memory_format=torch.channels_last)
+        target = None
+        if self.cutmix_alpha > 0 and self.num_classes:
+            x, target = cutmix(x, y, self.num_classes, self.cutmix_alpha)
+        last_micro = (self.micro + 1) % self.grad_accum == 0
+        ctx = self.ddp.no_sync() if not last_micro else _null()
+        with ctx:
+            with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.dev.type == "cuda"):
+                out = self.ddp(x) if not _is_composer(self.model) else self.ddp((x, y))
+            loss = self._loss(out, x, y, target) / self.grad_accum
+            loss.backward()
+        self.loss_sum += loss.detach().float() * self.grad_accum * y.shape[0]
+        self.correct += (out.detach().argmax(1) == y).sum()
+        self.count += y.shape[0]
+        self.micro += 1
+        if not last_micro:
+            return
+        self.ddp.finish_gradient_sync()
+        if self.o.grad_clip and self.zero is None:
+            torch.nn.utils.clip_grad_norm_([p for p in self.model.parameters() if p.grad is not None], self.o.grad_clip)
+        if self.zero is not None:
+            self.zero.step(grads_already_reduced=True)
+            with torch.no_grad():
+                for p, off in zip(self.ddp._params, self.ddp.flat.offsets):
+                    p.copy_(self._zero_master[off:off + p.numel()].view_as(p))
+        elif self.opt is not None:
+            self.opt.step()
+        self.ddp.zero_grad()
+
+    def read_metrics(self, reset: bool = True) -> Tuple[float, float]:
+        loss, corr = float(self.loss_sum.item()), float(self.correct.item())
+        if reset:
+            self.loss_sum.zero_()
+            self.correct.zero_()
+            self.count = 0
+        return loss, corr
+
+    @torch.no_grad()
+    def eval_batch(self, x, y) -> Tuple[float, int]:
+        self.model.eval()
+        x, y = x.to(self.dev), y.to(self.dev)
+        if self.dev.type == "cuda" and x.dim() == 4:
+            x = x.contiguous(memory_format=torch.channels_last)
+        with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.dev.type == "cuda"):
+            out = self.model((x, y)) if _is_composer(self.model) else self.model(x)
+        out = out.float()
+        m = unwrap(self.model)
+        if isinstance(m, _log_prob_types()):
+            loss = F.nll_loss(out, y, reduction="sum")
+        else:
+            loss = F.cross_entropy(out, y, reduction="sum")
+        return float(loss.item()), int((out.argmax(1) == y).sum().item())
+
+
+def _log_prob_types():
+    from ..models.mnist import Net
+    return (Net,)
+
+
+def _is_composer(model) -> bool:
+    from ..models.wrappers import ComposerResNet50
+    return isinstance(unwrap(model), ComposerResNet50)
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -45,11 +45,13 @@ class OptimConfig:
 
 class NativeTrainer:
     def __init__(self, model: nn.Module, batch: int, image_hw: Tuple[int, int], device: torch.device,
-                 optim: OptimConfig = OptimConfig(), label_smoothing: float = 0.0, use_graphs: bool = True,
+                 optim: Optional[OptimConfig] = None, label_smoothing: float = 0.0, use_graphs: bool = True,
                  bucket_cap_mb: float = 64.0, allreduce_dtype: torch.dtype = torch.float32,
-                 process_group=None):
+                 process_group=None, src_hw: Optional[Tuple[int, int]] = None, mean=None, std=None,
+                 zero_stage: int = 0):
         self.dev = device
-        self.prog = ResNetProgram(model, batch, image_hw, device)
+        optim = optim or OptimConfig()
+        self.prog = ResNetProgram(model, batch, image_hw, device, src_hw=src_hw, mean=mean, std=std)
         self.prog.build_backward()
         self.opt = optim
         self.smoothing = label_smoothing
@@ -68,6 +70,13 @@ class NativeTrainer:
         self.comm_stream = (torch.cuda.Stream(device=device, priority=-1)
                             if self.world > 1 and device.type == "cuda" else None)
         self.flip = None
+        self.zero = None
+        if zero_stage:
+            from ..parallel.zero import ZeroShardedOptimizer
+            self.zero = ZeroShardedOptimizer(self.prog.master, self.prog.grad, optim, stage=zero_stage,
+                                             process_group=process_group)
+            self.mom = self.zero.m  # shard-sized optimizer state only
+            self.mom2 = self.zero.v
         self._build_phases()
         # broadcast initial parameters from rank 0 (DDP constructor semantics, M2)
         if self.world > 1:
@@ -110,6 +119,11 @@ class NativeTrainer:
 
     def _optimizer_phase(self):
         p, o = self.prog, self.opt
+        if self.zero is not None:
+            # ZeRO-1/2: update this rank's shard of the flat master with its shard of the
+            # optimizer state, then all-gather the master (collective: runs eagerly, not captured)
+            self.zero.step(grads_already_reduced=(self.zero.stage == 1 or self.world == 1), lr=o.lr)
+            return
         gsp = None
         if o.grad_clip and o.grad_clip > 0:
             # clip on the averaged gradient: factor computed on device (no host sync)
@@ -127,6 +141,8 @@ class NativeTrainer:
 
     # ----------------------------------------------------------------------------------
     def _allreduce_range(self, lo: int, hi: int):
+        if self.zero is not None and self.zero.stage >= 2:
+            return  # ZeRO-2: gradients are reduce-scattered by the optimizer phase instead
         g = self.prog.grad
         pos = lo
         while pos < hi:
@@ -171,6 +187,10 @@ class NativeTrainer:
                 with torch.cuda.stream(self.comm_stream):
                     self._allreduce_range(*rg)
 
+    def _graph_phases(self):
+        # the ZeRO optimizer phase issues collectives: keep it out of the captured graphs
+        return [ph for ph in self.phases if not (ph[0] == "optimizer" and self.zero is not None and self.world > 1)]
+
     def _capture(self):
         """Capture each phase (or the whole step when world == 1) into HIP graphs."""
         torch.cuda.synchronize(self.dev)
@@ -186,7 +206,7 @@ class NativeTrainer:
                         fn()
                 self.graphs = [g]
             else:
-                for _, fn, _ in self.phases:
+                for _, fn, _ in self._graph_phases():
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=pool, stream=s):
                         fn()
@@ -199,7 +219,7 @@ class NativeTrainer:
         if self.world == 1:
             self.graphs[0].replay()
             return
-        for (name, _, rg), g in zip(self.phases, self.graphs):
+        for (name, _, rg), g in zip(self._graph_phases(), self.graphs):
             if name == "optimizer":
                 cur.wait_stream(self.comm_stream)
             g.replay()
@@ -207,18 +227,26 @@ class NativeTrainer:
                 self.comm_stream.wait_stream(cur)
                 with torch.cuda.stream(self.comm_stream):
                     self._allreduce_range(*rg)
+        if len(self.graphs) < len(self.phases):  # eager ZeRO optimizer phase
+            cur.wait_stream(self.comm_stream)
+            self._optimizer_phase()
 
     # ----------------------------------------------------------------------------------
     def step(self, images_u8: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
-             flip: Optional[torch.Tensor] = None):
-        """One training step. ``images_u8`` [N,H,W,C] uint8 and ``labels`` [N] int64 are copied
-        into the program's static input buffers (pass None to reuse what is already there)."""
+             boxes: Optional[torch.Tensor] = None, flips: Optional[torch.Tensor] = None):
+        """One training step. ``images_u8`` [N,Hs,Ws,C] uint8, ``labels`` [N] int64, optional
+        crop ``boxes`` [N,4] / ``flips`` [N] are copied into the program's static input buffers
+        (pass None to reuse what is already there)."""
         p = self.prog
         p.training = True
         if images_u8 is not None:
             p.img_u8.copy_(images_u8, non_blocking=True)
         if labels is not None:
             p.labels.copy_(labels, non_blocking=True)
+        if boxes is not None:
+            p.boxes.copy_(boxes, non_blocking=True)
+        if flips is not None:
+            p.flip.copy_(flips, non_blocking=True)
         self._set_hyper()
         if not self.use_graphs:
             self._run_phases_eager()
@@ -238,17 +266,23 @@ class NativeTrainer:
 
     # ----------------------------------------------------------------------------------
     @torch.no_grad()
-    def evaluate_batch(self, images_u8: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        """Eval-mode forward (running BN stats); returns logits (bf16) and accumulates metrics."""
+    def evaluate_batch(self, images_u8: torch.Tensor, labels: torch.Tensor,
+                       boxes: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Eval-mode forward (running BN stats); returns logits (bf16) and accumulates metrics.
+        A short final batch is padded (padding rows get label -> excluded by the caller)."""
         p = self.prog
         p.training = False
-        p.img_u8.copy_(images_u8)
-        p.labels.copy_(labels)
+        n = images_u8.shape[0]
+        p.img_u8[:n].copy_(images_u8)
+        p.labels[:n].copy_(labels)
+        if boxes is not None:
+            p.boxes[:n].copy_(boxes)
+        p.flip.zero_()
         p.prepare_weights()
         p.load_input_u8(None)
-        out = p.forward(smoothing=0.0, compute_grad=False)
+        out = p.forward(smoothing=0.0, compute_grad=False, metrics=False)
         p.training = True
-        return out
+        return out[:n]
 
     def read_metrics(self, reset: bool = True) -> Tuple[float, float]:
         m = self.prog.metrics[:2].tolist()

@@ -118,12 +118,17 @@ class ResNetProgram:
     """Compile a ResNet nn.Module into a fixed-shape NHWC program for (batch, H, W)."""
 
     def __init__(self, model: nn.Module, batch: int, image_hw: Tuple[int, int], device: torch.device,
-                 bn_momentum: Optional[float] = None):
+                 src_hw: Optional[Tuple[int, int]] = None, mean=None, std=None):
+        """``image_hw``: network input size; ``src_hw``: size of the uint8 images handed in
+        (crop/resize to image_hw happens on the GPU, ``augment_u8``); default = image_hw."""
         if not supports(model):
             raise TypeError(f"ResNetProgram does not support {type(model).__name__}")
         self.model = model
         self.N = batch
         self.H, self.W = image_hw
+        self.src_hw = tuple(src_hw) if src_hw else (self.H, self.W)
+        self.norm_mean = tuple(mean) if mean else None
+        self.norm_std = tuple(std) if std else None
         self.dev = device
         self.in_ch = model.conv1.in_channels
         self._build_layers()
@@ -333,7 +338,10 @@ class ResNetProgram:
         self.logits = E(N, self.num_classes)
         self.dlogits = E(N, self.num_classes)
         self.labels = torch.zeros(N, device=dev, dtype=torch.int64)
-        self.img_u8 = torch.zeros(N, self.H, self.W, 3 if self.in_ch != 1 else 1, device=dev, dtype=torch.uint8)
+        sh, sw = self.src_hw
+        self.img_u8 = torch.zeros(N, sh, sw, 3 if self.in_ch != 1 else 1, device=dev, dtype=torch.uint8)
+        self.boxes = torch.tensor([[0.0, 0.0, float(sh), float(sw)]] * N, device=dev)  # full-image default
+        self.flip = torch.zeros(N, device=dev, dtype=torch.uint8)
         self.metrics = torch.zeros(4, device=dev, dtype=torch.float32)  # loss sum, correct, -, -
         # BN state arena
         tot = 0
@@ -371,9 +379,12 @@ class ResNetProgram:
         self.fc_b16.copy_(self.fc.bias.detach())
 
     def load_input_u8(self, flip: Optional[torch.Tensor] = None):
-        mean = IMAGENET_MEAN if self.in_ch == 3 else (0.5, 0.5, 0.5)
-        std = IMAGENET_STD if self.in_ch == 3 else (0.5, 0.5, 0.5)
-        K.normalize_u8(self.img_u8, self.x4, mean, std, flip)
+        """uint8 images (+ per-sample crop boxes / flips in self.boxes / self.flip) -> bf16 NHWC4."""
+        mean = self.norm_mean or (IMAGENET_MEAN if self.in_ch == 3 else (0.5, 0.5, 0.5))
+        std = self.norm_std or (IMAGENET_STD if self.in_ch == 3 else (0.5, 0.5, 0.5))
+        if self.norm_mean and len(mean) == 1:
+            mean, std = mean * 3, std * 3
+        K.augment_u8(self.img_u8, self.x4, self.boxes, mean, std, self.flip if flip is None else flip)
 
     def _bn_fwd(self, bn: BNL, count: int):
         mod = bn.mod
@@ -384,7 +395,8 @@ class ResNetProgram:
         else:
             K.bn_eval_coeff(bn.gamma, bn.beta, mod.eps, mod.running_mean, mod.running_var, bn.scale, bn.shift)
 
-    def forward(self, smoothing: float = 0.0, compute_grad: bool = True, grad_scale: float = 1.0):
+    def forward(self, smoothing: float = 0.0, compute_grad: bool = True, grad_scale: float = 1.0,
+                metrics: bool = True):
         """Full forward incl. loss. Assumes x4 / labels filled and prepare_weights() done."""
         tr = self.training
         if tr:
@@ -420,8 +432,8 @@ class ResNetProgram:
             x = b.out
         K.avgpool_fwd(x, self.pooled)
         torch.addmm(self.fc_b16, self.pooled, self.fc_w16.t(), out=self.logits)
-        K.softmax_ce(self.logits, self.labels, self.dlogits if compute_grad else None, None, self.metrics,
-                     smoothing=smoothing, grad_scale=grad_scale)
+        K.softmax_ce(self.logits, self.labels, self.dlogits if compute_grad else None, None,
+                     self.metrics if metrics else None, smoothing=smoothing, grad_scale=grad_scale)
         return self.logits
 
     def backward_segments(self):
@@ -486,11 +498,15 @@ class ResNetProgram:
                 pc = b.convs[j - 1]
                 self._bn_bwd(pbn, b.das[j - 1], b.ys[j - 1], b.dys[j - 1], N * pc.OH * pc.OW, K.MASK_Y)
             else:
+                # identity shortcut: dx already holds g (written by the tail BN-backward) -> accumulate;
+                # downsample: conv1's dgrad writes every pixel, then the strided 1x1 dgrad accumulates
+                # into its phase only (no zero-fill of the untouched phases needed)
+                K.conv_dgrad(b.dys[0], cv.wt16, b.dx, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                             accumulate=b.ds_conv is None)
                 if b.ds_conv is not None:
                     dc = b.ds_conv
                     K.conv_wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
-                    K.conv_dgrad(b.dyd, dc.wt16, b.dx, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
-                K.conv_dgrad(b.dys[0], cv.wt16, b.dx, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad, accumulate=True)
+                    K.conv_dgrad(b.dyd, dc.wt16, b.dx, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad, accumulate=True)
 
     def _bwd_stem(self):
         st, sbn = self.stem, self.stem_bn

@@ -1,0 +1,167 @@
+"""HF-Accelerate-style API (`04_accelerate/01_cifar_accelerate.ipynb`) over our process group / DDP.
+
+``Accelerator().prepare(model, optimizer, train_loader, eval_loader, scheduler)`` moves the model to
+this rank's GPU (channels_last), wraps it in the flat-bucket DDP, re-shards the loaders with
+``ShardSampler`` and returns them; ``backward(loss)`` runs autograd and finishes the bucket
+all-reduces; ``gather`` / ``reduce`` are packed collectives; ``log`` forwards to the MLflow-compat
+tracker (``log_with="mlflow"``). bf16 autocast is enabled by ``mixed_precision="bf16"``.
+"""
+from __future__ import annotations
+
+import contextlib
+import random
+from typing import Any, List, Optional
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader
+
+from ..parallel import dist as ddist
+from ..parallel.ddp import DistributedDataParallel, unwrap
+from ..parallel.sampler import ShardSampler
+from ..utils import mlflow_compat as mlflow
+
+
+def set_seed(seed: int) -> None:
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+
+
+class _PreparedOptimizer:
+    def __init__(self, opt, acc):
+        self.opt, self.acc = opt, acc
+
+    def step(self, *a, **k):
+        for m in self.acc._models:
+            m.finish_gradient_sync()
+        return self.opt.step(*a, **k)
+
+    def zero_grad(self, set_to_none: bool = True):
+        for m in self.acc._models:
+            m.zero_grad()
+        self.opt.zero_grad(set_to_none=False)
+
+    def __getattr__(self, k):
+        return getattr(self.opt, k)
+
+    def state_dict(self):
+        return self.opt.state_dict()
+
+    def load_state_dict(self, sd):
+        return self.opt.load_state_dict(sd)
+
+
+class Accelerator:
+    def __init__(self, log_with: Optional[str] = None, mixed_precision: str = "bf16", cpu: bool = False, **_):
+        self.info = ddist.init_distributed(device="cpu" if cpu else None)
+        self.device = self.info.device
+        self.mixed_precision = mixed_precision
+        self.log_with = log_with
+        self._models: List[DistributedDataParallel] = []
+        self._trackers = False
+
+    @property
+    def num_processes(self) -> int:
+        return ddist.get_world_size()
+
+    @property
+    def process_index(self) -> int:
+        return ddist.get_rank()
+
+    @property
+    def local_process_index(self) -> int:
+        return self.info.local_rank
+
+    @property
+    def is_main_process(self) -> bool:
+        return ddist.get_rank() == 0
+
+    @property
+    def is_local_main_process(self) -> bool:
+        return self.info.local_rank == 0
+
+    def print(self, *a, **k):
+        if self.is_main_process:
+            print(*a, **k)
+
+    def _prep_one(self, obj):
+        if isinstance(obj, torch.nn.Module):
+            m = obj.to(self.device)
+            if self.device.type == "cuda":
+                m = m.to(memory_format=torch.channels_last)
+            d = DistributedDataParallel(m)
+            self._models.append(d)
+            return d
+        if isinstance(obj, torch.optim.Optimizer):
+            return _PreparedOptimizer(obj, self)
+        if isinstance(obj, DataLoader):
+            if ddist.get_world_size() == 1:
+                return obj
+            shuffle = not isinstance(obj.sampler, torch.utils.data.SequentialSampler)
+            return DataLoader(obj.dataset, batch_size=obj.batch_size, sampler=ShardSampler(obj.dataset, shuffle=shuffle),
+                              num_workers=obj.num_workers, collate_fn=obj.collate_fn, pin_memory=obj.pin_memory,
+                              drop_last=obj.drop_last)
+        return obj  # schedulers etc.
+
+    def prepare(self, *objs):
+        out = tuple(self._prep_one(o) for o in objs)
+        return out[0] if len(out) == 1 else out
+
+    def autocast(self):
+        enabled = self.device.type == "cuda" and self.mixed_precision == "bf16"
+        return torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=enabled)
+
+    def backward(self, loss: torch.Tensor) -> None:
+        loss.backward()
+        for m in self._models:
+            m.finish_gradient_sync()
+
+    def gather(self, t: torch.Tensor) -> torch.Tensor:
+        t = torch.as_tensor(t, device=self.device)
+        if ddist.get_world_size() == 1:
+            return t.reshape(1, *t.shape) if t.dim() == 0 else t
+        import torch.distributed as dist
+        parts = [torch.empty_like(t.reshape(-1) if t.dim() == 0 else t) for _ in range(ddist.get_world_size())]
+        dist.all_gather(parts, t.reshape(-1) if t.dim() == 0 else t)
+        return torch.cat(parts)
+
+    def reduce(self, t: torch.Tensor, reduction: str = "sum") -> torch.Tensor:
+        t = torch.as_tensor(t, device=self.device).clone()
+        ddist.all_reduce_tensor_(t)
+        if reduction == "mean":
+            t /= ddist.get_world_size()
+        return t
+
+    def wait_for_everyone(self) -> None:
+        ddist.barrier()
+
+    def unwrap_model(self, model):
+        return unwrap(model)
+
+    def init_trackers(self, project_name: str, config: Optional[dict] = None, **_):
+        if self.log_with == "mlflow" and self.is_main_process:
+            mlflow.set_experiment(project_name)
+            if mlflow.active_run() is None:
+                mlflow.start_run()
+            if config:
+                mlflow.log_params(config)
+            self._trackers = True
+
+    def log(self, values: dict, step: Optional[int] = None) -> None:
+        if self._trackers and self.is_main_process:
+            mlflow.log_metrics({k: float(v) for k, v in values.items()}, step=step)
+
+    def end_training(self) -> None:
+        if self._trackers and self.is_main_process and mlflow.active_run() is not None:
+            mlflow.end_run()
+        self._trackers = False
+
+    def save(self, obj, path: str) -> None:
+        if self.is_main_process:
+            torch.save(obj, path)
+
+    @contextlib.contextmanager
+    def no_sync(self, model):
+        with model.no_sync():
+            yield

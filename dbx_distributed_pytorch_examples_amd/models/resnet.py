@@ -240,7 +240,11 @@ def build_model(name: str, num_classes: int = 1000, **kw) -> nn.Module:
     key = name.lower()
     if key not in _FACTORIES:
         raise KeyError(f"unknown model {name!r}; known: {sorted(_FACTORIES)}")
-    return _FACTORIES[key](num_classes=num_classes, **kw)
+    m = _FACTORIES[key](num_classes=num_classes, **kw)
+    # factory spec: lets checkpoint / MLflow loaders rebuild the module without unpickling code
+    m._dbx_spec = {"name": key, "kwargs": dict(num_classes=num_classes, **{k: v for k, v in kw.items()
+                                                                          if isinstance(v, (int, float, str, bool))})}
+    return m
 
 
 def register_model(name: str, factory: Callable[..., nn.Module]) -> None:

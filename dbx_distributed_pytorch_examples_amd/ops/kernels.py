@@ -385,6 +385,22 @@ def normalize_u8(img, out, mean, std, flip=None):
 
 
 @_dispatch
+def augment_u8(img, out, boxes, mean, std, flip=None):
+    """uint8 NHWC -> bf16 NHWC4: per-sample crop box [N,4] (y0, x0, h, w; fp32) bilinear-resized to
+    out's H x W, optional flip [N] uint8, normalised."""
+    N, Hin, Win, Cin = img.shape
+    _, Ho, Wo, C4 = out.shape
+    _chk(img, torch.uint8, "img")
+    _chk(out, torch.bfloat16, "out", N * Ho * Wo * 4)
+    _chk(boxes, torch.float32, "boxes", N * 4)
+    if flip is not None:
+        _chk(flip, torch.uint8, "flip", N)
+    C().augment_u8(img.data_ptr(), out.data_ptr(), boxes.data_ptr(), _p(flip), N, Hin, Win, Cin, Ho, Wo,
+                   float(mean[0]), float(mean[1]), float(mean[2]), float(std[0]), float(std[1]), float(std[2]),
+                   stream_ptr())
+
+
+@_dispatch
 def weight_prep(master, wbuf, desc_dev, nlayers):
     C().weight_prep(master.data_ptr(), wbuf.data_ptr(), desc_dev.data_ptr(), nlayers, stream_ptr())
 

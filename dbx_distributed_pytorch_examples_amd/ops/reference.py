@@ -306,6 +306,32 @@ def normalize_u8(img, out, mean, std, flip=None):
     out.copy_(o.bfloat16())
 
 
+def augment_u8(img, out, boxes, mean, std, flip=None):
+    N, Hin, Win, Cin = img.shape
+    _, Ho, Wo, _ = out.shape
+    dev = img.device
+    res = torch.zeros(N, Ho, Wo, 4, device=dev)
+    oy = torch.arange(Ho, device=dev).float()
+    ox = torch.arange(Wo, device=dev).float()
+    m = torch.tensor(mean, device=dev)
+    s = torch.tensor(std, device=dev)
+    for n in range(N):
+        by, bx, bh, bw = (float(v) for v in boxes[n])
+        oxx = (Wo - 1 - ox) if (flip is not None and int(flip[n])) else ox
+        sy = (by + (oy + 0.5) * bh / Ho - 0.5).clamp(0, Hin - 1)
+        sx = (bx + (oxx + 0.5) * bw / Wo - 0.5).clamp(0, Win - 1)
+        y0, x0 = sy.floor().long(), sx.floor().long()
+        y1, x1 = (y0 + 1).clamp(max=Hin - 1), (x0 + 1).clamp(max=Win - 1)
+        wy, wx = (sy - y0)[:, None, None], (sx - x0)[None, :, None]
+        im = img[n].float()
+        if Cin == 1:
+            im = im.expand(Hin, Win, 3)
+        im = im[..., :3]
+        v = ((im[y0][:, x0] * (1 - wx) + im[y0][:, x1] * wx) * (1 - wy) + (im[y1][:, x0] * (1 - wx) + im[y1][:, x1] * wx) * wy)
+        res[n, ..., :3] = (v / 255.0 - m) / s
+    out.copy_(res.bfloat16())
+
+
 def weight_prep(master, wbuf, desc_dev, nlayers):
     d = desc_dev.view(-1, 10)
     for i in range(nlayers):

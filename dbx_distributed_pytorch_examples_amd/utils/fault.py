@@ -1,0 +1,69 @@
+"""Failure detection hooks used by the training loops (SURVEY.md §5.3 plan).
+
+* :func:`heartbeat` — progress beacon: touches ``$DBX_HEARTBEAT_DIR/rank<r>`` (set by
+  ``launch.Launcher``); the launcher's watchdog kills the job when a rank stops advancing.
+* :func:`maybe_inject` — deterministic fault injection for tests: ``DBX_FAULT="rank:step:kind"``
+  with kind ``exit`` (os._exit(3)), ``raise`` (RuntimeError), ``hang`` (sleep forever),
+  ``nan`` (returns True so the caller poisons its loss). Only fires on attempt
+  ``DBX_FAULT_ATTEMPT`` (default 0) so a restarted job can run clean.
+* :func:`check_finite` — cross-rank divergence / NaN guard (one all-reduce of a flag).
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Optional
+
+
+def _rank() -> int:
+    return int(os.environ.get("RANK", "0"))
+
+
+def heartbeat(step: Optional[int] = None) -> None:
+    d = os.environ.get("DBX_HEARTBEAT_DIR")
+    if not d:
+        return
+    path = os.path.join(d, f"rank{_rank()}")
+    try:
+        with open(path, "w") as f:
+            f.write(str(step if step is not None else time.time()))
+    except OSError:
+        pass
+
+
+def parse_fault(spec: Optional[str] = None):
+    spec = spec if spec is not None else os.environ.get("DBX_FAULT", "")
+    if not spec:
+        return None
+    r, s, kind = spec.split(":")
+    return int(r), int(s), kind
+
+
+def maybe_inject(step: int) -> bool:
+    f = parse_fault()
+    if f is None:
+        return False
+    r, s, kind = f
+    if int(os.environ.get("DBX_RESTART_COUNT", "0")) != int(os.environ.get("DBX_FAULT_ATTEMPT", "0")):
+        return False
+    if r != _rank() or s != step:
+        return False
+    if kind == "exit":
+        os._exit(3)
+    if kind == "raise":
+        raise RuntimeError(f"injected fault at rank {r} step {s}")
+    if kind == "hang":
+        while True:
+            time.sleep(60)
+    if kind == "nan":
+        return True
+    raise ValueError(f"unknown fault kind {kind!r}")
+
+
+def check_finite(value: float) -> bool:
+    """True iff ``value`` is finite on every rank (one tiny all-reduce when distributed)."""
+    import math
+
+    from ..parallel import dist as ddist
+    bad = 0.0 if math.isfinite(value) else 1.0
+    return ddist.all_reduce_sum([bad])[0] == 0.0

@@ -1,0 +1,239 @@
+"""Multi-process tests on CPU/gloo (world size 2): launcher, failure handling, DDP, ZeRO, the
+native program's bucketed all-reduce, and the reference-style frontends."""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.nn as nn
+
+from dbx_distributed_pytorch_examples_amd.launch import Launcher, LaunchError, TorchDistributor
+
+pytestmark = pytest.mark.timeout(600)
+
+
+def _env_fn(x):
+    return {"rank": int(os.environ["RANK"]), "world": int(os.environ["WORLD_SIZE"]), "x": x}
+
+
+def test_launcher_returns_rank0_result():
+    r = TorchDistributor(num_processes=2, local_mode=True, use_gpu=False).run(_env_fn, 7)
+    assert r == {"rank": 0, "world": 2, "x": 7}
+
+
+def _fail_rank1():
+    if os.environ["RANK"] == "1":
+        raise ValueError("boom from rank 1")
+    import time
+    time.sleep(30)
+
+
+def test_launcher_propagates_errors_fast():
+    import time
+    t = time.time()
+    with pytest.raises(LaunchError, match="boom from rank 1"):
+        Launcher(2, use_gpu=False).run(_fail_rank1)
+    assert time.time() - t < 25  # rank 0 was killed, not waited for
+
+
+def _faulty_steps(marker_dir):
+    from dbx_distributed_pytorch_examples_amd.utils import fault
+    for step in range(5):
+        fault.heartbeat(step)
+        fault.maybe_inject(step)
+    with open(os.path.join(marker_dir, f"done{os.environ['RANK']}_{os.environ['DBX_RESTART_COUNT']}"), "w"):
+        pass
+    return int(os.environ["DBX_RESTART_COUNT"])
+
+
+def test_fault_injection_and_restart(monkeypatch):
+    d = tempfile.mkdtemp()
+    monkeypatch.setenv("DBX_FAULT", "1:2:exit")
+    r = Launcher(2, use_gpu=False, max_restarts=1).run(_faulty_steps, d)
+    assert r == 1  # second attempt succeeded
+    assert os.path.exists(os.path.join(d, "done0_1")) and os.path.exists(os.path.join(d, "done1_1"))
+
+
+def test_watchdog_kills_hung_rank(monkeypatch):
+    monkeypatch.setenv("DBX_FAULT", "0:1:hang")
+    with pytest.raises(LaunchError, match="watchdog"):
+        Launcher(2, use_gpu=False, heartbeat_timeout=3).run(_faulty_steps, tempfile.mkdtemp())
+
+
+# ---------------------------------------------------------------------------------------------
+class TinyNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.c = nn.Conv2d(3, 8, 3, padding=1)
+        self.f = nn.Linear(8 * 8 * 8, 5)
+
+    def forward(self, x):
+        return self.f(torch.relu(self.c(x)).flatten(1))
+
+
+def _data(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(8, 3, 8, 8, generator=g), torch.randint(0, 5, (8,), generator=g)
+
+
+def _ddp_grads():
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    from dbx_distributed_pytorch_examples_amd.parallel.ddp import DistributedDataParallel
+    ddist.init_distributed(device="cpu")
+    torch.manual_seed(0)
+    m = DistributedDataParallel(TinyNet(), bucket_cap_mb=0.001)  # tiny buckets: several all-reduces
+    x, y = _data()
+    r = ddist.get_rank()
+    xs, ys = x[r * 4:(r + 1) * 4], y[r * 4:(r + 1) * 4]
+    nn.functional.cross_entropy(m(xs), ys).backward()
+    m.finish_gradient_sync()
+    out = {n: p.grad.clone() for n, p in m.module.named_parameters()}
+    ddist.destroy()
+    return out, len(m.buckets)
+
+
+def test_ddp_matches_single_process():
+    grads, nb = Launcher(2, use_gpu=False).run(_ddp_grads)
+    assert nb > 1
+    torch.manual_seed(0)
+    ref = TinyNet()
+    x, y = _data()
+    nn.functional.cross_entropy(ref(x), y).backward()
+    for n, p in ref.named_parameters():
+        assert torch.allclose(grads[n], p.grad, atol=1e-6, rtol=1e-5), n
+
+
+def _zero_run(stage):
+    from dbx_distributed_pytorch_examples_amd.config import OptimizerConfig
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    from dbx_distributed_pytorch_examples_amd.parallel.zero import ZeroShardedOptimizer
+    ddist.init_distributed(device="cpu")
+    torch.manual_seed(0)
+    n = 1000
+    master = torch.randn(n)
+    o = OptimizerConfig(name="adamw", lr=1e-2, weight_decay=0.01)
+    z = ZeroShardedOptimizer(master, torch.zeros(n), o, stage=stage)
+    r = ddist.get_rank()
+    for step in range(3):
+        z.grad.copy_(torch.randn(n, generator=torch.Generator().manual_seed(100 * step + r)))
+        z.step(grads_already_reduced=False)
+    out = master.clone()
+    ddist.destroy()
+    return out, z.m.numel()
+
+
+@pytest.mark.parametrize("stage", [1, 2])
+def test_zero_matches_plain_optimizer(stage):
+    master, shard = Launcher(2, use_gpu=False).run(_zero_run, stage)
+    assert shard == 512  # state is sharded
+    torch.manual_seed(0)
+    p = nn.Parameter(torch.randn(1000))
+    opt = torch.optim.AdamW([p], lr=1e-2, weight_decay=0.01)
+    for step in range(3):
+        g0 = torch.randn(1000, generator=torch.Generator().manual_seed(100 * step))
+        g1 = torch.randn(1000, generator=torch.Generator().manual_seed(100 * step + 1))
+        p.grad = (g0 + g1) / 2
+        opt.step()
+    assert torch.allclose(master, p.detach(), atol=1e-5), (master - p.detach()).abs().max()
+
+
+def _native_dist():
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    ddist.init_distributed(device="cpu")
+    torch.manual_seed(0)
+    tr = NativeTrainer(build_model("resnet18", num_classes=4), 4, (32, 32), torch.device("cpu"),
+                       optim=OptimConfig(lr=0.0, momentum=0.0, weight_decay=0.0), use_graphs=False,
+                       bucket_cap_mb=1.0)
+    g = torch.Generator().manual_seed(10 + ddist.get_rank())
+    tr.step(torch.randint(0, 256, (4, 32, 32, 3), dtype=torch.uint8, generator=g),
+            torch.randint(0, 4, (4,), generator=g))
+    out = (tr.prog.grad.clone(), tr.prog.master.clone())
+    ddist.destroy()
+    return out
+
+
+def test_native_program_bucket_allreduce():
+    """world-2 native step (CPU reference ops): grads are summed over ranks in every segment bucket."""
+    g2, m2 = Launcher(2, use_gpu=False).run(_native_dist)
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    gs = []
+    for r in range(2):
+        torch.manual_seed(0)
+        tr = NativeTrainer(build_model("resnet18", num_classes=4), 4, (32, 32), torch.device("cpu"),
+                           optim=OptimConfig(lr=0.0, momentum=0.0, weight_decay=0.0), use_graphs=False)
+        g = torch.Generator().manual_seed(10 + r)
+        tr.step(torch.randint(0, 256, (4, 32, 32, 3), dtype=torch.uint8, generator=g),
+                torch.randint(0, 4, (4,), generator=g))
+        gs.append(tr.prog.grad.clone())
+    assert torch.allclose(g2, gs[0] + gs[1], atol=1e-3, rtol=1e-3)
+
+
+def _mnist_main(d):
+    from dbx_distributed_pytorch_examples_amd.frontends import torch_distributor as td
+    os.environ["DBX_MLRUNS"] = os.path.join(d, "mlruns")
+    return td.main_fn(d, epochs=1)
+
+
+def test_mnist_main_fn_two_ranks():
+    d = tempfile.mkdtemp()
+    r = TorchDistributor(num_processes=2, local_mode=True, use_gpu=False).run(_mnist_main, d)
+    assert r == "finished"
+    assert os.path.exists(os.path.join(d, "checkpoint-1.pth.tar"))
+    st = torch.load(os.path.join(d, "checkpoint-1.pth.tar"), weights_only=True)
+    assert set(st["model"]) == {"conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "fc1.weight", "fc1.bias",
+                                "fc2.weight", "fc2.bias"}
+
+
+def _ray_loop(config):
+    from dbx_distributed_pytorch_examples_amd.frontends import ray as rt
+    from dbx_distributed_pytorch_examples_amd.utils.checkpoint import save_ray_checkpoint
+    m = rt.prepare_model(TinyNet())
+    opt = torch.optim.Adam(m.parameters(), lr=config["lr"])
+    x, y = _data(rt.get_context().get_world_rank())
+    for epoch in range(2):
+        loss = nn.functional.cross_entropy(m(x), y)
+        opt.zero_grad()
+        loss.backward()
+        if hasattr(m, "finish_gradient_sync"):
+            m.finish_gradient_sync()
+        opt.step()
+        d = tempfile.mkdtemp()
+        save_ray_checkpoint(d, m)
+        rt.report({"loss": loss.item(), "epoch": epoch}, checkpoint=rt.Checkpoint.from_directory(d))
+
+
+def test_ray_style_trainer():
+    from dbx_distributed_pytorch_examples_amd.frontends import ray as rt
+    store = tempfile.mkdtemp()
+    res = rt.TorchTrainer(_ray_loop, train_loop_config={"lr": 1e-2},
+                          scaling_config=rt.ScalingConfig(num_workers=2, use_gpu=False),
+                          run_config=rt.RunConfig(storage_path=store, name="t")).fit()
+    assert res.error is None, res.error
+    assert res.metrics["epoch"] == 1.0 and len(res.metrics_history) == 2
+    with res.checkpoint.as_directory() as d:
+        sd = torch.load(os.path.join(d, "model.pt"), weights_only=True)
+    assert "c.weight" in sd
+
+
+def _accel():
+    from dbx_distributed_pytorch_examples_amd.frontends.accelerate import Accelerator
+    acc = Accelerator(cpu=True)
+    torch.manual_seed(0)
+    model = TinyNet()
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    model, opt = acc.prepare(model, opt)
+    x, y = _data(acc.process_index)
+    loss = nn.functional.cross_entropy(model(x), y)
+    acc.backward(loss)
+    opt.step()
+    g = acc.gather(torch.tensor(float(acc.process_index)))
+    s = acc.reduce(torch.tensor(1.0))
+    return g.tolist(), float(s), [p.detach().clone() for p in acc.unwrap_model(model).parameters()]
+
+
+def test_accelerate_style_two_ranks():
+    g, s, params = Launcher(2, use_gpu=False).run(_accel)
+    assert g == [0.0, 1.0] and s == 2.0
