@@ -15,6 +15,25 @@ struct IGemmArgs {
   int nr, ns, r0, s0, tstep;
   // DGRAD: A gather ih = i + dh0 - tr ; output pixel (i*osub + oph, j*osub + opw) of [FH][FW]
   int dh0, dw0, osub, oph, opw, FH, FW;
+  // ---- DGRAD epilogue fusions --------------------------------------------------------
+  // accumulate: out = acc + addsrc[pixel / add_sub] (only at pixels with h, w % add_sub == 0);
+  // addsrc == null -> the output itself
+  const bf16* addsrc;
+  int add_sub;
+  // BN-backward epilogue (EPI 1: mask = mref > 0; EPI 2: mask = ybn*bsc + bsh > 0):
+  // g = mask * out (written instead of out), bstats1 += [sum g, sum g*(ybn-mean1)*inv1],
+  // bstats2 += [0, sum g*(ybn2-mean2)*inv2] (second BN fed by the same gradient, nullable)
+  const bf16* mref;
+  const bf16* ybn;
+  const bf16* ybn2;
+  const float* bsc;
+  const float* bsh;
+  const float* mean1;
+  const float* inv1;
+  const float* mean2;
+  const float* inv2;
+  float* bstats1;
+  float* bstats2;
 };
 struct WgradArgs {
   const bf16* dy;        // [M][OC]

@@ -13,7 +13,8 @@ namespace py = pybind11;
 #include "abi.h"
 
 extern "C" {
-int dbx_conv_igemm(int mode, int bm, int bn, const dbx::IGemmArgs* a, int pro, int stats, int accum, hipStream_t st);
+int dbx_conv_igemm(int mode, int bm, int bn, const dbx::IGemmArgs* a, int pro, int stats, int accum, int epi,
+                   hipStream_t st);
 int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, hipStream_t st);
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
 int dbx_bn_finalize(const float*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
@@ -69,12 +70,17 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t in_shift, int relu_in, uintptr_t stats, int nshard, int N, int IH, int IW, int IC,
                          int OH, int OW, int OC, int R, int S_, int stride, int pad, int accum, int nr, int ns, int r0,
                          int s0, int tstep, int dh0, int dw0, int osub, int oph, int opw, int FH, int FW,
-                         uintptr_t st) {
+                         uintptr_t addsrc, int add_sub, int epi, uintptr_t mref, uintptr_t ybn, uintptr_t ybn2,
+                         uintptr_t bsc, uintptr_t bsh, uintptr_t mean1, uintptr_t inv1, uintptr_t mean2,
+                         uintptr_t inv2, uintptr_t bstats1, uintptr_t bstats2, uintptr_t st) {
     dbx::IGemmArgs a{P<const bf16*>(x), P<const bf16*>(w), P<bf16*>(y), P<const float*>(in_scale),
                      P<const float*>(in_shift), P<float*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
                      N * OH * OW, nshard > 0 ? nshard : 1, relu_in, nr, ns, r0, s0, tstep, dh0, dw0, osub, oph, opw,
-                     FH, FW};
-    check(dbx_conv_igemm(mode, bm, bn, &a, in_scale != 0, stats != 0, accum, S(st)), "conv_igemm");
+                     FH, FW, P<const bf16*>(addsrc), add_sub, P<const bf16*>(mref), P<const bf16*>(ybn),
+                     P<const bf16*>(ybn2), P<const float*>(bsc), P<const float*>(bsh), P<const float*>(mean1),
+                     P<const float*>(inv1), P<const float*>(mean2), P<const float*>(inv2), P<float*>(bstats1),
+                     P<float*>(bstats2)};
+    check(dbx_conv_igemm(mode, bm, bn, &a, in_scale != 0, stats != 0, accum, epi, S(st)), "conv_igemm");
   });
   m.def("conv_wgrad", [](int mode, int bm, int bn, uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t in_scale,
                          uintptr_t in_shift, int relu_in, int N, int IH, int IW, int IC, int OH, int OW, int OC, int R,

@@ -32,7 +32,7 @@ namespace dbx {
 enum ConvMode { FWD = 0, DGRAD = 1, STEM = 2 };
 
 
-template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM>
+template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
   constexpr int BK = 64;
   constexpr int A_CH = BM * BK / 8 / 256;  // 16-byte chunks per thread (A)
@@ -253,31 +253,125 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
       atomicAdd(st + a.OC + n0 + tid, q);
     }
   }
-  constexpr int CPR = BN / 8;  // 16B chunks per output row
+  constexpr int CPR = BN / 8;  // 16B chunks per output row; a thread's chunk column is fixed
+  const int ccol = tid % CPR;
+  float bs[8], bq1[8], bq2[8];               // BN-backward partial sums of this thread's 8 channels
+  float e_m1[8], e_i1[8], e_m2[8], e_i2[8], e_sc[8], e_sh[8];
+  if constexpr (EPI > 0) {
+    const int c0 = n0 + ccol * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bs[j] = bq1[j] = bq2[j] = 0.f;
+      e_m1[j] = a.mean1[c0 + j]; e_i1[j] = a.inv1[c0 + j];
+      e_m2[j] = a.ybn2 ? a.mean2[c0 + j] : 0.f; e_i2[j] = a.ybn2 ? a.inv2[c0 + j] : 0.f;
+      e_sc[j] = (EPI == 2) ? a.bsc[c0 + j] : 0.f; e_sh[j] = (EPI == 2) ? a.bsh[c0 + j] : 0.f;
+    }
+  }
 #pragma unroll
   for (int it = 0; it < BM * CPR / 256; ++it) {
     const int idx = tid + it * 256;
-    const int row = idx / CPR, cc = idx - row * CPR;
+    const int row = idx / CPR, cc = ccol;
     const int m = m0 + row;
     if (m < a.M) {
       u32x4 v = *reinterpret_cast<const u32x4*>(sC + row * (BN + 8) + cc * 8);
       size_t pix = (size_t)m;
-      if (MODE == DGRAD && a.osub > 1) {
+      int ph = 0, pw = 0;
+      long long nimg = 0;
+      if (MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1))) {
         const int ohw = a.OH * a.OW;
         const int n = m / ohw, pq = m - (m / ohw) * ohw;
         const int i = pq / a.OW, j = pq - (pq / a.OW) * a.OW;
-        pix = ((size_t)n * a.FH + i * a.osub + a.oph) * a.FW + j * a.osub + a.opw;
+        ph = i * a.osub + a.oph; pw = j * a.osub + a.opw;
+        nimg = n;
+        pix = ((size_t)n * a.FH + ph) * a.FW + pw;
       }
-      bf16* dst = a.y + pix * a.OC + n0 + cc * 8;
-      if constexpr (ACCUM) {
-        float f[8], g[8];
+      const size_t e = pix * a.OC + n0 + cc * 8;
+      bf16* dst = a.y + e;
+      if constexpr (ACCUM || EPI > 0) {
+        float f[8];
         unpack8(v, f);
-        unpack8(*reinterpret_cast<const u32x4*>(dst), g);
+        if constexpr (ACCUM) {
+          const bf16* src = nullptr;
+          if (a.addsrc == nullptr) src = dst;
+          else if (a.add_sub <= 1) src = a.addsrc + e;
+          else if ((ph % a.add_sub) == 0 && (pw % a.add_sub) == 0) {
+            const int hh = a.FH / a.add_sub, ww = a.FW / a.add_sub;
+            src = a.addsrc + (((size_t)nimg * hh + ph / a.add_sub) * ww + pw / a.add_sub) * a.OC + n0 + cc * 8;
+          }
+          if (src) {
+            float g[8];
+            unpack8(*reinterpret_cast<const u32x4*>(src), g);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += g[j];
-        v = pack8(f);
+            for (int j = 0; j < 8; ++j) f[j] += g[j];
+          }
+        }
+        if constexpr (EPI > 0) {
+          float yv[8];
+          unpack8(*reinterpret_cast<const u32x4*>(a.ybn + e), yv);
+          if constexpr (EPI == 1) {
+            float mr[8];
+            unpack8(*reinterpret_cast<const u32x4*>(a.mref + e), mr);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = mr[j] > 0.f ? f[j] : 0.f;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = (yv[j] * e_sc[j] + e_sh[j]) > 0.f ? f[j] : 0.f;
+          }
+          v = pack8(f);
+          unpack8(v, f);  // statistics of the values actually stored (bf16-rounded)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { bs[j] += f[j]; bq1[j] += f[j] * (yv[j] - e_m1[j]) * e_i1[j]; }
+          if (a.ybn2) {
+            float y2[8];
+            unpack8(*reinterpret_cast<const u32x4*>(a.ybn2 + e), y2);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bq2[j] += f[j] * (y2[j] - e_m2[j]) * e_i2[j];
+          }
+        } else {
+          v = pack8(f);
+        }
       }
       *reinterpret_cast<u32x4*>(dst) = v;
+    }
+  }
+  if constexpr (EPI > 0) {
+    // reduce the per-thread partials over threads with the same chunk column: in-wave lanes
+    // l, l+CPR, ... by xor-shuffles, then the 4 waves through LDS, then one atomic per channel
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        bs[j] += __shfl_xor(bs[j], o, 64);
+        bq1[j] += __shfl_xor(bq1[j], o, 64);
+        bq2[j] += __shfl_xor(bq2[j], o, 64);
+      }
+    }
+    __syncthreads();  // sC / sStat reuse
+    float* red = reinterpret_cast<float*>(lds);  // [4 waves][3][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wid * 3 + 0) * BN + ccol * 8 + j] = bs[j];
+        red[(wid * 3 + 1) * BN + ccol * 8 + j] = bq1[j];
+        red[(wid * 3 + 2) * BN + ccol * 8 + j] = bq2[j];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float s = 0.f, q1 = 0.f, q2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        s += red[(w * 3 + 0) * BN + tid]; q1 += red[(w * 3 + 1) * BN + tid]; q2 += red[(w * 3 + 2) * BN + tid];
+      }
+      const int shard = (blockIdx.x % a.nshard);
+      float* st1 = a.bstats1 + (size_t)shard * 2 * a.OC;
+      atomicAdd(st1 + n0 + tid, s);
+      atomicAdd(st1 + a.OC + n0 + tid, q1);
+      if (a.bstats2) {
+        float* st2 = a.bstats2 + (size_t)shard * 2 * a.OC;
+        atomicAdd(st2 + n0 + tid, s);
+        atomicAdd(st2 + a.OC + n0 + tid, q2);
+      }
     }
   }
 }
@@ -521,44 +615,57 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
 // ======================================================================================
 using namespace dbx;
 
-template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM>
+template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI>
 static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
   const int nwg = (a.OC / BN) * ((a.M + BM - 1) / BM);
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, MODE, PRO, STATS, ACCUM>), dim3(nwg), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, MODE, PRO, STATS, ACCUM, EPI>), dim3(nwg), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
-template <int BM, int BN, int MODE>
-static int dispatch_flags(const IGemmArgs& a, bool pro, bool stats, bool accum, hipStream_t st) {
-  if (pro) {
-    if (stats) return accum ? launch_igemm_t<BM, BN, MODE, true, true, true>(a, st) : launch_igemm_t<BM, BN, MODE, true, true, false>(a, st);
-    return accum ? launch_igemm_t<BM, BN, MODE, true, false, true>(a, st) : launch_igemm_t<BM, BN, MODE, true, false, false>(a, st);
+template <int BM, int BN>
+static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, hipStream_t st) {
+  if (pro) return stats ? launch_igemm_t<BM, BN, FWD, true, true, false, 0>(a, st) : launch_igemm_t<BM, BN, FWD, true, false, false, 0>(a, st);
+  return stats ? launch_igemm_t<BM, BN, FWD, false, true, false, 0>(a, st) : launch_igemm_t<BM, BN, FWD, false, false, false, 0>(a, st);
+}
+
+template <int BM, int BN>
+static int dispatch_dgrad(const IGemmArgs& a, bool accum, int epi, hipStream_t st) {
+  if (accum) {
+    if (epi == 1) return launch_igemm_t<BM, BN, DGRAD, false, false, true, 1>(a, st);
+    if (epi == 2) return launch_igemm_t<BM, BN, DGRAD, false, false, true, 2>(a, st);
+    return launch_igemm_t<BM, BN, DGRAD, false, false, true, 0>(a, st);
   }
-  if (stats) return accum ? launch_igemm_t<BM, BN, MODE, false, true, true>(a, st) : launch_igemm_t<BM, BN, MODE, false, true, false>(a, st);
-  return accum ? launch_igemm_t<BM, BN, MODE, false, false, true>(a, st) : launch_igemm_t<BM, BN, MODE, false, false, false>(a, st);
+  if (epi == 1) return launch_igemm_t<BM, BN, DGRAD, false, false, false, 1>(a, st);
+  if (epi == 2) return launch_igemm_t<BM, BN, DGRAD, false, false, false, 2>(a, st);
+  return launch_igemm_t<BM, BN, DGRAD, false, false, false, 0>(a, st);
 }
 
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
-                              int accum, hipStream_t st) {
+                              int accum, int epi, hipStream_t st) {
   const IGemmArgs& a = *args;
   if (a.OC % bn != 0) return -1;
   if (mode == STEM) {
-    if (pro || accum) return -2;
-    if (bm == 128 && bn == 64) return dispatch_flags<128, 64, STEM>(a, false, stats, false, st);
+    if (pro || accum || epi) return -2;
+    if (bm == 128 && bn == 64) return stats ? launch_igemm_t<128, 64, STEM, false, true, false, 0>(a, st)
+                                            : launch_igemm_t<128, 64, STEM, false, false, false, 0>(a, st);
     return -3;
   }
   if (a.IC % 64 != 0) return -4;
   if (mode == FWD) {
-    if (bm == 128 && bn == 128) return dispatch_flags<128, 128, FWD>(a, pro, stats, accum, st);
-    if (bm == 128 && bn == 64) return dispatch_flags<128, 64, FWD>(a, pro, stats, accum, st);
-    if (bm == 64 && bn == 64) return dispatch_flags<64, 64, FWD>(a, pro, stats, accum, st);
+    if (accum || epi) return -2;
+    if (bm == 128 && bn == 128) return dispatch_fwd<128, 128>(a, pro, stats, st);
+    if (bm == 128 && bn == 64) return dispatch_fwd<128, 64>(a, pro, stats, st);
+    if (bm == 64 && bn == 64) return dispatch_fwd<64, 64>(a, pro, stats, st);
     return -3;
   }
   if (mode == DGRAD) {
-    if (pro) return -2;
-    if (bm == 128 && bn == 128) return dispatch_flags<128, 128, DGRAD>(a, false, stats, accum, st);
-    if (bm == 128 && bn == 64) return dispatch_flags<128, 64, DGRAD>(a, false, stats, accum, st);
-    if (bm == 64 && bn == 64) return dispatch_flags<64, 64, DGRAD>(a, false, stats, accum, st);
+    if (pro || stats) return -2;
+    if (epi && (a.ybn == nullptr || a.bstats1 == nullptr || a.mean1 == nullptr || a.inv1 == nullptr)) return -6;
+    if (epi == 1 && a.mref == nullptr) return -6;
+    if (epi == 2 && (a.bsc == nullptr || a.bsh == nullptr)) return -6;
+    if (bm == 128 && bn == 128) return dispatch_dgrad<128, 128>(a, accum, epi, st);
+    if (bm == 128 && bn == 64) return dispatch_dgrad<128, 64>(a, accum, epi, st);
+    if (bm == 64 && bn == 64) return dispatch_dgrad<64, 64>(a, accum, epi, st);
     return -3;
   }
   return -5;

@@ -111,6 +111,7 @@ class BlockL:
     dys: List[torch.Tensor] = field(default_factory=list)  # BN-input grads (per conv)
     das: List[torch.Tensor] = field(default_factory=list)  # grads wrt intermediate activations
     dyd: Optional[torch.Tensor] = None
+    dsbuf: Optional[torch.Tensor] = None
     dx: Optional[torch.Tensor] = None                       # grad wrt block input
 
 
@@ -321,8 +322,12 @@ class ResNetProgram:
             h, w, c = b.in_shape
             b.dx = E(N, h, w, c)
             if b.ds_conv is not None:
-                b.yd = E(N, b.ds_conv.OH, b.ds_conv.OW, b.ds_conv.OC)
-                b.dyd = E(N, b.ds_conv.OH, b.ds_conv.OW, b.ds_conv.OC)
+                dcv = b.ds_conv
+                if dcv.R != 1 or dcv.S != 1 or dcv.pad != 0:
+                    raise TypeError(f"{dcv.name}: downsample must be a 1x1 pad-0 conv")
+                b.yd = E(N, dcv.OH, dcv.OW, dcv.OC)
+                b.dyd = E(N, dcv.OH, dcv.OW, dcv.OC)
+                b.dsbuf = E(N, dcv.OH, dcv.OW, dcv.IC)  # dense dgrad of the strided 1x1
             oh, ow, oc = b.out_shape
             b.out = E(N, oh, ow, oc)
         for cv in self.convs:
@@ -333,6 +338,7 @@ class ResNetProgram:
         fh, fw = self.feat_hw
         self.dfeat = self.blocks[-1].out  # placeholder name; real grad buffer below
         self.dlast = E(N, fh, fw, self.feat_c)
+        self.g_last = E(N, fh, fw, self.feat_c)
         self.pooled = E(N, self.feat_c)
         self.dpooled = E(N, self.feat_c)
         self.logits = E(N, self.num_classes)
@@ -473,40 +479,69 @@ class ResNetProgram:
                        gout=gout)
 
     def _bwd_block(self, i: int):
+        """Backward of block i. On entry its output gradient is already masked by the block's
+        final ReLU and the tail BN statistics are accumulated: block i+1's last dgrad did both in
+        its epilogue (BNBwdEpilogue, MASK_OUT). The last block does them with explicit passes."""
         b = self.blocks[i]
         N = self.N
-        dout = self.dlast if i == len(self.blocks) - 1 else self.blocks[i + 1].dx
+        last = i == len(self.blocks) - 1
         x = self.p0 if i == 0 else self.blocks[i - 1].out
         nconv = len(b.convs)
-        lc = b.convs[-1]
+        lc, lbn = b.convs[-1], b.bns[-1]
         cnt_last = N * lc.OH * lc.OW
-        # block tail: out = relu(bn_last(y_last) + shortcut)
-        self._bn_bwd(b.bns[-1], dout, b.ys[-1], b.dys[-1], cnt_last, K.MASK_OUT, mref=b.out,
-                     gout=(b.dx if b.ds_conv is None else None))
+        if last:
+            # g = dlast * (out > 0) -> self.g_last ; tail BN reductions (and ds BN) from dlast
+            K.bn_bwd_reduce(self.dlast, b.ys[-1], lbn.mean, lbn.invstd, lbn.bstats, mask_mode=K.MASK_OUT, mref=b.out)
+            if b.ds_conv is not None:
+                K.bn_bwd_reduce(self.dlast, b.yd, b.ds_bn.mean, b.ds_bn.invstd, b.ds_bn.bstats,
+                                mask_mode=K.MASK_OUT, mref=b.out)
+            K.bn_bwd_coeff(lbn.bstats, cnt_last, lbn.gamma, lbn.mean, lbn.invstd, lbn.coeff, lbn.dgamma, lbn.dbeta)
+            K.bn_bwd_apply(self.dlast, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_OUT, mref=b.out,
+                           gout=self.g_last)
+            g = self.g_last
+        else:
+            g = self.blocks[i + 1].dx
+            K.bn_bwd_coeff(lbn.bstats, cnt_last, lbn.gamma, lbn.mean, lbn.invstd, lbn.coeff, lbn.dgamma, lbn.dbeta)
+            K.bn_bwd_apply(g, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_NONE)
+        if b.ds_conv is not None:
+            dc, dbn = b.ds_conv, b.ds_bn
+            K.bn_bwd_coeff(dbn.bstats, N * dc.OH * dc.OW, dbn.gamma, dbn.mean, dbn.invstd, dbn.coeff, dbn.dgamma,
+                           dbn.dbeta)
+            K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE)
+        # inner convs, last to second: dgrad epilogue masks with the previous BN's ReLU and
+        # accumulates that BN's backward statistics
+        for j in range(nconv - 1, 0, -1):
+            cv, pbn, pc = b.convs[j], b.bns[j - 1], b.convs[j - 1]
+            K.conv_wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                         in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
+            K.conv_dgrad(b.dys[j], cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                         epilogue=K.BNBwdEpilogue(K.MASK_Y, b.ys[j - 1], pbn.mean, pbn.invstd, pbn.bstats,
+                                                  scale=pbn.scale, shift=pbn.shift))
+            K.bn_bwd_coeff(pbn.bstats, N * pc.OH * pc.OW, pbn.gamma, pbn.mean, pbn.invstd, pbn.coeff, pbn.dgamma,
+                           pbn.dbeta)
+            K.bn_bwd_apply(b.das[j - 1], b.ys[j - 1], pbn.coeff, b.dys[j - 1], mask_mode=K.MASK_NONE)
+        # first conv: wgrad, then the block-input gradient = dgrad(conv1) + shortcut gradient
+        c0 = b.convs[0]
+        K.conv_wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
         if b.ds_conv is not None:
             dc = b.ds_conv
-            self._bn_bwd(b.ds_bn, dout, b.yd, b.dyd, N * dc.OH * dc.OW, K.MASK_OUT, mref=b.out)
-        # convs from last to first
-        for j in range(nconv - 1, -1, -1):
-            cv = b.convs[j]
-            src = x if j == 0 else b.ys[j - 1]
-            pbn = None if j == 0 else b.bns[j - 1]
-            K.conv_wgrad(b.dys[j], src, cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
-                         in_scale=pbn.scale if pbn else None, in_shift=pbn.shift if pbn else None, relu_in=True)
-            if j > 0:
-                K.conv_dgrad(b.dys[j], cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad)
-                pc = b.convs[j - 1]
-                self._bn_bwd(pbn, b.das[j - 1], b.ys[j - 1], b.dys[j - 1], N * pc.OH * pc.OW, K.MASK_Y)
-            else:
-                # identity shortcut: dx already holds g (written by the tail BN-backward) -> accumulate;
-                # downsample: conv1's dgrad writes every pixel, then the strided 1x1 dgrad accumulates
-                # into its phase only (no zero-fill of the untouched phases needed)
-                K.conv_dgrad(b.dys[0], cv.wt16, b.dx, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
-                             accumulate=b.ds_conv is None)
-                if b.ds_conv is not None:
-                    dc = b.ds_conv
-                    K.conv_wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
-                    K.conv_dgrad(b.dyd, dc.wt16, b.dx, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad, accumulate=True)
+            K.conv_wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
+            # 1x1 strided downsample: its dgrad is a dense GEMM onto the stride-subsampled pixels
+            K.conv_dgrad(b.dyd, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0)
+            addsrc, sub = b.dsbuf, dc.stride
+        else:
+            addsrc, sub = g, 1
+        epi = None
+        if i > 0:
+            pb = self.blocks[i - 1]
+            epi = K.BNBwdEpilogue(K.MASK_OUT, pb.ys[-1], pb.bns[-1].mean, pb.bns[-1].invstd, pb.bns[-1].bstats,
+                                  mref=pb.out,
+                                  ybn2=pb.yd if pb.ds_conv is not None else None,
+                                  mean2=pb.ds_bn.mean if pb.ds_conv is not None else None,
+                                  inv2=pb.ds_bn.invstd if pb.ds_conv is not None else None,
+                                  stats2=pb.ds_bn.bstats if pb.ds_conv is not None else None)
+        K.conv_dgrad(b.dys[0], c0.wt16, b.dx, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad,
+                     addsrc=addsrc, add_sub=sub, epilogue=epi)
 
     def _bwd_stem(self):
         st, sbn = self.stem, self.stem_bn

@@ -20,6 +20,9 @@ from . import reference as _ref
 from ._ext import C, stream_ptr, use_native
 
 FWD, DGRAD, STEM = 0, 1, 2
+# addsrc, add_sub, epi, mref, ybn, ybn2, bsc, bsh, mean1, inv1, mean2, inv2, bstats1, bstats2
+_NO_EPI = (0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
 
 
 def _dispatch(fn):
@@ -89,7 +92,7 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     bm, bn = tile or pick_tile(N * OH * OW, OC)
     C().conv_igemm(FWD, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
-                   R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, stream_ptr())
+                   R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, stream_ptr())
     return out
 
 
@@ -114,12 +117,54 @@ def dgrad_phases(H: int, W: int, R: int, S: int, stride: int, pad: int):
     return out
 
 
+class BNBwdEpilogue:
+    """Fused BN-backward epilogue for a dgrad: the dgrad result X (plus any residual addend) is
+    masked — by ``mref > 0`` (mode MASK_OUT: the ReLU after a residual add, mref = block output)
+    or by ``ybn*scale+shift > 0`` (MASK_Y: the ReLU after this BN) — and written as g, while
+    ``stats1 += [sum g, sum g*xhat(ybn)]`` (and ``stats2 += [sum g, sum g*xhat(ybn2)]`` for a second
+    BN fed by the same gradient: the downsample branch). Replaces a separate reduction pass."""
+
+    def __init__(self, mode, ybn, mean1, inv1, stats1, mref=None, scale=None, shift=None,
+                 ybn2=None, mean2=None, inv2=None, stats2=None):
+        self.mode, self.ybn, self.mean1, self.inv1, self.stats1 = mode, ybn, mean1, inv1, stats1
+        self.mref, self.scale, self.shift = mref, scale, shift
+        self.ybn2, self.mean2, self.inv2, self.stats2 = ybn2, mean2, inv2, stats2
+
+    def args(self):
+        return (self.mode, _p(self.mref), _p(self.ybn), _p(self.ybn2), _p(self.scale), _p(self.shift),
+                _p(self.mean1), _p(self.inv1), _p(self.mean2), _p(self.inv2), _p(self.stats1), _p(self.stats2))
+
+
+def dgrad_phases(H: int, W: int, R: int, S: int, stride: int, pad: int):
+    """Parity decomposition of a strided dgrad into stride-1 sub-problems.
+
+    Output pixel h receives tap r only where (h + pad - r) % stride == 0, so for each output
+    phase (ph, pw) only taps r = r0 + stride*t contribute and the gather is dense:
+    ih = i + (ph + pad - r0) // stride - t over the phase's sub-grid i (h = i*stride + ph).
+    Returns [(ph, pw, OHs, OWs, r0, nr, s0, ns, dh0, dw0)] (classes with no taps included, nr=0).
+    """
+    out = []
+    for ph in range(stride):
+        for pw in range(stride):
+            ohs = (H - ph + stride - 1) // stride
+            ows = (W - pw + stride - 1) // stride
+            r0 = (ph + pad) % stride
+            s0 = (pw + pad) % stride
+            nr = max(0, (R - r0 + stride - 1) // stride)
+            ns = max(0, (S - s0 + stride - 1) // stride)
+            out.append((ph, pw, ohs, ows, r0, nr, s0, ns, (ph + pad - r0) // stride, (pw + pad - s0) // stride))
+    return out
+
+
 @_dispatch
-def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None):
+def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, addsrc=None, add_sub=1,
+               epilogue: "BNBwdEpilogue" = None):
     """dX = conv_transpose(dY, W): dy [N,P,Q,K], wt16 [C, R*S*K] (CRSK), dx [N,H,W,C].
 
     Stride > 1 runs one dense launch per output phase (``dgrad_phases``): no MFMA work on the
     (stride^2 - 1)/stride^2 taps that a masked gather would multiply by zero.
+    ``accumulate``: dx += result (addsrc=None) or dx = result + addsrc (addsrc at 1/add_sub
+    resolution, e.g. the dense dgrad of a strided 1x1 downsample); ``epilogue``: fused BN backward.
     """
     N, P, Q, K = dy.shape
     _, H, W, Cc = dx.shape
@@ -130,17 +175,38 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None):
         raise ValueError("conv_dgrad: dy / dx shapes inconsistent with the conv geometry")
     if K % 64 or Cc % 64:
         raise ValueError("conv_dgrad needs channels % 64 == 0")
+    if addsrc is not None:
+        _chk(addsrc, torch.bfloat16, "addsrc", N * (H // add_sub) * (W // add_sub) * Cc)
+        if H % add_sub or W % add_sub:
+            raise ValueError("addsrc subsampling must divide the output size")
+        accumulate = True
+    epi = (0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+    if epilogue is not None:
+        e = epilogue
+        _chk(e.ybn, torch.bfloat16, "ybn", dx.numel())
+        _chk(e.stats1, torch.float32, "stats1", NSHARD * 2 * Cc)
+        if e.mode == MASK_OUT:
+            _chk(e.mref, torch.bfloat16, "mref", dx.numel())
+        if e.ybn2 is not None:
+            _chk(e.ybn2, torch.bfloat16, "ybn2", dx.numel())
+            _chk(e.stats2, torch.float32, "stats2", NSHARD * 2 * Cc)
+        epi = e.args()
     phases = dgrad_phases(H, W, R, S, stride, pad)
     if not accumulate and any(ph[5] == 0 or ph[7] == 0 for ph in phases):
+        if epilogue is not None:
+            raise ValueError("fused BN epilogue needs every output pixel covered by one launch")
         dx.zero_()  # phases without taps receive no contribution
         accumulate = True
     for (ph, pw, ohs, ows, r0, nr, s0, ns, dh0, dw0) in phases:
         if nr == 0 or ns == 0 or ohs == 0 or ows == 0:
+            if epilogue is not None or addsrc is not None:
+                raise ValueError("strided dgrad with empty phases cannot carry an epilogue / addend")
             continue
         bm, bn = tile or pick_tile(N * ohs * ows, Cc)
         C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
-                       nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W, stream_ptr())
+                       nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,
+                       _p(addsrc), add_sub, *epi, stream_ptr())
     return dx
 
 
@@ -161,7 +227,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
         raise ValueError("stem kernel supports R,S <= 8")
     C().conv_igemm(STEM, 128, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
-                   stream_ptr())
+                   *_NO_EPI, stream_ptr())
     return out
 
 
@@ -254,8 +320,6 @@ def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, 
                  out.data_ptr(), y.numel(), Cc, mode, int(relu), stream_ptr())
     return out
 
-
-MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
 
 
 @_dispatch

@@ -14,6 +14,7 @@ import torch
 import torch.nn.functional as F
 
 NSHARD = 32
+MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
 
 
 def _nchw(x):
@@ -54,14 +55,35 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     return out
 
 
-def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None):
+def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, addsrc=None, add_sub=1,
+               epilogue=None):
     N, P, Q, Kc = dy.shape
     _, H, W, Cc = dx.shape
     w = wt16.float().view(Cc, R, S, Kc).permute(3, 0, 1, 2)  # [K, C, R, S]
     g = torch.nn.grad.conv2d_input((N, Cc, H, W), w, _nchw(dy.float()), stride=stride, padding=pad)
-    g = _nhwc(g)
-    if accumulate:
+    g = _nhwc(g).bfloat16().float()  # the kernel rounds the tile to bf16 before the epilogue
+    if addsrc is not None:
+        add = torch.zeros_like(g)
+        add[:, ::add_sub, ::add_sub] = addsrc.float()
+        g = g + add
+    elif accumulate:
         g = g + dx.float()
+    if epilogue is not None:
+        e = epilogue
+        y = e.ybn.float()
+        if e.mode == MASK_OUT:
+            g = g * (e.mref.float() > 0)
+        else:
+            g = g * ((y * e.scale + e.shift) > 0)
+        g = g.bfloat16().float()
+        gf = g.reshape(-1, Cc)
+        st = e.stats1.view(NSHARD, 2, Cc)
+        st[0, 0] += gf.sum(0)
+        st[0, 1] += (gf * ((y - e.mean1) * e.inv1).reshape(-1, Cc)).sum(0)
+        if e.ybn2 is not None:
+            st2 = e.stats2.view(NSHARD, 2, Cc)
+            st2[0, 0] += gf.sum(0)
+            st2[0, 1] += (gf * ((e.ybn2.float() - e.mean2) * e.inv2).reshape(-1, Cc)).sum(0)
     dx.copy_(g.bfloat16())
     return dx
 

@@ -96,3 +96,20 @@ def test_program_trains_and_graph_replay():
         assert abs(l1 - l2) <= 2e-2 * max(1.0, abs(l2)), (i, l1, l2)
     assert losses[-1] < 0.5 * losses[0], losses
     assert _cos(t1.prog.master, t2.prog.master) > 0.9999
+
+
+def test_train_entrypoint_native_engine(tmp_path, monkeypatch):
+    """train() picks the graph-captured native engine on the GPU and runs loader + aug + eval + ckpt."""
+    monkeypatch.setenv("DBX_MLRUNS", str(tmp_path / "mlruns"))
+    from dbx_distributed_pytorch_examples_amd.config import TrainConfig
+    from dbx_distributed_pytorch_examples_amd.data.datasets import SyntheticImages
+    from dbx_distributed_pytorch_examples_amd.train.engine import train
+    cfg = TrainConfig(model="resnet18", num_classes=10, batch_size=32, epochs=2, log_every=0)
+    cfg.data.image_size = 32
+    cfg.optim.lr = 0.02
+    cfg.checkpoint_dir = str(tmp_path / "ck")
+    res = train(cfg, train_dataset=SyntheticImages(128, 32, 3, 10), eval_dataset=SyntheticImages(64, 32, 3, 10, seed=9))
+    assert res.engine == "native"
+    assert all(h["train_loss"] == h["train_loss"] for h in res.history)
+    assert "val_accuracy" in res.history[-1]
+    assert (tmp_path / "ck" / "checkpoint-2.pth.tar").exists()
