@@ -28,9 +28,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-# Reference-equivalent stock PyTorch ResNet-50 throughput measured on ONE MI355X with
-# `python bench.py --impl torch`. None until measured.
-BASELINE_IMG_PER_SEC_PER_GPU = None
+# Reference-equivalent stock PyTorch ResNet-50 throughput on ONE MI355X, measured with
+# `python bench.py --impl torch --batch B` (eager nn.Module, channels_last, autocast bf16, MIOpen
+# convs, torch.optim.SGD; BASELINE.md, profiles/r1_torch_reference/). Keyed by per-GPU batch.
+BASELINE_IMG_PER_SEC_PER_GPU = {256: 5941.96, 1024: 6496.62}
 
 
 def parse_args(argv=None):
@@ -38,7 +39,8 @@ def parse_args(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--batch", type=int, default=256, help="per-GPU batch (weak scaling)")
+    p.add_argument("--batch", type=int, default=1024,
+                   help="per-GPU batch (weak scaling); 1024 x 8 GPUs = the 8192 large-batch north-star config")
     p.add_argument("--impl", default="native", choices=["native", "torch"])
     p.add_argument("--model", default="resnet50")
     p.add_argument("--image-size", type=int, default=224)
@@ -77,9 +79,9 @@ def main(argv=None) -> int:
     n = info.world_size
     imgs = args.batch * n * args.steps
     value = imgs / elapsed
-    base = BASELINE_IMG_PER_SEC_PER_GPU
+    base = BASELINE_IMG_PER_SEC_PER_GPU.get(args.batch)
     out = {
-        "metric": "images/sec (whole node) ResNet-50 ImageNet-1K",
+        "metric": "images/sec (whole node) ResNet-50 ImageNet-1K at 1/2/4/8 MI355X; top-1 acc",
         "value": round(value, 2),
         "unit": "images/s",
         "n_gpus": n,
@@ -92,7 +94,8 @@ def main(argv=None) -> int:
         "dtype": "bf16",
         "data": "synthetic (uint8 NHWC 224x224 images + random labels, on-device; random-init weights)",
         "config": {
-            "model": f"{args.model} ImageNet-1K {args.image_size}x{args.image_size} {args.num_classes} classes",
+            "model": f"{args.model} ImageNet-1K {args.image_size}x{args.image_size} {args.num_classes} classes"
+                     + (" large-batch (global 8192 at 8 GPUs)" if args.batch == 1024 else ""),
             "global_batch": args.batch * n,
             "per_gpu_batch": args.batch,
             "seq_len": None,

@@ -267,13 +267,26 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
       e_sc[j] = (EPI == 2) ? a.bsc[c0 + j] : 0.f; e_sh[j] = (EPI == 2) ? a.bsh[c0 + j] : 0.f;
     }
   }
+  // Epilogue in groups of EG rows per thread: ALL global loads of a group (residual addend, mask
+  // reference, BN inputs) are issued before any store, so their latencies overlap instead of
+  // serialising behind the previous row's store (the compiler cannot reorder them across stores
+  // to possibly-aliasing pointers).
+  constexpr int NIT = BM * CPR / 256;
+  constexpr int EG = NIT < 4 ? NIT : 4;
 #pragma unroll
-  for (int it = 0; it < BM * CPR / 256; ++it) {
-    const int idx = tid + it * 256;
-    const int row = idx / CPR, cc = ccol;
-    const int m = m0 + row;
-    if (m < a.M) {
-      u32x4 v = *reinterpret_cast<const u32x4*>(sC + row * (BN + 8) + cc * 8);
+  for (int g0 = 0; g0 < NIT; g0 += EG) {
+    u32x4 vv[EG], va[EG], vm[EG], vy[EG], vy2[EG];
+    size_t ee[EG];
+    bool ok[EG], has_add[EG];
+#pragma unroll
+    for (int k = 0; k < EG; ++k) {
+      const int it = g0 + k;
+      const int row = (tid + it * 256) / CPR;
+      const int m = m0 + row;
+      ok[k] = m < a.M;
+      has_add[k] = false;
+      vv[k] = *reinterpret_cast<const u32x4*>(sC + row * (BN + 8) + ccol * 8);
+      if (!ok[k]) continue;
       size_t pix = (size_t)m;
       int ph = 0, pw = 0;
       long long nimg = 0;
@@ -285,32 +298,45 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
         nimg = n;
         pix = ((size_t)n * a.FH + ph) * a.FW + pw;
       }
-      const size_t e = pix * a.OC + n0 + cc * 8;
-      bf16* dst = a.y + e;
+      const size_t e = pix * a.OC + n0 + ccol * 8;
+      ee[k] = e;
+      if constexpr (ACCUM) {
+        const bf16* src = nullptr;
+        if (a.addsrc == nullptr) src = a.y + e;
+        else if (a.add_sub <= 1) src = a.addsrc + e;
+        else if ((ph % a.add_sub) == 0 && (pw % a.add_sub) == 0) {
+          const int hh = a.FH / a.add_sub, ww = a.FW / a.add_sub;
+          src = a.addsrc + (((size_t)nimg * hh + ph / a.add_sub) * ww + pw / a.add_sub) * a.OC + n0 + ccol * 8;
+        }
+        if (src) { va[k] = *reinterpret_cast<const u32x4*>(src); has_add[k] = true; }
+      }
+      if constexpr (EPI > 0) {
+        vy[k] = *reinterpret_cast<const u32x4*>(a.ybn + e);
+        if constexpr (EPI == 1) vm[k] = *reinterpret_cast<const u32x4*>(a.mref + e);
+        if (a.ybn2) vy2[k] = *reinterpret_cast<const u32x4*>(a.ybn2 + e);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < EG; ++k) {
+      if (!ok[k]) continue;
+      u32x4 v = vv[k];
       if constexpr (ACCUM || EPI > 0) {
         float f[8];
         unpack8(v, f);
         if constexpr (ACCUM) {
-          const bf16* src = nullptr;
-          if (a.addsrc == nullptr) src = dst;
-          else if (a.add_sub <= 1) src = a.addsrc + e;
-          else if ((ph % a.add_sub) == 0 && (pw % a.add_sub) == 0) {
-            const int hh = a.FH / a.add_sub, ww = a.FW / a.add_sub;
-            src = a.addsrc + (((size_t)nimg * hh + ph / a.add_sub) * ww + pw / a.add_sub) * a.OC + n0 + cc * 8;
-          }
-          if (src) {
+          if (has_add[k]) {
             float g[8];
-            unpack8(*reinterpret_cast<const u32x4*>(src), g);
+            unpack8(va[k], g);
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] += g[j];
           }
         }
         if constexpr (EPI > 0) {
           float yv[8];
-          unpack8(*reinterpret_cast<const u32x4*>(a.ybn + e), yv);
+          unpack8(vy[k], yv);
           if constexpr (EPI == 1) {
             float mr[8];
-            unpack8(*reinterpret_cast<const u32x4*>(a.mref + e), mr);
+            unpack8(vm[k], mr);
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] = mr[j] > 0.f ? f[j] : 0.f;
           } else {
@@ -323,7 +349,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
           for (int j = 0; j < 8; ++j) { bs[j] += f[j]; bq1[j] += f[j] * (yv[j] - e_m1[j]) * e_i1[j]; }
           if (a.ybn2) {
             float y2[8];
-            unpack8(*reinterpret_cast<const u32x4*>(a.ybn2 + e), y2);
+            unpack8(vy2[k], y2);
 #pragma unroll
             for (int j = 0; j < 8; ++j) bq2[j] += f[j] * (y2[j] - e_m2[j]) * e_i2[j];
           }
@@ -331,7 +357,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
           v = pack8(f);
         }
       }
-      *reinterpret_cast<u32x4*>(dst) = v;
+      *reinterpret_cast<u32x4*>(a.y + ee[k]) = v;
     }
   }
   if constexpr (EPI > 0) {
