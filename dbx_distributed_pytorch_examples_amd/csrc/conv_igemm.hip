@@ -32,20 +32,24 @@ namespace dbx {
 enum ConvMode { FWD = 0, DGRAD = 1, STEM = 2 };
 
 
-template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI>
-__global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
+template <int BM, int BN, int WM, int WN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI>
+__global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs a) {
+  constexpr int NT = 64 * WM * WN;        // threads; WM x WN waves, each owns a (BM/WM) x (BN/WN) tile
+  constexpr int NW = WM * WN;
   constexpr int BK = 64;
-  constexpr int A_CH = BM * BK / 8 / 256;  // 16-byte chunks per thread (A)
-  constexpr int B_CH = BN * BK / 8 / 256;
-  constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 MFMA tiles per wave (2x2 waves)
+  constexpr int RPP = NT / 8;             // tile rows covered per staging pass (8 x 16B per 64-wide row)
+  constexpr int A_CH = BM * BK / 8 / NT;  // 16-byte chunks per thread (A)
+  constexpr int B_CH = BN * BK / 8 / NT;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);  // 16x16 MFMA tiles per wave
   constexpr int LDS_AB = 2 * (BM + BN) * BK;  // bf16 elements
   constexpr int LDS_C = BM * (BN + 8);
-  constexpr int LDS_ELEMS = (LDS_AB > LDS_C + 4 * BN * 2) ? LDS_AB : (LDS_C + 4 * BN * 2);
+  constexpr int LDS_RED = 2 * (3 * NW * BN);  // fp32 reduction scratch (in bf16 units)
+  constexpr int LDS_ELEMS = (LDS_AB > LDS_C + LDS_RED) ? LDS_AB : (LDS_C + LDS_RED);
   __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
   bf16* sA = lds;                  // [2][BM][BK]
   bf16* sB = lds + 2 * BM * BK;    // [2][BN][BK]
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
   const int ntn = a.OC / BN, ntm = (a.M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, ntn * ntm);
   const int tm = bid / ntn, tn = bid - tm * ntn;
@@ -57,7 +61,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
   int ahb[A_CH], awb[A_CH];
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
-    const int m = m0 + (tid >> 3) + 32 * i;
+    const int m = m0 + (tid >> 3) + RPP * i;
     const int ohw = a.OH * a.OW;
     int n = m / ohw;
     const int pq = m - n * ohw;
@@ -152,19 +156,19 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
+      const int n = n0 + (tid >> 3) + RPP * i;
       rb[i] = *reinterpret_cast<const u32x4*>(a.w + (size_t)n * KTOT + koff);
     }
   };
   auto store_ab = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      const int row = (tid >> 3) + 32 * i;
+      const int row = (tid >> 3) + RPP * i;
       *reinterpret_cast<u32x4*>(sA + buf * BM * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      const int row = (tid >> 3) + 32 * i;
+      const int row = (tid >> 3) + RPP * i;
       *reinterpret_cast<u32x4*>(sB + buf * BN * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = rb[i];
     }
   };
@@ -191,12 +195,12 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
       const int ch = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / 2) + i * 16 + (lane & 15);
+        const int row = wm * (BM / WM) + i * 16 + (lane & 15);
         af[i] = *reinterpret_cast<const bf16x8*>(cA + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int row = wn * (BN / 2) + j * 16 + (lane & 15);
+        const int row = wn * (BN / WN) + j * 16 + (lane & 15);
         bfr[j] = *reinterpret_cast<const bf16x8*>(cB + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
       }
 #pragma unroll
@@ -210,17 +214,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
   }
 
   // ---- epilogue ------------------------------------------------------------------------
-  // acc[i][j][r]: row = wm*BM/2 + i*16 + (lane>>4)*4 + r, col = wn*BN/2 + j*16 + (lane&15)
+  // acc[i][j][r]: row = wm*BM/WM + i*16 + (lane>>4)*4 + r, col = wn*BN/WN + j*16 + (lane&15)
   bf16* sC = lds;  // [BM][BN+8]
-  float* sStat = reinterpret_cast<float*>(lds + LDS_C);  // [2 wm][2][BN]
+  float* sStat = reinterpret_cast<float*>(lds + LDS_C);  // [WM][2][BN]
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * (BN / 2) + j * 16 + (lane & 15);
+        const int row = wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * (BN / WN) + j * 16 + (lane & 15);
         sC[row * (BN + 8) + col] = (bf16)acc[i][j][r];
       }
   if constexpr (STATS) {
@@ -237,7 +241,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
       if (lane < 16) {
-        const int col = wn * (BN / 2) + j * 16 + lane;
+        const int col = wn * (BN / WN) + j * 16 + lane;
         sStat[(wm * 2 + 0) * BN + col] = s;
         sStat[(wm * 2 + 1) * BN + col] = q;
       }
@@ -246,8 +250,9 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
   __syncthreads();
   if constexpr (STATS) {
     if (tid < BN) {
-      const float s = sStat[0 * BN + tid] + sStat[2 * BN + tid];
-      const float q = sStat[1 * BN + tid] + sStat[3 * BN + tid];
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) { s += sStat[(w * 2) * BN + tid]; q += sStat[(w * 2 + 1) * BN + tid]; }
       float* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
       atomicAdd(st + n0 + tid, s);
       atomicAdd(st + a.OC + n0 + tid, q);
@@ -271,7 +276,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
   // reference, BN inputs) are issued before any store, so their latencies overlap instead of
   // serialising behind the previous row's store (the compiler cannot reorder them across stores
   // to possibly-aliasing pointers).
-  constexpr int NIT = BM * CPR / 256;
+  constexpr int NIT = BM * CPR / NT;
   constexpr int EG = NIT < 4 ? NIT : 4;
 #pragma unroll
   for (int g0 = 0; g0 < NIT; g0 += EG) {
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
 #pragma unroll
     for (int k = 0; k < EG; ++k) {
       const int it = g0 + k;
-      const int row = (tid + it * 256) / CPR;
+      const int row = (tid + it * NT) / CPR;
       const int m = m0 + row;
       ok[k] = m < a.M;
       has_add[k] = false;
@@ -373,7 +378,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
       }
     }
     __syncthreads();  // sC / sStat reuse
-    float* red = reinterpret_cast<float*>(lds);  // [4 waves][3][BN]
+    float* red = reinterpret_cast<float*>(lds);  // [NW waves][3][BN]
     if (lane < CPR) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -386,7 +391,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IGemmArgs a) {
     if (tid < BN) {
       float s = 0.f, q1 = 0.f, q2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < NW; ++w) {
         s += red[(w * 3 + 0) * BN + tid]; q1 += red[(w * 3 + 1) * BN + tid]; q2 += red[(w * 3 + 2) * BN + tid];
       }
       const int shard = (blockIdx.x % a.nshard);
@@ -643,8 +648,12 @@ using namespace dbx;
 
 template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI>
 static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
+  // tile shape -> wave layout: 128x128, 128x64, 64x64 on 2x2 waves (256 threads, 2 blocks/CU);
+  // 256x128 on 4x2 and 128x256 on 2x4 waves (512 threads, 1 block/CU, 96 KB LDS)
+  constexpr int WM = (BM == 256) ? 4 : 2;
+  constexpr int WN = (BN == 256) ? 4 : 2;
   const int nwg = (a.OC / BN) * ((a.M + BM - 1) / BM);
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, MODE, PRO, STATS, ACCUM, EPI>), dim3(nwg), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI>), dim3(nwg), dim3(64 * WM * WN), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -666,6 +675,14 @@ static int dispatch_dgrad(const IGemmArgs& a, bool accum, int epi, hipStream_t s
   return launch_igemm_t<BM, BN, DGRAD, false, false, false, 0>(a, st);
 }
 
+#define DBX_TILES(F, ...)                                                         \
+  if (bm == 128 && bn == 128) return F<128, 128>(__VA_ARGS__);                    \
+  if (bm == 128 && bn == 64) return F<128, 64>(__VA_ARGS__);                      \
+  if (bm == 64 && bn == 64) return F<64, 64>(__VA_ARGS__);                        \
+  if (bm == 256 && bn == 128) return F<256, 128>(__VA_ARGS__);                    \
+  if (bm == 128 && bn == 256) return F<128, 256>(__VA_ARGS__);                    \
+  if (bm == 256 && bn == 64) return F<256, 64>(__VA_ARGS__);
+
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
                               int accum, int epi, hipStream_t st) {
   const IGemmArgs& a = *args;
@@ -679,9 +696,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
   if (a.IC % 64 != 0) return -4;
   if (mode == FWD) {
     if (accum || epi) return -2;
-    if (bm == 128 && bn == 128) return dispatch_fwd<128, 128>(a, pro, stats, st);
-    if (bm == 128 && bn == 64) return dispatch_fwd<128, 64>(a, pro, stats, st);
-    if (bm == 64 && bn == 64) return dispatch_fwd<64, 64>(a, pro, stats, st);
+    DBX_TILES(dispatch_fwd, a, pro, stats, st)
     return -3;
   }
   if (mode == DGRAD) {
@@ -689,9 +704,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
     if (epi && (a.ybn == nullptr || a.bstats1 == nullptr || a.mean1 == nullptr || a.inv1 == nullptr)) return -6;
     if (epi == 1 && a.mref == nullptr) return -6;
     if (epi == 2 && (a.bsc == nullptr || a.bsh == nullptr)) return -6;
-    if (bm == 128 && bn == 128) return dispatch_dgrad<128, 128>(a, accum, epi, st);
-    if (bm == 128 && bn == 64) return dispatch_dgrad<128, 64>(a, accum, epi, st);
-    if (bm == 64 && bn == 64) return dispatch_dgrad<64, 64>(a, accum, epi, st);
+    DBX_TILES(dispatch_dgrad, a, accum, epi, st)
     return -3;
   }
   return -5;

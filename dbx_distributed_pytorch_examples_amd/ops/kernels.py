@@ -61,8 +61,35 @@ def conv_out_hw(h: int, w: int, r: int, s: int, stride: int, pad: int) -> Tuple[
     return (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
 
 
-def pick_tile(M: int, OC: int) -> Tuple[int, int]:
-    """Tile heuristic: biggest tile that still puts >= ~2 workgroups on each of the 256 CUs."""
+_TUNE = None
+
+
+def _tune_table():
+    global _TUNE
+    if _TUNE is None:
+        import json
+        import os
+        p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune_table.json")
+        _TUNE = {}
+        modes = os.environ.get("DBX_TUNE_MODES", "all").split(",")  # e.g. "none", "fwd,dgrad2"
+        if os.path.exists(p):
+            with open(p) as f:
+                _TUNE = {k: tuple(v) for k, v in json.load(f).items() if "all" in modes or k.split(":")[0] in modes}
+    return _TUNE
+
+
+def tune_key(mode: str, M: int, OC: int, K_in: int, R: int, stride: int) -> str:
+    return f"{mode}:M{M}:N{OC}:K{K_in}:R{R}:s{stride}"
+
+
+def pick_tile(M: int, OC: int, mode: str = "fwd", K_in: int = 0, R: int = 0, stride: int = 1,
+              use_table: bool = True) -> Tuple[int, int]:
+    """Measured winner from ops/tune_table.json (tools/tune_conv.py) if present, else the
+    heuristic: biggest tile that still puts >= ~2 workgroups on each of the 256 CUs."""
+    if use_table:
+        t = _tune_table().get(tune_key(mode, M, OC, K_in, R, stride))
+        if t is not None and OC % t[1] == 0:
+            return t
     if OC % 128 == 0 and ((M + 127) // 128) * (OC // 128) >= 512:
         return 128, 128
     if ((M + 127) // 128) * (OC // 64) >= 384:
@@ -89,7 +116,7 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     if in_scale is not None:
         _chk(in_scale, torch.float32, "in_scale", IC)
         _chk(in_shift, torch.float32, "in_shift", IC)
-    bm, bn = tile or pick_tile(N * OH * OW, OC)
+    bm, bn = tile or pick_tile(N * OH * OW, OC, "fwd", IC, R, stride)
     C().conv_igemm(FWD, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
                    R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, stream_ptr())
@@ -202,7 +229,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             if epilogue is not None or addsrc is not None:
                 raise ValueError("strided dgrad with empty phases cannot carry an epilogue / addend")
             continue
-        bm, bn = tile or pick_tile(N * ohs * ows, Cc)
+        bm, bn = tile or pick_tile(N * ohs * ows, Cc, f"dgrad{epilogue.mode if epilogue else 0}", K, R, stride)
         C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,

@@ -62,7 +62,7 @@ def test_conv_fwd(case, prologue):
         sc = torch.rand(IC, device=dev) + 0.5
         sh = torch.randn(IC, device=dev) * 0.1
         xe = torch.relu(x.float() * sc + sh).bfloat16().float()
-    for tile in [None, (128, 128), (128, 64), (64, 64)]:
+    for tile in [None, (128, 128), (128, 64), (64, 64), (256, 128), (128, 256), (256, 64)]:
         if tile and OC % tile[1]:
             continue
         stats.zero_()
@@ -383,7 +383,9 @@ def test_conv_dgrad_stride2_tiles():
     wt = w.permute(3, 1, 2, 0).contiguous().view(IC, -1)
     ref = nhwc(torch.nn.grad.conv2d_input((N, IC, H, W), w.float().permute(0, 3, 1, 2), nchw(dy.float()),
                                           stride=st, padding=pad))
-    for tile in [(128, 128), (128, 64), (64, 64)]:
+    for tile in [(128, 128), (128, 64), (64, 64), (256, 128), (128, 256), (256, 64)]:
+        if IC % tile[1]:
+            continue
         dx = torch.full((N, H, W, IC), 7.0, device=dev, dtype=torch.bfloat16)
         k.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad, tile=tile)
         assert relerr(dx, ref) < 1e-2, tile
@@ -410,7 +412,7 @@ def test_conv_dgrad_fused_epilogue(mode, sub, stride):
     k = K()
     from dbx_distributed_pytorch_examples_amd.ops import reference as R
     torch.manual_seed(11)
-    N, H, W, IC, OC, Rr = 2, 8, 8, 64, 128, 3
+    N, H, W, IC, OC, Rr = 2, 8, 8, 256, 128, 3
     pad = 1
     P = (H + 2 * pad - Rr) // stride + 1
     w = (torch.randn(OC, Rr, Rr, IC, device=dev) / math.sqrt(IC * 9)).bfloat16()
@@ -424,7 +426,7 @@ def test_conv_dgrad_fused_epilogue(mode, sub, stride):
     mean2, inv2 = torch.randn(IC, device=dev) * 0.1, torch.rand(IC, device=dev) + 0.5
     sc, sh = torch.rand(IC, device=dev) + 0.5, torch.randn(IC, device=dev) * 0.1
 
-    def run(mod, devc):
+    def run(mod, devc, tile=None):
         t = lambda v: v.to(devc)  # noqa: E731
         st1 = torch.zeros(k.NSHARD * 2 * IC, device=devc)
         st2 = torch.zeros(k.NSHARD * 2 * IC, device=devc)
@@ -435,13 +437,15 @@ def test_conv_dgrad_fused_epilogue(mode, sub, stride):
                                   ybn2=t(ybn2) if mode == 1 else None, mean2=t(mean2), inv2=t(inv2),
                                   stats2=st2 if mode == 1 else None)
         dx = torch.empty(N, H, W, IC, device=devc, dtype=torch.bfloat16)
-        mod.conv_dgrad(t(dy), t(wt), dx, R=Rr, S=Rr, stride=stride, pad=pad, addsrc=t(add), add_sub=sub, epilogue=epi)
+        mod.conv_dgrad(t(dy), t(wt), dx, R=Rr, S=Rr, stride=stride, pad=pad, addsrc=t(add), add_sub=sub, epilogue=epi,
+                       tile=tile)
         return dx.float().cpu(), st1.view(k.NSHARD, 2, IC).sum(0).cpu(), st2.view(k.NSHARD, 2, IC).sum(0).cpu()
 
-    g_dx, g_s1, g_s2 = run(k, dev)
     r_dx, r_s1, r_s2 = run(R, "cpu")
-    assert relerr(g_dx, r_dx) < 2e-2
-    if mode:
-        assert relerr(g_s1, r_s1) < 2e-2
-        if mode == 1:
-            assert relerr(g_s2, r_s2) < 2e-2
+    for tile in [None, (128, 128), (64, 64), (256, 128), (128, 256), (256, 64)]:
+        g_dx, g_s1, g_s2 = run(k, dev, tile)
+        assert relerr(g_dx, r_dx) < 2e-2, tile
+        if mode:
+            assert relerr(g_s1, r_s1) < 2e-2, tile
+            if mode == 1:
+                assert relerr(g_s2, r_s2) < 2e-2, tile

@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Tile autotuner for the implicit-GEMM conv kernels (fwd with BN prologue + stats epilogue, dgrad).
+
+For every conv of a ResNet at a given batch / image size, times every legal tile config
+interleaved in one process (median of rounds, random data) and writes the winners to
+``dbx_distributed_pytorch_examples_amd/ops/tune_table.json`` (consulted by ops.kernels.pick_tile).
+  python tools/tune_conv.py --model resnet50 --batch 1024 --image 224
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from dbx_distributed_pytorch_examples_amd.ops import kernels as K  # noqa: E402
+
+TILES = [(128, 128), (128, 64), (64, 64), (256, 128), (128, 256), (256, 64)]
+
+
+def convs_of(model_name, image, num_classes=1000):
+    from dbx_distributed_pytorch_examples_amd.engine.program import ResNetProgram
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    m = build_model(model_name, num_classes=num_classes)
+    p = ResNetProgram.__new__(ResNetProgram)
+    p.model, p.N, p.H, p.W = m, 1, image, image
+    p._build_layers()
+    seen = {}
+    for cv in p.convs[1:]:
+        key = (cv.IC, cv.OC, cv.R, cv.stride, cv.IH)
+        seen[key] = seen.get(key, 0) + 1
+    return seen
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--out", default=os.path.join(ROOT, "dbx_distributed_pytorch_examples_amd", "ops", "tune_table.json"))
+    ap.add_argument("--report", default=None)
+    a = ap.parse_args()
+    dev = "cuda"
+    N = a.batch
+    table = {}
+    if os.path.exists(a.out):
+        with open(a.out) as f:
+            table = json.load(f)
+    lines = ["| C→K | R s | H | count | mode | best tile | ms | TF/s | default tile ms |", "|---|---|---|---|---|---|---|---|---|"]
+    for (C, Kc, R, st, H), cnt in convs_of(a.model, a.image).items():
+        pad = R // 2
+        OH = (H + 2 * pad - R) // st + 1
+        x = torch.randn(N, H, H, C, device=dev).bfloat16()
+        w = (torch.randn(Kc, R, R, C, device=dev) / math.sqrt(C * R * R)).bfloat16()
+        w2 = w.view(Kc, -1)
+        wt = w.permute(3, 1, 2, 0).contiguous().view(C, -1)
+        y = torch.empty(N, OH, OH, Kc, device=dev, dtype=torch.bfloat16)
+        dy = torch.randn(N, OH, OH, Kc, device=dev).bfloat16()
+        dx = torch.empty_like(x)
+        stats = torch.zeros(K.NSHARD * 2 * Kc, device=dev)
+        sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+        gf = 2.0 * N * OH * OH * Kc * C * R * R / 1e9
+        ybn = torch.randn_like(x)
+        mref = torch.randn_like(x)
+        add = torch.randn_like(x)
+        st1 = torch.zeros(K.NSHARD * 2 * C, device=dev)
+        mean, inv = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+        jobs = [("fwd", N * OH * OH, Kc, C, R, st,
+                 lambda t: K.conv_fwd(x, w2, y, R=R, S=R, stride=st, pad=pad, stats=stats, in_scale=sc,
+                                      in_shift=sh, tile=t))]
+        if st > 1 and R == 1:
+            # strided 1x1 (downsample): the program runs a dense dgrad onto the subsampled grid
+            dxs = torch.empty(N, OH, OH, C, device=dev, dtype=torch.bfloat16)
+            jobs.append(("dgrad0", N * OH * OH, C, Kc, 1, 1,
+                         lambda t: K.conv_dgrad(dy, wt, dxs, R=1, S=1, stride=1, pad=0, tile=t)))
+        else:
+            e1 = K.BNBwdEpilogue(K.MASK_OUT, ybn, mean, inv, st1, mref=mref)
+            e2 = K.BNBwdEpilogue(K.MASK_Y, ybn, mean, inv, st1, scale=sc, shift=sh)
+            Md = N * H * H // (st * st)
+            jobs.append(("dgrad1", Md, C, Kc, R, st, lambda t: K.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad,
+                                                                            tile=t, addsrc=add, epilogue=e1)))
+            jobs.append(("dgrad2", Md, C, Kc, R, st, lambda t: K.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad,
+                                                                            tile=t, epilogue=e2)))
+        for mode, M, OCm, Kin, Rk, sk, make in jobs:
+            cands = [t for t in TILES if OCm % t[1] == 0]
+            res = {t: [] for t in cands}
+            for _ in range(a.rounds):
+                for t in cands:
+                    res[t].append(timeit(lambda t=t: make(t), a.iters))
+            med = {t: sorted(v)[len(v) // 2] for t, v in res.items()}
+            best = min(med, key=med.get)
+            default = K.pick_tile(M, OCm, use_table=False)
+            key = K.tune_key(mode, M, OCm, Kin, Rk, sk)
+            table[key] = list(best)
+            lines.append(f"| {C}→{Kc} | {R}x{R} s{st} | {H} | {cnt} | {mode} | {best[0]}x{best[1]} | {med[best]:.3f} | "
+                         f"{gf / med[best]:.0f} | {med.get(default, float('nan')):.3f} |")
+            print(lines[-1], flush=True)
+    with open(a.out, "w") as f:
+        json.dump(table, f, indent=1, sort_keys=True)
+    if a.report:
+        with open(a.report, "w") as f:
+            f.write(f"# conv tile tuning, {a.model} batch {N} image {a.image}\n\n" + "\n".join(lines) + "\n")
+
+
+if __name__ == "__main__":
+    main()
