@@ -78,6 +78,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 
   u32x4 ra[A_CH], rb[B_CH];
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
+  f32x4 ps0, ps1, ph0, ph1;  // prologue affine of the staged A chunks
+  unsigned avalid = 0;        // bit i: chunk i is a real (non-padding) tap
 
   auto load_a = [&](int kb) {
     if constexpr (MODE == STEM) {
@@ -105,12 +107,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       const int c0 = (kb - tap * cpt) * BK + ach * 8;
       const int tr = tap / a.ns, ts = tap - (tap / a.ns) * a.ns;
       const int r = a.r0 + a.tstep * tr, s = a.s0 + a.tstep * ts;
-      f32x4 ps0, ps1, ph0, ph1;  // prologue affine of this thread's 8 channels (same for all its rows)
-      if constexpr (PRO) {
+      if constexpr (PRO) {  // affine of this thread's 8 channels (same for all its rows), used by pro_a
         ps0 = *reinterpret_cast<const f32x4*>(a.in_scale + c0);
         ps1 = *reinterpret_cast<const f32x4*>(a.in_scale + c0 + 4);
         ph0 = *reinterpret_cast<const f32x4*>(a.in_shift + c0);
         ph1 = *reinterpret_cast<const f32x4*>(a.in_shift + c0 + 4);
+        avalid = 0;
       }
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
@@ -125,23 +127,31 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
         }
         if (v) {
           ra[i] = *reinterpret_cast<const u32x4*>(abase[i] + ((size_t)ih * a.IW + iw) * a.IC + c0);
-          if constexpr (PRO) {
-            float f[8];
-            unpack8(ra[i], f);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              f[j] = f[j] * ps0[j] + ph0[j];
-              f[j + 4] = f[j + 4] * ps1[j] + ph1[j];
-            }
-            if (a.relu_in) {
-#pragma unroll
-              for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-            }
-            ra[i] = pack8(f);
-          }
+          if constexpr (PRO) avalid |= 1u << i;
         } else {
           ra[i] = zero4;
         }
+      }
+    }
+  };
+  // BN-apply (+ReLU) prologue on the staged A chunks. Kept apart from load_a so the global loads
+  // of block kb+1 stay in flight across block kb's MFMAs (the transform waits on the data).
+  auto pro_a = [&]() {
+    if constexpr (PRO && MODE != STEM) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        float f[8];
+        unpack8(ra[i], f);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f[j] = f[j] * ps0[j] + ph0[j];
+          f[j + 4] = f[j + 4] * ps1[j] + ph1[j];
+        }
+        if (a.relu_in) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+        }
+        ra[i] = ((avalid >> i) & 1u) ? pack8(f) : zero4;  // padding taps stay exactly zero
       }
     }
   };
@@ -181,6 +191,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 
   load_a(0);
   load_b(0);
+  pro_a();
   store_ab(0);
   __syncthreads();
 
@@ -209,7 +220,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kb + 1 < KB) store_ab(buf ^ 1);
+    if (kb + 1 < KB) { pro_a(); store_ab(buf ^ 1); }
     __syncthreads();
   }
 
@@ -467,6 +478,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   }
   u32x4 ra[A_CH], rb[B_CH];
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
+  unsigned bvalid = 0;  // bit j: B chunk j is a real (non-padding) tap
   float psc[PRO ? B_CH : 1][8], psh[PRO ? B_CH : 1][8];  // prologue affine per B chunk (fixed)
   if constexpr (PRO) {
 #pragma unroll
@@ -508,21 +520,30 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
       } else {
         const int iw = ow * a.stride - a.pad + b_tap_w[j];
         const bool v = mv && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
+        if (j == 0) bvalid = 0;
         if (v) {
           rb[j] = *reinterpret_cast<const u32x4*>(base + ((size_t)ih * a.IW + iw) * a.IC + b_ch[j]);
-          if constexpr (PRO) {
-            float f[8];
-            unpack8(rb[j], f);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              f[e] = f[e] * psc[j][e] + psh[j][e];
-              if (a.relu_in) f[e] = fmaxf(f[e], 0.f);
-            }
-            rb[j] = pack8(f);
-          }
+          bvalid |= 1u << j;
         } else {
           rb[j] = zero4;
         }
+      }
+    }
+  };
+  // BN-apply (+ReLU) on the staged x chunks, after the MFMAs of the current block so the next
+  // block's loads stay in flight meanwhile; padding taps stay exactly zero.
+  auto pro_b = [&]() {
+    if constexpr (PRO && MODE != STEM) {
+#pragma unroll
+      for (int j = 0; j < B_CH; ++j) {
+        float f[8];
+        unpack8(rb[j], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          f[e] = f[e] * psc[j][e] + psh[j][e];
+          if (a.relu_in) f[e] = fmaxf(f[e], 0.f);
+        }
+        rb[j] = ((bvalid >> j) & 1u) ? pack8(f) : zero4;
       }
     }
   };
@@ -547,6 +568,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
 
   if (nkb > 0) {
     load(0);
+    pro_b();
     store(0);
   }
   __syncthreads();
@@ -593,7 +615,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kb + 1 < nkb) store(buf ^ 1);
+    if (kb + 1 < nkb) { pro_b(); store(buf ^ 1); }
     __syncthreads();
   }
   // partial slab write: ws[split][k][kk]

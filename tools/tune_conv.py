@@ -19,6 +19,7 @@ sys.path.insert(0, ROOT)
 from dbx_distributed_pytorch_examples_amd.ops import kernels as K  # noqa: E402
 
 TILES = [(128, 128), (128, 64), (64, 64), (256, 128), (128, 256), (256, 64)]
+WGRAD_TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
 
 
 def convs_of(model_name, image, num_classes=1000):
@@ -56,6 +57,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--out", default=os.path.join(ROOT, "dbx_distributed_pytorch_examples_amd", "ops", "tune_table.json"))
     ap.add_argument("--report", default=None)
+    ap.add_argument("--modes", default="fwd,dgrad0,dgrad1,dgrad2,wgrad")
     a = ap.parse_args()
     dev = "cuda"
     N = a.batch
@@ -98,15 +100,26 @@ def main():
                                                                             tile=t, addsrc=add, epilogue=e1)))
             jobs.append(("dgrad2", Md, C, Kc, R, st, lambda t: K.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad,
                                                                             tile=t, epilogue=e2)))
+        ws = torch.empty(max(64 * Kc * R * R * C, 16 << 20), device=dev)
+        dw = torch.empty(Kc * R * R * C, device=dev)
+        jobs.append(("wgrad", N * OH * OH, Kc, C, R, st,
+                     lambda t: K.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, in_scale=sc, in_shift=sh,
+                                            tile=t)))
         for mode, M, OCm, Kin, Rk, sk, make in jobs:
-            cands = [t for t in TILES if OCm % t[1] == 0]
+            if mode not in a.modes.split(","):
+                continue
+            if mode == "wgrad":
+                cands = [t for t in WGRAD_TILES if Kc % t[0] == 0 and C % t[1] == 0]
+            else:
+                cands = [t for t in TILES if OCm % t[1] == 0]
             res = {t: [] for t in cands}
             for _ in range(a.rounds):
                 for t in cands:
                     res[t].append(timeit(lambda t=t: make(t), a.iters))
             med = {t: sorted(v)[len(v) // 2] for t, v in res.items()}
             best = min(med, key=med.get)
-            default = K.pick_tile(M, OCm, use_table=False)
+            default = (K.pick_tile(M, OCm, use_table=False) if mode != "wgrad" else
+                       (128 if Kc % 128 == 0 else 64, 128 if C % 128 == 0 else 64))
             key = K.tune_key(mode, M, OCm, Kin, Rk, sk)
             table[key] = list(best)
             lines.append(f"| {C}→{Kc} | {R}x{R} s{st} | {H} | {cnt} | {mode} | {best[0]}x{best[1]} | {med[best]:.3f} | "
