@@ -76,12 +76,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   const int cpt = (MODE == STEM) ? 1 : a.IC / BK;              // K blocks per tap
   const int KB = (MODE == STEM) ? 4 : a.nr * a.ns * cpt;
 
-  u32x4 ra[A_CH], rb[B_CH];
+  // Two register staging sets: the loads of block kb+2 are issued while block kb+1's data (set
+  // issued one iteration earlier) is still landing, so each global load has two blocks of MFMA
+  // work to hide its latency instead of one. The K loop is unrolled by two so S is a constant.
+  u32x4 ra[2][A_CH], rb[2][B_CH];
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
-  f32x4 ps0, ps1, ph0, ph1;  // prologue affine of the staged A chunks
-  unsigned avalid = 0;        // bit i: chunk i is a real (non-padding) tap
+  f32x4 ps0[2], ps1[2], ph0[2], ph1[2];  // prologue affine of the staged A chunks
+  unsigned avalid[2] = {0u, 0u};          // bit i: chunk i is a real (non-padding) tap
 
-  auto load_a = [&](int kb) {
+  auto load_a = [&](int kb, int S) __attribute__((always_inline)) {
     if constexpr (MODE == STEM) {
       // k block kb covers filter rows r = 2kb, 2kb+1; chunk ach: r = 2kb + (ach>>2), pixels
       // s = 2*(ach&3), +1, 4 channels (8 bytes) each.
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
             w4[2 * p] = v.x; w4[2 * p + 1] = v.y;
           }
         }
-        ra[i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
+        ra[S][i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
       }
     } else {
       const int tap = kb / cpt;
@@ -108,12 +111,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       const int tr = tap / a.ns, ts = tap - (tap / a.ns) * a.ns;
       const int r = a.r0 + a.tstep * tr, s = a.s0 + a.tstep * ts;
       if constexpr (PRO) {  // affine of this thread's 8 channels (same for all its rows), used by pro_a
-        ps0 = *reinterpret_cast<const f32x4*>(a.in_scale + c0);
-        ps1 = *reinterpret_cast<const f32x4*>(a.in_scale + c0 + 4);
-        ph0 = *reinterpret_cast<const f32x4*>(a.in_shift + c0);
-        ph1 = *reinterpret_cast<const f32x4*>(a.in_shift + c0 + 4);
-        avalid = 0;
+        ps0[S] = *reinterpret_cast<const f32x4*>(a.in_scale + c0);
+        ps1[S] = *reinterpret_cast<const f32x4*>(a.in_scale + c0 + 4);
+        ph0[S] = *reinterpret_cast<const f32x4*>(a.in_shift + c0);
+        ph1[S] = *reinterpret_cast<const f32x4*>(a.in_shift + c0 + 4);
       }
+      avalid[S] = 0;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         int ih, iw;
@@ -125,37 +128,40 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
           ih = ahb[i] + r; iw = awb[i] + s;
           v = ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
         }
-        if (v) {
-          ra[i] = *reinterpret_cast<const u32x4*>(abase[i] + ((size_t)ih * a.IW + iw) * a.IC + c0);
-          if constexpr (PRO) avalid |= 1u << i;
-        } else {
-          ra[i] = zero4;
-        }
+        // branch-free: padding taps load a valid address and are zeroed at staging time
+        // (a conditional load would make hipcc branch around it and drain vmcnt to 0)
+        const bf16* src = v ? abase[i] + ((size_t)ih * a.IW + iw) * a.IC + c0 : a.x;
+        ra[S][i] = *reinterpret_cast<const u32x4*>(src);
+        avalid[S] |= (v ? 1u : 0u) << i;
       }
     }
   };
   // BN-apply (+ReLU) prologue on the staged A chunks. Kept apart from load_a so the global loads
   // of block kb+1 stay in flight across block kb's MFMAs (the transform waits on the data).
-  auto pro_a = [&]() {
+  auto pro_a = [&](int S) __attribute__((always_inline)) {
+    if constexpr (!PRO && MODE != STEM) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) ra[S][i] = ((avalid[S] >> i) & 1u) ? ra[S][i] : zero4;
+    }
     if constexpr (PRO && MODE != STEM) {
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         float f[8];
-        unpack8(ra[i], f);
+        unpack8(ra[S][i], f);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          f[j] = f[j] * ps0[j] + ph0[j];
-          f[j + 4] = f[j + 4] * ps1[j] + ph1[j];
+          f[j] = f[j] * ps0[S][j] + ph0[S][j];
+          f[j + 4] = f[j + 4] * ps1[S][j] + ph1[S][j];
         }
         if (a.relu_in) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
         }
-        ra[i] = ((avalid >> i) & 1u) ? pack8(f) : zero4;  // padding taps stay exactly zero
+        ra[S][i] = ((avalid[S] >> i) & 1u) ? pack8(f) : zero4;  // padding taps stay exactly zero
       }
     }
   };
-  auto load_b = [&](int kb) {
+  auto load_b = [&](int kb, int S) __attribute__((always_inline)) {
     int koff;
     if constexpr (MODE == STEM) {
       koff = kb * BK + ach * 8;
@@ -167,19 +173,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int n = n0 + (tid >> 3) + RPP * i;
-      rb[i] = *reinterpret_cast<const u32x4*>(a.w + (size_t)n * KTOT + koff);
+      rb[S][i] = *reinterpret_cast<const u32x4*>(a.w + (size_t)n * KTOT + koff);
     }
   };
-  auto store_ab = [&](int buf) {
+  auto store_ab = [&](int buf, int S) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid >> 3) + RPP * i;
-      *reinterpret_cast<u32x4*>(sA + buf * BM * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = ra[i];
+      *reinterpret_cast<u32x4*>(sA + buf * BM * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = ra[S][i];
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int row = (tid >> 3) + RPP * i;
-      *reinterpret_cast<u32x4*>(sB + buf * BN * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = rb[i];
+      *reinterpret_cast<u32x4*>(sB + buf * BN * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = rb[S][i];
     }
   };
 
@@ -189,15 +195,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_a(0);
-  load_b(0);
-  pro_a();
-  store_ab(0);
-  __syncthreads();
-
-  for (int kb = 0; kb < KB; ++kb) {
-    const int buf = kb & 1;
-    if (kb + 1 < KB) { load_a(kb + 1); load_b(kb + 1); }
+  auto mma = [&](int buf) __attribute__((always_inline)) {
     const bf16* cA = sA + buf * BM * BK;
     const bf16* cB = sB + buf * BN * BK;
 #pragma unroll
@@ -220,8 +218,36 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kb + 1 < KB) { pro_a(); store_ab(buf ^ 1); }
+  };
+  // one pipeline step on block kb (LDS buffer kb&1, register set S holds block kb+1)
+  // The prefetch is issued unconditionally (past the end it re-reads the last block, data unused)
+  // and the loop body is branch-free, so hipcc's waitcnt pass sees the same in-flight loads on
+  // every path and waits only for the older set (counted vmcnt) instead of draining to vmcnt(0).
+  auto step = [&](int kb, int S) __attribute__((always_inline)) {
+    const int kn = kb + 2 < KB ? kb + 2 : KB - 1;
+    load_a(kn, S ^ 1);
+    load_b(kn, S ^ 1);
+    mma(kb & 1);
+    pro_a(S);
+    store_ab((kb + 1) & 1, S);  // past the last block this fills the idle buffer, never read
     __syncthreads();
+  };
+
+  load_a(0, 0);
+  load_b(0, 0);
+  load_a(KB > 1 ? 1 : 0, 1);
+  load_b(KB > 1 ? 1 : 0, 1);
+  pro_a(0);
+  store_ab(0, 0);
+  __syncthreads();
+  int kb = 0;
+  for (; kb + 1 < KB; kb += 2) {
+    step(kb, 1);
+    step(kb + 1, 0);
+  }
+  if (kb < KB) {
+    mma(kb & 1);
+    __syncthreads();  // the epilogue's sC staging aliases the operand buffers
   }
 
   // ---- epilogue ------------------------------------------------------------------------
@@ -433,22 +459,25 @@ __device__ __forceinline__ int tr_swz(int row, int ch, int nch) {
   return ch ^ ((((row & 3) << 1) ^ (((row >> 3) & 1) << 1)) & 7);
 }
 
-template <int BM, int BN, int MODE, bool PRO>
+template <int BM, int BN, int MODE, bool PRO, int DEPTH = 2>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   constexpr int BKM = 64;                    // pixels per K block
   constexpr int NCA = BM / 8, NCB = BN / 8;  // 16B chunks per tile row
   constexpr int A_CH = BKM * NCA / 256, B_CH = BKM * NCB / 256;
   constexpr int TM = BM / 32, TN = BN / 32;
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * BKM * (BM + BN)];
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * BKM * (BM + BN) + (PRO ? 4 * BN : 0)];
   bf16* sA = lds;                   // [2][BKM][BM]
   bf16* sB = lds + 2 * BKM * BM;    // [2][BKM][BN]
+  float* sPro = reinterpret_cast<float*>(lds + 2 * BKM * (BM + BN));  // [2][BN] prologue scale, shift
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
   const int ntm = a.OC / BM, ntn = a.KTOT / BN;
   const int ntile = ntm * ntn;
-  // blockIdx.x = split * ntile + tile : consecutive blocks of a split share its dY rows
-  const int split = blockIdx.x / ntile;
-  const int tile = blockIdx.x - split * ntile;
+  // logical id = split * ntile + tile: consecutive ids share a split's dY / X rows, and the XCD
+  // remap keeps consecutive ids on one XCD so those rows are fetched into ONE L2, not eight
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / ntile;
+  const int tile = bid - split * ntile;
   const int tm = tile / ntn, tn = tile - (tile / ntn) * ntn;
   const int k0 = tm * BM, kk0 = tn * BN;
   const int mbeg = split * a.m_per_split;
@@ -476,23 +505,29 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
       b_tap_h[j] = tap / a.S; b_tap_w[j] = tap - (tap / a.S) * a.S;
     }
   }
-  u32x4 ra[A_CH], rb[B_CH];
+  // Two register staging sets (the K loop is unrolled by two so S is a constant): block kb+2 is
+  // loaded while block kb+1's set is still landing, so each load has two blocks of MFMA work to
+  // hide behind. The prologue affine of the tile's BN columns lives in LDS, not in registers.
+  u32x4 ra[2][A_CH], rb[2][B_CH];
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
-  unsigned bvalid = 0;  // bit j: B chunk j is a real (non-padding) tap
-  float psc[PRO ? B_CH : 1][8], psh[PRO ? B_CH : 1][8];  // prologue affine per B chunk (fixed)
+  unsigned bvalid[2] = {0u, 0u};  // bit j: B chunk j is a real (non-padding) tap
+  bool aok[2] = {false, false};   // this thread's A (dY) row lies inside the split
   if constexpr (PRO) {
-#pragma unroll
-    for (int j = 0; j < B_CH; ++j)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { psc[j][e] = a.in_scale[b_ch[j] + e]; psh[j][e] = a.in_shift[b_ch[j] + e]; }
+    for (int c = tid; c < BN; c += 256) {
+      const int kk = kk0 + c;
+      const int ch = kk - (kk / a.IC) * a.IC;
+      sPro[c] = a.in_scale[ch];
+      sPro[BN + c] = a.in_shift[ch];
+    }
   }
 
-  auto load = [&](int kb) {
+  auto load = [&](int kb, int S) __attribute__((always_inline)) {
     const int ma = mbeg + kb * BKM + a_row;
+    aok[S] = ma < mend;
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
       const int cc = a_c + j * ATPR;
-      ra[j] = (ma < mend) ? *reinterpret_cast<const u32x4*>(a.dy + (size_t)ma * a.OC + k0 + cc * 8) : zero4;
+      ra[S][j] = *reinterpret_cast<const u32x4*>(a.dy + (size_t)(ma < mend ? ma : mbeg) * a.OC + k0 + cc * 8);
     }
     const int mb = mbeg + kb * BKM + b_row;
     const bool mv = mb < mend;
@@ -501,6 +536,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
     const int pq = mb - n * ohw;
     const int oh = pq / a.OW, ow = pq - (pq / a.OW) * a.OW;
     const bf16* base = a.x + (size_t)n * a.IH * a.IW * a.IC;
+    bvalid[S] = 0;
 #pragma unroll
     for (int j = 0; j < B_CH; ++j) {
       const int ih = oh * a.stride - a.pad + b_tap_h[j];
@@ -516,47 +552,58 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
             w4[2 * p] = v.x; w4[2 * p + 1] = v.y;
           }
         }
-        rb[j] = u32x4{w4[0], w4[1], w4[2], w4[3]};
+        rb[S][j] = u32x4{w4[0], w4[1], w4[2], w4[3]};
       } else {
         const int iw = ow * a.stride - a.pad + b_tap_w[j];
         const bool v = mv && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
-        if (j == 0) bvalid = 0;
-        if (v) {
-          rb[j] = *reinterpret_cast<const u32x4*>(base + ((size_t)ih * a.IW + iw) * a.IC + b_ch[j]);
-          bvalid |= 1u << j;
-        } else {
-          rb[j] = zero4;
-        }
+        const bf16* src = v ? base + ((size_t)ih * a.IW + iw) * a.IC + b_ch[j] : a.x;  // branch-free
+        rb[S][j] = *reinterpret_cast<const u32x4*>(src);
+        bvalid[S] |= (v ? 1u : 0u) << j;
       }
     }
   };
   // BN-apply (+ReLU) on the staged x chunks, after the MFMAs of the current block so the next
-  // block's loads stay in flight meanwhile; padding taps stay exactly zero.
-  auto pro_b = [&]() {
+  // blocks' loads stay in flight meanwhile; padding taps stay exactly zero.
+  auto pro_b = [&](int S) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < A_CH; ++j) ra[S][j] = aok[S] ? ra[S][j] : zero4;  // rows past the split end
+    if constexpr (!PRO && MODE != STEM) {
+#pragma unroll
+      for (int j = 0; j < B_CH; ++j) rb[S][j] = ((bvalid[S] >> j) & 1u) ? rb[S][j] : zero4;
+    }
     if constexpr (PRO && MODE != STEM) {
 #pragma unroll
       for (int j = 0; j < B_CH; ++j) {
+        const int c = (b_c + j * BTPR) * 8;
+        const f32x4 s0 = *reinterpret_cast<const f32x4*>(sPro + c);
+        const f32x4 s1 = *reinterpret_cast<const f32x4*>(sPro + c + 4);
+        const f32x4 h0 = *reinterpret_cast<const f32x4*>(sPro + BN + c);
+        const f32x4 h1 = *reinterpret_cast<const f32x4*>(sPro + BN + c + 4);
         float f[8];
-        unpack8(rb[j], f);
+        unpack8(rb[S][j], f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          f[e] = f[e] * psc[j][e] + psh[j][e];
-          if (a.relu_in) f[e] = fmaxf(f[e], 0.f);
+        for (int e = 0; e < 4; ++e) {
+          f[e] = f[e] * s0[e] + h0[e];
+          f[e + 4] = f[e + 4] * s1[e] + h1[e];
         }
-        rb[j] = ((bvalid >> j) & 1u) ? pack8(f) : zero4;
+        if (a.relu_in) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+        }
+        rb[S][j] = ((bvalid[S] >> j) & 1u) ? pack8(f) : zero4;
       }
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int S) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
       const int cc = a_c + j * ATPR;
-      *reinterpret_cast<u32x4*>(sA + buf * BKM * BM + a_row * BM + (tr_swz(a_row, cc, NCA) << 3)) = ra[j];
+      *reinterpret_cast<u32x4*>(sA + buf * BKM * BM + a_row * BM + (tr_swz(a_row, cc, NCA) << 3)) = ra[S][j];
     }
 #pragma unroll
     for (int j = 0; j < B_CH; ++j) {
       const int cc = b_c + j * BTPR;
-      *reinterpret_cast<u32x4*>(sB + buf * BKM * BN + b_row * BN + (tr_swz(b_row, cc, NCB) << 3)) = rb[j];
+      *reinterpret_cast<u32x4*>(sB + buf * BKM * BN + b_row * BN + (tr_swz(b_row, cc, NCB) << 3)) = rb[S][j];
     }
   };
 
@@ -566,16 +613,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nkb > 0) {
-    load(0);
-    pro_b();
-    store(0);
-  }
-  __syncthreads();
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  for (int kb = 0; kb < nkb; ++kb) {
-    const int buf = kb & 1;
-    if (kb + 1 < nkb) load(kb + 1);
+  auto mma = [&](int buf) __attribute__((always_inline)) {
     const bf16* cA = sA + buf * BKM * BM;
     const bf16* cB = sB + buf * BKM * BN;
 #pragma unroll
@@ -615,8 +654,35 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kb + 1 < nkb) { pro_b(); store(buf ^ 1); }
+  };
+  // branch-free pipeline (see igemm_kernel): unconditional clamped prefetch, peeled odd tail
+  auto step = [&](int kb, int S) __attribute__((always_inline)) {
+    if constexpr (DEPTH == 2) {
+      load(kb + 2 < nkb ? kb + 2 : nkb - 1, S ^ 1);
+      mma(kb & 1);
+      pro_b(S);
+      store((kb + 1) & 1, S);
+    } else {
+      load(kb + 1 < nkb ? kb + 1 : nkb - 1, 0);
+      mma(kb & 1);
+      pro_b(0);
+      store((kb + 1) & 1, 0);
+    }
     __syncthreads();
+  };
+  __syncthreads();  // sPro visible
+  if (nkb > 0) {
+    load(0, 0);
+    if (DEPTH == 2) load(nkb > 1 ? 1 : 0, 1);
+    pro_b(0);
+    store(0, 0);
+    __syncthreads();
+    int kb = 0;
+    for (; kb + 1 < nkb; kb += 2) {
+      step(kb, 1);
+      step(kb + 1, DEPTH == 2 ? 0 : 1);
+    }
+    if (kb < nkb) mma(kb & 1);
   }
   // partial slab write: ws[split][k][kk]
   float* out = a.ws + (size_t)split * a.OC * a.KTOT;

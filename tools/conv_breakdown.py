@@ -32,6 +32,8 @@ def main():
     big2 = torch.empty_like(big)
     t = timeit(lambda: big2.copy_(big))
     print(f"copy 2 GiB: {t:.3f} ms  {2 * 2 * 2 ** 30 / t / 1e9:.2f} TB/s (read+write)")
+    if os.environ.get("ONLY_WGRAD"):
+        tiles = []
     for C, Kc, H in shapes:
         x = torch.randn(N, H, H, C, device=dev).bfloat16()
         w = (torch.randn(Kc, C, device=dev) / math.sqrt(C)).bfloat16()
@@ -69,6 +71,14 @@ def main():
                 b2 = dy.numel() * 2 + nb * dx.numel() * 2
                 r.append(f"{name} {ms:.3f}ms/{b2 / ms / 1e9:.1f}TB/s")
             print(f"  dgrad tile {tile}: " + "  ".join(r))
+        ws = torch.empty(max(64 * Kc * C, 16 << 20), device=dev)
+        dw = torch.empty(Kc * C, device=dev)
+        r = []
+        for pro in (0, 1):
+            ms = timeit(lambda: K.conv_wgrad(dy, x, dw, ws, R=1, S=1, stride=1, pad=0, in_scale=sc if pro else None,
+                                             in_shift=sh if pro else None))
+            r.append(f"{'P' if pro else '-'} {ms:.3f}ms/{2 * N * H * H * Kc * C / ms / 1e9:.0f}TF/s")
+        print("  wgrad: " + "  ".join(r))
         del x, y, dy, dx, ybn, mref, add
         torch.cuda.empty_cache()
 
