@@ -57,8 +57,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 
   // ---- per-thread A rows: decompose output pixel once ------------------------------
   const int ach = tid & 7;
-  const bf16* abase[A_CH];
-  int ahb[A_CH], awb[A_CH];
+  const bf16* abase[A_CH];   // STEM mode: image base
+  int ahb[A_CH], awb[A_CH];  // top-left input coordinate of the row's receptive field
+  int apix[A_CH];            // element offset of (n, ahb, awb, 0) in x: 32-bit (host checks numel < 2^31)
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
     const int m = m0 + (tid >> 3) + RPP * i;
@@ -70,8 +71,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     abase[i] = a.x + (size_t)n * a.IH * a.IW * a.IC;
     if (MODE == DGRAD) { ahb[i] = oh + a.dh0; awb[i] = ow + a.dw0; }
     else { ahb[i] = oh * a.stride - a.pad; awb[i] = ow * a.stride - a.pad; }
+    apix[i] = ((n * a.IH + ahb[i]) * a.IW + awb[i]) * a.IC;
     if (m >= a.M) ahb[i] = -(1 << 28);
   }
+  // wave-uniform: can a staged A chunk be invalid (padding tap / row past M)? 1x1 stride-1 and
+  // unpadded convs on full tiles skip the zero-selects
+  const bool asel = (MODE == DGRAD) ? (a.nr > 1 || a.ns > 1 || a.dh0 != 0 || a.dw0 != 0 || a.OH > a.IH ||
+                                     a.OW > a.IW || (a.M % BM) != 0)
+                                    : (a.pad != 0 || (a.M % BM) != 0);
   const int KTOT = (MODE == STEM) ? 256 : a.R * a.S * a.IC;  // weight row length
   const int cpt = (MODE == STEM) ? 1 : a.IC / BK;              // K blocks per tap
   const int KB = (MODE == STEM) ? 4 : a.nr * a.ns * cpt;
@@ -116,22 +123,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
         ph0[S] = *reinterpret_cast<const f32x4*>(a.in_shift + c0);
         ph1[S] = *reinterpret_cast<const f32x4*>(a.in_shift + c0 + 4);
       }
+      // tap displacement, the same for all of this thread's rows (32-bit element offsets)
+      const int dh = (MODE == DGRAD) ? -tr : r, dw = (MODE == DGRAD) ? -ts : s;
+      const int toff = (dh * a.IW + dw) * a.IC + c0;
       avalid[S] = 0;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
-        int ih, iw;
-        bool v;
-        if constexpr (MODE == DGRAD) {
-          ih = ahb[i] - tr; iw = awb[i] - ts;
-          v = ih >= 0 && iw >= 0 && ih < a.IH && iw < a.IW;
-        } else {
-          ih = ahb[i] + r; iw = awb[i] + s;
-          v = ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
-        }
+        const bool v = (unsigned)(ahb[i] + dh) < (unsigned)a.IH && (unsigned)(awb[i] + dw) < (unsigned)a.IW;
         // branch-free: padding taps load a valid address and are zeroed at staging time
         // (a conditional load would make hipcc branch around it and drain vmcnt to 0)
-        const bf16* src = v ? abase[i] + ((size_t)ih * a.IW + iw) * a.IC + c0 : a.x;
-        ra[S][i] = *reinterpret_cast<const u32x4*>(src);
+        ra[S][i] = *reinterpret_cast<const u32x4*>(a.x + (v ? apix[i] + toff : 0));
         avalid[S] |= (v ? 1u : 0u) << i;
       }
     }
@@ -140,8 +141,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // of block kb+1 stay in flight across block kb's MFMAs (the transform waits on the data).
   auto pro_a = [&](int S) __attribute__((always_inline)) {
     if constexpr (!PRO && MODE != STEM) {
+      if (asel) {  // only when some tap can be padding or the last tile is partial
 #pragma unroll
-      for (int i = 0; i < A_CH; ++i) ra[S][i] = ((avalid[S] >> i) & 1u) ? ra[S][i] : zero4;
+        for (int i = 0; i < A_CH; ++i) ra[S][i] = ((avalid[S] >> i) & 1u) ? ra[S][i] : zero4;
+      }
     }
     if constexpr (PRO && MODE != STEM) {
 #pragma unroll
@@ -454,9 +457,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 // ======================================================================================
 
 __device__ __forceinline__ int tr_swz(int row, int ch, int nch) {
-  // conflict-free for the transposed reads (see tools/lds_banks.py): 16 chunks per 256B row
-  if (nch == 16) return ch ^ ((((row & 3) | ((row >> 1) & 4)) << 1) & 15);
-  return ch ^ ((((row & 3) << 1) ^ (((row >> 3) & 1) << 1)) & 7);
+  // conflict-free for BOTH the ds_write_b128 staging stores (8-lane groups: the two rows a group
+  // covers must land on different 64-B halves of the 128-B bank window) and the
+  // ds_read_b64_tr_b16 fragment reads (32-lane groups over 8 rows); model: tools/lds_banks.py
+  if (nch == 16) return ch ^ ((((row & 1) << 2) | (row & 2) | (row & 8)) & 15);
+  return ch ^ ((((row & 1) << 2) ^ (row & 2) ^ (((row >> 3) & 1) << 2)) & 7);
 }
 
 template <int BM, int BN, int MODE, bool PRO, int DEPTH = 2>
@@ -491,8 +496,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   const int a_row = tid / ATPR, a_c = tid % ATPR;
   const int b_row = tid / BTPR, b_c = tid % BTPR;
 
-  // B column chunks: tap and channel per chunk (fixed over the K loop)
-  int b_tap_h[B_CH], b_tap_w[B_CH], b_ch[B_CH];
+  // B column chunks: tap and channel per chunk (fixed over the K loop), and the chunk's element
+  // offset relative to the receptive field's top-left pixel (32-bit)
+  int b_tap_h[B_CH], b_tap_w[B_CH], b_ch[B_CH], b_off[B_CH];
 #pragma unroll
   for (int j = 0; j < B_CH; ++j) {
     const int cc = b_c + j * BTPR;
@@ -504,6 +510,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
       b_ch[j] = kk - tap * a.IC;
       b_tap_h[j] = tap / a.S; b_tap_w[j] = tap - (tap / a.S) * a.S;
     }
+    b_off[j] = (b_tap_h[j] * a.IW + b_tap_w[j]) * a.IC + b_ch[j];
   }
   // Two register staging sets (the K loop is unrolled by two so S is a constant): block kb+2 is
   // loaded while block kb+1's set is still landing, so each load has two blocks of MFMA work to
@@ -511,6 +518,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   u32x4 ra[2][A_CH], rb[2][B_CH];
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
   unsigned bvalid[2] = {0u, 0u};  // bit j: B chunk j is a real (non-padding) tap
+  const bool bsel = a.pad != 0 || (a.M % BKM) != 0;  // wave-uniform: can a B chunk be invalid?
   bool aok[2] = {false, false};   // this thread's A (dY) row lies inside the split
   if constexpr (PRO) {
     for (int c = tid; c < BN; c += 256) {
@@ -536,10 +544,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
     const int pq = mb - n * ohw;
     const int oh = pq / a.OW, ow = pq - (pq / a.OW) * a.OW;
     const bf16* base = a.x + (size_t)n * a.IH * a.IW * a.IC;
+    const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+    const int pix = ((n * a.IH + ih0) * a.IW + iw0) * a.IC;
     bvalid[S] = 0;
 #pragma unroll
     for (int j = 0; j < B_CH; ++j) {
-      const int ih = oh * a.stride - a.pad + b_tap_h[j];
+      const int ih = ih0 + b_tap_h[j];
       if constexpr (MODE == STEM) {
         // 16B chunk = 2 pixels (s, s+1) x 4 channels
         unsigned int w4[4] = {0u, 0u, 0u, 0u};
@@ -554,10 +564,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
         }
         rb[S][j] = u32x4{w4[0], w4[1], w4[2], w4[3]};
       } else {
-        const int iw = ow * a.stride - a.pad + b_tap_w[j];
-        const bool v = mv && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
-        const bf16* src = v ? base + ((size_t)ih * a.IW + iw) * a.IC + b_ch[j] : a.x;  // branch-free
-        rb[S][j] = *reinterpret_cast<const u32x4*>(src);
+        const int iw = iw0 + b_tap_w[j];
+        const bool v = mv && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+        rb[S][j] = *reinterpret_cast<const u32x4*>(a.x + (v ? pix + b_off[j] : 0));  // branch-free
         bvalid[S] |= (v ? 1u : 0u) << j;
       }
     }
@@ -565,11 +574,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   // BN-apply (+ReLU) on the staged x chunks, after the MFMAs of the current block so the next
   // blocks' loads stay in flight meanwhile; padding taps stay exactly zero.
   auto pro_b = [&](int S) __attribute__((always_inline)) {
+    if (a.M % BKM) {  // rows past the end of M (only the last split's last block)
 #pragma unroll
-    for (int j = 0; j < A_CH; ++j) ra[S][j] = aok[S] ? ra[S][j] : zero4;  // rows past the split end
+      for (int j = 0; j < A_CH; ++j) ra[S][j] = aok[S] ? ra[S][j] : zero4;
+    }
     if constexpr (!PRO && MODE != STEM) {
+      if (bsel) {
 #pragma unroll
-      for (int j = 0; j < B_CH; ++j) rb[S][j] = ((bvalid[S] >> j) & 1u) ? rb[S][j] : zero4;
+        for (int j = 0; j < B_CH; ++j) rb[S][j] = ((bvalid[S] >> j) & 1u) ? rb[S][j] : zero4;
+      }
     }
     if constexpr (PRO && MODE != STEM) {
 #pragma unroll

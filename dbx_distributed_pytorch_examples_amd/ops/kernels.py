@@ -55,6 +55,9 @@ def _chk(t: torch.Tensor, dtype, name: str, numel: Optional[int] = None):
         raise ValueError(f"{name}: must be a GPU tensor")
     if numel is not None and t.numel() != numel:
         raise ValueError(f"{name}: expected {numel} elements, got {t.numel()} (shape {tuple(t.shape)})")
+    if t.numel() >= 2 ** 31:
+        # the conv gathers use 32-bit element offsets; split the batch above 2^31 elements
+        raise ValueError(f"{name}: {t.numel()} elements exceed the kernels' 32-bit offset range")
 
 
 def conv_out_hw(h: int, w: int, r: int, s: int, stride: int, pad: int) -> Tuple[int, int]:
