@@ -182,3 +182,46 @@ def build_dataset(name: str, root: str = "", train: bool = True, transform=None,
     if name in ("folder", "imagenet", "tiny_imagenet"):
         return ImageFolder(os.path.join(root, "train" if train else "val"), transform)
     raise KeyError(f"unknown dataset {name!r}")
+
+
+# ----------------------------------------------------------------------------------------
+# Dataset snapshots (`03a…:157-158` pickles whole Dataset objects with torch.save,
+# which only loads with weights_only=False). Here a snapshot is plain tensors — uint8 HWC images
+# and int64 labels — loadable with torch.load(weights_only=True).
+def save_tensor_dataset(ds, path: str, max_items: Optional[int] = None) -> str:
+    n = len(ds) if max_items is None else min(len(ds), max_items)
+    imgs, labels = [], []
+    for i in range(n):
+        img, y = ds[i]
+        if isinstance(img, torch.Tensor):
+            t = img
+            if t.is_floating_point():
+                t = (t.clamp(0, 1) * 255).round().to(torch.uint8)
+            if t.dim() == 3 and t.shape[0] in (1, 3) and t.shape[-1] not in (1, 3):
+                t = t.permute(1, 2, 0)
+        else:
+            arr = np.asarray(img)
+            t = torch.from_numpy(np.ascontiguousarray(arr if arr.ndim == 3 else arr[:, :, None]))
+        imgs.append(t.contiguous())
+        labels.append(int(y))
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    torch.save({"images": torch.stack(imgs), "labels": torch.tensor(labels, dtype=torch.int64)}, path)
+    return path
+
+
+class TensorImageDataset(Dataset):
+    """A ``save_tensor_dataset`` snapshot (uint8 HWC) with an optional transform."""
+
+    def __init__(self, path: str, transform=None):
+        d = torch.load(path, weights_only=True)
+        self.images, self.labels, self.transform = d["images"], d["labels"], transform
+        self.num_classes = int(self.labels.max().item()) + 1 if len(self.labels) else 0
+
+    def __len__(self) -> int:
+        return len(self.labels)
+
+    def __getitem__(self, i):
+        img = self.images[i]
+        if self.transform is not None:
+            img = self.transform(img.numpy())
+        return img, int(self.labels[i])

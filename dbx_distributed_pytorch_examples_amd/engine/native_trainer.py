@@ -27,6 +27,8 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import kernels as K
+from ..utils import debug as _debug
+from ..utils.profiling import PhaseTimer
 from .program import ResNetProgram
 
 
@@ -63,7 +65,11 @@ class NativeTrainer:
         self.hyper = torch.zeros(4, device=device)      # lr, bc1, bc2 (device-side, graph-safe)
         self.clip_work = torch.zeros(4, device=device)
         self.step_count = 0
-        self.use_graphs = use_graphs and device.type == "cuda"
+        # debug mode synchronizes after every kernel, which graph capture forbids; per-phase
+        # profiling (DBX_PROFILE_PHASES=1: hipEvent timers + roctx ranges) needs eager phases too
+        self.phase_timer = PhaseTimer() if os.environ.get("DBX_PROFILE_PHASES", "0") == "1" else None
+        self.use_graphs = (use_graphs and device.type == "cuda" and not _debug.enabled()
+                           and self.phase_timer is None)
         self.graphs: List[Optional[torch.cuda.CUDAGraph]] = []
         self.bucket_cap = int(bucket_cap_mb * (1 << 20) // 4)
         self.ar_dtype = allreduce_dtype
@@ -181,7 +187,11 @@ class NativeTrainer:
         for name, fn, rg in self.phases:
             if name == "optimizer" and self.world > 1:
                 cur.wait_stream(self.comm_stream)
-            fn()
+            if self.phase_timer is not None:
+                with self.phase_timer.phase(name):
+                    fn()
+            else:
+                fn()
             if rg is not None and self.world > 1:
                 self.comm_stream.wait_stream(cur)
                 with torch.cuda.stream(self.comm_stream):

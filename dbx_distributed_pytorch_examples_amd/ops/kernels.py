@@ -16,6 +16,7 @@ from typing import Optional, Tuple
 
 import torch
 
+from ..utils import debug as _debug
 from . import reference as _ref
 from ._ext import C, stream_ptr, use_native
 
@@ -26,19 +27,25 @@ MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
 
 
 def _dispatch(fn):
-    """Run the HIP kernel for GPU tensors, the PyTorch reference (ops/reference.py) otherwise."""
+    """Run the HIP kernel for GPU tensors, the PyTorch reference (ops/reference.py) otherwise.
+    With ``DBX_DEBUG=1`` every native launch is followed by a sync + output check (utils/debug.py)."""
     ref = getattr(_ref, fn.__name__)
+    checked = _debug.checked_op(fn)
 
     def wrapper(*args, **kw):
         t = args[0]
         if isinstance(t, torch.Tensor) and not use_native(t):
             return ref(*args, **kw)
+        if _debug.enabled():
+            return checked(*args, **kw)
         return fn(*args, **kw)
 
     wrapper.__name__ = fn.__name__
     wrapper.__doc__ = fn.__doc__
     wrapper.__wrapped__ = fn
     return wrapper
+
+
 NSHARD = 32  # BN-statistics shards (spreads the epilogue atomics over 32 copies)
 
 

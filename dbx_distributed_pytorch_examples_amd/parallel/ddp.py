@@ -83,6 +83,7 @@ class DistributedDataParallel(nn.Module):
         self._handles: List = []
         self._sync = True
         self._hooks = []
+        self.bucket_log: List[int] = []  # launch order of the last round (utils.debug.check_bucket_order)
         if self.world > 1:
             self._broadcast_state()
             for p in self._params:
@@ -98,6 +99,7 @@ class DistributedDataParallel(nn.Module):
     def _reset_round(self):
         self._pending = [len(b["params"]) for b in self.buckets]
         self._handles = []
+        self._order: List[int] = []
 
     def _on_grad(self, p: torch.Tensor):
         if not self._sync or self.world == 1:
@@ -109,6 +111,7 @@ class DistributedDataParallel(nn.Module):
             self._launch(bi)
 
     def _launch(self, bi: int):
+        self._order.append(bi)
         b = self.buckets[bi]
         chunk = self.flat.buffer[b["lo"]:b["hi"]]
         if self.predivide:
@@ -137,6 +140,7 @@ class DistributedDataParallel(nn.Module):
             h.wait()
             if chunk is not None:
                 chunk.copy_(wire)
+        self.bucket_log = list(self._order)
         self._reset_round()
 
     # ------------------------------------------------------------------------------

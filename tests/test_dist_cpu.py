@@ -237,3 +237,32 @@ def _accel():
 def test_accelerate_style_two_ranks():
     g, s, params = Launcher(2, use_gpu=False).run(_accel)
     assert g == [0.0, 1.0] and s == 2.0
+
+
+def _divergence_check():
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    from dbx_distributed_pytorch_examples_amd.parallel.ddp import DistributedDataParallel
+    from dbx_distributed_pytorch_examples_amd.utils import debug
+    ddist.init_distributed(device="cpu")
+    torch.manual_seed(0)
+    m = DistributedDataParallel(TinyNet(), bucket_cap_mb=0.001)
+    x, y = _data(ddist.get_rank())
+    nn.functional.cross_entropy(m(x), y).backward()
+    m.finish_gradient_sync()
+    debug.check_bucket_order(m.bucket_log)
+    debug.assert_replicas_in_sync([p.grad for p in m.module.parameters()], what="grads")  # synced: ok
+    caught = False
+    if ddist.get_rank() == 1:
+        with torch.no_grad():
+            next(m.module.parameters()).add_(1e-3)  # rank 1 drifts
+    try:
+        debug.assert_replicas_in_sync(list(m.module.parameters()))
+    except AssertionError:
+        caught = True
+    ddist.destroy()
+    return caught, len(m.bucket_log)
+
+
+def test_replica_divergence_and_bucket_order_checks():
+    caught, nb = Launcher(2, use_gpu=False).run(_divergence_check)
+    assert caught and nb > 1
