@@ -33,6 +33,15 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 # convs, torch.optim.SGD; BASELINE.md, profiles/r1_torch_reference/). Keyed by per-GPU batch.
 BASELINE_IMG_PER_SEC_PER_GPU = {256: 5941.96, 1024: 6496.62}
 
+# BASELINE.json's other configs (the headline default is ResNet-50 ImageNet-1K, 1024/GPU).
+PRESETS = {
+    "resnet18_cifar10": dict(model="resnet18", image_size=32, num_classes=10, batch=256),
+    "resnet50_tiny_imagenet": dict(model="resnet50", image_size=64, num_classes=200, batch=512),
+    "resnet50_imagenet_zero1": dict(model="resnet50", image_size=224, num_classes=1000, batch=256, optim="adamw",
+                                    zero=1),
+    "resnet50_imagenet_8192": dict(model="resnet50", image_size=224, num_classes=1000, batch=1024),
+}
+
 
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
@@ -46,9 +55,18 @@ def parse_args(argv=None):
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--num-classes", type=int, default=1000)
     p.add_argument("--channels-last", type=int, default=1, help="torch impl only")
-    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--lr", type=float, default=None, help="default: 0.1 (sgd) / 2e-4 (adamw)")
+    p.add_argument("--optim", default="sgd", choices=["sgd", "adamw"])
+    p.add_argument("--zero", type=int, default=0, choices=[0, 1, 2], help="native impl: ZeRO stage")
+    p.add_argument("--preset", default="", choices=[""] + sorted(PRESETS),
+                   help="one of BASELINE.json's other configs (sets model/size/classes/batch/optim)")
     p.add_argument("--json-out", default=None)
-    return p.parse_args(argv)
+    a = p.parse_args(argv)
+    for k, v in PRESETS.get(a.preset, {}).items():
+        setattr(a, k, v)
+    if a.lr is None:
+        a.lr = 0.1 if a.optim == "sgd" else 2e-4
+    return a
 
 
 def main(argv=None) -> int:
@@ -79,7 +97,8 @@ def main(argv=None) -> int:
     n = info.world_size
     imgs = args.batch * n * args.steps
     value = imgs / elapsed
-    base = BASELINE_IMG_PER_SEC_PER_GPU.get(args.batch)
+    headline = args.model == "resnet50" and args.image_size == 224 and args.num_classes == 1000 and args.optim == "sgd"
+    base = BASELINE_IMG_PER_SEC_PER_GPU.get(args.batch) if headline else None
     out = {
         "metric": "images/sec (whole node) ResNet-50 ImageNet-1K at 1/2/4/8 MI355X; top-1 acc",
         "value": round(value, 2),
@@ -101,7 +120,8 @@ def main(argv=None) -> int:
             "seq_len": None,
             "parallelism": f"dp{n}",
             "impl": args.impl,
-            "optimizer": "SGD momentum 0.9 nesterov=False wd 5e-5",
+            "optimizer": ("SGD momentum 0.9 nesterov=False wd 5e-5" if args.optim == "sgd"
+                          else "AdamW wd 0.01") + (f", ZeRO-{args.zero}" if args.zero else ""),
             **meta,
         },
     }

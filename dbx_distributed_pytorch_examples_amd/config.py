@@ -279,4 +279,5 @@ def from_deepspeed(ds: Dict[str, Any], base: Optional[TrainConfig] = None) -> Tr
                 setattr(cfg.zero, k, bool(z[k]))
         cfg.zero.offload_optimizer = bool(z.get("offload_optimizer", {}).get("device", "none") not in ("none", None))
         cfg.zero.offload_param = bool(z.get("offload_param", {}).get("device", "none") not in ("none", None))
+    cfg.deepspeed_applied = True  # train() then skips the launcher's DBX_DEEPSPEED_CONFIG env copy
     return cfg

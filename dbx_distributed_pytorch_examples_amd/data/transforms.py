@@ -176,7 +176,7 @@ class ToTensor:
         a = np.asarray(_to_pil(img) if not isinstance(img, np.ndarray) else img)
         if a.ndim == 2:
             a = a[:, :, None]
-        return torch.from_numpy(np.ascontiguousarray(a.transpose(2, 0, 1))).float().div_(255.0)
+        return torch.from_numpy(np.array(a.transpose(2, 0, 1), copy=True)).float().div_(255.0)
 
 
 class PILToUint8HWC:

@@ -49,6 +49,12 @@ zero_3_offload = _with_zero(3, offload_optimizer={"device": "cpu", "pin_memory":
                             offload_param={"device": "cpu", "pin_memory": True})
 deepspeed_config = zero_1
 
+# the reference module's names (`02_deepspeed/deepspeed_config.py:5-105`)
+shared_parameters = {"gradient_accumulation_steps": 1, "gradient_clipping": 0.3, "per_device_batch_size": 4,
+                     "learning_rate": 2e-4, "warmup_steps": 100}
+deepspeed_base = base_config
+deepspeed_zero_1, deepspeed_zero_2, deepspeed_zero_3, deepspeed_zero_3_offload = zero_1, zero_2, zero_3, zero_3_offload
+
 
 def train_func(*, train_dataset, test_dataset, batch_size: int = 128, num_epochs: int = 1,
                mlflow_parent_run=None, patience: Optional[int] = None, deepspeed_config: Optional[dict] = None,

@@ -27,7 +27,10 @@ def build_torch_step(args, info) -> Tuple[Callable[[], None], Dict]:
     if info.world_size > 1:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
                                                           bucket_cap_mb=25, gradient_as_bucket_view=True)
-    opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5)
+    if getattr(args, "optim", "sgd") == "adamw":
+        opt = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=0.01)
+    else:
+        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5)
     x8, y = synthetic_uint8_batch(args.batch, args.image_size, args.num_classes, dev, seed=info.rank)
     mean = torch.tensor(IMAGENET_MEAN, device=dev).view(1, 3, 1, 1) * 255.0
     std = torch.tensor(IMAGENET_STD, device=dev).view(1, 3, 1, 1) * 255.0

@@ -246,7 +246,7 @@ def _pick_engine(cfg: TrainConfig, model, ds, dev) -> str:
 
 def _apply_env_overrides(cfg: TrainConfig) -> TrainConfig:
     ds_json = os.environ.get("DBX_DEEPSPEED_CONFIG")
-    if ds_json:
+    if ds_json and not getattr(cfg, "deepspeed_applied", False):
         cfg = from_deepspeed(json.loads(ds_json), cfg)
     return cfg
 

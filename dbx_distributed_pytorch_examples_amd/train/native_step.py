@@ -13,11 +13,14 @@ def build_native_step(args, info):
     dev = info.device
     torch.manual_seed(0)  # identical init on every rank (DDP also broadcasts from rank 0)
     model = build_model(args.model, num_classes=args.num_classes)
-    opt = OptimConfig(name="sgd", lr=args.lr, momentum=0.9, weight_decay=5e-5)
+    if getattr(args, "optim", "sgd") == "adamw":
+        opt = OptimConfig(name="adamw", lr=args.lr, weight_decay=0.01)
+    else:
+        opt = OptimConfig(name="sgd", lr=args.lr, momentum=0.9, weight_decay=5e-5)
     use_graphs = os.environ.get("DBX_GRAPHS", "1") == "1"
     ar_dtype = torch.bfloat16 if os.environ.get("DBX_ALLREDUCE_BF16", "0") == "1" else torch.float32
     tr = NativeTrainer(model, args.batch, (args.image_size, args.image_size), dev, optim=opt,
-                       use_graphs=use_graphs, allreduce_dtype=ar_dtype)
+                       use_graphs=use_graphs, allreduce_dtype=ar_dtype, zero_stage=getattr(args, "zero", 0))
     g = torch.Generator(device="cpu").manual_seed(1000 + info.rank)
     img = torch.randint(0, 256, (args.batch, args.image_size, args.image_size, 3), dtype=torch.uint8, generator=g)
     lab = torch.randint(0, args.num_classes, (args.batch,), dtype=torch.int64, generator=g)

@@ -1,0 +1,37 @@
+"""The example scripts (one per reference notebook) run end to end on CPU/gloo with tiny
+synthetic datasets. ImageNet-224 / TinyImageNet variants are exercised by their frontends' tests
+and the GPU bench; here the fast ones run as subprocesses exactly as a user would launch them."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXAMPLES = [
+    "01_torch_distributor/01_basic_mnist.py",
+    "01_torch_distributor/02_cifar_resnet.py",
+    "01_torch_distributor/03a_tiny_imagenet_mds.py",
+    "02_deepspeed/01_cifar_deepspeed.py",
+    "03_composer/01_cifar_composer.py",
+    "04_accelerate/01_cifar_accelerate.py",
+    "05_ray/01_fashion_mnist_ray.py",
+    "05_ray/02_cifar_ray.py",
+]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("script", EXAMPLES)
+def test_example_runs_on_cpu(script, tmp_path):
+    env = dict(os.environ, DBX_MLRUNS=str(tmp_path / "mlruns"), PYTHONWARNINGS="ignore")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", script), "--cpu", "--samples", "32",
+                        "--batch-size", "8", "--out", str(tmp_path)], env=env, capture_output=True, text=True,
+                       timeout=540)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+def test_native_example_cli_prints_config():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "06_native", "resnet50_imagenet.py"),
+                        os.path.join(ROOT, "configs", "resnet50_imagenet_8192.yaml"), "--print-config"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and '"batch_size": 1024' in r.stdout
