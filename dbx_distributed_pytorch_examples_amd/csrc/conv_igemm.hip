@@ -300,24 +300,37 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   }
   constexpr int CPR = BN / 8;  // 16B chunks per output row; a thread's chunk column is fixed
   const int ccol = tid % CPR;
-  float bs[8], bq1[8], bq2[8];               // BN-backward partial sums of this thread's 8 channels
-  float e_m1[8], e_i1[8], e_m2[8], e_i2[8], e_sc[8], e_sh[8];
+  float bs[8], bq1[8], bq2[8];  // BN-backward partial sums of this thread's 8 channels
+  f32x4 e_m1[2], e_i1[2], e_m2[2], e_i2[2], e_sc[2], e_sh[2];
+  const bool has2 = EPI > 0 && a.ybn2 != nullptr;  // wave-uniform: second BN (downsample branch)
   if constexpr (EPI > 0) {
+    // vector loads of the per-channel coefficients; absent ones read a valid stand-in (no branch)
     const int c0 = n0 + ccol * 8;
+    const float* m2 = has2 ? a.mean2 : a.mean1;
+    const float* i2 = has2 ? a.inv2 : a.inv1;
+    const float* sc = (EPI == 2) ? a.bsc : a.mean1;
+    const float* sh = (EPI == 2) ? a.bsh : a.inv1;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bs[j] = bq1[j] = bq2[j] = 0.f;
-      e_m1[j] = a.mean1[c0 + j]; e_i1[j] = a.inv1[c0 + j];
-      e_m2[j] = a.ybn2 ? a.mean2[c0 + j] : 0.f; e_i2[j] = a.ybn2 ? a.inv2[c0 + j] : 0.f;
-      e_sc[j] = (EPI == 2) ? a.bsc[c0 + j] : 0.f; e_sh[j] = (EPI == 2) ? a.bsh[c0 + j] : 0.f;
+    for (int h = 0; h < 2; ++h) {
+      e_m1[h] = *reinterpret_cast<const f32x4*>(a.mean1 + c0 + 4 * h);
+      e_i1[h] = *reinterpret_cast<const f32x4*>(a.inv1 + c0 + 4 * h);
+      e_m2[h] = *reinterpret_cast<const f32x4*>(m2 + c0 + 4 * h);
+      e_i2[h] = *reinterpret_cast<const f32x4*>(i2 + c0 + 4 * h);
+      e_sc[h] = *reinterpret_cast<const f32x4*>(sc + c0 + 4 * h);
+      e_sh[h] = *reinterpret_cast<const f32x4*>(sh + c0 + 4 * h);
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bs[j] = bq1[j] = bq2[j] = 0.f;
   }
-  // Epilogue in groups of EG rows per thread: ALL global loads of a group (residual addend, mask
-  // reference, BN inputs) are issued before any store, so their latencies overlap instead of
-  // serialising behind the previous row's store (the compiler cannot reorder them across stores
-  // to possibly-aliasing pointers).
+  // Epilogue in groups of EG rows per thread, in three straight-line phases: (1) every global load
+  // of the group (residual addend, mask reference, BN inputs) — rows past M and absent addends read
+  // a valid stand-in address instead of branching; (2) all arithmetic; (3) all stores. No load is
+  // consumed after a store is issued and no load sits under divergent control flow, so hipcc waits
+  // with counted vmcnt instead of draining the queue (stores count in vmcnt too) once per row.
   constexpr int NIT = BM * CPR / NT;
-  constexpr int EG = NIT < 4 ? NIT : 4;
+  constexpr int EGMAX = (EPI == 1 || (ACCUM && EPI != 0)) ? 4 : 8;
+  constexpr int EG = NIT < EGMAX ? NIT : EGMAX;
+  const bool sub_geom = MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1));  // wave-uniform
 #pragma unroll
   for (int g0 = 0; g0 < NIT; g0 += EG) {
     u32x4 vv[EG], va[EG], vm[EG], vy[EG], vy2[EG];
@@ -325,19 +338,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     bool ok[EG], has_add[EG];
 #pragma unroll
     for (int k = 0; k < EG; ++k) {
-      const int it = g0 + k;
-      const int row = (tid + it * NT) / CPR;
+      const int row = (tid + (g0 + k) * NT) / CPR;
       const int m = m0 + row;
       ok[k] = m < a.M;
-      has_add[k] = false;
+      const int mc = ok[k] ? m : m0;  // m0 < M for every launched tile
       vv[k] = *reinterpret_cast<const u32x4*>(sC + row * (BN + 8) + ccol * 8);
-      if (!ok[k]) continue;
-      size_t pix = (size_t)m;
-      int ph = 0, pw = 0;
-      long long nimg = 0;
-      if (MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1))) {
+      size_t pix = (size_t)mc;
+      int ph = 0, pw = 0, nimg = 0;
+      if (sub_geom) {
         const int ohw = a.OH * a.OW;
-        const int n = m / ohw, pq = m - (m / ohw) * ohw;
+        const int n = mc / ohw, pq = mc - n * ohw;
         const int i = pq / a.OW, j = pq - (pq / a.OW) * a.OW;
         ph = i * a.osub + a.oph; pw = j * a.osub + a.opw;
         nimg = n;
@@ -346,35 +356,33 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       const size_t e = pix * a.OC + n0 + ccol * 8;
       ee[k] = e;
       if constexpr (ACCUM) {
-        const bf16* src = nullptr;
-        if (a.addsrc == nullptr) src = a.y + e;
-        else if (a.add_sub <= 1) src = a.addsrc + e;
-        else if ((ph % a.add_sub) == 0 && (pw % a.add_sub) == 0) {
+        size_t ae = e;
+        bool hv = true;
+        if (a.add_sub > 1) {
+          hv = (ph % a.add_sub) == 0 && (pw % a.add_sub) == 0;
           const int hh = a.FH / a.add_sub, ww = a.FW / a.add_sub;
-          src = a.addsrc + (((size_t)nimg * hh + ph / a.add_sub) * ww + pw / a.add_sub) * a.OC + n0 + ccol * 8;
+          ae = hv ? (((size_t)nimg * hh + ph / a.add_sub) * ww + pw / a.add_sub) * a.OC + n0 + ccol * 8 : 0;
         }
-        if (src) { va[k] = *reinterpret_cast<const u32x4*>(src); has_add[k] = true; }
+        has_add[k] = hv;
+        va[k] = *reinterpret_cast<const u32x4*>((a.addsrc ? a.addsrc : a.y) + ae);
       }
       if constexpr (EPI > 0) {
         vy[k] = *reinterpret_cast<const u32x4*>(a.ybn + e);
         if constexpr (EPI == 1) vm[k] = *reinterpret_cast<const u32x4*>(a.mref + e);
-        if (a.ybn2) vy2[k] = *reinterpret_cast<const u32x4*>(a.ybn2 + e);
+        vy2[k] = *reinterpret_cast<const u32x4*>((has2 ? a.ybn2 : a.ybn) + e);
       }
     }
 #pragma unroll
     for (int k = 0; k < EG; ++k) {
-      if (!ok[k]) continue;
       u32x4 v = vv[k];
       if constexpr (ACCUM || EPI > 0) {
         float f[8];
         unpack8(v, f);
         if constexpr (ACCUM) {
-          if (has_add[k]) {
-            float g[8];
-            unpack8(va[k], g);
+          float g[8];
+          unpack8(va[k], g);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] += g[j];
-          }
+          for (int j = 0; j < 8; ++j) f[j] += has_add[k] ? g[j] : 0.f;
         }
         if constexpr (EPI > 0) {
           float yv[8];
@@ -386,24 +394,29 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
             for (int j = 0; j < 8; ++j) f[j] = mr[j] > 0.f ? f[j] : 0.f;
           } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = (yv[j] * e_sc[j] + e_sh[j]) > 0.f ? f[j] : 0.f;
+            for (int j = 0; j < 8; ++j) f[j] = (yv[j] * e_sc[j >> 2][j & 3] + e_sh[j >> 2][j & 3]) > 0.f ? f[j] : 0.f;
           }
           v = pack8(f);
           unpack8(v, f);  // statistics of the values actually stored (bf16-rounded)
+          const float w = ok[k] ? 1.f : 0.f;  // rows past M contribute nothing
+          float y2[8];
+          unpack8(vy2[k], y2);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { bs[j] += f[j]; bq1[j] += f[j] * (yv[j] - e_m1[j]) * e_i1[j]; }
-          if (a.ybn2) {
-            float y2[8];
-            unpack8(vy2[k], y2);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) bq2[j] += f[j] * (y2[j] - e_m2[j]) * e_i2[j];
+          for (int j = 0; j < 8; ++j) {
+            const float fw = f[j] * w;
+            bs[j] += fw;
+            bq1[j] += fw * (yv[j] - e_m1[j >> 2][j & 3]) * e_i1[j >> 2][j & 3];
+            bq2[j] += fw * (y2[j] - e_m2[j >> 2][j & 3]) * e_i2[j >> 2][j & 3];
           }
         } else {
           v = pack8(f);
         }
       }
-      *reinterpret_cast<u32x4*>(a.y + ee[k]) = v;
+      vv[k] = v;
     }
+#pragma unroll
+    for (int k = 0; k < EG; ++k)
+      if (ok[k]) *reinterpret_cast<u32x4*>(a.y + ee[k]) = vv[k];
   }
   if constexpr (EPI > 0) {
     // reduce the per-thread partials over threads with the same chunk column: in-wave lanes
