@@ -331,6 +331,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   constexpr int EGMAX = (EPI == 1 || (ACCUM && EPI != 0)) ? 4 : 8;
   constexpr int EG = NIT < EGMAX ? NIT : EGMAX;
   const bool sub_geom = MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1));  // wave-uniform
+  const bool tail = m0 + BM > a.M;                                                  // wave-uniform
 #pragma unroll
   for (int g0 = 0; g0 < NIT; g0 += EG) {
     u32x4 vv[EG], va[EG], vm[EG], vy[EG], vy2[EG];
@@ -398,15 +399,22 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
           }
           v = pack8(f);
           unpack8(v, f);  // statistics of the values actually stored (bf16-rounded)
-          const float w = ok[k] ? 1.f : 0.f;  // rows past M contribute nothing
-          float y2[8];
-          unpack8(vy2[k], y2);
+          if (tail && !ok[k]) {  // rows past M contribute nothing (wave-uniform guard: last tile only)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = 0.f;
+          }
+          // raw moments: sum g, sum g*y (and g*y2); the centring/scaling by (mean, invstd) is
+          // applied once per channel after the reduction: sum g*xhat = inv * (sum g*y - mean * sum g)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float fw = f[j] * w;
-            bs[j] += fw;
-            bq1[j] += fw * (yv[j] - e_m1[j >> 2][j & 3]) * e_i1[j >> 2][j & 3];
-            bq2[j] += fw * (y2[j] - e_m2[j >> 2][j & 3]) * e_i2[j >> 2][j & 3];
+            bs[j] += f[j];
+            bq1[j] += f[j] * yv[j];
+          }
+          if (has2) {
+            float y2[8];
+            unpack8(vy2[k], y2);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bq2[j] += f[j] * y2[j];
           }
         } else {
           v = pack8(f);
@@ -447,6 +455,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       for (int w = 0; w < NW; ++w) {
         s += red[(w * 3 + 0) * BN + tid]; q1 += red[(w * 3 + 1) * BN + tid]; q2 += red[(w * 3 + 2) * BN + tid];
       }
+      const int c = n0 + tid;  // raw moments -> sum g*xhat
+      q1 = a.inv1[c] * (q1 - a.mean1[c] * s);
+      if (has2) q2 = a.inv2[c] * (q2 - a.mean2[c] * s);
       const int shard = (blockIdx.x % a.nshard);
       float* st1 = a.bstats1 + (size_t)shard * 2 * a.OC;
       atomicAdd(st1 + n0 + tid, s);
