@@ -24,6 +24,7 @@ Supported module trees: ``models.ResNet`` (BasicBlock / Bottleneck, any in_chann
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -132,6 +133,9 @@ class ResNetProgram:
         self.norm_std = tuple(std) if std else None
         self.dev = device
         self.in_ch = model.conv1.in_channels
+        self.overlap_wgrad = os.environ.get("DBX_OVERLAP_WGRAD", "1") == "1"
+        self._wstream = None
+        self._side_pending = False
         self._build_layers()
         self._alloc_params()
         self._alloc_activations()
@@ -461,8 +465,34 @@ class ResNetProgram:
             idx = list(reversed(stages[li]))
             segs.append((f"layer{li}", (lambda idx=idx: [self._bwd_block(i) for i in idx])))
         segs.append(("stem", self._bwd_stem))
-        self._segments = segs
-        return segs
+        # every segment ends with its weight gradients complete on the main stream (join)
+        self._segments = [(n, (lambda fn=fn: (fn(), self._join_side()))) for n, fn in segs]
+        return self._segments
+
+    # --------------------------------------------------------------------------------------
+    # wgrad overlap: a conv's weight gradient depends only on its dY and X, not on the dgrad
+    # chain, so it runs on a side stream while the main stream continues with the (memory-bound)
+    # dgrad epilogue / BN-backward kernels of the same and next layers. Forked and joined with
+    # stream waits, which HIP-graph capture records as parallel branches of the step graph.
+    # (Measured +0.4 % in graphs, +1 % eager at batch 1024: every launch already fills the GPU.)
+    def _side(self, fn):
+        if self.dev.type != "cuda" or not self.overlap_wgrad:
+            fn()
+            return
+        if self._wstream is None:
+            self._wstream = torch.cuda.Stream(device=self.dev)
+        self._wstream.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self._wstream):
+            fn()
+        self._side_pending = True
+
+    def _wgrad(self, *args, **kw):
+        self._side(lambda: K.conv_wgrad(*args, **kw))
+
+    def _join_side(self):
+        if self._side_pending:
+            torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
+            self._side_pending = False
 
     def _bwd_head(self):
         # fc: dW = dlogits^T @ pooled (fp32 accumulate), db = sum dlogits, dpooled = dlogits @ W
@@ -512,8 +542,8 @@ class ResNetProgram:
         # accumulates that BN's backward statistics
         for j in range(nconv - 1, 0, -1):
             cv, pbn, pc = b.convs[j], b.bns[j - 1], b.convs[j - 1]
-            K.conv_wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
-                         in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
+            self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                        in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
             K.conv_dgrad(b.dys[j], cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                          epilogue=K.BNBwdEpilogue(K.MASK_Y, b.ys[j - 1], pbn.mean, pbn.invstd, pbn.bstats,
                                                   scale=pbn.scale, shift=pbn.shift))
@@ -522,10 +552,10 @@ class ResNetProgram:
             K.bn_bwd_apply(b.das[j - 1], b.ys[j - 1], pbn.coeff, b.dys[j - 1], mask_mode=K.MASK_NONE)
         # first conv: wgrad, then the block-input gradient = dgrad(conv1) + shortcut gradient
         c0 = b.convs[0]
-        K.conv_wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
+        self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
         if b.ds_conv is not None:
             dc = b.ds_conv
-            K.conv_wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
+            self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
             # 1x1 strided downsample: its dgrad is a dense GEMM onto the stride-subsampled pixels
             K.conv_dgrad(b.dyd, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0)
             addsrc, sub = b.dsbuf, dc.stride
@@ -547,10 +577,12 @@ class ResNetProgram:
         st, sbn = self.stem, self.stem_bn
         K.maxpool_bwd(self.blocks[0].dx, self.parg, self.da0, K=self.pool_k, stride=self.pool_s, pad=self.pool_p)
         self._bn_bwd(sbn, self.da0, self.y0, self.dy0, self.N * st.OH * st.OW, K.MASK_Y)
-        K.conv_wgrad(self.dy0, self.x4, self.stem_grad_tmp, self.ws, R=st.R, S=st.S, stride=st.stride,
-                     pad=st.pad, stem=True)
-        g = self.grad[st.off:st.off + st.numel].view(st.OC, st.R, st.S, st.IC)
-        g.copy_(self.stem_grad_tmp.view(st.OC, 8, 8, 4)[:, :st.R, :st.S, :st.IC])
+        def stem_wgrad():
+            K.conv_wgrad(self.dy0, self.x4, self.stem_grad_tmp, self.ws, R=st.R, S=st.S, stride=st.stride,
+                         pad=st.pad, stem=True)
+            g = self.grad[st.off:st.off + st.numel].view(st.OC, st.R, st.S, st.IC)
+            g.copy_(self.stem_grad_tmp.view(st.OC, 8, 8, 4)[:, :st.R, :st.S, :st.IC])
+        self._side(stem_wgrad)
 
     def backward(self):
         for _, fn in self._segments:
