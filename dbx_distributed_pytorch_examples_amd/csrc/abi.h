@@ -20,10 +20,11 @@ struct IGemmArgs {
   // addsrc == null -> the output itself
   const bf16* addsrc;
   int add_sub;
-  // BN-backward epilogue (EPI 1: mask = mref > 0; EPI 2: mask = ybn*bsc + bsh > 0):
+  // BN-backward epilogue (EPI 1: mask = bit of mbits, the 1-bit ReLU mask of the block output
+  // written by bn_apply; EPI 2: mask = ybn*bsc + bsh > 0):
   // g = mask * out (written instead of out), bstats1 += [sum g, sum g*(ybn-mean1)*inv1],
   // bstats2 += [0, sum g*(ybn2-mean2)*inv2] (second BN fed by the same gradient, nullable)
-  const bf16* mref;
+  const unsigned char* mbits;  // [M][OC/8] bytes, bit j of byte (pix, c/8) = channel c
   const bf16* ybn;
   const bf16* ybn2;
   const float* bsc;

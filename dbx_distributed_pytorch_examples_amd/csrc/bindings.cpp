@@ -22,7 +22,7 @@ int dbx_bn_finalize(const float*, int, int, float, const float*, const float*, f
 int dbx_bn_eval_coeff(int, const float*, const float*, float, const float*, const float*, float*, float*, hipStream_t);
 int dbx_channel_stats(const bf16*, long long, int, float*, int, hipStream_t);
 int dbx_bn_apply(const bf16*, const float*, const float*, const bf16*, const float*, const float*, bf16*, long long, int,
-                 int, int, hipStream_t);
+                 int, int, unsigned char*, hipStream_t);
 int dbx_bn_bwd_reduce(const bf16*, const bf16*, const bf16*, const float*, const float*, const float*, const float*,
                       long long, int, float*, int, int, hipStream_t);
 int dbx_bn_bwd_coeff(const float*, int, int, float, const float*, const float*, const float*, float*, float*, float*,
@@ -70,13 +70,13 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t in_shift, int relu_in, uintptr_t stats, int nshard, int N, int IH, int IW, int IC,
                          int OH, int OW, int OC, int R, int S_, int stride, int pad, int accum, int nr, int ns, int r0,
                          int s0, int tstep, int dh0, int dw0, int osub, int oph, int opw, int FH, int FW,
-                         uintptr_t addsrc, int add_sub, int epi, uintptr_t mref, uintptr_t ybn, uintptr_t ybn2,
+                         uintptr_t addsrc, int add_sub, int epi, uintptr_t mbits, uintptr_t ybn, uintptr_t ybn2,
                          uintptr_t bsc, uintptr_t bsh, uintptr_t mean1, uintptr_t inv1, uintptr_t mean2,
                          uintptr_t inv2, uintptr_t bstats1, uintptr_t bstats2, uintptr_t st) {
     dbx::IGemmArgs a{P<const bf16*>(x), P<const bf16*>(w), P<bf16*>(y), P<const float*>(in_scale),
                      P<const float*>(in_shift), P<float*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
                      N * OH * OW, nshard > 0 ? nshard : 1, relu_in, nr, ns, r0, s0, tstep, dh0, dw0, osub, oph, opw,
-                     FH, FW, P<const bf16*>(addsrc), add_sub, P<const bf16*>(mref), P<const bf16*>(ybn),
+                     FH, FW, P<const bf16*>(addsrc), add_sub, P<const unsigned char*>(mbits), P<const bf16*>(ybn),
                      P<const bf16*>(ybn2), P<const float*>(bsc), P<const float*>(bsh), P<const float*>(mean1),
                      P<const float*>(inv1), P<const float*>(mean2), P<const float*>(inv2), P<float*>(bstats1),
                      P<float*>(bstats2)};
@@ -111,9 +111,10 @@ PYBIND11_MODULE(_C, m) {
     check(dbx_channel_stats(P<const bf16*>(y), M, C, P<float*>(stats), nshard, S(st)), "channel_stats");
   });
   m.def("bn_apply", [](uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t res, uintptr_t rsc, uintptr_t rsh,
-                       uintptr_t out, long long n, int C, int res_mode, int relu, uintptr_t st) {
+                       uintptr_t out, long long n, int C, int res_mode, int relu, uintptr_t mbits, uintptr_t st) {
     check(dbx_bn_apply(P<const bf16*>(y), P<const float*>(sc), P<const float*>(sh), P<const bf16*>(res),
-                       P<const float*>(rsc), P<const float*>(rsh), P<bf16*>(out), n, C, res_mode, relu, S(st)),
+                       P<const float*>(rsc), P<const float*>(rsh), P<bf16*>(out), n, C, res_mode, relu,
+                       P<unsigned char*>(mbits), S(st)),
           "bn_apply");
   });
   m.def("bn_bwd_reduce", [](uintptr_t dout, uintptr_t mref, uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t mean,

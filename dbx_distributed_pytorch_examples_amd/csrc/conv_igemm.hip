@@ -334,7 +334,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   const bool tail = m0 + BM > a.M;                                                  // wave-uniform
 #pragma unroll
   for (int g0 = 0; g0 < NIT; g0 += EG) {
-    u32x4 vv[EG], va[EG], vm[EG], vy[EG], vy2[EG];
+    u32x4 vv[EG], va[EG], vy[EG], vy2[EG];
+    unsigned vm[EG];  // EPI 1: this chunk's 8 mask bits
     size_t ee[EG];
     bool ok[EG], has_add[EG];
 #pragma unroll
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       }
       if constexpr (EPI > 0) {
         vy[k] = *reinterpret_cast<const u32x4*>(a.ybn + e);
-        if constexpr (EPI == 1) vm[k] = *reinterpret_cast<const u32x4*>(a.mref + e);
+        if constexpr (EPI == 1) vm[k] = a.mbits[e >> 3];
         vy2[k] = *reinterpret_cast<const u32x4*>((has2 ? a.ybn2 : a.ybn) + e);
       }
     }
@@ -389,10 +390,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
           float yv[8];
           unpack8(vy[k], yv);
           if constexpr (EPI == 1) {
-            float mr[8];
-            unpack8(vm[k], mr);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = mr[j] > 0.f ? f[j] : 0.f;
+            for (int j = 0; j < 8; ++j) f[j] = ((vm[k] >> j) & 1u) ? f[j] : 0.f;
           } else {
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] = (yv[j] * e_sc[j >> 2][j & 3] + e_sh[j >> 2][j & 3]) > 0.f ? f[j] : 0.f;
@@ -827,7 +826,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
   if (mode == DGRAD) {
     if (pro || stats) return -2;
     if (epi && (a.ybn == nullptr || a.bstats1 == nullptr || a.mean1 == nullptr || a.inv1 == nullptr)) return -6;
-    if (epi == 1 && a.mref == nullptr) return -6;
+    if (epi == 1 && a.mbits == nullptr) return -6;
     if (epi == 2 && (a.bsc == nullptr || a.bsh == nullptr)) return -6;
     DBX_TILES(dispatch_dgrad, a, accum, epi, st)
     return -3;

@@ -130,7 +130,7 @@ template <int RES, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ sc,
                                 const float* __restrict__ sh, const bf16* __restrict__ res,
                                 const float* __restrict__ rsc, const float* __restrict__ rsh,
-                                bf16* __restrict__ out, long long M, int C) {
+                                bf16* __restrict__ out, unsigned char* __restrict__ mbits, long long M, int C) {
   const RowMap rm(C);
   if (rm.r0 >= rm.rpb) return;
   const int c0 = rm.cg * 8;
@@ -154,7 +154,16 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
     }
-    *reinterpret_cast<u32x4*>(out + e) = pack8(f);
+    const u32x4 o = pack8(f);
+    *reinterpret_cast<u32x4*>(out + e) = o;
+    if (RELU && mbits) {  // 1-bit ReLU mask of the stored (bf16) values, for the backward pass
+      float q[8];
+      unpack8(o, q);
+      unsigned bits = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bits |= (q[j] > 0.f ? 1u : 0u) << j;
+      mbits[e >> 3] = (unsigned char)bits;
+    }
   }
 }
 
@@ -670,11 +679,12 @@ extern "C" int dbx_channel_stats(const bf16* y, long long M, int C, float* stats
   RET_LAST;
 }
 extern "C" int dbx_bn_apply(const bf16* y, const float* sc, const float* sh, const bf16* res, const float* rsc,
-                            const float* rsh, bf16* out, long long n, int C, int res_mode, int relu, hipStream_t st) {
+                            const float* rsh, bf16* out, long long n, int C, int res_mode, int relu,
+                            unsigned char* mbits, hipStream_t st) {
   if (n % C || C % 8 || C / 8 > 256) return -1;
   const long long M = n / C;
   const dim3 g(grid_for(M, 256 / (C / 8), 4096)), b(256);
-#define BA(R, A) hipLaunchKernelGGL((bn_apply_kernel<R, A>), g, b, 0, st, y, sc, sh, res, rsc, rsh, out, M, C)
+#define BA(R, A) hipLaunchKernelGGL((bn_apply_kernel<R, A>), g, b, 0, st, y, sc, sh, res, rsc, rsh, out, mbits, M, C)
   if (res_mode == 0) { if (relu) BA(0, true); else BA(0, false); }
   else if (res_mode == 1) { if (relu) BA(1, true); else BA(1, false); }
   else { if (relu) BA(2, true); else BA(2, false); }

@@ -334,6 +334,9 @@ class ResNetProgram:
                 b.dsbuf = E(N, dcv.OH, dcv.OW, dcv.IC)  # dense dgrad of the strided 1x1
             oh, ow, oc = b.out_shape
             b.out = E(N, oh, ow, oc)
+            # 1-bit ReLU mask of the block output (the next block's dgrad epilogue masks with it:
+            # 1/16 of the bytes of re-reading the bf16 output)
+            b.obits = torch.empty(N * oh * ow * oc // 8, device=dev, dtype=torch.uint8)
         for cv in self.convs:
             ktot = 256 if cv.stem else cv.R * cv.S * cv.IC
             wsmax = max(wsmax, cv.OC * ktot)
@@ -406,8 +409,10 @@ class ResNetProgram:
             K.bn_eval_coeff(bn.gamma, bn.beta, mod.eps, mod.running_mean, mod.running_var, bn.scale, bn.shift)
 
     def forward(self, smoothing: float = 0.0, compute_grad: bool = True, grad_scale: float = 1.0,
-                metrics: bool = True):
-        """Full forward incl. loss. Assumes x4 / labels filled and prepare_weights() done."""
+                metrics: bool = True, features_only: bool = False):
+        """Full forward incl. loss. Assumes x4 / labels filled and prepare_weights() done.
+        ``features_only``: stop after global average pooling and return ``self.pooled`` [N, C]
+        (frozen-backbone feature extraction; the fc / loss are left to the caller)."""
         tr = self.training
         if tr:
             self.stats_region.zero_()
@@ -436,11 +441,13 @@ class ResNetProgram:
                            stats=b.ds_bn.stats if tr else None)
                 self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
                 K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=b.yd, res_scale=b.ds_bn.scale,
-                           res_shift=b.ds_bn.shift, relu=True)
+                           res_shift=b.ds_bn.shift, relu=True, mbits=b.obits if tr else None)
             else:
-                K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=x, relu=True)
+                K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=x, relu=True, mbits=b.obits if tr else None)
             x = b.out
         K.avgpool_fwd(x, self.pooled)
+        if features_only:
+            return self.pooled
         torch.addmm(self.fc_b16, self.pooled, self.fc_w16.t(), out=self.logits)
         K.softmax_ce(self.logits, self.labels, self.dlogits if compute_grad else None, None,
                      self.metrics if metrics else None, smoothing=smoothing, grad_scale=grad_scale)
@@ -565,7 +572,7 @@ class ResNetProgram:
         if i > 0:
             pb = self.blocks[i - 1]
             epi = K.BNBwdEpilogue(K.MASK_OUT, pb.ys[-1], pb.bns[-1].mean, pb.bns[-1].invstd, pb.bns[-1].bstats,
-                                  mref=pb.out,
+                                  mbits=pb.obits,
                                   ybn2=pb.yd if pb.ds_conv is not None else None,
                                   mean2=pb.ds_bn.mean if pb.ds_conv is not None else None,
                                   inv2=pb.ds_bn.invstd if pb.ds_conv is not None else None,

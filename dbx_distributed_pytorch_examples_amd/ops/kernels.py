@@ -21,7 +21,7 @@ from . import reference as _ref
 from ._ext import C, stream_ptr, use_native
 
 FWD, DGRAD, STEM = 0, 1, 2
-# addsrc, add_sub, epi, mref, ybn, ybn2, bsc, bsh, mean1, inv1, mean2, inv2, bstats1, bstats2
+# addsrc, add_sub, epi, mbits, ybn, ybn2, bsc, bsh, mean1, inv1, mean2, inv2, bstats1, bstats2
 _NO_EPI = (0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
 MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
 
@@ -156,19 +156,20 @@ def dgrad_phases(H: int, W: int, R: int, S: int, stride: int, pad: int):
 
 class BNBwdEpilogue:
     """Fused BN-backward epilogue for a dgrad: the dgrad result X (plus any residual addend) is
-    masked — by ``mref > 0`` (mode MASK_OUT: the ReLU after a residual add, mref = block output)
+    masked — by the 1-bit mask ``mbits`` (mode MASK_OUT: the ReLU after a residual add, bits written
+    by ``bn_apply(..., mbits=)`` for the block output)
     or by ``ybn*scale+shift > 0`` (MASK_Y: the ReLU after this BN) — and written as g, while
     ``stats1 += [sum g, sum g*xhat(ybn)]`` (and ``stats2 += [sum g, sum g*xhat(ybn2)]`` for a second
     BN fed by the same gradient: the downsample branch). Replaces a separate reduction pass."""
 
-    def __init__(self, mode, ybn, mean1, inv1, stats1, mref=None, scale=None, shift=None,
+    def __init__(self, mode, ybn, mean1, inv1, stats1, mbits=None, scale=None, shift=None,
                  ybn2=None, mean2=None, inv2=None, stats2=None):
         self.mode, self.ybn, self.mean1, self.inv1, self.stats1 = mode, ybn, mean1, inv1, stats1
-        self.mref, self.scale, self.shift = mref, scale, shift
+        self.mbits, self.scale, self.shift = mbits, scale, shift
         self.ybn2, self.mean2, self.inv2, self.stats2 = ybn2, mean2, inv2, stats2
 
     def args(self):
-        return (self.mode, _p(self.mref), _p(self.ybn), _p(self.ybn2), _p(self.scale), _p(self.shift),
+        return (self.mode, _p(self.mbits), _p(self.ybn), _p(self.ybn2), _p(self.scale), _p(self.shift),
                 _p(self.mean1), _p(self.inv1), _p(self.mean2), _p(self.inv2), _p(self.stats1), _p(self.stats2))
 
 
@@ -223,7 +224,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         _chk(e.ybn, torch.bfloat16, "ybn", dx.numel())
         _chk(e.stats1, torch.float32, "stats1", NSHARD * 2 * Cc)
         if e.mode == MASK_OUT:
-            _chk(e.mref, torch.bfloat16, "mref", dx.numel())
+            _chk(e.mbits, torch.uint8, "mbits", dx.numel() // 8)
         if e.ybn2 is not None:
             _chk(e.ybn2, torch.bfloat16, "ybn2", dx.numel())
             _chk(e.stats2, torch.float32, "stats2", NSHARD * 2 * Cc)
@@ -345,7 +346,9 @@ def channel_stats(y, stats):
 
 
 @_dispatch
-def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True):
+def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True, mbits=None):
+    """out = relu(y*scale + shift [+ res | + res*res_scale + res_shift]); ``mbits`` (uint8,
+    numel/8): also store the 1-bit ReLU mask (bit j of byte i = element 8i+j > 0) for backward."""
     Cc = y.shape[-1]
     _chk(y, torch.bfloat16, "y")
     _chk(out, torch.bfloat16, "out", y.numel())
@@ -353,8 +356,10 @@ def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, 
     if res is not None:
         _chk(res, torch.bfloat16, "res", y.numel())
         mode = 2 if res_scale is not None else 1
+    if mbits is not None:
+        _chk(mbits, torch.uint8, "mbits", y.numel() // 8)
     C().bn_apply(y.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(res), _p(res_scale), _p(res_shift),
-                 out.data_ptr(), y.numel(), Cc, mode, int(relu), stream_ptr())
+                 out.data_ptr(), y.numel(), Cc, mode, int(relu), _p(mbits), stream_ptr())
     return out
 
 
@@ -511,3 +516,15 @@ def cast_f32_bf16(x, y):
     _chk(x, torch.float32, "x")
     _chk(y, torch.bfloat16, "y", x.numel())
     C().cast_f32_bf16(x.data_ptr(), y.data_ptr(), x.numel(), stream_ptr())
+
+
+def pack_mask_bits(x: torch.Tensor) -> torch.Tensor:
+    """uint8 [numel/8]: bit j of byte i = (x.flat[8i+j] > 0) — the layout bn_apply(mbits=) writes."""
+    b = (x.reshape(-1, 8) > 0).to(torch.uint8)
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=x.device)
+    return (b * w).sum(1, dtype=torch.int32).to(torch.uint8)
+
+
+def unpack_mask_bits(bits: torch.Tensor, shape) -> torch.Tensor:
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=bits.device)
+    return ((bits.view(-1, 1) & w) != 0).reshape(shape)

@@ -72,7 +72,9 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         e = epilogue
         y = e.ybn.float()
         if e.mode == MASK_OUT:
-            g = g * (e.mref.float() > 0)
+            w = 2 ** torch.arange(8, dtype=torch.int32, device=g.device)
+            bits = (e.mbits.to(torch.int32).view(-1, 1) & w) != 0
+            g = g * bits.reshape(g.shape)
         else:
             g = g * ((y * e.scale + e.shift) > 0)
         g = g.bfloat16().float()
@@ -149,7 +151,7 @@ def channel_stats(y, stats):
     _add_stats(stats, y)
 
 
-def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True):
+def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True, mbits=None):
     f = y.float() * scale + shift
     if res is not None:
         r = res.float()
@@ -159,6 +161,9 @@ def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, 
     if relu:
         f = torch.relu(f)
     out.copy_(f.bfloat16())
+    if mbits is not None:
+        b = (out.reshape(-1, 8).float() > 0).to(torch.int32)
+        mbits.copy_((b * (2 ** torch.arange(8, dtype=torch.int32))).sum(1).to(torch.uint8))
     return out
 
 

@@ -122,13 +122,20 @@ class _Native:
         if cfg.data.dataset in ("cifar10", "cifar"):
             from ..data.transforms import CIFAR_MEAN, CIFAR_STD
             mean, std = CIFAR_MEAN, CIFAR_STD
-        self.tr = NativeTrainer(model, cfg.batch_size, (s, s), dev,
-                                optim=OptimConfig(o.name, o.lr, o.momentum, 0.0, o.nesterov, o.weight_decay,
-                                                  tuple(o.betas), o.eps, o.grad_clip),
-                                label_smoothing=cfg.data.label_smoothing, use_graphs=cfg.graphs,
-                                bucket_cap_mb=cfg.bucket_cap_mb,
-                                allreduce_dtype=torch.bfloat16 if cfg.allreduce_dtype == "bf16" else torch.float32,
-                                src_hw=(h, w), mean=mean, std=std, zero_stage=cfg.zero.stage)
+        from ..models.wrappers import FrozenBackboneClassifier
+        ar = torch.bfloat16 if cfg.allreduce_dtype == "bf16" else torch.float32
+        if isinstance(model, FrozenBackboneClassifier):
+            from ..engine.frozen_trainer import FrozenFeatureTrainer
+            self.tr = FrozenFeatureTrainer(model, cfg.batch_size, (s, s), dev, o,
+                                           label_smoothing=cfg.data.label_smoothing, src_hw=(h, w), mean=mean,
+                                           std=std, bucket_cap_mb=cfg.bucket_cap_mb, allreduce_dtype=ar)
+        else:
+            self.tr = NativeTrainer(model, cfg.batch_size, (s, s), dev,
+                                    optim=OptimConfig(o.name, o.lr, o.momentum, 0.0, o.nesterov, o.weight_decay,
+                                                      tuple(o.betas), o.eps, o.grad_clip),
+                                    label_smoothing=cfg.data.label_smoothing, use_graphs=cfg.graphs,
+                                    bucket_cap_mb=cfg.bucket_cap_mb, allreduce_dtype=ar,
+                                    src_hw=(h, w), mean=mean, std=std, zero_stage=cfg.zero.stage)
         if not cfg.data.augment:
             aug = AugmentSpec()
         elif (h, w) == (s, s) and s <= 64:
@@ -185,7 +192,7 @@ class _Native:
 
     @property
     def model(self):
-        return self.tr.prog.model
+        return getattr(self.tr, "full_model", None) or self.tr.prog.model
 
 
 class _Autograd:
@@ -236,9 +243,13 @@ class _Autograd:
 
 def _pick_engine(cfg: TrainConfig, model, ds, dev) -> str:
     from ..engine.program import supports
+    from ..models.wrappers import FrozenBackboneClassifier
     if cfg.engine in ("native", "autograd"):
         return cfg.engine
-    if dev.type == "cuda" and supports(model) and _uint8_source(ds) and cfg.grad_accum == 1 \
+    frozen = isinstance(model, FrozenBackboneClassifier) and supports(model.resnet) and \
+        not any(p.requires_grad for p in model.resnet.parameters() if p is not None and
+                not any(p is q for q in model.resnet.fc.parameters()))
+    if dev.type == "cuda" and (supports(model) or frozen) and _uint8_source(ds) and cfg.grad_accum == 1 \
             and cfg.data.cutmix_alpha == 0:
         return "native"
     return "autograd"
@@ -382,7 +393,7 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
 
 def _trainer_state(runner) -> Dict[str, Any]:
     tr = runner.tr
-    if hasattr(tr, "prog"):  # native: flat optimizer state
+    if hasattr(tr, "prog") and hasattr(tr, "mom"):  # native: flat optimizer state
         st = {"kind": "native", "mom": tr.mom.detach().cpu(), "step_count": tr.step_count}
         if tr.mom2 is not None:
             st["mom2"] = tr.mom2.detach().cpu()
@@ -396,7 +407,7 @@ def _restore_trainer_state(runner, st):
     if not st:
         return
     tr = runner.tr
-    if st.get("kind") == "native" and hasattr(tr, "prog"):
+    if st.get("kind") == "native" and hasattr(tr, "mom"):
         tr.mom.copy_(st["mom"])
         if "mom2" in st and tr.mom2 is not None:
             tr.mom2.copy_(st["mom2"])

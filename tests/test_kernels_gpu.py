@@ -176,9 +176,12 @@ def test_bn_finalize_apply():
     assert relerr(rv, 0.9 + 0.1 * yf.var(0, unbiased=True)) < 1e-4
     out = torch.empty_like(y)
     res = torch.randn_like(yf).bfloat16()
-    k.bn_apply(y, scale, shift, out, res=res, relu=True)
+    bits = torch.empty(y.numel() // 8, device=dev, dtype=torch.uint8)
+    k.bn_apply(y, scale, shift, out, res=res, relu=True, mbits=bits)
     ref = torch.relu((yf - mean) / torch.sqrt(var + 1e-5) * gamma + beta + res.float())
     assert relerr(out, ref) < 1e-2
+    assert torch.equal(bits, k.pack_mask_bits(out))  # 1-bit ReLU mask of the stored values
+    assert torch.equal(k.unpack_mask_bits(bits, out.shape), out.float() > 0)
     rsc = torch.rand(Cc, device=dev)
     rsh = torch.randn(Cc, device=dev)
     k.bn_apply(y, scale, shift, out, res=res, res_scale=rsc, res_shift=rsh, relu=False)
@@ -432,7 +435,8 @@ def test_conv_dgrad_fused_epilogue(mode, sub, stride):
         st2 = torch.zeros(k.NSHARD * 2 * IC, device=devc)
         epi = None
         if mode:
-            epi = k.BNBwdEpilogue(mode, t(ybn), t(mean), t(inv), st1, mref=t(mref) if mode == 1 else None,
+            epi = k.BNBwdEpilogue(mode, t(ybn), t(mean), t(inv), st1,
+                                  mbits=k.pack_mask_bits(t(mref)) if mode == 1 else None,
                                   scale=t(sc) if mode == 2 else None, shift=t(sh) if mode == 2 else None,
                                   ybn2=t(ybn2) if mode == 1 else None, mean2=t(mean2), inv2=t(inv2),
                                   stats2=st2 if mode == 1 else None)

@@ -98,3 +98,40 @@ def test_segment_ranges_cover_all_params():
         covered[lo:hi] = True
     for name, off, n in tr.prog.param_ranges:
         assert covered[off:off + n].all(), name
+
+
+def test_frozen_backbone_native_features_and_head_step():
+    """FrozenFeatureTrainer: program features == eval-mode torch backbone; only the head trains."""
+    from dbx_distributed_pytorch_examples_amd.config import OptimizerConfig
+    from dbx_distributed_pytorch_examples_amd.engine.frozen_trainer import FrozenFeatureTrainer
+    from dbx_distributed_pytorch_examples_amd.models import FrozenBackboneClassifier
+    torch.manual_seed(0)
+    m = FrozenBackboneClassifier("resnet18", num_classes=5)
+    m.eval()
+    for mod in m.resnet.modules():  # non-trivial running stats
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.1, 0.1)
+            mod.running_var.uniform_(0.5, 1.5)
+    g = torch.Generator().manual_seed(1)
+    img = torch.randint(0, 256, (4, 32, 32, 3), dtype=torch.uint8, generator=g)
+    lab = torch.randint(0, 5, (4,), generator=g)
+    x = (img.permute(0, 3, 1, 2).float() / 255 - torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)) \
+        / torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    with torch.no_grad():
+        r = m.resnet
+        f = r.maxpool(r.relu(r.bn1(r.conv1(x))))
+        f = r.layer4(r.layer3(r.layer2(r.layer1(f))))
+        ref = torch.flatten(r.avgpool(f), 1)
+    backbone_before = [p.detach().clone() for n, p in m.resnet.named_parameters() if not n.startswith("fc")]
+    tr = FrozenFeatureTrainer(m, 4, (32, 32), torch.device("cpu"), OptimizerConfig(name="adam", lr=1e-2))
+    feats = tr._features(img, lab, None, None).float()
+    cos = torch.nn.functional.cosine_similarity(feats.flatten(), ref.flatten(), dim=0)
+    assert cos > 0.99, cos
+    head_before = [p.detach().clone() for p in m.resnet.fc.parameters()]
+    for _ in range(3):
+        tr.step(img, lab)
+    loss, corr = tr.read_metrics()
+    assert loss > 0
+    assert any(not torch.equal(a, b) for a, b in zip(head_before, m.resnet.fc.parameters()))
+    after = [p.detach() for n, p in m.resnet.named_parameters() if not n.startswith("fc")]
+    assert all(torch.equal(a, b) for a, b in zip(backbone_before, after))

@@ -5,6 +5,7 @@ by cosine similarity and relative norm error against fp32 autograd on the same (
 input, same weights, same labels.
 """
 import copy
+import math
 
 import pytest
 import torch
@@ -116,3 +117,34 @@ def test_train_entrypoint_native_engine(tmp_path, monkeypatch):
     assert all(h["train_loss"] == h["train_loss"] for h in res.history)
     assert "val_accuracy" in res.history[-1]
     assert (tmp_path / "ck" / "checkpoint-2.pth.tar").exists()
+
+
+@pytest.mark.gpu
+def test_frozen_backbone_native_gpu():
+    """Reference workload shape (frozen ResNet-50 backbone, new head, 64x64 TinyImageNet): native
+    inference-mode backbone on the HIP kernels + autograd head."""
+    from dbx_distributed_pytorch_examples_amd.config import OptimizerConfig
+    from dbx_distributed_pytorch_examples_amd.engine.frozen_trainer import FrozenFeatureTrainer
+    from dbx_distributed_pytorch_examples_amd.models import FrozenBackboneClassifier
+    torch.manual_seed(0)
+    m = FrozenBackboneClassifier("resnet50", num_classes=200)
+    m.eval()
+    img = torch.randint(0, 256, (16, 64, 64, 3), dtype=torch.uint8)
+    lab = torch.randint(0, 200, (16,))
+    x = (img.permute(0, 3, 1, 2).float() / 255 - torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)) \
+        / torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    with torch.no_grad():
+        r = m.resnet
+        f = r.maxpool(r.relu(r.bn1(r.conv1(x))))
+        ref = torch.flatten(r.avgpool(r.layer4(r.layer3(r.layer2(r.layer1(f))))), 1)
+    tr = FrozenFeatureTrainer(m, 16, (64, 64), torch.device("cuda"), OptimizerConfig(name="adam", lr=1e-3))
+    feats = tr._features(img.cuda(), lab.cuda(), None, None).float().cpu()
+    cos = torch.nn.functional.cosine_similarity(feats.flatten(), ref.flatten(), dim=0)
+    assert cos > 0.98, cos
+    w0 = m.resnet.fc[1].weight.detach().clone()
+    for _ in range(3):
+        tr.step(img.cuda(), lab.cuda())
+    torch.cuda.synchronize()
+    assert not torch.equal(w0, m.resnet.fc[1].weight.detach())
+    loss, _ = tr.read_metrics()
+    assert math.isfinite(loss) and loss > 0

@@ -59,7 +59,7 @@ def main():
         ybn, mref, add = torch.randn_like(x), torch.randn_like(x), torch.randn_like(x)
         st1 = torch.zeros(K.NSHARD * 2 * C, device=dev)
         mean, inv = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
-        e1 = K.BNBwdEpilogue(K.MASK_OUT, ybn, mean, inv, st1, mref=mref)
+        e1 = K.BNBwdEpilogue(K.MASK_OUT, ybn, mean, inv, st1, mbits=K.pack_mask_bits(mref))
         e2 = K.BNBwdEpilogue(K.MASK_Y, ybn, mean, inv, st1, scale=sc, shift=sh)
         for tile in tiles:
             if tile and C % tile[1]:

@@ -93,7 +93,7 @@ def main():
             jobs.append(("dgrad0", N * OH * OH, C, Kc, 1, 1,
                          lambda t: K.conv_dgrad(dy, wt, dxs, R=1, S=1, stride=1, pad=0, tile=t)))
         else:
-            e1 = K.BNBwdEpilogue(K.MASK_OUT, ybn, mean, inv, st1, mref=mref)
+            e1 = K.BNBwdEpilogue(K.MASK_OUT, ybn, mean, inv, st1, mbits=K.pack_mask_bits(mref))
             e2 = K.BNBwdEpilogue(K.MASK_Y, ybn, mean, inv, st1, scale=sc, shift=sh)
             Md = N * H * H // (st * st)
             jobs.append(("dgrad1", Md, C, Kc, R, st, lambda t: K.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad,
