@@ -27,6 +27,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import kernels as K
+from ..parallel.dist import host_sync_for_gloo
 from ..utils import debug as _debug
 from ..utils.profiling import PhaseTimer
 from .program import ResNetProgram
@@ -150,6 +151,7 @@ class NativeTrainer:
         if self.zero is not None and self.zero.stage >= 2:
             return  # ZeRO-2: gradients are reduce-scattered by the optimizer phase instead
         g = self.prog.grad
+        host_sync_for_gloo(g, self.pg)
         pos = lo
         while pos < hi:
             end = min(hi, pos + self.bucket_cap)

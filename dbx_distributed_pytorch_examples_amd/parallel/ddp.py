@@ -26,6 +26,8 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from .dist import host_sync_for_gloo
+
 
 class FlatGradBuffer:
     """Contiguous gradient storage with params' ``.grad`` as views (reverse order)."""
@@ -114,6 +116,7 @@ class DistributedDataParallel(nn.Module):
         self._order.append(bi)
         b = self.buckets[bi]
         chunk = self.flat.buffer[b["lo"]:b["hi"]]
+        host_sync_for_gloo(chunk, self.pg)
         if self.predivide:
             chunk.div_(self.world)
         if self.allreduce_dtype != chunk.dtype:

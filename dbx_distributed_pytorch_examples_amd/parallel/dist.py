@@ -71,7 +71,9 @@ def init_distributed(backend: Optional[str] = None, device: Optional[str] = None
     else:
         dev = torch.device("cpu")
     if backend is None:
-        backend = "nccl" if use_cuda else "gloo"
+        # DBX_DIST_BACKEND=gloo lets several ranks share one GPU (RCCL refuses duplicate devices),
+        # which is how the multi-rank GPU path is exercised on a single-GPU box
+        backend = os.environ.get("DBX_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
@@ -85,6 +87,14 @@ def init_distributed(backend: Optional[str] = None, device: Optional[str] = None
         backend = "none"
     _INFO = DistInfo(rank, local_rank, world, local_world, backend, dev)
     return _INFO
+
+
+def host_sync_for_gloo(t: torch.Tensor, group=None) -> None:
+    """gloo reads CUDA tensors through its own copies, which are not ordered after kernels queued on
+    the caller's stream: drain that stream first (gloo-on-GPU is the single-GPU multi-rank test
+    configuration; RCCL collectives are stream-ordered and never take this path)."""
+    if t.is_cuda and dist.is_initialized() and dist.get_backend(group) == "gloo":
+        torch.cuda.current_stream(t.device).synchronize()
 
 
 def info() -> DistInfo:

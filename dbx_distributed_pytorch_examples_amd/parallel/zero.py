@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import kernels as K
+from .dist import host_sync_for_gloo
 
 
 def shard_range(n: int, rank: int, world: int, align: int = 16) -> Tuple[int, int]:
@@ -92,6 +93,8 @@ class ZeroShardedOptimizer:
         n_own = self.hi - self.lo
         g = self._gshard
         g.zero_()
+        if self.world > 1:
+            host_sync_for_gloo(self.grad, self.pg)
         if self.world == 1:
             g[:n_own].copy_(self.grad[self.lo:self.hi])
         elif self.stage == 1 or grads_already_reduced:
@@ -113,6 +116,7 @@ class ZeroShardedOptimizer:
             # global norm over all shards: local sum of squares, all-reduced
             local = (g[:n_own] * self.grad_scale).float().pow(2).sum()
             if self.world > 1:
+                host_sync_for_gloo(local, self.pg)
                 dist.all_reduce(local, group=self.pg)
             self._clip[2] = torch.clamp(o.grad_clip / (local.sqrt() + 1e-6), max=1.0)
             gsp = self._clip[2:3]
@@ -129,6 +133,7 @@ class ZeroShardedOptimizer:
             self.master[self.lo:self.hi].copy_(p[:n_own])
             return
         full = torch.empty(self.padded, device=p.device, dtype=p.dtype)
+        host_sync_for_gloo(p, self.pg)
         dist.all_gather_into_tensor(full, p, group=self.pg)
         self.master.copy_(full[:self.master.numel()])
 

@@ -7,6 +7,8 @@ timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/test_gpu.log 
 tail -1 gpurun_out/test_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke FAILED"; tail -20 gpurun_out/smoke.log; exit 1; }
 echo "smoke ok"
+DBX_DIST_BACKEND=gloo timeout -k 10 400 python -m dbx_distributed_pytorch_examples_amd.launch --nproc-per-node 2 tools/dist_gpu_check.py > gpurun_out/dist_check.log 2>&1 || { echo "dist check FAILED"; tail -20 gpurun_out/dist_check.log; exit 1; }
+grep "dist_gpu_check" gpurun_out/dist_check.log
 timeout -k 10 300 python bench.py > gpurun_out/bench_default.log 2>&1 || { echo "bench FAILED"; tail -20 gpurun_out/bench_default.log; exit 1; }
 tail -1 gpurun_out/bench_default.log
 for p in resnet50_imagenet_zero1 resnet18_cifar10 resnet50_tiny_imagenet; do
