@@ -29,8 +29,11 @@ def _pybind_includes():
     return [pybind11.get_include(), sysconfig.get_paths()["include"]]
 
 
-def ext_path() -> str:
-    return os.path.join(HERE, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+def ext_path(variant: str = "") -> str:
+    """``_C<suffix>``; an A/B variant build is ``_C_variant_<name><suffix>`` (loaded by setting
+    ``DBX_EXT_VARIANT=<name>``, see ops/_ext.py) so two kernel versions can be timed in one box."""
+    stem = "_C" + (f"_variant_{variant}" if variant else "")
+    return os.path.join(HERE, stem + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
 def _newer(target: str, deps) -> bool:
@@ -40,17 +43,19 @@ def _newer(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, jobs: int = 8) -> str:
+def build(verbose: bool = False, jobs: int = 8, variant: str = "", defines=()) -> str:
     arch = os.environ.get("DBX_ARCH", "gfx950")
-    os.makedirs(BUILD, exist_ok=True)
+    bdir = BUILD if not variant else BUILD + "_" + variant
+    os.makedirs(bdir, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip"))) + [os.path.join(CSRC, "bindings.cpp")]
     extra_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     dbg = ["-g", "-DDBX_DEBUG"] if os.environ.get("DBX_DEBUG") == "1" else []
-    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}"] + [f"-I{p}" for p in _pybind_includes()] + dbg
+    common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC}"] + [f"-I{p}" for p in _pybind_includes()] + dbg + \
+        [f"-D{d}" for d in defines]
     objs, cmds = [], []
     for s in srcs + extra_srcs:
-        o = os.path.join(BUILD, os.path.basename(s) + ".o")
+        o = os.path.join(bdir, os.path.basename(s) + ".o")
         objs.append(o)
         if _newer(o, [s] + headers):
             if s.endswith(".hip"):
@@ -71,7 +76,7 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
         for err in ex.map(run, cmds):
             if verbose and err.strip():
                 print(err)
-    out = ext_path()
+    out = ext_path(variant)
     if _newer(out, objs):
         link = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={arch}", "-o", out] + objs + [
             "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
@@ -80,5 +85,10 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
 
 
 if __name__ == "__main__":
-    p = build(verbose="-v" in sys.argv)
-    print(p)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-v", action="store_true")
+    ap.add_argument("--variant", default="", help="A/B build name (-> _C_variant_<name>)")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="preprocessor define for the variant")
+    a = ap.parse_args()
+    print(build(verbose=a.v, variant=a.variant, defines=a.defines))

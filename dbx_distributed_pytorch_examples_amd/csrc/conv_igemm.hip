@@ -487,18 +487,20 @@ __device__ __forceinline__ int tr_swz(int row, int ch, int nch) {
   return ch ^ ((((row & 1) << 2) ^ (row & 2) ^ (((row >> 3) & 1) << 2)) & 7);
 }
 
-template <int BM, int BN, int MODE, bool PRO, int DEPTH = 2>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
+// WM x WN waves (64*WM*WN threads), each owning a (BM/WM) x (BN/WN) block of dW.
+template <int BM, int BN, int WM, int WN, int MODE, bool PRO, int DEPTH = 2>
+__global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const WgradArgs a) {
+  constexpr int NT = 64 * WM * WN;
   constexpr int BKM = 64;                    // pixels per K block
   constexpr int NCA = BM / 8, NCB = BN / 8;  // 16B chunks per tile row
-  constexpr int A_CH = BKM * NCA / 256, B_CH = BKM * NCB / 256;
-  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int A_CH = BKM * NCA / NT, B_CH = BKM * NCB / NT;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * BKM * (BM + BN) + (PRO ? 4 * BN : 0)];
   bf16* sA = lds;                   // [2][BKM][BM]
   bf16* sB = lds + 2 * BKM * BM;    // [2][BKM][BN]
   float* sPro = reinterpret_cast<float*>(lds + 2 * BKM * (BM + BN));  // [2][BN] prologue scale, shift
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
   const int ntm = a.OC / BM, ntn = a.KTOT / BN;
   const int ntile = ntm * ntn;
   // logical id = split * ntile + tile: consecutive ids share a split's dY / X rows, and the XCD
@@ -512,7 +514,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   const int mend = min(a.M, mbeg + a.m_per_split);
   const int nkb = (mend - mbeg + BKM - 1) / BKM;
 
-  // A (dY) loader: thread -> (pixel row ra_row = tid / (256/A_CH... )
+  // A (dY) loader: thread -> (pixel row a_row, chunk column a_c)
   // each thread owns one pixel row and A_CH chunks of it (chunk = c0 + j*stride)
   constexpr int ATPR = NCA / A_CH;   // threads per pixel row for A
   constexpr int BTPR = NCB / B_CH;   // threads per pixel row for B
@@ -544,7 +546,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   const bool bsel = a.pad != 0 || (a.M % BKM) != 0;  // wave-uniform: can a B chunk be invalid?
   bool aok[2] = {false, false};   // this thread's A (dY) row lies inside the split
   if constexpr (PRO) {
-    for (int c = tid; c < BN; c += 256) {
+    for (int c = tid; c < BN; c += NT) {
       const int kk = kk0 + c;
       const int ch = kk - (kk / a.IC) * a.IC;
       sPro[c] = a.in_scale[ch];
@@ -658,7 +660,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int col = wm * (BM / 2) + i * 16 + 4 * p;
+        const int col = wm * (BM / WM) + i * 16 + 4 * p;
         s16x4 lo, hi;
         {
           const int row = ks * 32 + 8 * g + q;
@@ -672,7 +674,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = wn * (BN / 2) + j * 16 + 4 * p;
+        const int col = wn * (BN / WN) + j * 16 + 4 * p;
         s16x4 lo, hi;
         {
           const int row = ks * 32 + 8 * g + q;
@@ -728,8 +730,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int k = k0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-        const int kk = kk0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        const int k = k0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
+        const int kk = kk0 + wn * (BN / WN) + j * 16 + (lane & 15);
         out[(size_t)k * a.KTOT + kk] = acc[i][j][r];
       }
 }
@@ -834,29 +836,36 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
   return -5;
 }
 
+template <int BM, int BN, bool PRO>
+static void launch_wgrad_t(const WgradArgs& a, int nblk, hipStream_t st) {
+  // 256-wide tiles on 8 waves (4x2 / 2x4), the rest on 2x2 waves
+  constexpr int WM = (BM == 256) ? 4 : 2;
+  constexpr int WN = (BN == 256) ? 4 : 2;
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, FWD, PRO>), dim3(nblk), dim3(64 * WM * WN), 0, st, a);
+}
+
 extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, int pro, hipStream_t st) {
   const WgradArgs& a = *args;
   if (a.OC % bm != 0 || a.KTOT % bn != 0) return -1;
   const int nblk = (a.OC / bm) * (a.KTOT / bn) * a.nsplit;
   if (mode == STEM) {
-    if (bm == 64 && bn == 128) hipLaunchKernelGGL((wgrad_kernel<64, 128, STEM, false>), dim3(nblk), dim3(256), 0, st, a);
+    if (bm == 64 && bn == 128) hipLaunchKernelGGL((wgrad_kernel<64, 128, 2, 2, STEM, false>), dim3(nblk), dim3(256), 0, st, a);
     else return -3;
     return (int)hipGetLastError();
   }
-  if (a.IC % bn != 0 && !(bn == 128 && a.IC == 64 && false)) {
-    // a column tile must stay inside one tap
-    if (a.IC % bn != 0) return -4;
-  }
-#define WG(BM_, BN_)                                                                                   \
-  if (bm == BM_ && bn == BN_) {                                                                        \
-    if (pro) hipLaunchKernelGGL((wgrad_kernel<BM_, BN_, FWD, true>), dim3(nblk), dim3(256), 0, st, a); \
-    else hipLaunchKernelGGL((wgrad_kernel<BM_, BN_, FWD, false>), dim3(nblk), dim3(256), 0, st, a);    \
-    return (int)hipGetLastError();                                                                     \
+  if (a.IC % bn != 0) return -4;  // a column tile must stay inside one tap
+#define WG(BM_, BN_)                                                  \
+  if (bm == BM_ && bn == BN_) {                                       \
+    if (pro) launch_wgrad_t<BM_, BN_, true>(a, nblk, st);             \
+    else launch_wgrad_t<BM_, BN_, false>(a, nblk, st);                \
+    return (int)hipGetLastError();                                    \
   }
   WG(128, 128)
   WG(128, 64)
   WG(64, 128)
   WG(64, 64)
+  WG(256, 128)
+  WG(128, 256)
 #undef WG
   return -3;
 }

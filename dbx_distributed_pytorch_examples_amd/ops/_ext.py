@@ -10,7 +10,9 @@ the extension binds to.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sysconfig
 
 import torch  # noqa: F401  (must precede the extension: shared HIP runtime)
 
@@ -23,7 +25,15 @@ def _try_load():
     if _C is not None or _ERR is not None:
         return _C
     try:
-        _C = importlib.import_module("dbx_distributed_pytorch_examples_amd._C")
+        variant = os.environ.get("DBX_EXT_VARIANT", "")
+        if variant:  # A/B kernel builds (build_ext --variant NAME): same module, other binary
+            path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                f"_C_variant_{variant}" + sysconfig.get_config_var("EXT_SUFFIX"))
+            spec = importlib.util.spec_from_file_location("dbx_distributed_pytorch_examples_amd._C", path)
+            _C = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_C)
+        else:
+            _C = importlib.import_module("dbx_distributed_pytorch_examples_amd._C")
     except Exception as e:  # pragma: no cover - depends on build state
         _ERR = e
     return _C

@@ -273,7 +273,8 @@ def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int
     """Split the pixel reduction so that ~1024 workgroups stream (>= 8 K-blocks each); the
     workspace holds nsplit slabs + up to 64 level-1 partial slabs of the reduction."""
     tiles = (OC // bm) * (KTOT // bn)
-    target = max(1, 1024 // tiles)
+    # ~4 rounds of workgroups over the 256 CUs: 8-wave (256-wide) tiles run one per CU, 4-wave two
+    target = max(1, (512 if max(bm, bn) >= 256 else 1024) // tiles)
     ms = max(512, ((M + target - 1) // target + 63) // 64 * 64)
     nsplit = (M + ms - 1) // ms
     while (nsplit + min(64, nsplit)) * OC * KTOT > max_ws_elems and nsplit > 1:
@@ -303,8 +304,12 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         if tile:
             bm, bn = tile
         else:
-            bm = 128 if OC % 128 == 0 else 64
-            bn = 128 if IC % 128 == 0 else 64
+            t = _tune_table().get(tune_key("wgrad", N * OH * OW, OC, IC, R, stride))
+            if t is not None and OC % t[0] == 0 and IC % t[1] == 0:
+                bm, bn = t
+            else:
+                bm = 128 if OC % 128 == 0 else 64
+                bn = 128 if IC % 128 == 0 else 64
     if in_scale is not None:
         _chk(in_scale, torch.float32, "in_scale", IC)
         _chk(in_shift, torch.float32, "in_shift", IC)

@@ -31,6 +31,7 @@ def build_native_step(args, info):
         tr.step()
 
     return step, {"memory_format": "nhwc", "graphs": use_graphs,
-                  "ddp": (f"flat-bucket RCCL all-reduce, {tr.bucket_cap * 4 >> 20} MiB chunks, "
+                  "ddp": (f"flat-bucket {'RCCL' if info.backend == 'nccl' else info.backend} all-reduce, "
+                          f"{tr.bucket_cap * 4 >> 20} MiB chunks, "
                           f"{str(ar_dtype).split('.')[-1]}, overlapped per backward segment") if tr.world > 1 else "none",
                   "kernels": "dbx HIP (conv implicit-GEMM MFMA + fused BN/ReLU/pool/CE/SGD)"}

@@ -114,9 +114,12 @@ def test_conv_wgrad(case, prologue):
         sc = torch.rand(IC, device=dev) + 0.5
         sh = torch.randn(IC, device=dev) * 0.1
         xe = torch.relu(x.float() * sc + sh).bfloat16().float()
-    k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, in_scale=sc, in_shift=sh)
     ref = torch.nn.grad.conv2d_weight(nchw(xe), (OC, IC, R, R), nchw(dy.float()), stride=st, padding=pad)
-    assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2
+    for tile in [None, (128, 128), (128, 64), (64, 128), (64, 64), (256, 128), (128, 256)]:
+        if tile and (OC % tile[0] or IC % tile[1]):
+            continue
+        k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, in_scale=sc, in_shift=sh, tile=tile)
+        assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2, tile
 
 
 def test_stem_fwd_wgrad():
@@ -357,9 +360,12 @@ def test_conv_wgrad_split(shape):
     ws = torch.empty(64 * 1024 * 1024, device=dev)
     nsplit, _ = k.wgrad_splits(N * OH * OW, OC, R * R * IC, 64, 64, ws.numel())
     assert nsplit > 1
-    k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad)
     ref = torch.nn.grad.conv2d_weight(nchw(x.float()), (OC, IC, R, R), nchw(dy.float()), stride=st, padding=pad)
-    assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2
+    for tile in [None, (256, 128), (128, 256)]:
+        if tile and (OC % tile[0] or IC % tile[1]):
+            continue
+        k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, tile=tile)
+        assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2, tile
 
 
 def test_stem_wgrad_split():

@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 from dbx_distributed_pytorch_examples_amd.ops import kernels as K  # noqa: E402
 
 TILES = [(128, 128), (128, 64), (64, 64), (256, 128), (128, 256), (256, 64)]
-WGRAD_TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
+WGRAD_TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (256, 128), (128, 256)]
 
 
 def convs_of(model_name, image, num_classes=1000):
