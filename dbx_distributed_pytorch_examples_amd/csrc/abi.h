@@ -8,7 +8,7 @@ struct IGemmArgs {
   bf16* y;                // out, [M][OC]
   const float* in_scale;  // prologue affine per input channel (nullable)
   const float* in_shift;
-  float* stats;           // [nshard][2][OC] (sum, sumsq) or null
+  double* stats;          // [nshard][2][OC] (sum, sumsq) or null; fp64 so the atomics are order-independent
   int N, IH, IW, IC, OH, OW, OC, R, S, stride, pad;
   int M, nshard, relu_in;
   // tap subset iterated by the K loop: r = r0 + tstep*tr (tr < nr), s = s0 + tstep*ts (ts < ns)
@@ -33,8 +33,8 @@ struct IGemmArgs {
   const float* inv1;
   const float* mean2;
   const float* inv2;
-  float* bstats1;
-  float* bstats2;
+  double* bstats1;  // fp64 [nshard][2][C]
+  double* bstats2;
 };
 struct WgradArgs {
   const bf16* dy;        // [M][OC]

@@ -17,15 +17,15 @@ int dbx_conv_igemm(int mode, int bm, int bn, const dbx::IGemmArgs* a, int pro, i
                    hipStream_t st);
 int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, hipStream_t st);
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
-int dbx_bn_finalize(const float*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
+int dbx_bn_finalize(const double*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
                     float*, float*, float*, hipStream_t);
 int dbx_bn_eval_coeff(int, const float*, const float*, float, const float*, const float*, float*, float*, hipStream_t);
-int dbx_channel_stats(const bf16*, long long, int, float*, int, hipStream_t);
+int dbx_channel_stats(const bf16*, long long, int, double*, int, hipStream_t);
 int dbx_bn_apply(const bf16*, const float*, const float*, const bf16*, const float*, const float*, bf16*, long long, int,
                  int, int, unsigned char*, hipStream_t);
 int dbx_bn_bwd_reduce(const bf16*, const bf16*, const bf16*, const float*, const float*, const float*, const float*,
-                      long long, int, float*, int, int, hipStream_t);
-int dbx_bn_bwd_coeff(const float*, int, int, float, const float*, const float*, const float*, float*, float*, float*,
+                      long long, int, double*, int, int, hipStream_t);
+int dbx_bn_bwd_coeff(const double*, int, int, float, const float*, const float*, const float*, float*, float*, float*,
                      int, hipStream_t);
 int dbx_bn_bwd_apply(const bf16*, const bf16*, const bf16*, const float*, const float*, const float*, bf16*, bf16*,
                      long long, int, int, hipStream_t);
@@ -34,13 +34,13 @@ int dbx_maxpool_fwd(const bf16*, const float*, const float*, bf16*, unsigned cha
 int dbx_maxpool_bwd(const bf16*, const unsigned char*, bf16*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int dbx_avgpool_fwd(const bf16*, bf16*, int, int, int, hipStream_t);
 int dbx_avgpool_bwd(const bf16*, bf16*, int, int, int, hipStream_t);
-int dbx_softmax_ce(const void*, int, const long long*, void*, float*, float*, int, int, float, float, hipStream_t);
+int dbx_softmax_ce(const void*, int, const long long*, void*, float*, double*, int, int, float, float, hipStream_t);
 int dbx_sgd(float*, const float*, float*, bf16*, long long, const float*, float, float, float, float, int, int,
             const float*, float, hipStream_t);
 int dbx_adam(float*, const float*, float*, float*, bf16*, long long, const float*, float, float, float, float, float, int,
              float, float, const float*, float, hipStream_t);
-int dbx_sumsq(const float*, long long, float*, hipStream_t);
-int dbx_clip_factor(const float*, float, float*, hipStream_t);
+int dbx_sumsq(const float*, long long, double*, hipStream_t);
+int dbx_clip_factor(const double*, float, float*, hipStream_t);
 int dbx_normalize_u8(const unsigned char*, bf16*, const unsigned char*, int, int, int, int, float, float, float, float,
                      float, float, hipStream_t);
 int dbx_weight_prep(const float*, bf16*, const void*, int, hipStream_t);
@@ -74,12 +74,12 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t bsc, uintptr_t bsh, uintptr_t mean1, uintptr_t inv1, uintptr_t mean2,
                          uintptr_t inv2, uintptr_t bstats1, uintptr_t bstats2, uintptr_t st) {
     dbx::IGemmArgs a{P<const bf16*>(x), P<const bf16*>(w), P<bf16*>(y), P<const float*>(in_scale),
-                     P<const float*>(in_shift), P<float*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
+                     P<const float*>(in_shift), P<double*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
                      N * OH * OW, nshard > 0 ? nshard : 1, relu_in, nr, ns, r0, s0, tstep, dh0, dw0, osub, oph, opw,
                      FH, FW, P<const bf16*>(addsrc), add_sub, P<const unsigned char*>(mbits), P<const bf16*>(ybn),
                      P<const bf16*>(ybn2), P<const float*>(bsc), P<const float*>(bsh), P<const float*>(mean1),
-                     P<const float*>(inv1), P<const float*>(mean2), P<const float*>(inv2), P<float*>(bstats1),
-                     P<float*>(bstats2)};
+                     P<const float*>(inv1), P<const float*>(mean2), P<const float*>(inv2), P<double*>(bstats1),
+                     P<double*>(bstats2)};
     check(dbx_conv_igemm(mode, bm, bn, &a, in_scale != 0, stats != 0, accum, epi, S(st)), "conv_igemm");
   });
   m.def("conv_wgrad", [](int mode, int bm, int bn, uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t in_scale,
@@ -96,7 +96,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_finalize", [](uintptr_t stats, int nshard, int C, float count, uintptr_t gamma, uintptr_t beta, float eps,
                           float momentum, uintptr_t rm, uintptr_t rv, uintptr_t scale, uintptr_t shift, uintptr_t smean,
                           uintptr_t sinv, uintptr_t st) {
-    check(dbx_bn_finalize(P<const float*>(stats), nshard, C, count, P<const float*>(gamma), P<const float*>(beta), eps,
+    check(dbx_bn_finalize(P<const double*>(stats), nshard, C, count, P<const float*>(gamma), P<const float*>(beta), eps,
                           momentum, P<float*>(rm), P<float*>(rv), P<float*>(scale), P<float*>(shift), P<float*>(smean),
                           P<float*>(sinv), S(st)),
           "bn_finalize");
@@ -108,7 +108,7 @@ PYBIND11_MODULE(_C, m) {
           "bn_eval_coeff");
   });
   m.def("channel_stats", [](uintptr_t y, long long M, int C, uintptr_t stats, int nshard, uintptr_t st) {
-    check(dbx_channel_stats(P<const bf16*>(y), M, C, P<float*>(stats), nshard, S(st)), "channel_stats");
+    check(dbx_channel_stats(P<const bf16*>(y), M, C, P<double*>(stats), nshard, S(st)), "channel_stats");
   });
   m.def("bn_apply", [](uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t res, uintptr_t rsc, uintptr_t rsh,
                        uintptr_t out, long long n, int C, int res_mode, int relu, uintptr_t mbits, uintptr_t st) {
@@ -122,12 +122,12 @@ PYBIND11_MODULE(_C, m) {
                             uintptr_t st) {
     check(dbx_bn_bwd_reduce(P<const bf16*>(dout), P<const bf16*>(mref), P<const bf16*>(y), P<const float*>(sc),
                             P<const float*>(sh), P<const float*>(mean), P<const float*>(invstd), M, C,
-                            P<float*>(stats), nshard, mask_mode, S(st)),
+                            P<double*>(stats), nshard, mask_mode, S(st)),
           "bn_bwd_reduce");
   });
   m.def("bn_bwd_coeff", [](uintptr_t stats, int nshard, int C, float count, uintptr_t gamma, uintptr_t mean,
                            uintptr_t invstd, uintptr_t coeff, uintptr_t dgamma, uintptr_t dbeta, int acc, uintptr_t st) {
-    check(dbx_bn_bwd_coeff(P<const float*>(stats), nshard, C, count, P<const float*>(gamma), P<const float*>(mean),
+    check(dbx_bn_bwd_coeff(P<const double*>(stats), nshard, C, count, P<const float*>(gamma), P<const float*>(mean),
                            P<const float*>(invstd), P<float*>(coeff), P<float*>(dgamma), P<float*>(dbeta), acc, S(st)),
           "bn_bwd_coeff");
   });
@@ -159,7 +159,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("softmax_ce", [](uintptr_t logits, int is_bf16, uintptr_t labels, uintptr_t dlogits, uintptr_t loss_out,
                          uintptr_t stats, int B, int C, float smoothing, float gscale, uintptr_t st) {
     check(dbx_softmax_ce(P<const void*>(logits), is_bf16, P<const long long*>(labels), P<void*>(dlogits),
-                         P<float*>(loss_out), P<float*>(stats), B, C, smoothing, gscale, S(st)),
+                         P<float*>(loss_out), P<double*>(stats), B, C, smoothing, gscale, S(st)),
           "softmax_ce");
   });
   m.def("sgd", [](uintptr_t p, uintptr_t g, uintptr_t v, uintptr_t p16, long long n, uintptr_t hyper, float lr,
@@ -176,10 +176,10 @@ PYBIND11_MODULE(_C, m) {
           "adam");
   });
   m.def("sumsq", [](uintptr_t x, long long n, uintptr_t out, uintptr_t st) {
-    check(dbx_sumsq(P<const float*>(x), n, P<float*>(out), S(st)), "sumsq");
+    check(dbx_sumsq(P<const float*>(x), n, P<double*>(out), S(st)), "sumsq");
   });
   m.def("clip_factor", [](uintptr_t sumsq, float max_norm, uintptr_t out, uintptr_t st) {
-    check(dbx_clip_factor(P<const float*>(sumsq), max_norm, P<float*>(out), S(st)), "clip_factor");
+    check(dbx_clip_factor(P<const double*>(sumsq), max_norm, P<float*>(out), S(st)), "clip_factor");
   });
   m.def("normalize_u8", [](uintptr_t in, uintptr_t out, uintptr_t flip, int N, int H, int W, int Cin, float m0, float m1,
                            float m2, float s0, float s1, float s2, uintptr_t st) {

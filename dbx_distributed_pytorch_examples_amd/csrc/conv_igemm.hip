@@ -18,7 +18,9 @@
 //   * prologue: BN-apply (+ReLU) of the PREVIOUS layer on the A operand while staging it
 //     (y_prev * scale[c] + shift[c], max 0), so BN outputs are never materialised;
 //   * epilogue: per-output-channel sum / sum-of-squares for THIS layer's BN, from the fp32
-//     accumulators, written as per-tile-row partials into sharded fp32 slabs (atomics);
+//     accumulators: fp32 per-tile partials added into sharded fp64 slabs (fp64 atomics: the
+//     sum of fp32 partials is exact in fp64 for any realistic spread, so the result does not
+//     depend on the order the tiles finish in -> bit-reproducible training);
 //   * epilogue: accumulate into the existing output (dX of a block = dgrad(conv1) + dgrad(ds)).
 //
 // Tiles: BM x BN x 64, 256 threads = 2x2 waves, double-buffered LDS with register staging
@@ -293,9 +295,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       float s = 0.f, q = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) { s += sStat[(w * 2) * BN + tid]; q += sStat[(w * 2 + 1) * BN + tid]; }
-      float* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
-      atomicAdd(st + n0 + tid, s);
-      atomicAdd(st + a.OC + n0 + tid, q);
+      double* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
+      atomicAdd(st + n0 + tid, (double)s);
+      atomicAdd(st + a.OC + n0 + tid, (double)q);
     }
   }
   constexpr int CPR = BN / 8;  // 16B chunks per output row; a thread's chunk column is fixed
@@ -458,13 +460,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       q1 = a.inv1[c] * (q1 - a.mean1[c] * s);
       if (has2) q2 = a.inv2[c] * (q2 - a.mean2[c] * s);
       const int shard = (blockIdx.x % a.nshard);
-      float* st1 = a.bstats1 + (size_t)shard * 2 * a.OC;
-      atomicAdd(st1 + n0 + tid, s);
-      atomicAdd(st1 + a.OC + n0 + tid, q1);
+      double* st1 = a.bstats1 + (size_t)shard * 2 * a.OC;
+      atomicAdd(st1 + n0 + tid, (double)s);
+      atomicAdd(st1 + a.OC + n0 + tid, (double)q1);
       if (a.bstats2) {
-        float* st2 = a.bstats2 + (size_t)shard * 2 * a.OC;
-        atomicAdd(st2 + n0 + tid, s);
-        atomicAdd(st2 + a.OC + n0 + tid, q2);
+        double* st2 = a.bstats2 + (size_t)shard * 2 * a.OC;
+        atomicAdd(st2 + n0 + tid, (double)s);
+        atomicAdd(st2 + a.OC + n0 + tid, (double)q2);
       }
     }
   }

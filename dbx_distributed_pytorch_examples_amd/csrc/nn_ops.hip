@@ -18,16 +18,17 @@
 namespace dbx {
 
 // ----------------------------------------------------------------------------------------
-// BN finalize: stats[nshard][2][C] -> scale/shift (+ saved mean/invstd, running stats)
+// BN finalize: stats[nshard][2][C] (fp64, see conv_igemm.hip) -> scale/shift (+ saved mean/invstd,
+// running stats). Shards are summed in a fixed order, so the result is bit-reproducible.
 // ----------------------------------------------------------------------------------------
 // One block per 8 channels: thread (k, j) loads shard k of channel c0+j, LDS tree over the shards
 // (the 32 shard loads are issued in parallel instead of as a dependent chain).
-__device__ __forceinline__ void shard_sums(const float* stats, int nshard, int C, int c0, float& s_out, float& q_out,
-                                           bool& active, int& c) {
-  __shared__ float rs[8][33], rq[8][33];
+__device__ __forceinline__ void shard_sums(const double* stats, int nshard, int C, int c0, double& s_out,
+                                           double& q_out, bool& active, int& c) {
+  __shared__ double rs[8][33], rq[8][33];
   const int j = threadIdx.x & 7, k = threadIdx.x >> 3;  // k in 0..31
   c = c0 + j;
-  float s = 0.f, q = 0.f;
+  double s = 0.0, q = 0.0;
   if (c < C) {
     for (int kk = k; kk < nshard; kk += 32) { s += stats[(size_t)kk * 2 * C + c]; q += stats[(size_t)kk * 2 * C + C + c]; }
   }
@@ -35,23 +36,23 @@ __device__ __forceinline__ void shard_sums(const float* stats, int nshard, int C
   __syncthreads();
   active = (k == 0) && (c < C);
   if (active) {
-    float ss = 0.f, qq = 0.f;
+    double ss = 0.0, qq = 0.0;
     for (int t = 0; t < 32; ++t) { ss += rs[j][t]; qq += rq[j][t]; }
     s_out = ss; q_out = qq;
   }
 }
 
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, int nshard, int C, float count,
+__global__ void bn_finalize_kernel(const double* __restrict__ stats, int nshard, int C, float count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float eps, float momentum, float* running_mean, float* running_var,
                                    float* scale, float* shift, float* save_mean, float* save_invstd) {
-  float s = 0.f, q = 0.f;
+  double s = 0.0, q = 0.0;
   bool active;
   int c;
   shard_sums(stats, nshard, C, blockIdx.x * 8, s, q, active, c);
   if (!active) return;
-  const double mean = (double)s / count;
-  double var = (double)q / count - mean * mean;
+  const double mean = s / count;
+  double var = q / count - mean * mean;
   if (var < 0.0) var = 0.0;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
@@ -78,7 +79,7 @@ __global__ void bn_eval_coeff_kernel(int C, const float* gamma, const float* bet
 }
 
 // Channel sums of a bf16 [M][C] tensor (stats pass for layers whose producer cannot emit them)
-__global__ void channel_stats_kernel(const bf16* __restrict__ y, long long M, int C, float* stats, int nshard) {
+__global__ void channel_stats_kernel(const bf16* __restrict__ y, long long M, int C, double* stats, int nshard) {
   const int tpr = C / 8, rpb = 256 / tpr;
   const int tid = threadIdx.x;
   const int cg = tid % tpr, r0 = tid / tpr;
@@ -95,13 +96,13 @@ __global__ void channel_stats_kernel(const bf16* __restrict__ y, long long M, in
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[0][tid * 8 + j] = s[j]; red[1][tid * 8 + j] = q[j]; }
   __syncthreads();
-  float* st = stats + (size_t)(blockIdx.x % nshard) * 2 * C;
+  double* st = stats + (size_t)(blockIdx.x % nshard) * 2 * C;
   for (int c = tid; c < C; c += 256) {
     const int g = c / 8, j = c % 8;
     float ss = 0.f, qq = 0.f;
     for (int r = 0; r < rpb; ++r) { ss += red[0][(r * tpr + g) * 8 + j]; qq += red[1][(r * tpr + g) * 8 + j]; }
-    atomicAdd(st + c, ss);
-    atomicAdd(st + C + c, qq);
+    atomicAdd(st + c, (double)ss);
+    atomicAdd(st + C + c, (double)qq);
   }
 }
 
@@ -194,7 +195,7 @@ template <int MASK>
 __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ mref,
                                      const bf16* __restrict__ y, const float* __restrict__ sc,
                                      const float* __restrict__ sh, const float* __restrict__ mean,
-                                     const float* __restrict__ invstd, long long M, int C, float* stats,
+                                     const float* __restrict__ invstd, long long M, int C, double* stats,
                                      int nshard) {
   const int tpr = C / 8, rpb = 256 / tpr;
   const int tid = threadIdx.x;
@@ -217,26 +218,27 @@ __global__ void bn_bwd_reduce_kernel(const bf16* __restrict__ dout, const bf16* 
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[0][tid * 8 + j] = s[j]; red[1][tid * 8 + j] = q[j]; }
   __syncthreads();
-  float* st = stats + (size_t)(blockIdx.x % nshard) * 2 * C;
+  double* st = stats + (size_t)(blockIdx.x % nshard) * 2 * C;
   for (int c = tid; c < C; c += 256) {
     const int g = c / 8, j = c % 8;
     float ss = 0.f, qq = 0.f;
     for (int r = 0; r < rpb; ++r) { ss += red[0][(r * tpr + g) * 8 + j]; qq += red[1][(r * tpr + g) * 8 + j]; }
-    atomicAdd(st + c, ss);
-    atomicAdd(st + C + c, qq);
+    atomicAdd(st + c, (double)ss);
+    atomicAdd(st + C + c, (double)qq);
   }
 }
 
 // per-channel backward coefficients + parameter grads (fp32, written into the flat grad buffer)
-__global__ void bn_bwd_coeff_kernel(const float* __restrict__ stats, int nshard, int C, float count,
+__global__ void bn_bwd_coeff_kernel(const double* __restrict__ stats, int nshard, int C, float count,
                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, float* coeff /*[3][C]*/,
                                     float* dgamma, float* dbeta, int accumulate) {
-  float s = 0.f, q = 0.f;
+  double sd = 0.0, qd = 0.0;
   bool active;
   int c;
-  shard_sums(stats, nshard, C, blockIdx.x * 8, s, q, active, c);
+  shard_sums(stats, nshard, C, blockIdx.x * 8, sd, qd, active, c);
   if (!active) return;
+  const float s = (float)sd, q = (float)qd;
   const float g = gamma ? gamma[c] : 1.f, is = invstd[c], mu = mean[c];
   const float sg = s / count, sgx = q / count;
   const float k1 = g * is;
@@ -395,11 +397,12 @@ __global__ void avgpool_bwd_kernel(const bf16* __restrict__ dout, bf16* __restri
 // ----------------------------------------------------------------------------------------
 // Softmax cross-entropy (+label smoothing) fused with dlogits, argmax-correct count.
 // One 256-thread block per row; logits fp32 or bf16; dlogits = (p - target)/B * gscale.
-// out_stats[0] += sum loss, out_stats[1] += correct   (device accumulators: no host sync)
+// out_stats[0] += sum loss, out_stats[1] += correct   (fp64 device accumulators: no host sync,
+// order-independent sums)
 // ----------------------------------------------------------------------------------------
 template <typename T>
 __global__ void softmax_ce_kernel(const T* __restrict__ logits, const long long* __restrict__ labels,
-                                  T* __restrict__ dlogits, float* __restrict__ loss_out, float* stats,
+                                  T* __restrict__ dlogits, float* __restrict__ loss_out, double* stats,
                                   int B, int C, float smoothing, float gscale) {
   const int row = blockIdx.x;
   const T* x = logits + (size_t)row * C;
@@ -449,8 +452,8 @@ __global__ void softmax_ce_kernel(const T* __restrict__ logits, const long long*
   if (tid == 0) {
     if (loss_out) loss_out[row] = loss;
     if (stats) {
-      atomicAdd(stats, loss);
-      atomicAdd(stats + 1, (amx == lab) ? 1.f : 0.f);
+      atomicAdd(stats, (double)loss);
+      atomicAdd(stats + 1, (amx == lab) ? 1.0 : 0.0);
     }
   }
   if (dlogits) {
@@ -533,20 +536,21 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
-// sum of squares over a flat fp32 buffer (global-norm clipping), one atomic per block
-__global__ void sumsq_kernel(const float* __restrict__ x, long long n, float* out) {
+// sum of squares over a flat fp32 buffer (global-norm clipping), one fp64 atomic per block
+// (fp32 block partials add exactly in fp64: the norm does not depend on block order)
+__global__ void sumsq_kernel(const float* __restrict__ x, long long n, double* out) {
   float s = 0.f;
   for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) s += x[k] * x[k];
   s = wave_sum(s);
   __shared__ float red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) atomicAdd(out, (double)(red[0] + red[1] + red[2] + red[3]));
 }
 
 // clip factor = min(1, max_norm / (sqrt(sumsq) + 1e-6)) written to out[0]
-__global__ void clip_factor_kernel(const float* sumsq, float max_norm, float* out) {
-  const float nrm = sqrtf(sumsq[0]);
+__global__ void clip_factor_kernel(const double* sumsq, float max_norm, float* out) {
+  const float nrm = (float)sqrt(sumsq[0]);
   out[0] = fminf(1.f, max_norm / (nrm + 1e-6f));
   out[1] = nrm;
 }
@@ -660,7 +664,7 @@ static inline int grid_for(long long n, int block = 256, int cap = 8192) {
 }
 #define RET_LAST return (int)hipGetLastError()
 
-extern "C" int dbx_bn_finalize(const float* stats, int nshard, int C, float count, const float* gamma,
+extern "C" int dbx_bn_finalize(const double* stats, int nshard, int C, float count, const float* gamma,
                                const float* beta, float eps, float momentum, float* rm, float* rv,
                                float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 7) / 8), dim3(256), 0, st, stats, nshard, C, count, gamma,
@@ -672,7 +676,7 @@ extern "C" int dbx_bn_eval_coeff(int C, const float* gamma, const float* beta, f
   hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, eps, rm, rv, scale, shift);
   RET_LAST;
 }
-extern "C" int dbx_channel_stats(const bf16* y, long long M, int C, float* stats, int nshard, hipStream_t st) {
+extern "C" int dbx_channel_stats(const bf16* y, long long M, int C, double* stats, int nshard, hipStream_t st) {
   if (C % 8 || C / 8 > 256) return -1;
   const int rpb = 256 / (C / 8);
   hipLaunchKernelGGL(channel_stats_kernel, dim3(grid_for(M, rpb, 2048)), dim3(256), 0, st, y, M, C, stats, nshard);
@@ -692,7 +696,7 @@ extern "C" int dbx_bn_apply(const bf16* y, const float* sc, const float* sh, con
   RET_LAST;
 }
 extern "C" int dbx_bn_bwd_reduce(const bf16* dout, const bf16* mref, const bf16* y, const float* sc, const float* sh,
-                                 const float* mean, const float* invstd, long long M, int C, float* stats,
+                                 const float* mean, const float* invstd, long long M, int C, double* stats,
                                  int nshard, int mask_mode, hipStream_t st) {
   if (C % 8 || C / 8 > 256) return -1;
   const int rpb = 256 / (C / 8);
@@ -702,7 +706,7 @@ extern "C" int dbx_bn_bwd_reduce(const bf16* dout, const bf16* mref, const bf16*
   else hipLaunchKernelGGL((bn_bwd_reduce_kernel<2>), g, b, 0, st, dout, mref, y, sc, sh, mean, invstd, M, C, stats, nshard);
   RET_LAST;
 }
-extern "C" int dbx_bn_bwd_coeff(const float* stats, int nshard, int C, float count, const float* gamma,
+extern "C" int dbx_bn_bwd_coeff(const double* stats, int nshard, int C, float count, const float* gamma,
                                 const float* mean, const float* invstd, float* coeff, float* dgamma, float* dbeta,
                                 int accumulate, hipStream_t st) {
   hipLaunchKernelGGL(bn_bwd_coeff_kernel, dim3((C + 7) / 8), dim3(256), 0, st, stats, nshard, C, count, gamma,
@@ -749,7 +753,7 @@ extern "C" int dbx_avgpool_bwd(const bf16* dout, bf16* dx, int N, int HW, int C,
   RET_LAST;
 }
 extern "C" int dbx_softmax_ce(const void* logits, int is_bf16, const long long* labels, void* dlogits, float* loss_out,
-                              float* stats, int B, int C, float smoothing, float gscale, hipStream_t st) {
+                              double* stats, int B, int C, float smoothing, float gscale, hipStream_t st) {
   if (is_bf16)
     hipLaunchKernelGGL(softmax_ce_kernel<bf16>, dim3(B), dim3(256), 0, st, (const bf16*)logits, labels, (bf16*)dlogits,
                        loss_out, stats, B, C, smoothing, gscale);
@@ -772,11 +776,11 @@ extern "C" int dbx_adam(float* p, const float* g, float* m, float* v, bf16* p16,
                      decoupled, bc1, bc2, gscale_ptr, gscale);
   RET_LAST;
 }
-extern "C" int dbx_sumsq(const float* x, long long n, float* out, hipStream_t st) {
+extern "C" int dbx_sumsq(const float* x, long long n, double* out, hipStream_t st) {
   hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, x, n, out);
   RET_LAST;
 }
-extern "C" int dbx_clip_factor(const float* sumsq, float max_norm, float* out, hipStream_t st) {
+extern "C" int dbx_clip_factor(const double* sumsq, float max_norm, float* out, hipStream_t st) {
   hipLaunchKernelGGL(clip_factor_kernel, dim3(1), dim3(1), 0, st, sumsq, max_norm, out);
   RET_LAST;
 }

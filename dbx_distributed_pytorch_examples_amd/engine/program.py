@@ -355,21 +355,19 @@ class ResNetProgram:
         self.img_u8 = torch.zeros(N, sh, sw, 3 if self.in_ch != 1 else 1, device=dev, dtype=torch.uint8)
         self.boxes = torch.tensor([[0.0, 0.0, float(sh), float(sw)]] * N, device=dev)  # full-image default
         self.flip = torch.zeros(N, device=dev, dtype=torch.uint8)
-        self.metrics = torch.zeros(4, device=dev, dtype=torch.float32)  # loss sum, correct, -, -
+        self.metrics = torch.zeros(2, device=dev, dtype=torch.float64)  # loss sum, correct (fp64 atomics)
         # BN state arena
-        tot = 0
-        for bn in self.bns:
-            tot += 7 * bn.C + 2 * 2 * K.NSHARD * bn.C
-        self.bn_arena = torch.zeros(tot, device=dev, dtype=torch.float32)
+        # fp64 statistics slabs, contiguous: zeroed by ONE memset per step
+        self.stats_region = torch.zeros(sum(2 * 2 * K.NSHARD * bn.C for bn in self.bns), device=dev,
+                                        dtype=torch.float64)
         o = 0
-        self.stats_lo = None
-        # stats slabs first (contiguous: zeroed by ONE memset per step)
         for bn in self.bns:
-            bn.stats = self.bn_arena[o:o + 2 * K.NSHARD * bn.C]
+            bn.stats = self.stats_region[o:o + 2 * K.NSHARD * bn.C]
             o += 2 * K.NSHARD * bn.C
-            bn.bstats = self.bn_arena[o:o + 2 * K.NSHARD * bn.C]
+            bn.bstats = self.stats_region[o:o + 2 * K.NSHARD * bn.C]
             o += 2 * K.NSHARD * bn.C
-        self.stats_region = self.bn_arena[:o]
+        self.bn_arena = torch.zeros(sum(7 * bn.C for bn in self.bns), device=dev, dtype=torch.float32)
+        o = 0
         for bn in self.bns:
             bn.scale = self.bn_arena[o:o + bn.C]; o += bn.C
             bn.shift = self.bn_arena[o:o + bn.C]; o += bn.C

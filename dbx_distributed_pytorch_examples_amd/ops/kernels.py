@@ -8,7 +8,7 @@ calls are captured by ``torch.cuda.graph``), and never synchronises. Layout conv
   except the stem which takes the NHWC4 image);
 * conv weights: KRSC bf16 ``[OC, R*S*IC]`` for forward, CRSK ``[IC, R*S*OC]`` for dgrad,
   the stem as ``[64, 8*8*4]`` (7x7x3 zero-padded to 8x8x4);
-* BN statistics: fp32 ``[nshard, 2, C]`` slabs accumulated by conv epilogues.
+* BN statistics: fp64 ``[nshard, 2, C]`` slabs accumulated by conv epilogues (order-independent).
 """
 from __future__ import annotations
 
@@ -47,6 +47,12 @@ def _dispatch(fn):
 
 
 NSHARD = 32  # BN-statistics shards (spreads the epilogue atomics over 32 copies)
+
+
+def new_stats(C: int, device=None) -> torch.Tensor:
+    """Zeroed BN-statistics slab ``[NSHARD, 2, C]`` (flat, fp64: the epilogue atomics add fp32
+    partials exactly, so statistics do not depend on tile completion order)."""
+    return torch.zeros(NSHARD * 2 * C, device=device, dtype=torch.float64)
 
 
 def _p(t: Optional[torch.Tensor]) -> int:
@@ -122,7 +128,7 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     if IC % 64 or OC % 64:
         raise ValueError(f"conv_fwd needs IC,OC % 64 == 0 (got {IC},{OC})")
     if stats is not None:
-        _chk(stats, torch.float32, "stats", NSHARD * 2 * OC)
+        _chk(stats, torch.float64, "stats", NSHARD * 2 * OC)
     if in_scale is not None:
         _chk(in_scale, torch.float32, "in_scale", IC)
         _chk(in_shift, torch.float32, "in_shift", IC)
@@ -222,12 +228,12 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
     if epilogue is not None:
         e = epilogue
         _chk(e.ybn, torch.bfloat16, "ybn", dx.numel())
-        _chk(e.stats1, torch.float32, "stats1", NSHARD * 2 * Cc)
+        _chk(e.stats1, torch.float64, "stats1", NSHARD * 2 * Cc)
         if e.mode == MASK_OUT:
             _chk(e.mbits, torch.uint8, "mbits", dx.numel() // 8)
         if e.ybn2 is not None:
             _chk(e.ybn2, torch.bfloat16, "ybn2", dx.numel())
-            _chk(e.stats2, torch.float32, "stats2", NSHARD * 2 * Cc)
+            _chk(e.stats2, torch.float64, "stats2", NSHARD * 2 * Cc)
         epi = e.args()
     phases = dgrad_phases(H, W, R, S, stride, pad)
     if not accumulate and any(ph[5] == 0 or ph[7] == 0 for ph in phases):
@@ -260,7 +266,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
     _chk(w16s, torch.bfloat16, "w16s", OC * 256)
     _chk(out, torch.bfloat16, "out", N * OH * OW * OC)
     if stats is not None:
-        _chk(stats, torch.float32, "stats", NSHARD * 2 * OC)
+        _chk(stats, torch.float64, "stats", NSHARD * 2 * OC)
     if R > 8 or S > 8:
         raise ValueError("stem kernel supports R,S <= 8")
     C().conv_igemm(STEM, 128, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
@@ -346,7 +352,7 @@ def bn_eval_coeff(gamma, beta, eps, running_mean, running_var, scale, shift):
 def channel_stats(y, stats):
     Cc = y.shape[-1]
     _chk(y, torch.bfloat16, "y")
-    _chk(stats, torch.float32, "stats", NSHARD * 2 * Cc)
+    _chk(stats, torch.float64, "stats", NSHARD * 2 * Cc)
     C().channel_stats(y.data_ptr(), y.numel() // Cc, Cc, stats.data_ptr(), NSHARD, stream_ptr())
 
 
@@ -374,7 +380,7 @@ def bn_bwd_reduce(dout, y, mean, invstd, stats, *, mask_mode, mref=None, scale=N
     Cc = y.shape[-1]
     _chk(dout, torch.bfloat16, "dout", y.numel())
     _chk(y, torch.bfloat16, "y")
-    _chk(stats, torch.float32, "stats", NSHARD * 2 * Cc)
+    _chk(stats, torch.float64, "stats", NSHARD * 2 * Cc)
     if mask_mode == MASK_OUT:
         _chk(mref, torch.bfloat16, "mref", y.numel())
     C().bn_bwd_reduce(dout.data_ptr(), _p(mref), y.data_ptr(), _p(scale), _p(shift), mean.data_ptr(),
@@ -443,6 +449,8 @@ def softmax_ce(logits, labels, dlogits=None, loss_out=None, stats=None, smoothin
     _chk(labels, torch.int64, "labels", B)
     if dlogits is not None:
         _chk(dlogits, logits.dtype, "dlogits", B * Cc)
+    if stats is not None:
+        _chk(stats, torch.float64, "stats", 2)
     C().softmax_ce(logits.data_ptr(), int(logits.dtype == torch.bfloat16), labels.data_ptr(), _p(dlogits),
                    _p(loss_out), _p(stats), B, Cc, float(smoothing), float(grad_scale), stream_ptr())
 
@@ -477,7 +485,8 @@ def adam_step(p, g, m, v, p16=None, *, lr, beta1, beta2, eps, weight_decay, deco
 
 @_dispatch
 def global_norm_clip_factor(g, max_norm, work):
-    """work: fp32[4] scratch; returns work[2:4] = (factor, norm) on device (no host sync)."""
+    """work: fp32[4] scratch (work[0:2] holds the fp64 sum of squares); returns work[2:4] =
+    (factor, norm) on device (no host sync)."""
     work.zero_()
     C().sumsq(g.data_ptr(), g.numel(), work.data_ptr(), stream_ptr())
     C().clip_factor(work.data_ptr(), float(max_norm), work[2:].data_ptr(), stream_ptr())

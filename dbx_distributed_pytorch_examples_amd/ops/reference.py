@@ -190,7 +190,7 @@ def bn_bwd_reduce(dout, y, mean, invstd, stats, *, mask_mode, mref=None, scale=N
 
 def bn_bwd_coeff(stats, count, gamma, mean, invstd, coeff, dgamma=None, dbeta=None, accumulate=False):
     C = mean.numel()
-    st = stats.view(NSHARD, 2, C).sum(0)
+    st = stats.view(NSHARD, 2, C).sum(0).float()
     s, q = st[0], st[1]
     g = gamma if gamma is not None else torch.ones_like(mean)
     sg, sgx = s / count, q / count
@@ -311,8 +311,9 @@ def adam_step(p, g, m, v, p16=None, *, lr, beta1, beta2, eps, weight_decay, deco
 
 def global_norm_clip_factor(g, max_norm, work):
     work.zero_()
-    work[0] = (g.float() ** 2).sum()
-    nrm = torch.sqrt(work[0])
+    ss = (g.double() ** 2).sum()
+    work[0:2].view(torch.float64)[0] = ss
+    nrm = torch.sqrt(ss).float()
     work[2] = torch.clamp(max_norm / (nrm + 1e-6), max=1.0)
     work[3] = nrm
     return work[2:3]

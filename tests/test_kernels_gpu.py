@@ -55,7 +55,7 @@ def test_conv_fwd(case, prologue):
     w = (torch.randn(OC, R, R, IC, device=dev) / math.sqrt(IC * R * R)).bfloat16()
     OH, OW = k.conv_out_hw(H, W, R, R, st, pad)
     out = torch.empty(N, OH, OW, OC, device=dev, dtype=torch.bfloat16)
-    stats = torch.zeros(k.NSHARD * 2 * OC, device=dev)
+    stats = k.new_stats(OC, dev)
     sc = sh = None
     xe = x.float()
     if prologue:
@@ -70,7 +70,7 @@ def test_conv_fwd(case, prologue):
                    relu_in=True, tile=tile)
         ref = nhwc(F.conv2d(nchw(xe), w.float().permute(0, 3, 1, 2), stride=st, padding=pad))
         assert relerr(out, ref) < 1e-2, (tile, relerr(out, ref))
-        s = stats.view(k.NSHARD, 2, OC).sum(0)
+        s = stats.view(k.NSHARD, 2, OC).sum(0).float()
         o32 = out.float().view(-1, OC)
         assert relerr(s[0], o32.sum(0)) < 1e-3
         assert relerr(s[1], (o32 * o32).sum(0)) < 1e-3
@@ -136,7 +136,7 @@ def test_stem_fwd_wgrad():
     w16s = ws_.bfloat16().view(64, 256)
     OH, OW = k.conv_out_hw(H, W, 7, 7, 2, 3)
     out = torch.empty(N, OH, OW, 64, device=dev, dtype=torch.bfloat16)
-    stats = torch.zeros(k.NSHARD * 2 * 64, device=dev)
+    stats = k.new_stats(64, dev)
     k.conv_stem_fwd(x4, w16s, out, stats=stats)
     xr = nchw(x4[..., :3].float())
     wr = ws_.bfloat16().float()[:, :7, :7, :3].permute(0, 3, 1, 2)
@@ -162,7 +162,7 @@ def test_bn_finalize_apply():
     k = K()
     M, Cc = 4096, 128
     y = _bn_ref_setup(M, Cc)
-    stats = torch.zeros(k.NSHARD * 2 * Cc, device=dev)
+    stats = k.new_stats(Cc, dev)
     k.channel_stats(y, stats)
     gamma = torch.rand(Cc, device=dev) + 0.5
     beta = torch.randn(Cc, device=dev)
@@ -225,7 +225,7 @@ def test_bn_backward(mask_mode):
     invstd = 1 / torch.sqrt(y.float().var(0, unbiased=False) + 1e-5)
     scale = gamma * invstd
     shift = beta - mean * scale
-    stats = torch.zeros(k.NSHARD * 2 * Cc, device=dev)
+    stats = k.new_stats(Cc, dev)
     k.bn_bwd_reduce(dout, y, mean, invstd, stats, mask_mode=mask_mode, mref=mref, scale=scale, shift=shift)
     coeff = torch.empty(3 * Cc, device=dev)
     dg = torch.empty(Cc, device=dev)
@@ -286,7 +286,7 @@ def test_softmax_ce(dtype, smoothing):
     loss.backward()
     dl = torch.empty_like(logits)
     lo = torch.empty(B, device=dev)
-    st = torch.zeros(2, device=dev)
+    st = torch.zeros(2, device=dev, dtype=torch.float64)
     k.softmax_ce(logits, labels, dl, lo, st, smoothing=smoothing)
     assert abs(lo.mean().item() - loss.item()) < 1e-3 * max(1, loss.item())
     assert abs(st[0].item() / B - loss.item()) < 1e-3 * max(1, loss.item())
@@ -437,8 +437,8 @@ def test_conv_dgrad_fused_epilogue(mode, sub, stride):
 
     def run(mod, devc, tile=None):
         t = lambda v: v.to(devc)  # noqa: E731
-        st1 = torch.zeros(k.NSHARD * 2 * IC, device=devc)
-        st2 = torch.zeros(k.NSHARD * 2 * IC, device=devc)
+        st1 = k.new_stats(IC, devc)
+        st2 = k.new_stats(IC, devc)
         epi = None
         if mode:
             epi = k.BNBwdEpilogue(mode, t(ybn), t(mean), t(inv), st1,
@@ -449,7 +449,7 @@ def test_conv_dgrad_fused_epilogue(mode, sub, stride):
         dx = torch.empty(N, H, W, IC, device=devc, dtype=torch.bfloat16)
         mod.conv_dgrad(t(dy), t(wt), dx, R=Rr, S=Rr, stride=stride, pad=pad, addsrc=t(add), add_sub=sub, epilogue=epi,
                        tile=tile)
-        return dx.float().cpu(), st1.view(k.NSHARD, 2, IC).sum(0).cpu(), st2.view(k.NSHARD, 2, IC).sum(0).cpu()
+        return dx.float().cpu(), st1.view(k.NSHARD, 2, IC).sum(0).float().cpu(), st2.view(k.NSHARD, 2, IC).sum(0).float().cpu()
 
     r_dx, r_s1, r_s2 = run(R, "cpu")
     for tile in [None, (128, 128), (64, 64), (256, 128), (128, 256), (256, 64)]:

@@ -60,7 +60,7 @@ def main():
         dy = torch.randn(N, OH, OH, Kc, device=dev).bfloat16()
         dx = torch.empty_like(x)
         dw = torch.empty(Kc, R * R * C, device=dev)
-        stats = torch.zeros(K.NSHARD * 2 * Kc, device=dev)
+        stats = K.new_stats(Kc, dev)
         xc = x.permute(0, 3, 1, 2)  # channels_last view
         wc = w.permute(0, 3, 1, 2)
         dyc = dy.permute(0, 3, 1, 2)

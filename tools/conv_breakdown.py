@@ -38,7 +38,7 @@ def main():
         x = torch.randn(N, H, H, C, device=dev).bfloat16()
         w = (torch.randn(Kc, C, device=dev) / math.sqrt(C)).bfloat16()
         y = torch.empty(N, H, H, Kc, device=dev, dtype=torch.bfloat16)
-        stats = torch.zeros(K.NSHARD * 2 * Kc, device=dev)
+        stats = K.new_stats(Kc, dev)
         sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
         byt = (x.numel() + y.numel()) * 2
         print(f"--- {C}->{Kc} @{H}  fwd bytes {byt / 1e9:.2f} GB, copy-roof {byt / 6.0e9:.3f} ms")
@@ -57,7 +57,7 @@ def main():
         wt = w.t().contiguous()
         dx = torch.empty_like(x)
         ybn, mref, add = torch.randn_like(x), torch.randn_like(x), torch.randn_like(x)
-        st1 = torch.zeros(K.NSHARD * 2 * C, device=dev)
+        st1 = K.new_stats(C, dev)
         mean, inv = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
         e1 = K.BNBwdEpilogue(K.MASK_OUT, ybn, mean, inv, st1, mbits=K.pack_mask_bits(mref))
         e2 = K.BNBwdEpilogue(K.MASK_Y, ybn, mean, inv, st1, scale=sc, shift=sh)

@@ -76,13 +76,13 @@ def main():
         y = torch.empty(N, OH, OH, Kc, device=dev, dtype=torch.bfloat16)
         dy = torch.randn(N, OH, OH, Kc, device=dev).bfloat16()
         dx = torch.empty_like(x)
-        stats = torch.zeros(K.NSHARD * 2 * Kc, device=dev)
+        stats = K.new_stats(Kc, dev)
         sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
         gf = 2.0 * N * OH * OH * Kc * C * R * R / 1e9
         ybn = torch.randn_like(x)
         mref = torch.randn_like(x)
         add = torch.randn_like(x)
-        st1 = torch.zeros(K.NSHARD * 2 * C, device=dev)
+        st1 = K.new_stats(C, dev)
         mean, inv = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
         jobs = [("fwd", N * OH * OH, Kc, C, R, st,
                  lambda t: K.conv_fwd(x, w2, y, R=R, S=R, stride=st, pad=pad, stats=stats, in_scale=sc,
