@@ -32,6 +32,9 @@ int dbx_bn_bwd_apply(const bf16*, const bf16*, const bf16*, const float*, const 
 int dbx_maxpool_fwd(const bf16*, const float*, const float*, bf16*, unsigned char*, int, int, int, int, int, int, int,
                     int, int, int, hipStream_t);
 int dbx_maxpool_bwd(const bf16*, const unsigned char*, bf16*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int dbx_pool_bn_bwd(const bf16*, const unsigned char*, const bf16*, const float*, const float*, const float*,
+                    const float*, const float*, bf16*, double*, int, int, int, int, int, int, int, int, int, int, int,
+                    hipStream_t);
 int dbx_avgpool_fwd(const bf16*, bf16*, int, int, int, hipStream_t);
 int dbx_avgpool_bwd(const bf16*, bf16*, int, int, int, hipStream_t);
 int dbx_softmax_ce(const void*, int, const long long*, void*, float*, double*, int, int, float, float, hipStream_t);
@@ -149,6 +152,14 @@ PYBIND11_MODULE(_C, m) {
     check(dbx_maxpool_bwd(P<const bf16*>(dout), P<const unsigned char*>(arg), P<bf16*>(dx), N, H, W, C, Pp, Q, K,
                           stride, pad, S(st)),
           "maxpool_bwd");
+  });
+  m.def("pool_bn_bwd", [](uintptr_t dpool, uintptr_t arg, uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t c1,
+                          uintptr_t c2, uintptr_t c3, uintptr_t dy, uintptr_t stats, int nshard, int N, int H, int W,
+                          int C, int Pp, int Q, int K, int stride, int pad, int apply, uintptr_t st) {
+    check(dbx_pool_bn_bwd(P<const bf16*>(dpool), P<const unsigned char*>(arg), P<const bf16*>(y), P<const float*>(sc),
+                          P<const float*>(sh), P<const float*>(c1), P<const float*>(c2), P<const float*>(c3),
+                          P<bf16*>(dy), P<double*>(stats), nshard, N, H, W, C, Pp, Q, K, stride, pad, apply, S(st)),
+          "pool_bn_bwd");
   });
   m.def("avgpool_fwd", [](uintptr_t x, uintptr_t out, int N, int HW, int C, uintptr_t st) {
     check(dbx_avgpool_fwd(P<const bf16*>(x), P<bf16*>(out), N, HW, C, S(st)), "avgpool_fwd");

@@ -103,14 +103,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       for (int i = 0; i < A_CH; ++i) {
         const int ih = ahb[i] + r;
         const bool rv = (r < a.R) && ih >= 0 && ih < a.IH;
-        unsigned int w4[4] = {0u, 0u, 0u, 0u};
+        unsigned int w4[4];
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
+          // branch-free: an out-of-image pixel loads the image base and is zeroed by the select
           const int s = s0 + p, iw = awb[i] + s;
-          if (rv && s < a.S && iw >= 0 && iw < a.IW) {
-            const uint2 v = *reinterpret_cast<const uint2*>(abase[i] + ((size_t)ih * a.IW + iw) * 4);
-            w4[2 * p] = v.x; w4[2 * p + 1] = v.y;
-          }
+          const bool v = rv && s < a.S && (unsigned)iw < (unsigned)a.IW;
+          const uint2 t = *reinterpret_cast<const uint2*>(abase[i] + (v ? (ih * a.IW + iw) * 4 : 0));
+          w4[2 * p] = v ? t.x : 0u; w4[2 * p + 1] = v ? t.y : 0u;
         }
         ra[S][i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
       }
@@ -579,15 +579,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const WgradArgs 
       const int ih = ih0 + b_tap_h[j];
       if constexpr (MODE == STEM) {
         // 16B chunk = 2 pixels (s, s+1) x 4 channels
-        unsigned int w4[4] = {0u, 0u, 0u, 0u};
+        unsigned int w4[4];
         const bool rv = mv && b_tap_h[j] < a.R && ih >= 0 && ih < a.IH;
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
+        for (int p = 0; p < 2; ++p) {  // branch-free (see the stem A loader in igemm_kernel)
           const int s = b_tap_w[j] + p, iw = ow * a.stride - a.pad + s;
-          if (rv && s < a.S && iw >= 0 && iw < a.IW) {
-            const uint2 v = *reinterpret_cast<const uint2*>(base + ((size_t)ih * a.IW + iw) * 4);
-            w4[2 * p] = v.x; w4[2 * p + 1] = v.y;
-          }
+          const bool v = rv && s < a.S && (unsigned)iw < (unsigned)a.IW;
+          const uint2 t = *reinterpret_cast<const uint2*>(base + (v ? (ih * a.IW + iw) * 4 : 0));
+          w4[2 * p] = v ? t.x : 0u; w4[2 * p + 1] = v ? t.y : 0u;
         }
         rb[S][j] = u32x4{w4[0], w4[1], w4[2], w4[3]};
       } else {

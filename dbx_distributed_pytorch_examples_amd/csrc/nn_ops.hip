@@ -360,6 +360,110 @@ __global__ void maxpool_bwd_kernel(const bf16* __restrict__ dout, const unsigned
 }
 
 // ----------------------------------------------------------------------------------------
+// Stem backward without the pooled-gradient tensor: the max-pool backward (gather form) is
+// recomputed inside the BN-backward reduce and apply passes of the stem BN, so the [N,112,112,64]
+// gradient of the pool input is never written or re-read (3 x 1.6 GB at batch 1024).
+//   g[n,h,w,c] = sum over pool windows (p,q) containing (h,w) with argmax == (h,w): dpool[n,p,q,c]
+//   g *= (y*sc + sh > 0)                       (the ReLU between the stem BN and the pool)
+//   reduce: stats += [sum g, sum g*xhat]       apply: dy = k1*g + k2*y + k3
+// A block walks whole image rows (n, h): the window rows p are block-uniform, and at most two
+// windows per dimension contain a pixel (host-checked: ceil(K/stride) <= 2), so the gather is a
+// fixed 2x2 candidate set with clamped addresses and selects (no branches around loads).
+// 32-bit offsets: host checks N*H*W*C < 2^31.
+// ----------------------------------------------------------------------------------------
+template <bool APPLY>
+__global__ __launch_bounds__(256) void pool_bn_bwd_kernel(const bf16* __restrict__ dpool,
+                                                          const unsigned char* __restrict__ arg,
+                                                          const bf16* __restrict__ y, const float* __restrict__ sc,
+                                                          const float* __restrict__ sh, const float* __restrict__ c1,
+                                                          const float* __restrict__ c2, const float* __restrict__ c3,
+                                                          bf16* __restrict__ dy, double* __restrict__ stats, int nshard,
+                                                          int N, int H, int W, int C, int P, int Q, int K, int stride,
+                                                          int pad) {
+  const int cpt = C >> 3;  // 256 % cpt == 0 (host): a thread's channel group is fixed
+  const int tid = threadIdx.x;
+  const int c0 = (tid % cpt) * 8;
+  float s_[8], h_[8], k1[8], k2[8], k3[8];
+  load8f(sc + c0, s_);
+  load8f(sh + c0, h_);
+  load8f(c1 + c0, k1);  // reduce: mean, invstd ; apply: k1, k2, k3
+  load8f(c2 + c0, k2);
+  if (APPLY) load8f(c3 + c0, k3);
+  float as[8] = {0, 0, 0, 0, 0, 0, 0, 0}, aq[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int rows = N * H, per_row = W * cpt;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int n = row / H, h = row - n * H;
+    const int p_lo = max(0, (h + pad - K + stride) / stride), p_hi = min(P - 1, (h + pad) / stride);
+    const int r_lo = h + pad - p_lo * stride;
+    const bool p1 = p_hi >= p_lo, p2 = p_hi > p_lo;  // block-uniform: first / second window row exist
+    const int pc = p1 ? p_lo : 0;
+    const int prow0 = (n * P + pc) * Q, prow1 = (n * P + (p2 ? p_lo + 1 : pc)) * Q;
+    for (int i = tid; i < per_row; i += 256) {
+      const int w = i / cpt;
+      const int q_lo = max(0, (w + pad - K + stride) / stride);
+      u32x4 gd[2][2];
+      uint2 av[2][2];
+      bool ok[2][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int q = q_lo + t;
+        const int s = w + pad - q * stride;
+        const bool vq = q < Q && s >= 0 && s < K;
+        const int qq = vq ? q : 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int o = ((u ? prow1 : prow0) + qq) * C + c0;
+          gd[u][t] = *reinterpret_cast<const u32x4*>(dpool + o);
+          av[u][t] = *reinterpret_cast<const uint2*>(arg + o);
+          ok[u][t] = vq && (u == 0 ? p1 : p2);
+        }
+      }
+      const int e = (row * W + w) * C + c0;
+      float yv[8];
+      unpack8(*reinterpret_cast<const u32x4*>(y + e), yv);
+      float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int r = r_lo - u * stride, s = w + pad - (q_lo + t) * stride;
+          const unsigned me = (unsigned)(r * K + s);
+          float gv[8];
+          unpack8(gd[u][t], gv);
+          const unsigned char* a8 = reinterpret_cast<const unsigned char*>(&av[u][t]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] += (ok[u][t] && a8[j] == me) ? gv[j] : 0.f;
+        }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (yv[j] * s_[j] + h_[j]) > 0.f ? g[j] : 0.f;
+      if (APPLY) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = k1[j] * g[j] + k2[j] * yv[j] + k3[j];
+        *reinterpret_cast<u32x4*>(dy + e) = pack8(o);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { as[j] += g[j]; aq[j] += g[j] * (yv[j] - k1[j]) * k2[j]; }
+      }
+    }
+  }
+  if (!APPLY) {
+    __shared__ float red[2][256 * 8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[0][tid * 8 + j] = as[j]; red[1][tid * 8 + j] = aq[j]; }
+    __syncthreads();
+    double* st = stats + (size_t)(blockIdx.x % nshard) * 2 * C;
+    for (int c = tid; c < C; c += 256) {
+      const int gi = c / 8, j = c % 8;
+      float ss = 0.f, qq = 0.f;
+      for (int r = 0; r < 256 / cpt; ++r) { ss += red[0][(r * cpt + gi) * 8 + j]; qq += red[1][(r * cpt + gi) * 8 + j]; }
+      atomicAdd(st + c, (double)ss);
+      atomicAdd(st + C + c, (double)qq);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // Global average pool [N][HW][C] -> [N][C] (bf16 out, fp32 accumulate) and its backward
 // ----------------------------------------------------------------------------------------
 __global__ void avgpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ out, int N, int HW, int C) {
@@ -740,6 +844,21 @@ extern "C" int dbx_maxpool_bwd(const bf16* dout, const unsigned char* arg, bf16*
   const long long total = (long long)N * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, st, dout, arg, dx, N, H, W, C, P, Q, K,
                      stride, pad);
+  RET_LAST;
+}
+extern "C" int dbx_pool_bn_bwd(const bf16* dpool, const unsigned char* arg, const bf16* y, const float* sc,
+                               const float* sh, const float* c1, const float* c2, const float* c3, bf16* dy,
+                               double* stats, int nshard, int N, int H, int W, int C, int P, int Q, int K, int stride,
+                               int pad, int apply, hipStream_t st) {
+  if (C % 8 || 256 % (C / 8) || (K + stride - 1) / stride > 2) return -1;
+  if ((long long)N * H * W * C >= (1LL << 31) || (long long)N * P * Q * C >= (1LL << 31)) return -2;
+  const dim3 g(grid_for((long long)N * H, 1, apply ? 8192 : 2048)), b(256);
+  if (apply)
+    hipLaunchKernelGGL((pool_bn_bwd_kernel<true>), g, b, 0, st, dpool, arg, y, sc, sh, c1, c2, c3, dy, stats, nshard,
+                       N, H, W, C, P, Q, K, stride, pad);
+  else
+    hipLaunchKernelGGL((pool_bn_bwd_kernel<false>), g, b, 0, st, dpool, arg, y, sc, sh, c1, c2, c3, dy, stats, nshard,
+                       N, H, W, C, P, Q, K, stride, pad);
   RET_LAST;
 }
 extern "C" int dbx_avgpool_fwd(const bf16* x, bf16* out, int N, int HW, int C, hipStream_t st) {

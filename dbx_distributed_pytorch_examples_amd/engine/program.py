@@ -316,7 +316,8 @@ class ResNetProgram:
         self.p0 = E(N, ph, pw, st.OC)
         self.parg = torch.empty(N, ph, pw, st.OC, device=dev, dtype=torch.uint8)
         self.dp0 = E(N, ph, pw, st.OC)
-        self.da0 = E(N, st.OH, st.OW, st.OC)
+        # pooled-gradient buffer only for pool geometries the fused stem backward does not cover
+        self.da0 = None if K.pool_bn_bwd_supported(st.OC, self.pool_k, self.pool_s) else E(N, st.OH, st.OW, st.OC)
         self.dy0 = E(N, st.OH, st.OW, st.OC)
         wsmax = 0
         for b in self.blocks:
@@ -580,8 +581,17 @@ class ResNetProgram:
 
     def _bwd_stem(self):
         st, sbn = self.stem, self.stem_bn
-        K.maxpool_bwd(self.blocks[0].dx, self.parg, self.da0, K=self.pool_k, stride=self.pool_s, pad=self.pool_p)
-        self._bn_bwd(sbn, self.da0, self.y0, self.dy0, self.N * st.OH * st.OW, K.MASK_Y)
+        dp = self.blocks[0].dx
+        if K.pool_bn_bwd_supported(st.OC, self.pool_k, self.pool_s):
+            # max-pool backward folded into the stem BN's reduce/apply passes (no pooled-grad tensor)
+            pk = dict(K=self.pool_k, stride=self.pool_s, pad=self.pool_p)
+            K.pool_bn_bwd_reduce(dp, self.parg, self.y0, sbn.scale, sbn.shift, sbn.mean, sbn.invstd, sbn.bstats, **pk)
+            K.bn_bwd_coeff(sbn.bstats, self.N * st.OH * st.OW, sbn.gamma, sbn.mean, sbn.invstd, sbn.coeff,
+                           sbn.dgamma, sbn.dbeta)
+            K.pool_bn_bwd_apply(dp, self.parg, self.y0, sbn.scale, sbn.shift, sbn.coeff, self.dy0, **pk)
+        else:
+            K.maxpool_bwd(dp, self.parg, self.da0, K=self.pool_k, stride=self.pool_s, pad=self.pool_p)
+            self._bn_bwd(sbn, self.da0, self.y0, self.dy0, self.N * st.OH * st.OW, K.MASK_Y)
         def stem_wgrad():
             K.conv_wgrad(self.dy0, self.x4, self.stem_grad_tmp, self.ws, R=st.R, S=st.S, stride=st.stride,
                          pad=st.pad, stem=True)

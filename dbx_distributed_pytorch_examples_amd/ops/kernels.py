@@ -179,27 +179,6 @@ class BNBwdEpilogue:
                 _p(self.mean1), _p(self.inv1), _p(self.mean2), _p(self.inv2), _p(self.stats1), _p(self.stats2))
 
 
-def dgrad_phases(H: int, W: int, R: int, S: int, stride: int, pad: int):
-    """Parity decomposition of a strided dgrad into stride-1 sub-problems.
-
-    Output pixel h receives tap r only where (h + pad - r) % stride == 0, so for each output
-    phase (ph, pw) only taps r = r0 + stride*t contribute and the gather is dense:
-    ih = i + (ph + pad - r0) // stride - t over the phase's sub-grid i (h = i*stride + ph).
-    Returns [(ph, pw, OHs, OWs, r0, nr, s0, ns, dh0, dw0)] (classes with no taps included, nr=0).
-    """
-    out = []
-    for ph in range(stride):
-        for pw in range(stride):
-            ohs = (H - ph + stride - 1) // stride
-            ows = (W - pw + stride - 1) // stride
-            r0 = (ph + pad) % stride
-            s0 = (pw + pad) % stride
-            nr = max(0, (R - r0 + stride - 1) // stride)
-            ns = max(0, (S - s0 + stride - 1) // stride)
-            out.append((ph, pw, ohs, ows, r0, nr, s0, ns, (ph + pad - r0) // stride, (pw + pad - s0) // stride))
-    return out
-
-
 @_dispatch
 def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, addsrc=None, add_sub=1,
                epilogue: "BNBwdEpilogue" = None):
@@ -423,6 +402,44 @@ def maxpool_bwd(dout, arg, dx, *, K=3, stride=2, pad=1):
     _chk(arg, torch.uint8, "arg", dout.numel())
     _chk(dx, torch.bfloat16, "dx")
     C().maxpool_bwd(dout.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, H, W, Cc, P, Q, K, stride, pad, stream_ptr())
+
+
+def _pool_bn_bwd_check(dpool, arg, y, K, stride):
+    N, H, W, Cc = y.shape
+    _chk(dpool, torch.bfloat16, "dpool")
+    _chk(arg, torch.uint8, "arg", dpool.numel())
+    _chk(y, torch.bfloat16, "y")
+    if dpool.shape[0] != N or dpool.shape[3] != Cc:
+        raise ValueError("pool_bn_bwd: dpool / y shapes disagree")
+    if Cc % 8 or 256 % (Cc // 8) or (K + stride - 1) // stride > 2:
+        raise ValueError("pool_bn_bwd: unsupported channel count / pool geometry")
+    return N, H, W, Cc, dpool.shape[1], dpool.shape[2]
+
+
+def pool_bn_bwd_supported(C: int, K: int, stride: int) -> bool:
+    return C % 8 == 0 and 256 % (C // 8) == 0 and (K + stride - 1) // stride <= 2
+
+
+@_dispatch
+def pool_bn_bwd_reduce(dpool, arg, y, scale, shift, mean, invstd, stats, *, K=3, stride=2, pad=1):
+    """BN-backward reduce of the stem BN with the max-pool backward folded in: g = maxpool_bwd(dpool)
+    masked by relu(y*scale+shift) > 0; stats += [sum g, sum g*xhat]. The pooled-gradient
+    tensor at the pool input resolution is never materialised."""
+    N, H, W, Cc, Pp, Q = _pool_bn_bwd_check(dpool, arg, y, K, stride)
+    _chk(stats, torch.float64, "stats", NSHARD * 2 * Cc)
+    C().pool_bn_bwd(dpool.data_ptr(), arg.data_ptr(), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                    mean.data_ptr(), invstd.data_ptr(), 0, 0, stats.data_ptr(), NSHARD, N, H, W, Cc, Pp, Q, K,
+                    stride, pad, 0, stream_ptr())
+
+
+@_dispatch
+def pool_bn_bwd_apply(dpool, arg, y, scale, shift, coeff, dy, *, K=3, stride=2, pad=1):
+    """dy = k1*g + k2*y + k3 with g recomputed as in ``pool_bn_bwd_reduce``."""
+    N, H, W, Cc, Pp, Q = _pool_bn_bwd_check(dpool, arg, y, K, stride)
+    _chk(dy, torch.bfloat16, "dy", y.numel())
+    C().pool_bn_bwd(dpool.data_ptr(), arg.data_ptr(), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                    coeff.data_ptr(), coeff.data_ptr() + 4 * Cc, coeff.data_ptr() + 8 * Cc, dy.data_ptr(), 0, NSHARD,
+                    N, H, W, Cc, Pp, Q, K, stride, pad, 1, stream_ptr())
 
 
 @_dispatch

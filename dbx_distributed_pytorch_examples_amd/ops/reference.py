@@ -247,6 +247,36 @@ def maxpool_bwd(dout, arg, dx, *, K=3, stride=2, pad=1):
     dx.copy_(_nhwc(acc[:, :, pad:pad + H, pad:pad + W]).bfloat16())
 
 
+def _pool_g(dpool, arg, y, scale, shift, K, stride, pad):
+    N, H, W, C = y.shape
+    _, P, Q, _ = dpool.shape
+    acc = torch.zeros(N, C, H + 2 * pad, W + 2 * pad, dtype=torch.float32, device=y.device)
+    g = _nchw(dpool.float())
+    a = _nchw(arg)
+    for r in range(K):
+        for s in range(K):
+            acc[:, :, r:r + stride * (P - 1) + 1:stride, s:s + stride * (Q - 1) + 1:stride] += torch.where(
+                a == r * K + s, g, torch.zeros_like(g))
+    da = _nhwc(acc[:, :, pad:pad + H, pad:pad + W])
+    return torch.where(y.float() * scale + shift > 0, da, torch.zeros_like(da))
+
+
+def pool_bn_bwd_reduce(dpool, arg, y, scale, shift, mean, invstd, stats, *, K=3, stride=2, pad=1):
+    C = y.shape[-1]
+    g = _pool_g(dpool, arg, y, scale, shift, K, stride, pad).reshape(-1, C)
+    xhat = ((y.float() - mean) * invstd).reshape(-1, C)
+    st = stats.view(NSHARD, 2, C)
+    st[0, 0] += g.sum(0).double()
+    st[0, 1] += (g * xhat).sum(0).double()
+
+
+def pool_bn_bwd_apply(dpool, arg, y, scale, shift, coeff, dy, *, K=3, stride=2, pad=1):
+    C = y.shape[-1]
+    g = _pool_g(dpool, arg, y, scale, shift, K, stride, pad)
+    k = coeff.view(3, C)
+    dy.copy_((k[0] * g + k[1] * y.float() + k[2]).bfloat16())
+
+
 def avgpool_fwd(x, out):
     out.copy_(x.float().mean((1, 2)).bfloat16())
 

@@ -261,6 +261,57 @@ def test_maxpool():
     assert relerr(dx.float() * m, act.grad * m) < 2e-2
 
 
+@pytest.mark.parametrize("hw", [(16, 16), (15, 13), (112, 112)])
+def test_pool_bn_bwd_fused(hw):
+    """Stem backward with the max-pool backward folded into the BN reduce/apply passes, against
+    fp32 autograd of relu(bn(y)) -> maxpool (odd sizes exercise the window-edge cases)."""
+    k = K()
+    H, W = hw
+    N, Cc = (2 if H > 64 else 3), 64
+    torch.manual_seed(6)
+    y = torch.randn(N, H, W, Cc, device=dev).bfloat16()
+    mean = y.float().mean((0, 1, 2))
+    invstd = 1.0 / y.float().var((0, 1, 2), unbiased=False).add(1e-5).sqrt()
+    gamma = torch.rand(Cc, device=dev) + 0.5
+    beta = torch.randn(Cc, device=dev) * 0.2
+    sc, sh = (gamma * invstd).contiguous(), (beta - mean * gamma * invstd).contiguous()
+    P, Q = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
+    pooled = torch.empty(N, P, Q, Cc, device=dev, dtype=torch.bfloat16)
+    arg = torch.empty(N, P, Q, Cc, device=dev, dtype=torch.uint8)
+    k.maxpool_fwd(y, pooled, arg, scale=sc, shift=sh, relu=True)
+    dpool = torch.randn(N, P, Q, Cc, device=dev).bfloat16()
+    # fp32 reference: BN (batch stats) -> relu -> maxpool, autograd
+    yr = y.float().requires_grad_(True)
+    xh = (yr - mean) * invstd
+    out = F.max_pool2d(nchw(torch.relu(xh * gamma + beta)), 3, 2, 1)
+    out.backward(nchw(dpool.float()))
+    # the batch-statistics BN backward of the same graph: dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
+    act = torch.relu(xh * gamma + beta).detach().requires_grad_(True)
+    F.max_pool2d(nchw(act), 3, 2, 1).backward(nchw(dpool.float()))
+    g = act.grad * (act.detach() > 0)
+    xhd = xh.detach()
+    cnt = N * H * W
+    sg, sgx = g.sum((0, 1, 2)), (g * xhd).sum((0, 1, 2))
+    dy_ref = gamma * invstd * (g - sg / cnt - xhd * sgx / cnt)
+    stats = k.new_stats(Cc, dev)
+    k.pool_bn_bwd_reduce(dpool, arg, y, sc, sh, mean.contiguous(), invstd.contiguous(), stats)
+    st = stats.view(k.NSHARD, 2, Cc).sum(0)
+    assert relerr(st[0], sg) < 1e-3 and relerr(st[1], sgx) < 1e-3
+    coeff = torch.empty(3 * Cc, device=dev)
+    dgamma, dbeta = torch.empty(Cc, device=dev), torch.empty(Cc, device=dev)
+    k.bn_bwd_coeff(stats, cnt, gamma, mean.contiguous(), invstd.contiguous(), coeff, dgamma, dbeta)
+    dy = torch.empty_like(y)
+    k.pool_bn_bwd_apply(dpool, arg, y, sc, sh, coeff, dy)
+    assert relerr(dy, dy_ref) < 2e-2
+    assert relerr(dbeta, sg) < 1e-3 and relerr(dgamma, sgx) < 1e-3
+    # CPU reference implementation agrees with the kernel
+    st_ref = k.new_stats(Cc, "cpu")
+    cpu = lambda t: t.cpu()  # noqa: E731
+    from dbx_distributed_pytorch_examples_amd.ops import reference as R
+    R.pool_bn_bwd_reduce(cpu(dpool), cpu(arg), cpu(y), cpu(sc), cpu(sh), cpu(mean), cpu(invstd), st_ref)
+    assert relerr(st_ref.view(k.NSHARD, 2, Cc).sum(0), st.cpu()) < 1e-4
+
+
 def test_avgpool():
     k = K()
     x = torch.randn(4, 7, 7, 256, device=dev).bfloat16()
