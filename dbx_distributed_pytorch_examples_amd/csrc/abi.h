@@ -44,5 +44,6 @@ struct WgradArgs {
   const float* in_shift;
   int N, IH, IW, IC, OH, OW, OC, R, S, stride, pad;
   int M, KTOT, nsplit, m_per_split, relu_in;
+  unsigned long long mag_ow, mag_ohw;  // ceil(2^40 / OW), ceil(2^40 / (OH*OW)): pixel -> (n, oh, ow)
 };
 }  // namespace dbx

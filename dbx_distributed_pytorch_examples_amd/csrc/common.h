@@ -35,6 +35,19 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return __builtin_bit_cast(u32x4, b);
 }
 
+// ReLU of 8 packed bf16: a bf16 bit pattern read as int16 is negative exactly when the value is
+// (incl. -0), so max(x, 0) is one v_pk_max_i16 per 2 elements instead of 2 fp32 max
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ u32x4 relu_bf16x8(const u32x4 v) {
+  const s16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  return __builtin_bit_cast(u32x4, __builtin_elementwise_max(__builtin_bit_cast(s16x8, v), z));
+}
+
+// floor(x / d) for 0 <= x, x * d < 2^40 with mag = ceil(2^40 / d) (host: div_magic)
+__device__ __forceinline__ int mdiv(int x, unsigned long long mag) {
+  return (int)(((unsigned long long)(unsigned)x * mag) >> 40);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -57,3 +70,16 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Raw buffer loads (SRD in SGPRs, 32-bit per-lane byte offset). An offset at or past num_records
+// returns zeros, which is how the conv gathers zero-fill padding taps and rows past M without a
+// select on the data; built from kernel arguments only, so the descriptor is provably uniform.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr unsigned kOOB = 0xFFFFFF00u;  // an offset no tensor reaches (num_records <= kOOB)
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned long long bytes) {
+  const unsigned n = bytes < (unsigned long long)kOOB ? (unsigned)bytes : kOOB;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ u32x4 buf_load16(rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}

@@ -46,10 +46,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   constexpr int LDS_AB = 2 * (BM + BN) * BK;  // bf16 elements
   constexpr int LDS_C = BM * (BN + 8);
   constexpr int LDS_RED = 2 * (3 * NW * BN);  // fp32 reduction scratch (in bf16 units)
-  constexpr int LDS_ELEMS = (LDS_AB > LDS_C + LDS_RED) ? LDS_AB : (LDS_C + LDS_RED);
-  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
+  constexpr int PRO_MAXC = 512;                            // prologue channels held in LDS (host-checked)
+  constexpr int LDS_PRO = (PRO && MODE != STEM) ? 4 * PRO_MAXC : 0;  // fp32 scale + shift (bf16 units)
+  constexpr int LDS_MAIN = (LDS_AB > LDS_C + LDS_RED) ? LDS_AB : (LDS_C + LDS_RED);
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_MAIN + LDS_PRO];
   bf16* sA = lds;                  // [2][BM][BK]
   bf16* sB = lds + 2 * BM * BK;    // [2][BN][BK]
+  // prologue affine of ALL input channels, staged once: the per-block coefficients are read from
+  // LDS at transform time instead of living in registers across the pipeline
+  float* sPro = reinterpret_cast<float*>(lds + LDS_MAIN);  // [2][PRO_MAXC]: scale, shift
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
   const int ntn = a.OC / BN, ntm = (a.M + BM - 1) / BM;
@@ -61,7 +66,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   const int ach = tid & 7;
   const bf16* abase[A_CH];   // STEM mode: image base
   int ahb[A_CH], awb[A_CH];  // top-left input coordinate of the row's receptive field
-  int apix[A_CH];            // element offset of (n, ahb, awb, 0) in x: 32-bit (host checks numel < 2^31)
+  unsigned apix[A_CH];       // byte offset of (n, ahb, awb, ach*8) in x (host: bytes < kOOB)
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
     const int m = m0 + (tid >> 3) + RPP * i;
@@ -73,15 +78,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     abase[i] = a.x + (size_t)n * a.IH * a.IW * a.IC;
     if (MODE == DGRAD) { ahb[i] = oh + a.dh0; awb[i] = ow + a.dw0; }
     else { ahb[i] = oh * a.stride - a.pad; awb[i] = ow * a.stride - a.pad; }
-    apix[i] = ((n * a.IH + ahb[i]) * a.IW + awb[i]) * a.IC;
+    apix[i] = 2u * (unsigned)(((n * a.IH + ahb[i]) * a.IW + awb[i]) * a.IC + ach * 8);
     if (m >= a.M) ahb[i] = -(1 << 28);
   }
-  // wave-uniform: can a staged A chunk be invalid (padding tap / row past M)? 1x1 stride-1 and
-  // unpadded convs on full tiles skip the zero-selects
-  const bool asel = (MODE == DGRAD) ? (a.nr > 1 || a.ns > 1 || a.dh0 != 0 || a.dw0 != 0 || a.OH > a.IH ||
-                                     a.OW > a.IW || (a.M % BM) != 0)
-                                    : (a.pad != 0 || (a.M % BM) != 0);
+  const rsrc_t xr = make_rsrc(a.x, 2ull * a.N * a.IH * a.IW * a.IC);
   const int KTOT = (MODE == STEM) ? 256 : a.R * a.S * a.IC;  // weight row length
+  const rsrc_t wr = make_rsrc(a.w, 2ull * a.OC * KTOT);
   const int cpt = (MODE == STEM) ? 1 : a.IC / BK;              // K blocks per tap
   const int KB = (MODE == STEM) ? 4 : a.nr * a.ns * cpt;
 
@@ -90,14 +92,31 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // work to hide its latency instead of one. The K loop is unrolled by two so S is a constant.
   u32x4 ra[2][A_CH], rb[2][B_CH];
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
-  f32x4 ps0[2], ps1[2], ph0[2], ph1[2];  // prologue affine of the staged A chunks
   unsigned avalid[2] = {0u, 0u};          // bit i: chunk i is a real (non-padding) tap
+  int pcb[2] = {0, 0};                    // channel block of the staged set (prologue coefficients)
+  if constexpr (PRO && MODE != STEM) {
+    for (int c = tid; c < a.IC; c += NT) {
+      sPro[c] = a.in_scale[c];
+      sPro[PRO_MAXC + c] = a.in_shift[c];
+    }
+    __syncthreads();
+  }
+  // decomposition of the NEXT block to load (kb -> channel block, tap row, tap column), advanced
+  // by one per load instead of dividing kb (wave-uniform scalars); it stops at the last block, so
+  // the unconditional prefetch past the end re-loads block KB-1 (data unused)
+  int lk = 0, lcb = 0, lts = 0, ltr = 0;
+  auto advance = [&]() __attribute__((always_inline)) {
+    if (lk < KB - 1) {
+      ++lk;
+      if (++lcb == cpt) { lcb = 0; if (++lts == a.ns) { lts = 0; ++ltr; } }
+    }
+  };
 
-  auto load_a = [&](int kb, int S) __attribute__((always_inline)) {
+  auto load_a = [&](int S) __attribute__((always_inline)) {
     if constexpr (MODE == STEM) {
-      // k block kb covers filter rows r = 2kb, 2kb+1; chunk ach: r = 2kb + (ach>>2), pixels
+      // k block lk covers filter rows r = 2lk, 2lk+1; chunk ach: r = 2lk + (ach>>2), pixels
       // s = 2*(ach&3), +1, 4 channels (8 bytes) each.
-      const int r = 2 * kb + (ach >> 2);
+      const int r = 2 * lk + (ach >> 2);
       const int s0 = 2 * (ach & 3);
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
@@ -115,70 +134,57 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
         ra[S][i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
       }
     } else {
-      const int tap = kb / cpt;
-      const int c0 = (kb - tap * cpt) * BK + ach * 8;
-      const int tr = tap / a.ns, ts = tap - (tap / a.ns) * a.ns;
-      const int r = a.r0 + a.tstep * tr, s = a.s0 + a.tstep * ts;
-      if constexpr (PRO) {  // affine of this thread's 8 channels (same for all its rows), used by pro_a
-        ps0[S] = *reinterpret_cast<const f32x4*>(a.in_scale + c0);
-        ps1[S] = *reinterpret_cast<const f32x4*>(a.in_scale + c0 + 4);
-        ph0[S] = *reinterpret_cast<const f32x4*>(a.in_shift + c0);
-        ph1[S] = *reinterpret_cast<const f32x4*>(a.in_shift + c0 + 4);
-      }
-      // tap displacement, the same for all of this thread's rows (32-bit element offsets)
-      const int dh = (MODE == DGRAD) ? -tr : r, dw = (MODE == DGRAD) ? -ts : s;
-      const int toff = (dh * a.IW + dw) * a.IC + c0;
+      const int cb = lcb * BK;
+      const int r = a.r0 + a.tstep * ltr, s = a.s0 + a.tstep * lts;
+      if constexpr (PRO) pcb[S] = cb;
+      // tap displacement, the same for all of this thread's rows (uniform, bytes)
+      const int dh = (MODE == DGRAD) ? -ltr : r, dw = (MODE == DGRAD) ? -lts : s;
+      const unsigned toff = 2u * (unsigned)((dh * a.IW + dw) * a.IC + cb);
       avalid[S] = 0;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         const bool v = (unsigned)(ahb[i] + dh) < (unsigned)a.IH && (unsigned)(awb[i] + dw) < (unsigned)a.IW;
-        // branch-free: padding taps load a valid address and are zeroed at staging time
-        // (a conditional load would make hipcc branch around it and drain vmcnt to 0)
-        ra[S][i] = *reinterpret_cast<const u32x4*>(a.x + (v ? apix[i] + toff : 0));
-        avalid[S] |= (v ? 1u : 0u) << i;
+        // padding taps / rows past M read out of the buffer's range: the hardware returns zeros
+        ra[S][i] = buf_load16(xr, v ? apix[i] + toff : kOOB);
+        if constexpr (PRO) avalid[S] |= (v ? 1u : 0u) << i;
       }
     }
   };
   // BN-apply (+ReLU) prologue on the staged A chunks. Kept apart from load_a so the global loads
   // of block kb+1 stay in flight across block kb's MFMAs (the transform waits on the data).
   auto pro_a = [&](int S) __attribute__((always_inline)) {
-    if constexpr (!PRO && MODE != STEM) {
-      if (asel) {  // only when some tap can be padding or the last tile is partial
-#pragma unroll
-        for (int i = 0; i < A_CH; ++i) ra[S][i] = ((avalid[S] >> i) & 1u) ? ra[S][i] : zero4;
-      }
-    }
     if constexpr (PRO && MODE != STEM) {
+      const int c0 = pcb[S] + ach * 8;  // this thread's 8 channels (the same for all its rows)
+      const f32x4 ps0 = *reinterpret_cast<const f32x4*>(sPro + c0);
+      const f32x4 ps1 = *reinterpret_cast<const f32x4*>(sPro + c0 + 4);
+      const f32x4 ph0 = *reinterpret_cast<const f32x4*>(sPro + PRO_MAXC + c0);
+      const f32x4 ph1 = *reinterpret_cast<const f32x4*>(sPro + PRO_MAXC + c0 + 4);
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         float f[8];
         unpack8(ra[S][i], f);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          f[j] = f[j] * ps0[S][j] + ph0[S][j];
-          f[j + 4] = f[j + 4] * ps1[S][j] + ph1[S][j];
+          f[j] = f[j] * ps0[j] + ph0[j];
+          f[j + 4] = f[j + 4] * ps1[j] + ph1[j];
         }
-        if (a.relu_in) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-        }
-        ra[S][i] = ((avalid[S] >> i) & 1u) ? pack8(f) : zero4;  // padding taps stay exactly zero
+        u32x4 t = pack8(f);
+        t = relu_bf16x8(t);  // PRO implies ReLU (host-checked)
+        ra[S][i] = ((avalid[S] >> i) & 1u) ? t : zero4;  // padding taps stay exactly zero
       }
     }
   };
-  auto load_b = [&](int kb, int S) __attribute__((always_inline)) {
+  auto load_b = [&](int S) __attribute__((always_inline)) {
     int koff;
     if constexpr (MODE == STEM) {
-      koff = kb * BK + ach * 8;
+      koff = lk * BK + ach * 8;
     } else {
-      const int tap = kb / cpt;
-      const int tr = tap / a.ns, ts = tap - (tap / a.ns) * a.ns;
-      koff = ((a.r0 + a.tstep * tr) * a.S + a.s0 + a.tstep * ts) * a.IC + (kb - tap * cpt) * BK + ach * 8;
+      koff = ((a.r0 + a.tstep * ltr) * a.S + a.s0 + a.tstep * lts) * a.IC + lcb * BK + ach * 8;
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int n = n0 + (tid >> 3) + RPP * i;
-      rb[S][i] = *reinterpret_cast<const u32x4*>(a.w + (size_t)n * KTOT + koff);
+      rb[S][i] = buf_load16(wr, 2u * (unsigned)(n * KTOT + koff));
     }
   };
   auto store_ab = [&](int buf, int S) __attribute__((always_inline)) {
@@ -229,19 +235,21 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // and the loop body is branch-free, so hipcc's waitcnt pass sees the same in-flight loads on
   // every path and waits only for the older set (counted vmcnt) instead of draining to vmcnt(0).
   auto step = [&](int kb, int S) __attribute__((always_inline)) {
-    const int kn = kb + 2 < KB ? kb + 2 : KB - 1;
-    load_a(kn, S ^ 1);
-    load_b(kn, S ^ 1);
+    load_a(S ^ 1);  // block min(kb + 2, KB - 1)
+    load_b(S ^ 1);
+    advance();
     mma(kb & 1);
     pro_a(S);
     store_ab((kb + 1) & 1, S);  // past the last block this fills the idle buffer, never read
     __syncthreads();
   };
 
-  load_a(0, 0);
-  load_b(0, 0);
-  load_a(KB > 1 ? 1 : 0, 1);
-  load_b(KB > 1 ? 1 : 0, 1);
+  load_a(0);
+  load_b(0);
+  advance();
+  load_a(1);
+  load_b(1);
+  advance();
   pro_a(0);
   store_ab(0, 0);
   __syncthreads();
@@ -544,9 +552,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const WgradArgs 
   // hide behind. The prologue affine of the tile's BN columns lives in LDS, not in registers.
   u32x4 ra[2][A_CH], rb[2][B_CH];
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
-  unsigned bvalid[2] = {0u, 0u};  // bit j: B chunk j is a real (non-padding) tap
-  const bool bsel = a.pad != 0 || (a.M % BKM) != 0;  // wave-uniform: can a B chunk be invalid?
-  bool aok[2] = {false, false};   // this thread's A (dY) row lies inside the split
+  unsigned bvalid[2] = {0u, 0u};  // bit j: B chunk j is a real (non-padding) tap (PRO only)
   if constexpr (PRO) {
     for (int c = tid; c < BN; c += NT) {
       const int kk = kk0 + c;
@@ -556,23 +562,26 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const WgradArgs 
     }
   }
 
+  const rsrc_t dyr = make_rsrc(a.dy, 2ull * a.M * a.OC);
+  const rsrc_t xr = make_rsrc(a.x, 2ull * a.N * a.IH * a.IW * a.IC);
   auto load = [&](int kb, int S) __attribute__((always_inline)) {
+    // dY rows past the split read out of range (zeros): they add nothing to the reduction
     const int ma = mbeg + kb * BKM + a_row;
-    aok[S] = ma < mend;
+    const bool av = ma < mend;
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
       const int cc = a_c + j * ATPR;
-      ra[S][j] = *reinterpret_cast<const u32x4*>(a.dy + (size_t)(ma < mend ? ma : mbeg) * a.OC + k0 + cc * 8);
+      ra[S][j] = buf_load16(dyr, av ? 2u * (unsigned)(ma * a.OC + k0 + cc * 8) : kOOB);
     }
     const int mb = mbeg + kb * BKM + b_row;
     const bool mv = mb < mend;
     const int ohw = a.OH * a.OW;
-    const int n = mv ? mb / ohw : 0;
+    const int n = mv ? mdiv(mb, a.mag_ohw) : 0;
     const int pq = mb - n * ohw;
-    const int oh = pq / a.OW, ow = pq - (pq / a.OW) * a.OW;
+    const int oh = mdiv(pq, a.mag_ow), ow = pq - oh * a.OW;
     const bf16* base = a.x + (size_t)n * a.IH * a.IW * a.IC;
     const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
-    const int pix = ((n * a.IH + ih0) * a.IW + iw0) * a.IC;
+    const unsigned pix = 2u * (unsigned)(((n * a.IH + ih0) * a.IW + iw0) * a.IC);
     bvalid[S] = 0;
 #pragma unroll
     for (int j = 0; j < B_CH; ++j) {
@@ -592,24 +601,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const WgradArgs 
       } else {
         const int iw = iw0 + b_tap_w[j];
         const bool v = mv && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
-        rb[S][j] = *reinterpret_cast<const u32x4*>(a.x + (v ? pix + b_off[j] : 0));  // branch-free
-        bvalid[S] |= (v ? 1u : 0u) << j;
+        // padding taps / pixels past the split read out of range: zeros from the hardware
+        rb[S][j] = buf_load16(xr, v ? pix + 2u * (unsigned)b_off[j] : kOOB);
+        if constexpr (PRO) bvalid[S] |= (v ? 1u : 0u) << j;
       }
     }
   };
   // BN-apply (+ReLU) on the staged x chunks, after the MFMAs of the current block so the next
   // blocks' loads stay in flight meanwhile; padding taps stay exactly zero.
   auto pro_b = [&](int S) __attribute__((always_inline)) {
-    if (a.M % BKM) {  // rows past the end of M (only the last split's last block)
-#pragma unroll
-      for (int j = 0; j < A_CH; ++j) ra[S][j] = aok[S] ? ra[S][j] : zero4;
-    }
-    if constexpr (!PRO && MODE != STEM) {
-      if (bsel) {
-#pragma unroll
-        for (int j = 0; j < B_CH; ++j) rb[S][j] = ((bvalid[S] >> j) & 1u) ? rb[S][j] : zero4;
-      }
-    }
     if constexpr (PRO && MODE != STEM) {
 #pragma unroll
       for (int j = 0; j < B_CH; ++j) {
@@ -625,11 +625,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const WgradArgs 
           f[e] = f[e] * s0[e] + h0[e];
           f[e + 4] = f[e + 4] * s1[e] + h1[e];
         }
-        if (a.relu_in) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
-        }
-        rb[S][j] = ((bvalid[S] >> j) & 1u) ? pack8(f) : zero4;
+        u32x4 t = pack8(f);
+        t = relu_bf16x8(t);  // PRO implies ReLU (host-checked)
+        rb[S][j] = ((bvalid[S] >> j) & 1u) ? t : zero4;
       }
     }
   };
@@ -813,6 +811,8 @@ static int dispatch_dgrad(const IGemmArgs& a, bool accum, int epi, hipStream_t s
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
                               int accum, int epi, hipStream_t st) {
   const IGemmArgs& a = *args;
+  if (pro && !a.relu_in) return -7;  // the BN prologue always ends in ReLU (ResNet dataflow)
+  if (pro && a.IC > 512) return -8;   // prologue coefficients staged in LDS (PRO_MAXC)
   if (a.OC % bn != 0) return -1;
   if (mode == STEM) {
     if (pro || accum || epi) return -2;
@@ -842,11 +842,14 @@ static void launch_wgrad_t(const WgradArgs& a, int nblk, hipStream_t st) {
   // 256-wide tiles on 8 waves (4x2 / 2x4), the rest on 2x2 waves
   constexpr int WM = (BM == 256) ? 4 : 2;
   constexpr int WN = (BN == 256) ? 4 : 2;
-  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, FWD, PRO>), dim3(nblk), dim3(64 * WM * WN), 0, st, a);
+  // 8-wave tiles with the BN prologue: one register staging set (two spill at the 256-VGPR cap)
+  constexpr int DEPTH = (PRO && (BM == 256 || BN == 256)) ? 1 : 2;
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, FWD, PRO, DEPTH>), dim3(nblk), dim3(64 * WM * WN), 0, st, a);
 }
 
 extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, int pro, hipStream_t st) {
   const WgradArgs& a = *args;
+  if (pro && !a.relu_in) return -7;  // the BN prologue always ends in ReLU (ResNet dataflow)
   if (a.OC % bm != 0 || a.KTOT % bn != 0) return -1;
   const int nblk = (a.OC / bm) * (a.KTOT / bn) * a.nsplit;
   if (mode == STEM) {

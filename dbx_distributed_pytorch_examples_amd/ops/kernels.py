@@ -68,7 +68,7 @@ def _chk(t: torch.Tensor, dtype, name: str, numel: Optional[int] = None):
         raise ValueError(f"{name}: must be a GPU tensor")
     if numel is not None and t.numel() != numel:
         raise ValueError(f"{name}: expected {numel} elements, got {t.numel()} (shape {tuple(t.shape)})")
-    if t.numel() >= 2 ** 31:
+    if t.numel() >= 2 ** 31 - 256:
         # the conv gathers use 32-bit element offsets; split the batch above 2^31 elements
         raise ValueError(f"{name}: {t.numel()} elements exceed the kernels' 32-bit offset range")
 
@@ -85,7 +85,8 @@ def _tune_table():
     if _TUNE is None:
         import json
         import os
-        p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune_table.json")
+        p = os.environ.get("DBX_TUNE_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                            "tune_table.json")
         _TUNE = {}
         modes = os.environ.get("DBX_TUNE_MODES", "all").split(",")  # e.g. "none", "fwd,dgrad2"
         if os.path.exists(p):

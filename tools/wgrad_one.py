@@ -1,4 +1,7 @@
-"""Run one conv kernel shape repeatedly (for rocprofv3 counter collection)."""
+"""Run one conv kernel shape repeatedly (for rocprofv3 counter collection).
+
+  python tools/wgrad_one.py N C K H R {fwd|dgrad|wgrad}
+"""
 import math
 import os
 import sys
@@ -21,6 +24,8 @@ y = torch.empty(N, H, H, Kc, device=dev, dtype=torch.bfloat16)
 for _ in range(5):
     if kind == "wgrad":
         K.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=1, pad=pad)
+    elif kind == "dgrad":
+        K.conv_dgrad(dy, w.permute(3, 1, 2, 0).contiguous().view(C, -1), x, R=R, S=R, stride=1, pad=pad)
     else:
         K.conv_fwd(x, w.view(Kc, -1), y, R=R, S=R, stride=1, pad=pad)
 torch.cuda.synchronize()
