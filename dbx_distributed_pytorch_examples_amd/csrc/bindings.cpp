@@ -29,6 +29,8 @@ int dbx_bn_bwd_coeff(const double*, int, int, float, const float*, const float*,
                      int, hipStream_t);
 int dbx_bn_bwd_apply(const bf16*, const bf16*, const bf16*, const float*, const float*, const float*, bf16*, bf16*,
                      long long, int, int, hipStream_t);
+int dbx_bn_bwd_apply2(const bf16*, const bf16*, const float*, bf16*, const bf16*, const float*, bf16*, long long, int,
+                      hipStream_t);
 int dbx_maxpool_fwd(const bf16*, const float*, const float*, bf16*, unsigned char*, int, int, int, int, int, int, int,
                     int, int, int, hipStream_t);
 int dbx_maxpool_bwd(const bf16*, const unsigned char*, bf16*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -143,6 +145,12 @@ PYBIND11_MODULE(_C, m) {
                            P<const float*>(sh), P<const float*>(coeff), P<bf16*>(dy), P<bf16*>(gout), n, C, mask_mode,
                            S(st)),
           "bn_bwd_apply");
+  });
+  m.def("bn_bwd_apply2", [](uintptr_t g, uintptr_t y1, uintptr_t c1, uintptr_t dy1, uintptr_t y2, uintptr_t c2,
+                            uintptr_t dy2, long long n, int C, uintptr_t st) {
+    check(dbx_bn_bwd_apply2(P<const bf16*>(g), P<const bf16*>(y1), P<const float*>(c1), P<bf16*>(dy1),
+                            P<const bf16*>(y2), P<const float*>(c2), P<bf16*>(dy2), n, C, S(st)),
+          "bn_bwd_apply2");
   });
   m.def("maxpool_fwd", [](uintptr_t x, uintptr_t sc, uintptr_t sh, uintptr_t out, uintptr_t arg, int N, int H, int W,
                           int C, int Pp, int Q, int K, int stride, int pad, int relu, uintptr_t st) {

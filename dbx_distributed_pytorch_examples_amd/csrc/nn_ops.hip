@@ -274,6 +274,38 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
   }
 }
 
+// Two BN backward applies fed by the same gradient (the block tail of a downsample block:
+// bn3 of the main branch and the downsample BN): g is read once for both outputs.
+__global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const bf16* __restrict__ g_in, const bf16* __restrict__ y1,
+                                                            const float* __restrict__ coeff1, bf16* __restrict__ dy1,
+                                                            const bf16* __restrict__ y2, const float* __restrict__ coeff2,
+                                                            bf16* __restrict__ dy2, long long M, int C) {
+  const RowMap rm(C);
+  if (rm.r0 >= rm.rpb) return;
+  const int c0 = rm.cg * 8;
+  float a1[8], a2[8], a3[8], b1[8], b2[8], b3[8];
+  load8f(coeff1 + c0, a1);
+  load8f(coeff1 + C + c0, a2);
+  load8f(coeff1 + 2 * C + c0, a3);
+  load8f(coeff2 + c0, b1);
+  load8f(coeff2 + C + c0, b2);
+  load8f(coeff2 + 2 * C + c0, b3);
+  for (long long m = (long long)blockIdx.x * rm.rpb + rm.r0; m < M; m += (long long)gridDim.x * rm.rpb) {
+    const long long e = m * C + c0;
+    float g[8], u[8], v[8], o1[8], o2[8];
+    unpack8(*reinterpret_cast<const u32x4*>(g_in + e), g);
+    unpack8(*reinterpret_cast<const u32x4*>(y1 + e), u);
+    unpack8(*reinterpret_cast<const u32x4*>(y2 + e), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o1[j] = a1[j] * g[j] + a2[j] * u[j] + a3[j];
+      o2[j] = b1[j] * g[j] + b2[j] * v[j] + b3[j];
+    }
+    *reinterpret_cast<u32x4*>(dy1 + e) = pack8(o1);
+    *reinterpret_cast<u32x4*>(dy2 + e) = pack8(o2);
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // MaxPool 3x3 s2 p1 (NHWC) with BN-apply + ReLU prologue; argmax (0..8) saved as uint8.
 // ----------------------------------------------------------------------------------------
@@ -828,6 +860,14 @@ extern "C" int dbx_bn_bwd_apply(const bf16* dout, const bf16* mref, const bf16* 
   else if (mask_mode == 1) { if (gout) BB(1, true); else BB(1, false); }
   else { if (gout) BB(2, true); else BB(2, false); }
 #undef BB
+  RET_LAST;
+}
+extern "C" int dbx_bn_bwd_apply2(const bf16* g, const bf16* y1, const float* c1, bf16* dy1, const bf16* y2,
+                                 const float* c2, bf16* dy2, long long n, int C, hipStream_t st) {
+  if (n % C || C % 8 || C / 8 > 256) return -1;
+  const long long M = n / C;
+  hipLaunchKernelGGL(bn_bwd_apply2_kernel, dim3(grid_for(M, 256 / (C / 8), 4096)), dim3(256), 0, st, g, y1, c1, dy1,
+                     y2, c2, dy2, M, C);
   RET_LAST;
 }
 extern "C" int dbx_maxpool_fwd(const bf16* x, const float* sc, const float* sh, bf16* out, unsigned char* arg, int N,

@@ -538,12 +538,16 @@ class ResNetProgram:
         else:
             g = self.blocks[i + 1].dx
             K.bn_bwd_coeff(lbn.bstats, cnt_last, lbn.gamma, lbn.mean, lbn.invstd, lbn.coeff, lbn.dgamma, lbn.dbeta)
-            K.bn_bwd_apply(g, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_NONE)
         if b.ds_conv is not None:
             dc, dbn = b.ds_conv, b.ds_bn
             K.bn_bwd_coeff(dbn.bstats, N * dc.OH * dc.OW, dbn.gamma, dbn.mean, dbn.invstd, dbn.coeff, dbn.dgamma,
                            dbn.dbeta)
-            K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE)
+            if last:
+                K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE)
+            else:  # both tail BNs from one read of the block-output gradient
+                K.bn_bwd_apply2(g, b.ys[-1], lbn.coeff, b.dys[-1], b.yd, dbn.coeff, b.dyd)
+        elif not last:
+            K.bn_bwd_apply(g, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_NONE)
         # inner convs, last to second: dgrad epilogue masks with the previous BN's ReLU and
         # accumulates that BN's backward statistics
         for j in range(nconv - 1, 0, -1):

@@ -385,6 +385,19 @@ def bn_bwd_apply(dout, y, coeff, dy, *, mask_mode, mref=None, scale=None, shift=
 
 
 @_dispatch
+def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2):
+    """Two unmasked BN-backward applies sharing the gradient g (one read of g):
+    dy1 = k1*g + k2*y1 + k3 (coeff1), dy2 likewise with y2 / coeff2."""
+    Cc = y1.shape[-1]
+    for t, nm in ((g, "g"), (y1, "y1"), (dy1, "dy1"), (y2, "y2"), (dy2, "dy2")):
+        _chk(t, torch.bfloat16, nm, y1.numel())
+    _chk(coeff1, torch.float32, "coeff1", 3 * Cc)
+    _chk(coeff2, torch.float32, "coeff2", 3 * Cc)
+    C().bn_bwd_apply2(g.data_ptr(), y1.data_ptr(), coeff1.data_ptr(), dy1.data_ptr(), y2.data_ptr(),
+                      coeff2.data_ptr(), dy2.data_ptr(), y1.numel(), Cc, stream_ptr())
+
+
+@_dispatch
 def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True):
     N, H, W, Cc = x.shape
     _, P, Q, _ = out.shape

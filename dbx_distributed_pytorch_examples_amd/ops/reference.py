@@ -213,6 +213,11 @@ def bn_bwd_apply(dout, y, coeff, dy, *, mask_mode, mref=None, scale=None, shift=
     dy.copy_((k[0] * g + k[1] * y.float() + k[2]).bfloat16())
 
 
+def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2):
+    bn_bwd_apply(g, y1, coeff1, dy1, mask_mode=0)
+    bn_bwd_apply(g, y2, coeff2, dy2, mask_mode=0)
+
+
 def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True):
     f = x.float()
     if scale is not None:

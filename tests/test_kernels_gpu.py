@@ -510,3 +510,18 @@ def test_conv_dgrad_fused_epilogue(mode, sub, stride):
             assert relerr(g_s1, r_s1) < 2e-2, tile
             if mode == 1:
                 assert relerr(g_s2, r_s2) < 2e-2, tile
+
+
+def test_bn_bwd_apply2_matches_two_applies():
+    k = K()
+    torch.manual_seed(11)
+    N, H, W, Cc = 3, 7, 5, 128
+    g = torch.randn(N, H, W, Cc, device=dev).bfloat16()
+    y1, y2 = torch.randn_like(g), torch.randn_like(g)
+    c1, c2 = torch.randn(3 * Cc, device=dev), torch.randn(3 * Cc, device=dev)
+    d1, d2 = torch.empty_like(g), torch.empty_like(g)
+    k.bn_bwd_apply2(g, y1, c1, d1, y2, c2, d2)
+    for y, c, d in ((y1, c1, d1), (y2, c2, d2)):
+        kk = c.view(3, Cc)
+        ref = kk[0] * g.float() + kk[1] * y.float() + kk[2]
+        assert relerr(d, ref) < 1e-2

@@ -55,12 +55,14 @@ def swz_old(row, ch, nch):
 
 
 def swz_new(row, ch, nch):
+    if nch == 32:  # 256-wide tiles (8 waves): row bits 0,1,3 -> chunk bits 1,2,3
+        return ch ^ (((row & 1) << 1) | ((row & 2) << 1) | (row & 8))
     if nch == 16:  # bit2 <- row bit0 (write pairs), bit1 <- row bit1, bit3 <- row bit3 (read sets)
         return ch ^ ((((row & 1) << 2) | (row & 2) | (row & 8)) & 15)
     return ch ^ ((((row & 1) << 2) ^ (row & 2) ^ (((row >> 3) & 1) << 2)) & 7)
 
 
 if __name__ == "__main__":
-    for nch, a_ch in ((16, 4), (8, 2)):
+    for nch, a_ch in ((32, 4), (16, 4), (8, 2)):
         for name, f in (("old", swz_old), ("new", swz_new)):
             print(f"nch={nch} {name}: write extra cycles {writes(nch, f, a_ch)}, read extra cycles {reads(nch, f, 0)}")
