@@ -102,21 +102,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     __syncthreads();
   }
   // decomposition of the NEXT block to load (kb -> channel block, tap row, tap column), advanced
-  // by one per load instead of dividing kb (wave-uniform scalars); it stops at the last block, so
-  // the unconditional prefetch past the end re-loads block KB-1 (data unused)
+  // by one per load instead of dividing kb (wave-uniform scalars). The pipeline's unconditional
+  // prefetch runs two blocks past the end: those loads use an out-of-range offset for every lane,
+  // so they cost an instruction issue but no memory traffic (short-K 1x1 convs: KB = 1..4)
   int lk = 0, lcb = 0, lts = 0, ltr = 0;
   auto advance = [&]() __attribute__((always_inline)) {
-    if (lk < KB - 1) {
-      ++lk;
-      if (++lcb == cpt) { lcb = 0; if (++lts == a.ns) { lts = 0; ++ltr; } }
-    }
+    ++lk;
+    if (++lcb == cpt) { lcb = 0; if (++lts == a.ns) { lts = 0; ++ltr; } }
   };
 
   auto load_a = [&](int S) __attribute__((always_inline)) {
     if constexpr (MODE == STEM) {
       // k block lk covers filter rows r = 2lk, 2lk+1; chunk ach: r = 2lk + (ach>>2), pixels
       // s = 2*(ach&3), +1, 4 channels (8 bytes) each.
-      const int r = 2 * lk + (ach >> 2);
+      const int r = 2 * (lk < KB ? lk : KB - 1) + (ach >> 2);
       const int s0 = 2 * (ach & 3);
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
@@ -140,10 +139,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       // tap displacement, the same for all of this thread's rows (uniform, bytes)
       const int dh = (MODE == DGRAD) ? -ltr : r, dw = (MODE == DGRAD) ? -lts : s;
       const unsigned toff = 2u * (unsigned)((dh * a.IW + dw) * a.IC + cb);
+      const bool live = lk < KB;  // wave-uniform: false for the prefetches past the last block
       avalid[S] = 0;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
-        const bool v = (unsigned)(ahb[i] + dh) < (unsigned)a.IH && (unsigned)(awb[i] + dw) < (unsigned)a.IW;
+        const bool v = live && (unsigned)(ahb[i] + dh) < (unsigned)a.IH && (unsigned)(awb[i] + dw) < (unsigned)a.IW;
         // padding taps / rows past M read out of the buffer's range: the hardware returns zeros
         ra[S][i] = buf_load16(xr, v ? apix[i] + toff : kOOB);
         if constexpr (PRO) avalid[S] |= (v ? 1u : 0u) << i;
@@ -181,10 +181,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     } else {
       koff = ((a.r0 + a.tstep * ltr) * a.S + a.s0 + a.tstep * lts) * a.IC + lcb * BK + ach * 8;
     }
+    const bool live = lk < KB;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int n = n0 + (tid >> 3) + RPP * i;
-      rb[S][i] = buf_load16(wr, 2u * (unsigned)(n * KTOT + koff));
+      rb[S][i] = buf_load16(wr, live ? 2u * (unsigned)(n * KTOT + koff) : kOOB);
     }
   };
   auto store_ab = [&](int buf, int S) __attribute__((always_inline)) {
