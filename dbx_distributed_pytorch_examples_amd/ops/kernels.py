@@ -46,7 +46,7 @@ def _dispatch(fn):
     return wrapper
 
 
-NSHARD = 32  # BN-statistics shards (spreads the epilogue atomics over 32 copies)
+NSHARD = _ref.NSHARD  # BN-statistics shards (spreads the epilogue atomics over NSHARD copies)
 
 
 def new_stats(C: int, device=None) -> torch.Tensor:

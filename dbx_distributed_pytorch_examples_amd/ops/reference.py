@@ -13,7 +13,9 @@ import math
 import torch
 import torch.nn.functional as F
 
-NSHARD = 32
+import os as _os
+
+NSHARD = int(_os.environ.get("DBX_NSHARD", "32"))  # BN-statistics shards (see kernels.NSHARD)
 MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
 
 
