@@ -111,8 +111,7 @@ class NativeTrainer:
         def fwd_phase():
             p.prepare_weights()
             p.load_input_u8(self.flip)
-            for bn in p.bns:
-                bn.mod.num_batches_tracked.add_(1)
+            p.nbt.add_(1)  # every BN's num_batches_tracked (views of one tensor)
             p.forward(smoothing=self.smoothing)
 
         phases: List[Tuple[str, Callable, Optional[Tuple[int, int]]]] = []

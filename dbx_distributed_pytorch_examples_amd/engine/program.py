@@ -234,6 +234,8 @@ class ResNetProgram:
         self.master = torch.zeros(total, device=dev, dtype=torch.float32)
         self.grad = torch.zeros(total, device=dev, dtype=torch.float32)
         self.param_ranges: List[Tuple[str, int, int]] = []  # (param name, off, numel) for bucketing
+        nbt_vals: List[int] = []
+        nbt_mods: List[nn.BatchNorm2d] = []
         with torch.no_grad():
             for (kind, obj, attr, n), off in zip(entries, offs):
                 if kind == "conv":
@@ -261,7 +263,10 @@ class ResNetProgram:
                     # running stats stay module buffers (moved to device, updated in place)
                     mod.running_mean.data = mod.running_mean.data.to(dev, torch.float32)
                     mod.running_var.data = mod.running_var.data.to(dev, torch.float32)
-                    mod.num_batches_tracked.data = mod.num_batches_tracked.data.to(dev)
+                    if kind == "bn_w" and mod.num_batches_tracked is not None:
+                        # one int64 counter per BN, all views of self.nbt (one add per step)
+                        nbt_vals.append(int(mod.num_batches_tracked))
+                        nbt_mods.append(mod)
                 else:
                     p = getattr(self.fc, attr)
                     flat = self.master[off:off + n]
@@ -273,6 +278,9 @@ class ResNetProgram:
                     else:
                         self.fc_b_off, self.fc_b_grad = off, self.grad[off:off + n]
                     self.param_ranges.append((f"fc.{attr}", off, n))
+        self.nbt = torch.tensor(nbt_vals, dtype=torch.int64, device=dev)
+        for i, mod in enumerate(nbt_mods):
+            mod.num_batches_tracked.data = self.nbt[i]
         # bf16 compute copies: KRSC fwd + CRSK dgrad per conv, fc weight
         n16 = 0
         descs = []
