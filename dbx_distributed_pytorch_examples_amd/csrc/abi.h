@@ -35,6 +35,10 @@ struct IGemmArgs {
   const float* inv2;
   double* bstats1;  // fp64 [nshard][2][C]
   double* bstats2;
+  // DGRAD with the MASK_Y epilogue (EPI 2): also store the BN output relu(ybn*bsc + bsh) it
+  // computes for the mask (same shape as the output) -> the input the conv's weight gradient
+  // needs, so that wgrad runs without a BN prologue (nullable)
+  bf16* a_out;
 };
 struct WgradArgs {
   const bf16* dy;        // [M][OC]

@@ -339,13 +339,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // consumed after a store is issued and no load sits under divergent control flow, so hipcc waits
   // with counted vmcnt instead of draining the queue (stores count in vmcnt too) once per row.
   constexpr int NIT = BM * CPR / NT;
-  constexpr int EGMAX = (EPI == 1 || (ACCUM && EPI != 0)) ? 4 : 8;
+  constexpr int EGMAX = (EPI != 0) ? 4 : 8;  // BN epilogues hold 4-5 vectors per row: stay clear of spills
   constexpr int EG = NIT < EGMAX ? NIT : EGMAX;
   const bool sub_geom = MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1));  // wave-uniform
   const bool tail = m0 + BM > a.M;                                                  // wave-uniform
 #pragma unroll
   for (int g0 = 0; g0 < NIT; g0 += EG) {
-    u32x4 vv[EG], va[EG], vy[EG], vy2[EG];
+    u32x4 vv[EG], va[EG], vy[EG], vy2[EG], va2[EG];
     unsigned vm[EG];  // EPI 1: this chunk's 8 mask bits
     size_t ee[EG];
     bool ok[EG], has_add[EG];
@@ -404,8 +404,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] = ((vm[k] >> j) & 1u) ? f[j] : 0.f;
           } else {
+            float t[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = (yv[j] * e_sc[j >> 2][j & 3] + e_sh[j >> 2][j & 3]) > 0.f ? f[j] : 0.f;
+            for (int j = 0; j < 8; ++j) {
+              t[j] = yv[j] * e_sc[j >> 2][j & 3] + e_sh[j >> 2][j & 3];
+              f[j] = t[j] > 0.f ? f[j] : 0.f;
+            }
+            va2[k] = relu_bf16x8(pack8(t));  // the BN output itself (a.a_out write-back)
           }
           v = pack8(f);
           unpack8(v, f);  // statistics of the values actually stored (bf16-rounded)
@@ -435,6 +440,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 #pragma unroll
     for (int k = 0; k < EG; ++k)
       if (ok[k]) *reinterpret_cast<u32x4*>(a.y + ee[k]) = vv[k];
+    if constexpr (EPI == 2) {
+      if (a.a_out) {  // wave-uniform
+#pragma unroll
+        for (int k = 0; k < EG; ++k)
+          if (ok[k]) *reinterpret_cast<u32x4*>(a.a_out + ee[k]) = va2[k];
+      }
+    }
   }
   if constexpr (EPI > 0) {
     // reduce the per-thread partials over threads with the same chunk column: in-wave lanes
@@ -815,6 +827,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
   const IGemmArgs& a = *args;
   if (pro && !a.relu_in) return -7;  // the BN prologue always ends in ReLU (ResNet dataflow)
   if (pro && a.IC > 512) return -8;   // prologue coefficients staged in LDS (PRO_MAXC)
+  if (a.a_out && (mode != DGRAD || epi != 2)) return -9;  // write-back: the MASK_Y epilogue computes it
   if (a.OC % bn != 0) return -1;
   if (mode == STEM) {
     if (pro || accum || epi) return -2;

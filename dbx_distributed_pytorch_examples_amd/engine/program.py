@@ -106,6 +106,8 @@ class BlockL:
     out_shape: Tuple[int, int, int]
     # activations
     ys: List[torch.Tensor] = field(default_factory=list)   # raw conv outputs
+    # relu(bn(ys[j])) for j < nconv-1 when conv j+1 can write it back (stride 1): its wgrad input
+    acts: List[Optional[torch.Tensor]] = field(default_factory=list)
     yd: Optional[torch.Tensor] = None
     out: Optional[torch.Tensor] = None
     # gradients
@@ -134,6 +136,8 @@ class ResNetProgram:
         self.dev = device
         self.in_ch = model.conv1.in_channels
         self.overlap_wgrad = os.environ.get("DBX_OVERLAP_WGRAD", "1") == "1"
+        # store block-internal BN outputs from the MASK_Y dgrad epilogue for the wgrads (A/B switch)
+        self.act_writeback = os.environ.get("DBX_ACT_WRITEBACK", "1") == "1"
         self._wstream = None
         self._side_pending = False
         self._build_layers()
@@ -332,6 +336,10 @@ class ResNetProgram:
             b.ys = [E(N, cv.OH, cv.OW, cv.OC) for cv in b.convs]
             b.dys = [E(N, cv.OH, cv.OW, cv.OC) for cv in b.convs]
             b.das = [E(N, cv.OH, cv.OW, cv.OC) for cv in b.convs[:-1]]
+            # BN outputs inside the block (inputs of convs 1..n-1), written in backward by the MASK_Y
+            # dgrad epilogue that computes them for the ReLU mask anyway: the weight gradient then
+            # reads them instead of re-applying BN+ReLU to every staged tile
+            b.acts = [E(N, cv.OH, cv.OW, cv.OC) if self.act_writeback else None for cv in b.convs[:-1]]
             h, w, c = b.in_shape
             b.dx = E(N, h, w, c)
             if b.ds_conv is not None:
@@ -560,11 +568,17 @@ class ResNetProgram:
         # accumulates that BN's backward statistics
         for j in range(nconv - 1, 0, -1):
             cv, pbn, pc = b.convs[j], b.bns[j - 1], b.convs[j - 1]
-            self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
-                        in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
+            # dgrad first: its epilogue also stores the BN output acts[j-1] = this conv's input,
+            # which the (side-stream) weight gradient then reads without a BN prologue
+            act = b.acts[j - 1]
+            if act is None:  # wgrad re-applies BN+ReLU to its staged input tiles (BN prologue)
+                self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                            in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
             K.conv_dgrad(b.dys[j], cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                          epilogue=K.BNBwdEpilogue(K.MASK_Y, b.ys[j - 1], pbn.mean, pbn.invstd, pbn.bstats,
-                                                  scale=pbn.scale, shift=pbn.shift))
+                                                  scale=pbn.scale, shift=pbn.shift, act_out=act))
+            if act is not None:
+                self._wgrad(b.dys[j], act, cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad)
             K.bn_bwd_coeff(pbn.bstats, N * pc.OH * pc.OW, pbn.gamma, pbn.mean, pbn.invstd, pbn.coeff, pbn.dgamma,
                            pbn.dbeta)
             K.bn_bwd_apply(b.das[j - 1], b.ys[j - 1], pbn.coeff, b.dys[j - 1], mask_mode=K.MASK_NONE)

@@ -136,7 +136,7 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     bm, bn = tile or pick_tile(N * OH * OW, OC, "fwd", IC, R, stride)
     C().conv_igemm(FWD, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
-                   R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, stream_ptr())
+                   R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, stream_ptr())
     return out
 
 
@@ -170,8 +170,9 @@ class BNBwdEpilogue:
     BN fed by the same gradient: the downsample branch). Replaces a separate reduction pass."""
 
     def __init__(self, mode, ybn, mean1, inv1, stats1, mbits=None, scale=None, shift=None,
-                 ybn2=None, mean2=None, inv2=None, stats2=None):
+                 ybn2=None, mean2=None, inv2=None, stats2=None, act_out=None):
         self.mode, self.ybn, self.mean1, self.inv1, self.stats1 = mode, ybn, mean1, inv1, stats1
+        self.act_out = act_out  # MASK_Y only: also store relu(ybn*scale+shift) (the BN output)
         self.mbits, self.scale, self.shift = mbits, scale, shift
         self.ybn2, self.mean2, self.inv2, self.stats2 = ybn2, mean2, inv2, stats2
 
@@ -214,7 +215,14 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         if e.ybn2 is not None:
             _chk(e.ybn2, torch.bfloat16, "ybn2", dx.numel())
             _chk(e.stats2, torch.float64, "stats2", NSHARD * 2 * Cc)
+        if e.act_out is not None:
+            if e.mode != MASK_Y:
+                raise ValueError("act_out needs the MASK_Y epilogue")
+            _chk(e.act_out, torch.bfloat16, "act_out", dx.numel())
         epi = e.args()
+        act_ptr = _p(e.act_out)
+    else:
+        act_ptr = 0
     phases = dgrad_phases(H, W, R, S, stride, pad)
     if not accumulate and any(ph[5] == 0 or ph[7] == 0 for ph in phases):
         if epilogue is not None:
@@ -230,7 +238,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,
-                       _p(addsrc), add_sub, *epi, stream_ptr())
+                       _p(addsrc), add_sub, *epi, act_ptr, stream_ptr())
     return dx
 
 
@@ -251,7 +259,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
         raise ValueError("stem kernel supports R,S <= 8")
     C().conv_igemm(STEM, 128, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
-                   *_NO_EPI, stream_ptr())
+                   *_NO_EPI, 0, stream_ptr())
     return out
 
 

@@ -78,7 +78,10 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             bits = (e.mbits.to(torch.int32).view(-1, 1) & w) != 0
             g = g * bits.reshape(g.shape)
         else:
-            g = g * ((y * e.scale + e.shift) > 0)
+            t = y * e.scale + e.shift
+            g = g * (t > 0)
+            if getattr(e, "act_out", None) is not None:
+                e.act_out.copy_(torch.relu(t).bfloat16())
         g = g.bfloat16().float()
         gf = g.reshape(-1, Cc)
         st = e.stats1.view(NSHARD, 2, Cc)

@@ -525,3 +525,33 @@ def test_bn_bwd_apply2_matches_two_applies():
         kk = c.view(3, Cc)
         ref = kk[0] * g.float() + kk[1] * y.float() + kk[2]
         assert relerr(d, ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 64, 3, 1, 1), (2, 14, 14, 128, 256, 1, 1, 0), (3, 7, 7, 512, 512, 3, 1, 1),
+                                  (4, 9, 9, 64, 128, 3, 2, 1), (2, 14, 14, 128, 128, 3, 2, 1)])
+def test_dgrad_epilogue_act_out(case):
+    """The MASK_Y dgrad epilogue also stores the BN output relu(ybn*scale+shift) (every element,
+    strided phases included); gradient and statistics are unchanged by it."""
+    k = K()
+    N, H, W, IC, OC, R, st, pad = case
+    torch.manual_seed(12)
+    OH, OW = k.conv_out_hw(H, W, R, R, st, pad)
+    w = (torch.randn(OC, R, R, IC, device=dev) / math.sqrt(IC * R * R)).bfloat16()
+    wt = w.permute(3, 1, 2, 0).contiguous().view(IC, -1)
+    dy = torch.randn(N, OH, OW, OC, device=dev).bfloat16()
+    ybn = torch.randn(N, H, W, IC, device=dev).bfloat16()
+    sc = torch.rand(IC, device=dev) + 0.5
+    sh = torch.randn(IC, device=dev) * 0.1
+    mean, inv = torch.randn(IC, device=dev) * 0.1, torch.rand(IC, device=dev) + 0.5
+    act_ref = torch.relu(ybn.float() * sc + sh)
+    outs = []
+    for act in (None, torch.full_like(ybn, float("nan"))):
+        st1 = k.new_stats(IC, dev)
+        dx = torch.empty_like(ybn)
+        e = k.BNBwdEpilogue(k.MASK_Y, ybn, mean, inv, st1, scale=sc, shift=sh, act_out=act)
+        k.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad, epilogue=e)
+        outs.append((dx, st1))
+        if act is not None:
+            assert not torch.isnan(act.float()).any()
+            assert relerr(act, act_ref) < 1e-2 and (act.float() - act_ref).abs().max().item() < 0.07
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

@@ -96,7 +96,7 @@ def main():
     torch.cuda.synchronize()
     for n in ["conv_fwd", "conv_dgrad", "conv_wgrad", "conv_stem_fwd", "bn_apply", "bn_bwd_apply", "bn_bwd_reduce",
               "bn_bwd_coeff", "bn_finalize", "maxpool_fwd", "maxpool_bwd", "avgpool_fwd", "avgpool_bwd",
-              "softmax_ce", "sgd_step", "weight_prep", "augment_u8", "pool_bn_bwd_reduce", "pool_bn_bwd_apply"]:
+              "softmax_ce", "sgd_step", "weight_prep", "augment_u8", "pool_bn_bwd_reduce", "pool_bn_bwd_apply", "bn_bwd_apply2"]:
         wrap(n)
     s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s0.record()
