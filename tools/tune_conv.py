@@ -97,7 +97,8 @@ def main():
                          lambda t: K.conv_dgrad(dy, wt, dxs, R=1, S=1, stride=1, pad=0, tile=t)))
         else:
             e1 = K.BNBwdEpilogue(K.MASK_OUT, ybn, mean, inv, st1, mbits=K.pack_mask_bits(mref))
-            e2 = K.BNBwdEpilogue(K.MASK_Y, ybn, mean, inv, st1, scale=sc, shift=sh)
+            act = torch.empty_like(x)  # the program's MASK_Y dgrads also store the BN output
+            e2 = K.BNBwdEpilogue(K.MASK_Y, ybn, mean, inv, st1, scale=sc, shift=sh, act_out=act)
             Md = N * H * H // (st * st)
             jobs.append(("dgrad1", Md, C, Kc, R, st, lambda t: K.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad,
                                                                             tile=t, addsrc=add, epilogue=e1)))
@@ -105,9 +106,9 @@ def main():
                                                                             tile=t, epilogue=e2)))
         ws = torch.empty(max(64 * Kc * R * R * C, 16 << 20), device=dev)
         dw = torch.empty(Kc * R * R * C, device=dev)
+        # wgrads read stored activations (no BN prologue) since the dgrad-epilogue write-back
         jobs.append(("wgrad", N * OH * OH, Kc, C, R, st,
-                     lambda t: K.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, in_scale=sc, in_shift=sh,
-                                            tile=t)))
+                     lambda t: K.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, tile=t)))
         for mode, M, OCm, Kin, Rk, sk, make in jobs:
             if mode not in a.modes.split(","):
                 continue
