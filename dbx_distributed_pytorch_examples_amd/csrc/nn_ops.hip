@@ -720,37 +720,59 @@ __global__ void normalize_u8_kernel(const unsigned char* __restrict__ in, bf16* 
 // (x/255 - mean)/std, channel 3 = 0. Covers RandomResizedCrop / RandomCrop(pad) / Resize /
 // CenterCrop + RandomHorizontalFlip + Normalize of the reference's CPU transform chains.
 // ----------------------------------------------------------------------------------------
-__global__ void augment_u8_kernel(const unsigned char* __restrict__ in, bf16* __restrict__ out,
-                                  const float* __restrict__ boxes, const unsigned char* __restrict__ flip,
-                                  int N, int Hin, int Win, int Cin, int Ho, int Wo, float m0, float m1, float m2,
-                                  float s0, float s1, float s2) {
-  const long long total = (long long)N * Ho * Wo;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int ox = (int)(i % Wo);
-    const long long t = i / Wo;
-    const int oy = (int)(t % Ho);
-    const int n = (int)(t / Ho);
-    const float by = boxes[4 * n], bx = boxes[4 * n + 1], bh = boxes[4 * n + 2], bw = boxes[4 * n + 3];
-    const int oxx = (flip && flip[n]) ? (Wo - 1 - ox) : ox;
-    // source coordinate of the output pixel centre
-    float sy = by + (oy + 0.5f) * bh / Ho - 0.5f;
-    float sx = bx + (oxx + 0.5f) * bw / Wo - 0.5f;
-    sy = fminf(fmaxf(sy, 0.f), (float)(Hin - 1));
-    sx = fminf(fmaxf(sx, 0.f), (float)(Win - 1));
-    const int y0 = (int)sy, x0 = (int)sx;
-    const int y1 = min(y0 + 1, Hin - 1), x1 = min(x0 + 1, Win - 1);
-    const float wy = sy - y0, wx = sx - x0;
-    const unsigned char* base = in + (size_t)n * Hin * Win * Cin;
-    float v[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const int cc = Cin == 1 ? 0 : c;
-      const float a = base[((size_t)y0 * Win + x0) * Cin + cc], b = base[((size_t)y0 * Win + x1) * Cin + cc];
-      const float d = base[((size_t)y1 * Win + x0) * Cin + cc], e = base[((size_t)y1 * Win + x1) * Cin + cc];
-      v[c] = ((a * (1.f - wx) + b * wx) * (1.f - wy) + (d * (1.f - wx) + e * wx) * wy) * (1.f / 255.f);
+// One block per output row (n, oy): the box, flip and the two source rows are block-uniform, so
+// per pixel only the column interpolation is computed (32-bit index math throughout).
+__global__ __launch_bounds__(256) void augment_u8_kernel(const unsigned char* __restrict__ in, bf16* __restrict__ out,
+                                                         const float* __restrict__ boxes,
+                                                         const unsigned char* __restrict__ flip, int N, int Hin,
+                                                         int Win, int Cin, int Ho, int Wo, float m0, float m1,
+                                                         float m2, float s0, float s1, float s2) {
+  constexpr int kRowMax = 4096;
+  __shared__ __attribute__((aligned(16))) unsigned char srow[2][kRowMax];
+  for (int row = blockIdx.x; row < N * Ho; row += gridDim.x) {  // row = n * Ho + oy
+  const int n = row / Ho, oy = row - n * Ho;
+  const float by = boxes[4 * n], bx = boxes[4 * n + 1], bh = boxes[4 * n + 2], bw = boxes[4 * n + 3];
+  const bool fl = flip && flip[n];
+  float sy = by + (oy + 0.5f) * bh / Ho - 0.5f;
+  sy = fminf(fmaxf(sy, 0.f), (float)(Hin - 1));
+  const int y0 = (int)sy, y1 = min(y0 + 1, Hin - 1);
+  const float wy = sy - y0;
+  const unsigned char* g0 = in + ((size_t)n * Hin + y0) * Win * Cin;
+  const unsigned char* g1 = in + ((size_t)n * Hin + y1) * Win * Cin;
+  // the two source rows are staged in LDS with 16-byte loads (the bilinear taps are byte gathers)
+  const int rb = Win * Cin;
+  const bool staged = rb <= kRowMax && (((size_t)g0 | (size_t)g1) & 15) == 0 && (rb & 15) == 0;  // block-uniform
+  if (staged) {
+    for (int o = threadIdx.x * 16; o < rb; o += blockDim.x * 16) {
+      *reinterpret_cast<u32x4*>(&srow[0][o]) = *reinterpret_cast<const u32x4*>(g0 + o);
+      *reinterpret_cast<u32x4*>(&srow[1][o]) = *reinterpret_cast<const u32x4*>(g1 + o);
     }
-    bf16x4 o = {(bf16)((v[0] - m0) / s0), (bf16)((v[1] - m1) / s1), (bf16)((v[2] - m2) / s2), (bf16)0.f};
-    *reinterpret_cast<bf16x4*>(out + i * 4) = o;
+    __syncthreads();
+  }
+  const float sxs = bw / Wo;
+  const float i0 = 1.f / (255.f * s0), i1 = 1.f / (255.f * s1), i2 = 1.f / (255.f * s2);
+  auto body = [&](const unsigned char* r0, const unsigned char* r1) __attribute__((always_inline)) {
+    for (int ox = threadIdx.x; ox < Wo; ox += blockDim.x) {
+      const int oxx = fl ? (Wo - 1 - ox) : ox;
+      float sx = bx + (oxx + 0.5f) * sxs - 0.5f;
+      sx = fminf(fmaxf(sx, 0.f), (float)(Win - 1));
+      const int x0 = (int)sx, x1 = min(x0 + 1, Win - 1);
+      const float wx = sx - x0;
+      float v[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int cc = Cin == 1 ? 0 : c;
+        const float a = r0[x0 * Cin + cc], b = r0[x1 * Cin + cc];
+        const float d = r1[x0 * Cin + cc], e = r1[x1 * Cin + cc];
+        v[c] = (a * (1.f - wx) + b * wx) * (1.f - wy) + (d * (1.f - wx) + e * wx) * wy;  // 0..255
+      }
+      bf16x4 o = {(bf16)(v[0] * i0 - m0 / s0), (bf16)(v[1] * i1 - m1 / s1), (bf16)(v[2] * i2 - m2 / s2), (bf16)0.f};
+      *reinterpret_cast<bf16x4*>(out + ((size_t)row * Wo + ox) * 4) = o;
+    }
+  };
+  if (staged) body(&srow[0][0], &srow[1][0]);  // LDS byte gathers (ds_read_u8)
+  else body(g0, g1);
+  __syncthreads();  // srow reuse by the next row
   }
 }
 
@@ -758,22 +780,51 @@ __global__ void augment_u8_kernel(const unsigned char* __restrict__ in, bf16* __
 // Weight prep: fp32 KRSC master -> bf16 KRSC (fwd) and bf16 CRSK (dgrad) ; batched over layers
 // ----------------------------------------------------------------------------------------
 struct WDesc { long long src, fwd, tr; int K, RS, C, pad; };
-__global__ void weight_prep_kernel(const float* __restrict__ master, bf16* __restrict__ wbuf,
-                                   const WDesc* __restrict__ desc, int nlayers) {
+// blockIdx.y = layer. Layers with a dgrad copy (K, C multiples of 64) are processed in 64x64
+// (k, c) tiles per tap through LDS so both the KRSC and the transposed CRSK stores are
+// coalesced; the others (fc) are a plain vectorised cast.
+__global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restrict__ master, bf16* __restrict__ wbuf,
+                                                          const WDesc* __restrict__ desc, int nlayers) {
   const WDesc d = desc[blockIdx.y];
-  const long long n = (long long)d.K * d.RS * d.C;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float v = master[d.src + i];
-    const bf16 b = (bf16)v;
-    if (d.fwd >= 0) wbuf[d.fwd + i] = b;
-    if (d.tr >= 0) {
-      // i = (k*RS + t)*C + c  ->  tr index (c*RS + t)*K + k
-      const int c = (int)(i % d.C);
-      const long long kt = i / d.C;
-      const int t = (int)(kt % d.RS);
-      const int k = (int)(kt / d.RS);
-      wbuf[d.tr + ((long long)c * d.RS + t) * d.K + k] = b;
+  const int tid = threadIdx.x;
+  if (d.tr < 0) {
+    const long long n = (long long)d.K * d.RS * d.C;
+    const long long n4 = n / 4;
+    const float4* m4 = reinterpret_cast<const float4*>(master + d.src);
+    for (long long i = (long long)blockIdx.x * 256 + tid; i < n4; i += (long long)gridDim.x * 256) {
+      const float4 v = m4[i];
+      const bf16x4 b = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+      *reinterpret_cast<bf16x4*>(wbuf + d.fwd + 4 * i) = b;
     }
+    for (long long i = 4 * n4 + (long long)blockIdx.x * 256 + tid; i < n; i += (long long)gridDim.x * 256)
+      wbuf[d.fwd + i] = (bf16)master[d.src + i];
+    return;
+  }
+  __shared__ bf16 tile[64][64 + 4];
+  const int tk = d.K / 64, tc = d.C / 64, ntiles = tk * tc * d.RS;
+  const int rs = d.RS * d.C;  // master row length (per k)
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int kc = t / d.RS, tap = t - kc * d.RS;
+    const int k0 = (kc / tc) * 64, c0 = (kc - (kc / tc) * tc) * 64;
+    // load 64 k-rows x 64 channels (fp32, 4 per thread per pass), write the KRSC bf16 copy
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int kr = p * 16 + (tid >> 4), cq = (tid & 15) * 4;
+      const long long e = (long long)(k0 + kr) * rs + tap * d.C + c0 + cq;
+      const float4 v = *reinterpret_cast<const float4*>(master + d.src + e);
+      const bf16x4 b = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+      *reinterpret_cast<bf16x4*>(wbuf + d.fwd + e) = b;
+      tile[kr][cq] = b[0]; tile[kr][cq + 1] = b[1]; tile[kr][cq + 2] = b[2]; tile[kr][cq + 3] = b[3];
+    }
+    __syncthreads();
+    // transposed CRSK: row (c, tap), 64 consecutive k
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int cr = p * 16 + (tid >> 4), kq = (tid & 15) * 4;
+      const bf16x4 b = {tile[kq][cr], tile[kq + 1][cr], tile[kq + 2][cr], tile[kq + 3][cr]};
+      *reinterpret_cast<bf16x4*>(wbuf + d.tr + ((long long)(c0 + cr) * d.RS + tap) * d.K + k0 + kq) = b;
+    }
+    __syncthreads();
   }
 }
 
@@ -952,12 +1003,12 @@ extern "C" int dbx_normalize_u8(const unsigned char* in, bf16* out, const unsign
 extern "C" int dbx_augment_u8(const unsigned char* in, bf16* out, const float* boxes, const unsigned char* flip, int N,
                               int Hin, int Win, int Cin, int Ho, int Wo, float m0, float m1, float m2, float s0, float s1,
                               float s2, hipStream_t st) {
-  hipLaunchKernelGGL(augment_u8_kernel, dim3(grid_for((long long)N * Ho * Wo)), dim3(256), 0, st, in, out, boxes, flip, N,
+  hipLaunchKernelGGL(augment_u8_kernel, dim3(N * Ho < 4096 ? N * Ho : 4096), dim3(Wo >= 256 ? 256 : ((Wo + 63) / 64) * 64), 0, st, in, out, boxes, flip, N,
                      Hin, Win, Cin, Ho, Wo, m0, m1, m2, s0, s1, s2);
   RET_LAST;
 }
 extern "C" int dbx_weight_prep(const float* master, bf16* wbuf, const void* desc_dev, int nlayers, hipStream_t st) {
-  hipLaunchKernelGGL(weight_prep_kernel, dim3(64, nlayers), dim3(256), 0, st, master, wbuf, (const WDesc*)desc_dev, nlayers);
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(512, nlayers), dim3(256), 0, st, master, wbuf, (const WDesc*)desc_dev, nlayers);
   RET_LAST;
 }
 extern "C" int dbx_cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t st) {
