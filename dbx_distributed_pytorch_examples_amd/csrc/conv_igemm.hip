@@ -853,16 +853,19 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
 }
 
 template <int BM, int BN, bool PRO>
-static void launch_wgrad_t(const WgradArgs& a, int nblk, hipStream_t st) {
+static void launch_wgrad_t(const WgradArgs& a, int nblk, hipStream_t st, unsigned lds_pad) {
   // 256-wide tiles on 8 waves (4x2 / 2x4), the rest on 2x2 waves
   constexpr int WM = (BM == 256) ? 4 : 2;
   constexpr int WN = (BN == 256) ? 4 : 2;
   // 8-wave tiles with the BN prologue: one register staging set (two spill at the 256-VGPR cap)
   constexpr int DEPTH = (PRO && (BM == 256 || BN == 256)) ? 1 : 2;
-  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, FWD, PRO, DEPTH>), dim3(nblk), dim3(64 * WM * WN), 0, st, a);
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, FWD, PRO, DEPTH>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
 }
 
-extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, int pro, hipStream_t st) {
+// lds_pad: extra dynamic LDS per workgroup (bytes) -- an occupancy cap, so that a weight gradient
+// running on the side stream leaves room on each CU for the main stream's memory-bound kernels
+extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, int pro, hipStream_t st,
+                              unsigned lds_pad) {
   const WgradArgs& a = *args;
   if (pro && !a.relu_in) return -7;  // the BN prologue always ends in ReLU (ResNet dataflow)
   if (a.OC % bm != 0 || a.KTOT % bn != 0) return -1;
@@ -875,8 +878,8 @@ extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, i
   if (a.IC % bn != 0) return -4;  // a column tile must stay inside one tap
 #define WG(BM_, BN_)                                                  \
   if (bm == BM_ && bn == BN_) {                                       \
-    if (pro) launch_wgrad_t<BM_, BN_, true>(a, nblk, st);             \
-    else launch_wgrad_t<BM_, BN_, false>(a, nblk, st);                \
+    if (pro) launch_wgrad_t<BM_, BN_, true>(a, nblk, st, lds_pad);    \
+    else launch_wgrad_t<BM_, BN_, false>(a, nblk, st, lds_pad);       \
     return (int)hipGetLastError();                                    \
   }
   WG(128, 128)

@@ -136,6 +136,7 @@ class ResNetProgram:
         self.dev = device
         self.in_ch = model.conv1.in_channels
         self.overlap_wgrad = os.environ.get("DBX_OVERLAP_WGRAD", "1") == "1"
+        self.wgrad_lds_pad = int(os.environ.get("DBX_WGRAD_LDS_PAD", "0"))
         # store block-internal BN outputs from the MASK_Y dgrad epilogue for the wgrads (A/B switch)
         self.act_writeback = os.environ.get("DBX_ACT_WRITEBACK", "1") == "1"
         self._wstream = None
@@ -509,6 +510,8 @@ class ResNetProgram:
         self._side_pending = True
 
     def _wgrad(self, *args, **kw):
+        if self.wgrad_lds_pad and self.dev.type == "cuda" and self.overlap_wgrad:
+            kw["lds_pad"] = self.wgrad_lds_pad  # occupancy cap: leave room for the main stream's kernels
         self._side(lambda: K.conv_wgrad(*args, **kw))
 
     def _join_side(self):

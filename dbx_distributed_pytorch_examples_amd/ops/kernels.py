@@ -279,7 +279,7 @@ def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int
 
 @_dispatch
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True,
-               scale=1.0, accumulate=False, stem=False, tile=None):
+               scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0):
     """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace."""
     N, OH, OW, OC = dy.shape
     _, IH, IW, IC = x.shape
@@ -313,7 +313,7 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         raise ValueError("wgrad workspace too small")
     C().conv_wgrad(STEM if stem else FWD, bm, bn, dy.data_ptr(), x.data_ptr(), ws.data_ptr(), _p(in_scale),
                    _p(in_shift), int(relu_in), N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, KTOT, nsplit, ms,
-                   stream_ptr())
+                   stream_ptr(), int(lds_pad))
     C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsplit, float(scale), int(accumulate), stream_ptr())
     return dw
 
