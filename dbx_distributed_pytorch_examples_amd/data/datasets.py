@@ -47,6 +47,36 @@ class SyntheticImages(Dataset):
         return img, int(self.labels[i])
 
 
+def learnable_synthetic(n: int, image_size: int, num_classes: int, seed: int = 0, noise: float = 48.0,
+                        device=None, proto_res: int = 8):
+    """A learnable synthetic classification task (for accuracy checks without a dataset): every
+    class has a fixed random low-resolution RGB prototype (``proto_res``^2, bilinearly upsampled);
+    a sample is its class prototype under a random brightness/contrast change, a random shift of
+    up to 1/8 of the image and Gaussian pixel noise (std ``noise`` in 0..255 units). Returns uint8
+    NHWC images [n, S, S, 3] and int64 labels, generated on ``device`` (deterministic in seed)."""
+    import torch
+    import torch.nn.functional as F
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    protos = torch.rand(num_classes, 3, proto_res, proto_res, generator=torch.Generator().manual_seed(12345)) * 255
+    protos = F.interpolate(protos, size=(image_size, image_size), mode="bilinear", align_corners=False)
+    labels = torch.randint(0, num_classes, (n,), generator=g)
+    gain = 0.7 + 0.6 * torch.rand(n, 1, 1, 1, generator=g)
+    bias = (torch.rand(n, 1, 1, 1, generator=g) - 0.5) * 60
+    sh = image_size // 8
+    dy = torch.randint(-sh, sh + 1, (n,), generator=g)
+    dx = torch.randint(-sh, sh + 1, (n,), generator=g)
+    out = torch.empty(n, image_size, image_size, 3, dtype=torch.uint8)
+    for i0 in range(0, n, 1024):
+        sl = slice(i0, min(n, i0 + 1024))
+        x = protos[labels[sl]] * gain[sl] + bias[sl]
+        x = torch.stack([torch.roll(xi, shifts=(int(a), int(b)), dims=(1, 2)) for xi, a, b in zip(x, dy[sl], dx[sl])])
+        x = x + noise * torch.randn(x.shape, generator=g)
+        out[sl] = x.clamp_(0, 255).round_().to(torch.uint8).permute(0, 2, 3, 1)
+    if device is not None:
+        out, labels = out.to(device), labels.to(device)
+    return out, labels
+
+
 def _open(path):
     return gzip.open(path, "rb") if path.endswith(".gz") else open(path, "rb")
 
