@@ -39,6 +39,15 @@ struct IGemmArgs {
   // computes for the mask (same shape as the output) -> the input the conv's weight gradient
   // needs, so that wgrad runs without a BN prologue (nullable)
   bf16* a_out;
+  // ---- FWD "tail" prologue: the previous block's output computed on the fly ---------------
+  // A = relu(x*in_scale + in_shift + r), r = res (identity shortcut) or res*res_scale + res_shift
+  // (downsample branch); the first N tile also stores A to tail_out and its 1-bit ReLU mask to
+  // tail_bits: the block output and mask a separate bn_apply pass would have written
+  const bf16* res;
+  const float* res_scale;
+  const float* res_shift;
+  bf16* tail_out;
+  unsigned char* tail_bits;
 };
 struct WgradArgs {
   const bf16* dy;        // [M][OC]

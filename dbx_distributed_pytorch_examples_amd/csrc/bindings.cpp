@@ -77,14 +77,17 @@ PYBIND11_MODULE(_C, m) {
                          int s0, int tstep, int dh0, int dw0, int osub, int oph, int opw, int FH, int FW,
                          uintptr_t addsrc, int add_sub, int epi, uintptr_t mbits, uintptr_t ybn, uintptr_t ybn2,
                          uintptr_t bsc, uintptr_t bsh, uintptr_t mean1, uintptr_t inv1, uintptr_t mean2,
-                         uintptr_t inv2, uintptr_t bstats1, uintptr_t bstats2, uintptr_t a_out, uintptr_t st) {
+                         uintptr_t inv2, uintptr_t bstats1, uintptr_t bstats2, uintptr_t a_out, uintptr_t res,
+                         uintptr_t res_scale, uintptr_t res_shift, uintptr_t tail_out, uintptr_t tail_bits,
+                         uintptr_t st) {
     dbx::IGemmArgs a{P<const bf16*>(x), P<const bf16*>(w), P<bf16*>(y), P<const float*>(in_scale),
                      P<const float*>(in_shift), P<double*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
                      N * OH * OW, nshard > 0 ? nshard : 1, relu_in, nr, ns, r0, s0, tstep, dh0, dw0, osub, oph, opw,
                      FH, FW, P<const bf16*>(addsrc), add_sub, P<const unsigned char*>(mbits), P<const bf16*>(ybn),
                      P<const bf16*>(ybn2), P<const float*>(bsc), P<const float*>(bsh), P<const float*>(mean1),
                      P<const float*>(inv1), P<const float*>(mean2), P<const float*>(inv2), P<double*>(bstats1),
-                     P<double*>(bstats2), P<bf16*>(a_out)};
+                     P<double*>(bstats2), P<bf16*>(a_out), P<const bf16*>(res), P<const float*>(res_scale),
+                     P<const float*>(res_shift), P<bf16*>(tail_out), P<unsigned char*>(tail_bits)};
     check(dbx_conv_igemm(mode, bm, bn, &a, in_scale != 0, stats != 0, accum, epi, S(st)), "conv_igemm");
   });
   m.def("conv_wgrad", [](int mode, int bm, int bn, uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t in_scale,

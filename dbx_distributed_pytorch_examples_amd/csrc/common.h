@@ -83,6 +83,9 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned long long by
 __device__ __forceinline__ u32x4 buf_load16(rsrc_t r, unsigned off) {
   return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
+__device__ __forceinline__ void buf_store8(rsrc_t r, unsigned off, unsigned char v) {
+  __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, 0);
+}
 // a store at an out-of-range offset is dropped by the hardware (branch-free conditional store)
 __device__ __forceinline__ void buf_store16(rsrc_t r, unsigned off, u32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r, off, 0, 0);

@@ -34,7 +34,10 @@ namespace dbx {
 enum ConvMode { FWD = 0, DGRAD = 1, STEM = 2 };
 
 
-template <int BM, int BN, int WM, int WN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI>
+// TAIL (FWD, with PRO): the A operand is the previous residual block's output, computed while
+// staging from that block's raw conv3 output (x) and its shortcut (res): no separate bn_apply pass
+// and no re-read of the block output; the first N tile writes the output + ReLU mask back.
+template <int BM, int BN, int WM, int WN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI, bool TAIL = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs a) {
   constexpr int NT = 64 * WM * WN;        // threads; WM x WN waves, each owns a (BM/WM) x (BN/WN) tile
   constexpr int NW = WM * WN;
@@ -46,15 +49,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   constexpr int LDS_AB = 2 * (BM + BN) * BK;  // bf16 elements
   constexpr int LDS_C = BM * (BN + 8);
   constexpr int LDS_RED = 2 * (3 * NW * BN);  // fp32 reduction scratch (in bf16 units)
-  constexpr int PRO_MAXC = 512;                            // prologue channels held in LDS (host-checked)
-  constexpr int LDS_PRO = (PRO && MODE != STEM) ? 4 * PRO_MAXC : 0;  // fp32 scale + shift (bf16 units)
+  constexpr int PRO_MAXC = TAIL ? 1024 : 512;              // prologue channels held in LDS (host-checked)
+  constexpr int LDS_PRO = (PRO && MODE != STEM) ? (TAIL ? 8 : 4) * PRO_MAXC : 0;  // fp32 arrays (bf16 units)
   constexpr int LDS_MAIN = (LDS_AB > LDS_C + LDS_RED) ? LDS_AB : (LDS_C + LDS_RED);
   __shared__ __attribute__((aligned(16))) bf16 lds[LDS_MAIN + LDS_PRO];
   bf16* sA = lds;                  // [2][BM][BK]
   bf16* sB = lds + 2 * BM * BK;    // [2][BN][BK]
   // prologue affine of ALL input channels, staged once: the per-block coefficients are read from
   // LDS at transform time instead of living in registers across the pipeline
-  float* sPro = reinterpret_cast<float*>(lds + LDS_MAIN);  // [2][PRO_MAXC]: scale, shift
+  float* sPro = reinterpret_cast<float*>(lds + LDS_MAIN);  // [2 or 4][PRO_MAXC]: scale, shift (, rs, rh)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
   const int ntn = a.OC / BN, ntm = (a.M + BM - 1) / BM;
@@ -91,6 +94,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // issued one iteration earlier) is still landing, so each global load has two blocks of MFMA
   // work to hide its latency instead of one. The K loop is unrolled by two so S is a constant.
   u32x4 ra[2][A_CH], rb[2][B_CH];
+  u32x4 rr[2][TAIL ? A_CH : 1];           // TAIL: staged shortcut chunks
   const u32x4 zero4 = {0u, 0u, 0u, 0u};
   unsigned avalid[2] = {0u, 0u};          // bit i: chunk i is a real (non-padding) tap
   int pcb[2] = {0, 0};                    // channel block of the staged set (prologue coefficients)
@@ -98,9 +102,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     for (int c = tid; c < a.IC; c += NT) {
       sPro[c] = a.in_scale[c];
       sPro[PRO_MAXC + c] = a.in_shift[c];
+      if constexpr (TAIL) {
+        sPro[2 * PRO_MAXC + c] = a.res_scale ? a.res_scale[c] : 1.f;
+        sPro[3 * PRO_MAXC + c] = a.res_scale ? a.res_shift[c] : 0.f;
+      }
     }
     __syncthreads();
   }
+  // TAIL write-back: wave-uniform per staged set (first N tile, live block)
+  bool wlive[2] = {false, false};
+  unsigned wtoff[2] = {0u, 0u};
+  const rsrc_t rresr = make_rsrc(a.res, TAIL ? 2ull * a.N * a.IH * a.IW * a.IC : 0ull);
+  const rsrc_t toutr = make_rsrc(a.tail_out, (TAIL && a.tail_out) ? 2ull * a.N * a.IH * a.IW * a.IC : 0ull);
+  const rsrc_t tbitr = make_rsrc(a.tail_bits, (TAIL && a.tail_bits) ? 1ull * a.N * a.IH * a.IW * a.IC / 8 : 0ull);
   // decomposition of the NEXT block to load (kb -> channel block, tap row, tap column), advanced
   // by one per load instead of dividing kb (wave-uniform scalars). The pipeline's unconditional
   // prefetch runs two blocks past the end: those loads use an out-of-range offset for every lane,
@@ -136,6 +150,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       const int cb = lcb * BK;
       const int r = a.r0 + a.tstep * ltr, s = a.s0 + a.tstep * lts;
       if constexpr (PRO) pcb[S] = cb;
+      if constexpr (TAIL) { wlive[S] = lk < KB && tn == 0; wtoff[S] = 2u * (unsigned)cb; }
       // tap displacement, the same for all of this thread's rows (uniform, bytes)
       const int dh = (MODE == DGRAD) ? -ltr : r, dw = (MODE == DGRAD) ? -lts : s;
       const unsigned toff = 2u * (unsigned)((dh * a.IW + dw) * a.IC + cb);
@@ -146,6 +161,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
         const bool v = live && (unsigned)(ahb[i] + dh) < (unsigned)a.IH && (unsigned)(awb[i] + dw) < (unsigned)a.IW;
         // padding taps / rows past M read out of the buffer's range: the hardware returns zeros
         ra[S][i] = buf_load16(xr, v ? apix[i] + toff : kOOB);
+        if constexpr (TAIL) rr[S][i] = buf_load16(rresr, v ? apix[i] + toff : kOOB);
         if constexpr (PRO) avalid[S] |= (v ? 1u : 0u) << i;
       }
     }
@@ -159,6 +175,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       const f32x4 ps1 = *reinterpret_cast<const f32x4*>(sPro + c0 + 4);
       const f32x4 ph0 = *reinterpret_cast<const f32x4*>(sPro + PRO_MAXC + c0);
       const f32x4 ph1 = *reinterpret_cast<const f32x4*>(sPro + PRO_MAXC + c0 + 4);
+      f32x4 pr0, pr1, pq0, pq1;
+      if constexpr (TAIL) {
+        pr0 = *reinterpret_cast<const f32x4*>(sPro + 2 * PRO_MAXC + c0);
+        pr1 = *reinterpret_cast<const f32x4*>(sPro + 2 * PRO_MAXC + c0 + 4);
+        pq0 = *reinterpret_cast<const f32x4*>(sPro + 3 * PRO_MAXC + c0);
+        pq1 = *reinterpret_cast<const f32x4*>(sPro + 3 * PRO_MAXC + c0 + 4);
+      }
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         float f[8];
@@ -168,9 +191,29 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
           f[j] = f[j] * ps0[j] + ph0[j];
           f[j + 4] = f[j + 4] * ps1[j] + ph1[j];
         }
+        if constexpr (TAIL) {  // + shortcut (identity: rs = 1, rh = 0), as bn_apply computes it
+          float g[8];
+          unpack8(rr[S][i], g);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f[j] += g[j] * pr0[j] + pq0[j];
+            f[j + 4] += g[j + 4] * pr1[j] + pq1[j];
+          }
+        }
         u32x4 t = pack8(f);
         t = relu_bf16x8(t);  // PRO implies ReLU (host-checked)
-        ra[S][i] = ((avalid[S] >> i) & 1u) ? t : zero4;  // padding taps stay exactly zero
+        const bool vi = (avalid[S] >> i) & 1u;
+        ra[S][i] = vi ? t : zero4;  // padding taps stay exactly zero
+        if constexpr (TAIL) {
+          // block output + 1-bit mask (bit j: element j > 0) written back by the first N tile
+          const unsigned off = (wlive[S] && vi) ? apix[i] + wtoff[S] : kOOB;
+          buf_store16(toutr, off, t);
+          unsigned bits = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            bits |= (((t[q] & 0xFFFFu) ? 1u : 0u) << (2 * q)) | (((t[q] >> 16) ? 1u : 0u) << (2 * q + 1));
+          buf_store8(tbitr, off == kOOB ? kOOB : (off >> 4), (unsigned char)bits);
+        }
       }
     }
   };
@@ -785,19 +828,25 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
 // ======================================================================================
 using namespace dbx;
 
-template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI>
+template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI, bool TAIL = false>
 static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
   // tile shape -> wave layout: 128x128, 128x64, 64x64 on 2x2 waves (256 threads, 2 blocks/CU);
   // 256x128 on 4x2 and 128x256 on 2x4 waves (512 threads, 1 block/CU, 96 KB LDS)
   constexpr int WM = (BM == 256) ? 4 : 2;
   constexpr int WN = (BN == 256) ? 4 : 2;
   const int nwg = (a.OC / BN) * ((a.M + BM - 1) / BM);
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI>), dim3(nwg), dim3(64 * WM * WN), 0, st, a);
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI, TAIL>), dim3(nwg), dim3(64 * WM * WN), 0, st, a);
   return (int)hipGetLastError();
 }
 
 template <int BM, int BN>
 static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, hipStream_t st) {
+  if (a.res) {
+    // the staged shortcut chunks push the 128x256 tile past 256 VGPRs: same-area 256x128 instead
+    constexpr int TM = (BM == 128 && BN == 256) ? 256 : BM, TN = (BM == 128 && BN == 256) ? 128 : BN;
+    return stats ? launch_igemm_t<TM, TN, FWD, true, true, false, 0, true>(a, st)
+                 : launch_igemm_t<TM, TN, FWD, true, false, false, 0, true>(a, st);
+  }
   if (pro) return stats ? launch_igemm_t<BM, BN, FWD, true, true, false, 0>(a, st) : launch_igemm_t<BM, BN, FWD, true, false, false, 0>(a, st);
   return stats ? launch_igemm_t<BM, BN, FWD, false, true, false, 0>(a, st) : launch_igemm_t<BM, BN, FWD, false, false, false, 0>(a, st);
 }
@@ -826,7 +875,9 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
                               int accum, int epi, hipStream_t st) {
   const IGemmArgs& a = *args;
   if (pro && !a.relu_in) return -7;  // the BN prologue always ends in ReLU (ResNet dataflow)
-  if (pro && a.IC > 512) return -8;   // prologue coefficients staged in LDS (PRO_MAXC)
+  if (pro && a.IC > (a.res ? 1024 : 512)) return -8;  // prologue coefficients staged in LDS (PRO_MAXC)
+  if (a.res && (!pro || mode != FWD || a.R != 1 || a.S != 1 || a.stride != 1 || a.pad != 0))
+    return -10;  // the tail prologue is for 1x1 stride-1 consumers (output pixel == input pixel)
   if (a.a_out && (mode != DGRAD || epi != 2)) return -9;  // write-back: the MASK_Y epilogue computes it
   if (a.OC % bn != 0) return -1;
   if (mode == STEM) {

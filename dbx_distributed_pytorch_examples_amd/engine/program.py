@@ -139,6 +139,8 @@ class ResNetProgram:
         self.wgrad_lds_pad = int(os.environ.get("DBX_WGRAD_LDS_PAD", "0"))
         # store block-internal BN outputs from the MASK_Y dgrad epilogue for the wgrads (A/B switch)
         self.act_writeback = os.environ.get("DBX_ACT_WRITEBACK", "1") == "1"
+        # compute block outputs inside the next block's conv1 prologue instead of a bn_apply pass
+        self.fuse_tail = os.environ.get("DBX_FUSE_TAIL", "1") == "1"
         self._wstream = None
         self._side_pending = False
         self._build_layers()
@@ -440,14 +442,23 @@ class ResNetProgram:
         K.maxpool_fwd(self.y0, self.p0, self.parg, K=self.pool_k, stride=self.pool_s, pad=self.pool_p,
                       scale=sbn.scale, shift=sbn.shift, relu=True)
         x = self.p0
-        for b in self.blocks:
+        pending = None  # previous block whose output this block's conv1 computes (tail prologue)
+        for bi, b in enumerate(self.blocks):
             prev_bn = None
             for i, cv in enumerate(b.convs):
-                src = x if i == 0 else b.ys[i - 1]
-                K.conv_fwd(src, cv.w16, b.ys[i], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
-                           stats=b.bns[i].stats if tr else None,
-                           in_scale=prev_bn.scale if prev_bn else None, in_shift=prev_bn.shift if prev_bn else None,
-                           relu_in=True)
+                if i == 0 and pending is not None:
+                    pb, res, rsc, rsh = pending
+                    K.conv_fwd(pb.ys[-1], cv.w16, b.ys[0], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                               stats=b.bns[0].stats if tr else None, in_scale=pb.bns[-1].scale,
+                               in_shift=pb.bns[-1].shift, relu_in=True, tail_res=res, tail_res_scale=rsc,
+                               tail_res_shift=rsh, tail_out=pb.out, tail_bits=pb.obits if tr else None)
+                    pending = None
+                else:
+                    src = x if i == 0 else b.ys[i - 1]
+                    K.conv_fwd(src, cv.w16, b.ys[i], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                               stats=b.bns[i].stats if tr else None,
+                               in_scale=prev_bn.scale if prev_bn else None,
+                               in_shift=prev_bn.shift if prev_bn else None, relu_in=True)
                 self._bn_fwd(b.bns[i], N * cv.OH * cv.OW)
                 prev_bn = b.bns[i]
             last = b.bns[-1]
@@ -456,10 +467,16 @@ class ResNetProgram:
                 K.conv_fwd(x, dc.w16, b.yd, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad,
                            stats=b.ds_bn.stats if tr else None)
                 self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
-                K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=b.yd, res_scale=b.ds_bn.scale,
-                           res_shift=b.ds_bn.shift, relu=True, mbits=b.obits if tr else None)
+                res, rsc, rsh = b.yd, b.ds_bn.scale, b.ds_bn.shift
             else:
-                K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=x, relu=True, mbits=b.obits if tr else None)
+                res, rsc, rsh = x, None, None
+            nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
+            c1 = nxt.convs[0] if nxt is not None else None
+            if self.fuse_tail and c1 is not None and K.tail_supported(b.out_shape[2], c1.R, c1.S, c1.stride, c1.pad):
+                pending = (b, res, rsc, rsh)  # b.out (+ its mask) is written by the next block's conv1
+            else:
+                K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=res, res_scale=rsc, res_shift=rsh,
+                           relu=True, mbits=b.obits if tr else None)
             x = b.out
         K.avgpool_fwd(x, self.pooled)
         if features_only:

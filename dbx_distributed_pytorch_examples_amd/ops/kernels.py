@@ -119,7 +119,13 @@ def pick_tile(M: int, OC: int, mode: str = "fwd", K_in: int = 0, R: int = 0, str
 # --------------------------------------------------------------------------------------
 @_dispatch
 def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None,
-             relu_in=True, tile=None):
+             relu_in=True, tile=None, tail_res=None, tail_res_scale=None, tail_res_shift=None, tail_out=None,
+             tail_bits=None):
+    """Y = conv(act(X), W); act = relu(X*in_scale + in_shift) with a BN prologue. "Tail" mode
+    (``tail_res`` given; 1x1 stride-1 convs): act = relu(X*in_scale + in_shift + r), r = tail_res or
+    tail_res*tail_res_scale + tail_res_shift -- the previous residual block's output computed on the
+    fly -- and act / its 1-bit ReLU mask are stored to ``tail_out`` / ``tail_bits`` (bn_apply's
+    outputs), so that pass and the re-read of the block output disappear."""
     N, IH, IW, IC = x.shape
     OH, OW = conv_out_hw(IH, IW, R, S, stride, pad)
     OC = w16.shape[0]
@@ -133,11 +139,28 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     if in_scale is not None:
         _chk(in_scale, torch.float32, "in_scale", IC)
         _chk(in_shift, torch.float32, "in_shift", IC)
+    if tail_res is not None:
+        if not tail_supported(IC, R, S, stride, pad) or in_scale is None or not relu_in:
+            raise ValueError("tail prologue needs a 1x1 stride-1 conv, <= 1024 input channels and a BN prologue")
+        _chk(tail_res, torch.bfloat16, "tail_res", x.numel())
+        if tail_res_scale is not None:
+            _chk(tail_res_scale, torch.float32, "tail_res_scale", IC)
+            _chk(tail_res_shift, torch.float32, "tail_res_shift", IC)
+        if tail_out is not None:
+            _chk(tail_out, torch.bfloat16, "tail_out", x.numel())
+        if tail_bits is not None:
+            _chk(tail_bits, torch.uint8, "tail_bits", x.numel() // 8)
     bm, bn = tile or pick_tile(N * OH * OW, OC, "fwd", IC, R, stride)
     C().conv_igemm(FWD, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
-                   R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, stream_ptr())
+                   R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
+                   _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr())
     return out
+
+
+def tail_supported(IC: int, R: int, S: int, stride: int, pad: int) -> bool:
+    """Can a conv consume the previous block's output through the fused tail prologue?"""
+    return R == 1 and S == 1 and stride == 1 and pad == 0 and IC <= 1024 and IC % 64 == 0
 
 
 def dgrad_phases(H: int, W: int, R: int, S: int, stride: int, pad: int):
@@ -238,7 +261,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,
-                       _p(addsrc), add_sub, *epi, act_ptr, stream_ptr())
+                       _p(addsrc), add_sub, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr())
     return dx
 
 
@@ -259,7 +282,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
         raise ValueError("stem kernel supports R,S <= 8")
     C().conv_igemm(STEM, 128, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
-                   *_NO_EPI, 0, stream_ptr())
+                   *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr())
     return out
 
 

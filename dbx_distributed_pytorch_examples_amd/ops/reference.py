@@ -45,10 +45,17 @@ def _add_stats(stats, y):
     st[0, 1] += (yf * yf).sum(0)
 
 
-def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None, relu_in=True, tile=None):
+def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None, relu_in=True, tile=None,
+             tail_res=None, tail_res_scale=None, tail_res_shift=None, tail_out=None, tail_bits=None):
     OC = w16.shape[0]
     IC = x.shape[-1]
-    xf = _act_in(x, in_scale, in_shift, relu_in)
+    if tail_res is not None:  # previous block's output relu(bn3(x) + shortcut): bn_apply's semantics
+        act = tail_out if tail_out is not None else torch.empty_like(x)
+        bn_apply(x, in_scale, in_shift, act, res=tail_res, res_scale=tail_res_scale, res_shift=tail_res_shift,
+                 relu=True, mbits=tail_bits)
+        xf = act.float()
+    else:
+        xf = _act_in(x, in_scale, in_shift, relu_in)
     w = w16.float().view(OC, R, S, IC).permute(0, 3, 1, 2)
     y = _nhwc(F.conv2d(_nchw(xf), w, stride=stride, padding=pad)).bfloat16()
     out.copy_(y.reshape(out.shape))

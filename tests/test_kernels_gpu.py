@@ -555,3 +555,39 @@ def test_dgrad_epilogue_act_out(case):
             assert not torch.isnan(act.float()).any()
             assert relerr(act, act_ref) < 1e-2 and (act.float() - act_ref).abs().max().item() < 0.07
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("tile", [(64, 64), (128, 64), (128, 128), (256, 64), (256, 128), (128, 256)])
+@pytest.mark.parametrize("case", [(2, 14, 14, 256, 64, False), (2, 7, 7, 1024, 256, True), (3, 9, 9, 512, 128, False)])
+def test_conv_fwd_tail_prologue(case, tile):
+    """conv1 with the tail prologue == bn_apply(conv3 out, shortcut) followed by a plain conv1: the
+    block output and its ReLU mask are written back as bn_apply writes them, the conv output and the
+    BN statistics match (identity shortcut: bit-exact block output)."""
+    k = K()
+    N, H, W, IC, OC, ds = case
+    if OC % tile[1]:
+        pytest.skip("tile wider than OC")
+    torch.manual_seed(21)
+    x = torch.randn(N, H, W, IC, device=dev).bfloat16()
+    res = torch.randn(N, H, W, IC, device=dev).bfloat16()
+    sc, sh = torch.rand(IC, device=dev) + 0.5, torch.randn(IC, device=dev) * 0.1
+    rsc, rsh = (torch.rand(IC, device=dev) + 0.5, torch.randn(IC, device=dev) * 0.1) if ds else (None, None)
+    w = (torch.randn(OC, 1, 1, IC, device=dev) / math.sqrt(IC)).bfloat16()
+    out_ref, bits_ref = torch.empty_like(x), torch.empty(x.numel() // 8, device=dev, dtype=torch.uint8)
+    k.bn_apply(x, sc, sh, out_ref, res=res, res_scale=rsc, res_shift=rsh, relu=True, mbits=bits_ref)
+    y_ref, st_ref = torch.empty(N, H, W, OC, device=dev).bfloat16(), k.new_stats(OC, dev)
+    k.conv_fwd(out_ref, w, y_ref, R=1, S=1, stride=1, pad=0, stats=st_ref, tile=tile)
+    out, bits = torch.full_like(x, float("nan")), torch.zeros_like(bits_ref)
+    y, st = torch.empty_like(y_ref), k.new_stats(OC, dev)
+    k.conv_fwd(x, w, y, R=1, S=1, stride=1, pad=0, stats=st, in_scale=sc, in_shift=sh, tile=tile, tail_res=res,
+               tail_res_scale=rsc, tail_res_shift=rsh, tail_out=out, tail_bits=bits)
+    torch.cuda.synchronize()
+    if ds:
+        assert (out.float() - out_ref.float()).abs().max().item() < 0.07
+        assert (bits != bits_ref).float().mean().item() < 1e-3
+        assert relerr(y, y_ref) < 1e-2
+    else:
+        assert torch.equal(out, out_ref) and torch.equal(bits, bits_ref)
+        assert relerr(y, y_ref) < 2e-3
+    s, s_ref = st.view(-1, 2, OC).sum(0), st_ref.view(-1, 2, OC).sum(0)
+    assert ((s - s_ref).abs() / (s_ref.abs() + N * H * W)).max().item() < 1e-2
