@@ -28,6 +28,11 @@ __device__ __forceinline__ void unpack8(const u32x4 v, float* f) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = (float)b[j];
 }
+__device__ __forceinline__ unsigned pack2(float lo, float hi) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t b = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, b);
+}
 __device__ __forceinline__ u32x4 pack8(const float* f) {
   bf16x8 b;
 #pragma unroll

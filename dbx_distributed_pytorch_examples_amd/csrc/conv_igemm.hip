@@ -271,7 +271,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          // operands swapped (C^T = W X^T): a lane's 4 accumulators are 4 consecutive output
+          // channels of one pixel, so the epilogue stages them with one 8-byte LDS write
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   };
   // one pipeline step on block kb (LDS buffer kb&1, register set S holds block kb+1)
@@ -308,53 +310,26 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   }
 
   // ---- epilogue ------------------------------------------------------------------------
-  // acc[i][j][r]: row = wm*BM/WM + i*16 + (lane>>4)*4 + r, col = wn*BN/WN + j*16 + (lane&15)
+  // acc[i][j][r] (C^T): pixel row = wm*BM/WM + i*16 + (lane&15), channel = wn*BN/WN + j*16 + (lane>>4)*4 + r
+  // staged bf16 through LDS ([BM][BN+8]: the 8-byte writes of a wave hit each bank 4 times, the
+  // minimum for 512 B) and re-read as 16-byte row chunks for coalesced global stores
+  static_assert(!(STATS && EPI), "forward BN statistics and BN-backward epilogues are exclusive");
   bf16* sC = lds;  // [BM][BN+8]
-  float* sStat = reinterpret_cast<float*>(lds + LDS_C);  // [WM][2][BN]
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * (BN / WN) + j * 16 + (lane & 15);
-        sC[row * (BN + 8) + col] = (bf16)acc[i][j][r];
-      }
-  if constexpr (STATS) {
-#pragma unroll
     for (int j = 0; j < TN; ++j) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = (float)(bf16)acc[i][j][r];
-          s += v; q += v * v;
-        }
-      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-      if (lane < 16) {
-        const int col = wn * (BN / WN) + j * 16 + lane;
-        sStat[(wm * 2 + 0) * BN + col] = s;
-        sStat[(wm * 2 + 1) * BN + col] = q;
-      }
+      const int row = wm * (BM / WM) + i * 16 + (lane & 15);
+      const int col = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
+      *reinterpret_cast<uint2*>(sC + row * (BN + 8) + col) =
+          uint2{pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3])};
     }
-  }
   __syncthreads();
-  if constexpr (STATS) {
-    if (tid < BN) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) { s += sStat[(w * 2) * BN + tid]; q += sStat[(w * 2 + 1) * BN + tid]; }
-      double* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
-      atomicAdd(st + n0 + tid, (double)s);
-      atomicAdd(st + a.OC + n0 + tid, (double)q);
-    }
-  }
   constexpr int CPR = BN / 8;  // 16B chunks per output row; a thread's chunk column is fixed
   const int ccol = tid % CPR;
-  float bs[8], bq1[8], bq2[8];  // BN-backward partial sums of this thread's 8 channels
+  // per-thread partial sums of this thread's 8 channels: STATS: sum y, sum y^2 of the stored
+  // (bf16-rounded) outputs; EPI: BN-backward raw moments
+  float bs[8], bq1[8], bq2[8];
   f32x4 e_m1[2], e_i1[2], e_m2[2], e_i2[2], e_sc[2], e_sh[2];
   const bool has2 = EPI > 0 && a.ybn2 != nullptr;  // wave-uniform: second BN (downsample branch)
   if constexpr (EPI > 0) {
@@ -376,13 +351,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 #pragma unroll
     for (int j = 0; j < 8; ++j) bs[j] = bq1[j] = bq2[j] = 0.f;
   }
+  if constexpr (STATS) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bs[j] = bq1[j] = 0.f;
+  }
   // Epilogue in groups of EG rows per thread, in three straight-line phases: (1) every global load
   // of the group (residual addend, mask reference, BN inputs) — rows past M and absent addends read
   // a valid stand-in address instead of branching; (2) all arithmetic; (3) all stores. No load is
   // consumed after a store is issued and no load sits under divergent control flow, so hipcc waits
   // with counted vmcnt instead of draining the queue (stores count in vmcnt too) once per row.
   constexpr int NIT = BM * CPR / NT;
-  constexpr int EGMAX = (EPI != 0) ? 4 : 8;  // BN epilogues hold 4-5 vectors per row: stay clear of spills
+  constexpr int EGMAX = (EPI != 0 || (STATS && TAIL)) ? 4 : 8;  // BN epilogues hold 4-5 vectors per row: stay clear of spills
   constexpr int EG = NIT < EGMAX ? NIT : EGMAX;
   const bool sub_geom = MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1));  // wave-uniform
   const bool tail = m0 + BM > a.M;                                                  // wave-uniform
@@ -478,6 +457,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
           v = pack8(f);
         }
       }
+      if constexpr (STATS) {  // statistics of the stored values (ACCUM never combines with STATS)
+        float f[8];
+        unpack8(v, f);
+        if (tail && !ok[k]) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          bs[j] += f[j];
+          bq1[j] += f[j] * f[j];
+        }
+      }
       vv[k] = v;
     }
 #pragma unroll
@@ -489,6 +481,36 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
         for (int k = 0; k < EG; ++k)
           if (ok[k]) *reinterpret_cast<u32x4*>(a.a_out + ee[k]) = va2[k];
       }
+    }
+  }
+  if constexpr (STATS) {
+    // per-channel sum / sum of squares: in-wave lanes with the same chunk column by xor-shuffles,
+    // then the waves through LDS, then one fp64 atomic pair per channel into shard tm % nshard
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        bs[j] += __shfl_xor(bs[j], o, 64);
+        bq1[j] += __shfl_xor(bq1[j], o, 64);
+      }
+    }
+    __syncthreads();  // sC reuse
+    float* red = reinterpret_cast<float*>(lds);  // [NW waves][2][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wid * 2 + 0) * BN + ccol * 8 + j] = bs[j];
+        red[(wid * 2 + 1) * BN + ccol * 8 + j] = bq1[j];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) { s += red[(w * 2) * BN + tid]; q += red[(w * 2 + 1) * BN + tid]; }
+      double* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
+      atomicAdd(st + n0 + tid, (double)s);
+      atomicAdd(st + a.OC + n0 + tid, (double)q);
     }
   }
   if constexpr (EPI > 0) {

@@ -105,6 +105,8 @@ def pick_tile(M: int, OC: int, mode: str = "fwd", K_in: int = 0, R: int = 0, str
     heuristic: biggest tile that still puts >= ~2 workgroups on each of the 256 CUs."""
     if use_table:
         t = _tune_table().get(tune_key(mode, M, OC, K_in, R, stride))
+        if t is None and mode == "fwdt":  # tail-prologue fwd: the plain fwd winner if not tuned apart
+            t = _tune_table().get(tune_key("fwd", M, OC, K_in, R, stride))
         if t is not None and OC % t[1] == 0:
             return t
     if OC % 128 == 0 and ((M + 127) // 128) * (OC // 128) >= 512:
@@ -150,7 +152,7 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
             _chk(tail_out, torch.bfloat16, "tail_out", x.numel())
         if tail_bits is not None:
             _chk(tail_bits, torch.uint8, "tail_bits", x.numel() // 8)
-    bm, bn = tile or pick_tile(N * OH * OW, OC, "fwd", IC, R, stride)
+    bm, bn = tile or pick_tile(N * OH * OW, OC, "fwd" if tail_res is None else "fwdt", IC, R, stride)
     C().conv_igemm(FWD, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
                    R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),

@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--out", default=os.path.join(ROOT, "dbx_distributed_pytorch_examples_amd", "ops", "tune_table.json"))
     ap.add_argument("--report", default=None)
-    ap.add_argument("--modes", default="fwd,dgrad0,dgrad1,dgrad2,wgrad")
+    ap.add_argument("--modes", default="fwd,fwdt,dgrad0,dgrad1,dgrad2,wgrad")
     a = ap.parse_args()
     dev = "cuda"
     N = a.batch
@@ -90,6 +90,13 @@ def main():
         jobs = [("fwd", N * OH * OH, Kc, C, R, st,
                  lambda t: K.conv_fwd(x, w2, y, R=R, S=R, stride=st, pad=pad, stats=stats, in_scale=psc,
                                       in_shift=psh, tile=t))]
+        if R == 1 and st == 1 and Kc < C and K.tail_supported(C, R, R, st, pad):
+            # bottleneck conv1 consuming the previous block's output through the tail prologue
+            tres, tout = torch.randn_like(x), torch.empty_like(x)
+            tbits = torch.empty(x.numel() // 8, device=dev, dtype=torch.uint8)
+            jobs.append(("fwdt", N * OH * OH, Kc, C, R, st,
+                         lambda t: K.conv_fwd(x, w2, y, R=R, S=R, stride=st, pad=pad, stats=stats, in_scale=sc,
+                                              in_shift=sh, tile=t, tail_res=tres, tail_out=tout, tail_bits=tbits)))
         if st > 1 and R == 1:
             # strided 1x1 (downsample): the program runs a dense dgrad onto the subsampled grid
             dxs = torch.empty(N, OH, OH, C, device=dev, dtype=torch.bfloat16)
