@@ -31,8 +31,8 @@ int dbx_bn_bwd_apply(const bf16*, const bf16*, const bf16*, const float*, const 
                      long long, int, int, hipStream_t);
 int dbx_bn_bwd_apply2(const bf16*, const bf16*, const float*, bf16*, const bf16*, const float*, bf16*, long long, int,
                       hipStream_t);
-int dbx_maxpool_fwd(const bf16*, const float*, const float*, bf16*, unsigned char*, int, int, int, int, int, int, int,
-                    int, int, int, hipStream_t);
+int dbx_maxpool_fwd(const bf16*, const float*, const float*, bf16*, unsigned char*, bf16*, int, int, int, int, int,
+                    int, int, int, int, int, hipStream_t);
 int dbx_maxpool_bwd(const bf16*, const unsigned char*, bf16*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int dbx_pool_bn_bwd(const bf16*, const unsigned char*, const bf16*, const float*, const float*, const float*,
                     const float*, const float*, bf16*, double*, int, int, int, int, int, int, int, int, int, int, int,
@@ -156,10 +156,10 @@ PYBIND11_MODULE(_C, m) {
                             P<const bf16*>(y2), P<const float*>(c2), P<bf16*>(dy2), n, C, S(st)),
           "bn_bwd_apply2");
   });
-  m.def("maxpool_fwd", [](uintptr_t x, uintptr_t sc, uintptr_t sh, uintptr_t out, uintptr_t arg, int N, int H, int W,
-                          int C, int Pp, int Q, int K, int stride, int pad, int relu, uintptr_t st) {
+  m.def("maxpool_fwd", [](uintptr_t x, uintptr_t sc, uintptr_t sh, uintptr_t out, uintptr_t arg, uintptr_t ymax, int N,
+                          int H, int W, int C, int Pp, int Q, int K, int stride, int pad, int relu, uintptr_t st) {
     check(dbx_maxpool_fwd(P<const bf16*>(x), P<const float*>(sc), P<const float*>(sh), P<bf16*>(out),
-                          P<unsigned char*>(arg), N, H, W, C, Pp, Q, K, stride, pad, relu, S(st)),
+                          P<unsigned char*>(arg), P<bf16*>(ymax), N, H, W, C, Pp, Q, K, stride, pad, relu, S(st)),
           "maxpool_fwd");
   });
   m.def("maxpool_bwd", [](uintptr_t dout, uintptr_t arg, uintptr_t dx, int N, int H, int W, int C, int Pp, int Q, int K,

@@ -311,8 +311,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const bf16* __restri
 // ----------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ sc,
                                    const float* __restrict__ sh, bf16* __restrict__ out,
-                                   unsigned char* __restrict__ arg, int N, int H, int W, int C, int P,
-                                   int Q, int K, int stride, int pad, int relu) {
+                                   unsigned char* __restrict__ arg, bf16* __restrict__ ymax, int N, int H, int W,
+                                   int C, int P, int Q, int K, int stride, int pad, int relu) {
   const RowMap rm(C);
   if (rm.r0 >= rm.rpb) return;
   const int c0 = rm.cg * 8;
@@ -328,10 +328,10 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16* __restrict
     const long long t = pix / Q;
     const int p = (int)(t % P);
     const int n = (int)(t / P);
-    float best[8];
+    float best[8], braw[8];
     unsigned char bi[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; braw[j] = 0.f; bi[j] = 0; }
     for (int r = 0; r < K; ++r) {
       const int hh = p * stride - pad + r;
       if (hh < 0 || hh >= H) continue;
@@ -344,13 +344,16 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16* __restrict
         for (int j = 0; j < 8; ++j) {
           float v = f[j] * s[j] + h[j];
           if (relu) v = fmaxf(v, 0.f);
-          if (v > best[j]) { best[j] = v; bi[j] = (unsigned char)(r * K + ss); }
+          if (v > best[j]) { best[j] = v; braw[j] = f[j]; bi[j] = (unsigned char)(r * K + ss); }
         }
       }
     }
     const size_t o = (size_t)pix * C + c0;
     *reinterpret_cast<u32x4*>(out + o) = pack8(best);
     *reinterpret_cast<uint2*>(arg + o) = *reinterpret_cast<uint2*>(bi);
+    // the pre-BN value at the argmax: the stem BN-backward reduction then runs over the pooled
+    // positions (sum over windows == sum over pixels of the scattered gradient), 1/4 of the bytes
+    if (ymax) *reinterpret_cast<u32x4*>(ymax + o) = pack8(braw);
   }
 }
 
@@ -921,12 +924,13 @@ extern "C" int dbx_bn_bwd_apply2(const bf16* g, const bf16* y1, const float* c1,
                      y2, c2, dy2, M, C);
   RET_LAST;
 }
-extern "C" int dbx_maxpool_fwd(const bf16* x, const float* sc, const float* sh, bf16* out, unsigned char* arg, int N,
-                               int H, int W, int C, int P, int Q, int K, int stride, int pad, int relu, hipStream_t st) {
+extern "C" int dbx_maxpool_fwd(const bf16* x, const float* sc, const float* sh, bf16* out, unsigned char* arg,
+                               bf16* ymax, int N, int H, int W, int C, int P, int Q, int K, int stride, int pad, int relu,
+                               hipStream_t st) {
   if (C % 8) return -1;
   if (C / 8 > 256) return -1;
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * P * Q, 256 / (C / 8), 4096)), dim3(256), 0, st,
-                     x, sc, sh, out, arg, N, H, W, C, P, Q, K, stride, pad, relu);
+                     x, sc, sh, out, arg, ymax, N, H, W, C, P, Q, K, stride, pad, relu);
   RET_LAST;
 }
 extern "C" int dbx_maxpool_bwd(const bf16* dout, const unsigned char* arg, bf16* dx, int N, int H, int W, int C, int P,

@@ -141,6 +141,7 @@ class ResNetProgram:
         self.act_writeback = os.environ.get("DBX_ACT_WRITEBACK", "1") == "1"
         # compute block outputs inside the next block's conv1 prologue instead of a bn_apply pass
         self.fuse_tail = os.environ.get("DBX_FUSE_TAIL", "1") == "1"
+        self.pool_reduce = os.environ.get("DBX_POOL_REDUCE", "1") == "1"
         self._wstream = None
         self._side_pending = False
         self._build_layers()
@@ -333,6 +334,9 @@ class ResNetProgram:
         self.dp0 = E(N, ph, pw, st.OC)
         # pooled-gradient buffer only for pool geometries the fused stem backward does not cover
         self.da0 = None if K.pool_bn_bwd_supported(st.OC, self.pool_k, self.pool_s) else E(N, st.OH, st.OW, st.OC)
+        # pre-BN stem value at each pool argmax (training): the stem BN-backward reduction runs over
+        # the pooled positions instead of gathering over the full-resolution stem output
+        self.pymax = E(N, ph, pw, st.OC) if self.da0 is None and self.pool_reduce else None
         self.dy0 = E(N, st.OH, st.OW, st.OC)
         wsmax = 0
         for b in self.blocks:
@@ -440,7 +444,7 @@ class ResNetProgram:
                         stats=sbn.stats if tr else None)
         self._bn_fwd(sbn, N * st.OH * st.OW)
         K.maxpool_fwd(self.y0, self.p0, self.parg, K=self.pool_k, stride=self.pool_s, pad=self.pool_p,
-                      scale=sbn.scale, shift=sbn.shift, relu=True)
+                      scale=sbn.scale, shift=sbn.shift, relu=True, ymax=self.pymax if tr else None)
         x = self.p0
         pending = None  # previous block whose output this block's conv1 computes (tail prologue)
         for bi, b in enumerate(self.blocks):
@@ -631,7 +635,12 @@ class ResNetProgram:
         if K.pool_bn_bwd_supported(st.OC, self.pool_k, self.pool_s):
             # max-pool backward folded into the stem BN's reduce/apply passes (no pooled-grad tensor)
             pk = dict(K=self.pool_k, stride=self.pool_s, pad=self.pool_p)
-            K.pool_bn_bwd_reduce(dp, self.parg, self.y0, sbn.scale, sbn.shift, sbn.mean, sbn.invstd, sbn.bstats, **pk)
+            if self.pymax is not None:  # sum over windows of dpool * [y at argmax] == sum over pixels
+                K.bn_bwd_reduce(dp, self.pymax, sbn.mean, sbn.invstd, sbn.bstats, mask_mode=K.MASK_Y,
+                                scale=sbn.scale, shift=sbn.shift)
+            else:
+                K.pool_bn_bwd_reduce(dp, self.parg, self.y0, sbn.scale, sbn.shift, sbn.mean, sbn.invstd, sbn.bstats,
+                                     **pk)
             K.bn_bwd_coeff(sbn.bstats, self.N * st.OH * st.OW, sbn.gamma, sbn.mean, sbn.invstd, sbn.coeff,
                            sbn.dgamma, sbn.dbeta)
             K.pool_bn_bwd_apply(dp, self.parg, self.y0, sbn.scale, sbn.shift, sbn.coeff, self.dy0, **pk)

@@ -431,14 +431,18 @@ def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2):
 
 
 @_dispatch
-def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True):
+def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True, ymax=None):
+    """out = max over windows of relu(x*scale + shift), arg = window index of the max; ``ymax``
+    (optional) = the raw x at the argmax (the stem BN backward reduces over pooled positions)."""
     N, H, W, Cc = x.shape
     _, P, Q, _ = out.shape
     _chk(x, torch.bfloat16, "x")
     _chk(out, torch.bfloat16, "out")
     _chk(arg, torch.uint8, "arg", out.numel())
-    C().maxpool_fwd(x.data_ptr(), _p(scale), _p(shift), out.data_ptr(), arg.data_ptr(), N, H, W, Cc, P, Q, K,
-                    stride, pad, int(relu), stream_ptr())
+    if ymax is not None:
+        _chk(ymax, torch.bfloat16, "ymax", out.numel())
+    C().maxpool_fwd(x.data_ptr(), _p(scale), _p(shift), out.data_ptr(), arg.data_ptr(), _p(ymax), N, H, W, Cc, P, Q,
+                    K, stride, pad, int(relu), stream_ptr())
 
 
 @_dispatch

@@ -230,7 +230,7 @@ def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2):
     bn_bwd_apply(g, y2, coeff2, dy2, mask_mode=0)
 
 
-def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True):
+def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True, ymax=None):
     f = x.float()
     if scale is not None:
         f = f * scale + shift
@@ -239,16 +239,23 @@ def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, re
     N, H, W, C = f.shape
     _, P, Q, _ = out.shape
     fp = F.pad(_nchw(f), (pad, pad, pad, pad), value=-math.inf)
+    xp = F.pad(_nchw(x.float()), (pad, pad, pad, pad))
     best = torch.full((N, C, P, Q), -math.inf, dtype=torch.float32, device=x.device)
+    braw = torch.zeros((N, C, P, Q), dtype=torch.float32, device=x.device)
     bidx = torch.zeros((N, C, P, Q), dtype=torch.uint8, device=x.device)
     for r in range(K):
         for s in range(K):
-            win = fp[:, :, r:r + stride * (P - 1) + 1:stride, s:s + stride * (Q - 1) + 1:stride]
+            sl = (slice(None), slice(None), slice(r, r + stride * (P - 1) + 1, stride),
+                  slice(s, s + stride * (Q - 1) + 1, stride))
+            win = fp[sl]
             upd = win > best
             best = torch.where(upd, win, best)
+            braw = torch.where(upd, xp[sl], braw)
             bidx = torch.where(upd, torch.full_like(bidx, r * K + s), bidx)
     out.copy_(_nhwc(best).bfloat16())
     arg.copy_(_nhwc(bidx))
+    if ymax is not None:
+        ymax.copy_(_nhwc(braw).bfloat16())
 
 
 def maxpool_bwd(dout, arg, dx, *, K=3, stride=2, pad=1):

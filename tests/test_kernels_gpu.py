@@ -261,6 +261,30 @@ def test_maxpool():
     assert relerr(dx.float() * m, act.grad * m) < 2e-2
 
 
+def test_maxpool_ymax_matches_reference_and_stem_reduce():
+    """maxpool_fwd's ymax (raw input at the argmax) equals the reference's, and the stem BN-backward
+    reduction over pooled positions (dpool, ymax, MASK_Y) equals the full-resolution gather form."""
+    k = K()
+    from dbx_distributed_pytorch_examples_amd.ops import reference as R
+    N, H, W, Cc = 2, 112, 112, 64
+    torch.manual_seed(6)
+    x = torch.randn(N, H, W, Cc, device=dev).bfloat16()
+    sc, sh = torch.rand(Cc, device=dev) + 0.5, torch.randn(Cc, device=dev) * 0.1
+    out, arg, ym = (torch.empty(N, 56, 56, Cc, device=dev, dtype=t) for t in (torch.bfloat16, torch.uint8,
+                                                                               torch.bfloat16))
+    k.maxpool_fwd(x, out, arg, scale=sc, shift=sh, relu=True, ymax=ym)
+    xc, oc, ac, yc = x.cpu(), torch.empty_like(out).cpu(), torch.empty_like(arg).cpu(), torch.empty_like(ym).cpu()
+    R.maxpool_fwd(xc, oc, ac, scale=sc.cpu(), shift=sh.cpu(), relu=True, ymax=yc)
+    assert torch.equal(out.cpu(), oc) and torch.equal(arg.cpu(), ac) and torch.equal(ym.cpu(), yc)
+    dp = torch.randn(N, 56, 56, Cc, device=dev).bfloat16()
+    mean, inv = torch.randn(Cc, device=dev) * 0.1, torch.rand(Cc, device=dev) + 0.5
+    st_full, st_pool = k.new_stats(Cc, dev), k.new_stats(Cc, dev)
+    k.pool_bn_bwd_reduce(dp, arg, x, sc, sh, mean, inv, st_full, K=3, stride=2, pad=1)
+    k.bn_bwd_reduce(dp, ym, mean, inv, st_pool, mask_mode=k.MASK_Y, scale=sc, shift=sh)
+    a, b = st_full.view(-1, 2, Cc).sum(0), st_pool.view(-1, 2, Cc).sum(0)
+    assert ((a - b).abs() / (a.abs() + 1.0)).max().item() < 1e-4
+
+
 @pytest.mark.parametrize("hw", [(16, 16), (15, 13), (112, 112)])
 def test_pool_bn_bwd_fused(hw):
     """Stem backward with the max-pool backward folded into the BN reduce/apply passes, against
