@@ -34,9 +34,11 @@ namespace dbx {
 enum ConvMode { FWD = 0, DGRAD = 1, STEM = 2 };
 
 
-// TAIL (FWD, with PRO): the A operand is the previous residual block's output, computed while
-// staging from that block's raw conv3 output (x) and its shortcut (res): no separate bn_apply pass
-// and no re-read of the block output; the first N tile writes the output + ReLU mask back.
+// TAIL (with PRO), A = x*s + h + (res*rs + rh) computed while staging; the first N tile writes A
+// back (tail_out). FWD: the previous residual block's output relu(bn3(x) + shortcut) -- no separate
+// bn_apply pass, no re-read of the block output, ReLU mask written too. DGRAD (1x1 stride-1): the
+// BN-backward apply dy = k1*g + k2*y + k3 (x = g, res = y, no ReLU) -- the BN-backward apply pass
+// is gone and its output is still stored for the weight gradient.
 template <int BM, int BN, int WM, int WN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI, bool TAIL = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs a) {
   constexpr int NT = 64 * WM * WN;        // threads; WM x WN waves, each owns a (BM/WM) x (BN/WN) tile
@@ -104,7 +106,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       sPro[PRO_MAXC + c] = a.in_shift[c];
       if constexpr (TAIL) {
         sPro[2 * PRO_MAXC + c] = a.res_scale ? a.res_scale[c] : 1.f;
-        sPro[3 * PRO_MAXC + c] = a.res_scale ? a.res_shift[c] : 0.f;
+        sPro[3 * PRO_MAXC + c] = a.res_shift ? a.res_shift[c] : 0.f;
       }
     }
     __syncthreads();
@@ -201,13 +203,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
           }
         }
         u32x4 t = pack8(f);
-        t = relu_bf16x8(t);  // PRO implies ReLU (host-checked)
+        if constexpr (MODE != DGRAD) t = relu_bf16x8(t);  // forward PRO implies ReLU (host-checked)
         const bool vi = (avalid[S] >> i) & 1u;
         ra[S][i] = vi ? t : zero4;  // padding taps stay exactly zero
         if constexpr (TAIL) {
           // block output + 1-bit mask (bit j: element j > 0) written back by the first N tile
           const unsigned off = (wlive[S] && vi) ? apix[i] + wtoff[S] : kOOB;
           buf_store16(toutr, off, t);
+          if constexpr (MODE == DGRAD) continue;
           unsigned bits = 0;
 #pragma unroll
           for (int q = 0; q < 4; ++q)
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // consumed after a store is issued and no load sits under divergent control flow, so hipcc waits
   // with counted vmcnt instead of draining the queue (stores count in vmcnt too) once per row.
   constexpr int NIT = BM * CPR / NT;
-  constexpr int EGMAX = (EPI != 0 || (STATS && TAIL)) ? 4 : 8;  // BN epilogues hold 4-5 vectors per row: stay clear of spills
+  constexpr int EGMAX = (EPI != 0 || TAIL) ? 4 : 8;  // BN epilogues hold 4-5 vectors per row: stay clear of spills
   constexpr int EG = NIT < EGMAX ? NIT : EGMAX;
   const bool sub_geom = MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1));  // wave-uniform
   const bool tail = m0 + BM > a.M;                                                  // wave-uniform
@@ -875,6 +878,16 @@ static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, hipStream_t st
 
 template <int BM, int BN>
 static int dispatch_dgrad(const IGemmArgs& a, bool accum, int epi, hipStream_t st) {
+  if (a.res) {  // BN-backward apply prologue (1x1 stride-1 dgrads of the bottleneck)
+    constexpr int TM = (BM == 128 && BN == 256) ? 256 : BM, TN = (BM == 128 && BN == 256) ? 128 : BN;
+    if (accum) {
+      if (epi == 1) return launch_igemm_t<TM, TN, DGRAD, true, false, true, 1, true>(a, st);
+      if (epi == 0) return launch_igemm_t<TM, TN, DGRAD, true, false, true, 0, true>(a, st);
+      return -11;
+    }
+    if (epi == 2) return launch_igemm_t<TM, TN, DGRAD, true, false, false, 2, true>(a, st);
+    return -11;
+  }
   if (accum) {
     if (epi == 1) return launch_igemm_t<BM, BN, DGRAD, false, false, true, 1>(a, st);
     if (epi == 2) return launch_igemm_t<BM, BN, DGRAD, false, false, true, 2>(a, st);
@@ -896,10 +909,11 @@ static int dispatch_dgrad(const IGemmArgs& a, bool accum, int epi, hipStream_t s
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
                               int accum, int epi, hipStream_t st) {
   const IGemmArgs& a = *args;
-  if (pro && !a.relu_in) return -7;  // the BN prologue always ends in ReLU (ResNet dataflow)
+  if (pro && mode == FWD && !a.relu_in) return -7;  // the forward BN prologue always ends in ReLU
   if (pro && a.IC > (a.res ? 1024 : 512)) return -8;  // prologue coefficients staged in LDS (PRO_MAXC)
-  if (a.res && (!pro || mode != FWD || a.R != 1 || a.S != 1 || a.stride != 1 || a.pad != 0))
+  if (a.res && (!pro || mode == STEM || a.R != 1 || a.S != 1 || a.stride != 1 || a.pad != 0))
     return -10;  // the tail prologue is for 1x1 stride-1 consumers (output pixel == input pixel)
+  if (a.res && mode == DGRAD && a.tail_bits) return -10;
   if (a.a_out && (mode != DGRAD || epi != 2)) return -9;  // write-back: the MASK_Y epilogue computes it
   if (a.OC % bn != 0) return -1;
   if (mode == STEM) {
@@ -915,7 +929,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
     return -3;
   }
   if (mode == DGRAD) {
-    if (pro || stats) return -2;
+    if ((pro && !a.res) || stats) return -2;
     if (epi && (a.ybn == nullptr || a.bstats1 == nullptr || a.mean1 == nullptr || a.inv1 == nullptr)) return -6;
     if (epi == 1 && a.mbits == nullptr) return -6;
     if (epi == 2 && (a.bsc == nullptr || a.bsh == nullptr)) return -6;

@@ -142,6 +142,8 @@ class ResNetProgram:
         # compute block outputs inside the next block's conv1 prologue instead of a bn_apply pass
         self.fuse_tail = os.environ.get("DBX_FUSE_TAIL", "1") == "1"
         self.pool_reduce = os.environ.get("DBX_POOL_REDUCE", "1") == "1"
+        # BN-backward apply of a 1x1 conv's output BN computed in that conv's dgrad prologue
+        self.fuse_bwd_apply = os.environ.get("DBX_FUSE_BWD_APPLY", "1") == "1"
         self._wstream = None
         self._side_pending = False
         self._build_layers()
@@ -565,6 +567,7 @@ class ResNetProgram:
         nconv = len(b.convs)
         lc, lbn = b.convs[-1], b.bns[-1]
         cnt_last = N * lc.OH * lc.OW
+        pend, gin = None, None  # BN-backward apply deferred into the next dgrad's prologue
         if last:
             # g = dlast * (out > 0) -> self.g_last ; tail BN reductions (and ds BN) from dlast
             K.bn_bwd_reduce(self.dlast, b.ys[-1], lbn.mean, lbn.invstd, lbn.bstats, mask_mode=K.MASK_OUT, mref=b.out)
@@ -587,7 +590,11 @@ class ResNetProgram:
             else:  # both tail BNs from one read of the block-output gradient
                 K.bn_bwd_apply2(g, b.ys[-1], lbn.coeff, b.dys[-1], b.yd, dbn.coeff, b.dyd)
         elif not last:
-            K.bn_bwd_apply(g, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_NONE)
+            if self._fold(lc):  # folded into conv3's dgrad prologue (it stores dys[-1] for the wgrad)
+                pend = dict(bwd_y=b.ys[-1], bwd_coeff=lbn.coeff, dy_out=b.dys[-1])
+                gin = g
+            else:
+                K.bn_bwd_apply(g, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_NONE)
         # inner convs, last to second: dgrad epilogue masks with the previous BN's ReLU and
         # accumulates that BN's backward statistics
         for j in range(nconv - 1, 0, -1):
@@ -595,20 +602,33 @@ class ResNetProgram:
             # dgrad first: its epilogue also stores the BN output acts[j-1] = this conv's input,
             # which the (side-stream) weight gradient then reads without a BN prologue
             act = b.acts[j - 1]
-            if act is None:  # wgrad re-applies BN+ReLU to its staged input tiles (BN prologue)
+            kw, src = (pend, gin) if pend else ({}, b.dys[j])
+            pend = None
+            pre = act is None and not kw  # wgrad re-applies BN+ReLU to its staged input tiles (BN prologue)
+            if pre:
                 self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                             in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
-            K.conv_dgrad(b.dys[j], cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+            K.conv_dgrad(src, cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                          epilogue=K.BNBwdEpilogue(K.MASK_Y, b.ys[j - 1], pbn.mean, pbn.invstd, pbn.bstats,
-                                                  scale=pbn.scale, shift=pbn.shift, act_out=act))
+                                                  scale=pbn.scale, shift=pbn.shift, act_out=act), **kw)
             if act is not None:
                 self._wgrad(b.dys[j], act, cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad)
+            elif not pre:
+                self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                            in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
             K.bn_bwd_coeff(pbn.bstats, N * pc.OH * pc.OW, pbn.gamma, pbn.mean, pbn.invstd, pbn.coeff, pbn.dgamma,
                            pbn.dbeta)
-            K.bn_bwd_apply(b.das[j - 1], b.ys[j - 1], pbn.coeff, b.dys[j - 1], mask_mode=K.MASK_NONE)
-        # first conv: wgrad, then the block-input gradient = dgrad(conv1) + shortcut gradient
+            if self._fold(pc):  # the next dgrad (conv j-1) applies it while staging
+                pend = dict(bwd_y=b.ys[j - 1], bwd_coeff=pbn.coeff, dy_out=b.dys[j - 1])
+                gin = b.das[j - 1]
+            else:
+                K.bn_bwd_apply(b.das[j - 1], b.ys[j - 1], pbn.coeff, b.dys[j - 1], mask_mode=K.MASK_NONE)
+        # first conv: wgrad (after the dgrad when that stores dys[0]), then the block-input gradient
+        # = dgrad(conv1) + shortcut gradient
         c0 = b.convs[0]
-        self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
+        kw0, src0 = (pend, gin) if pend else ({}, b.dys[0])
+        if not kw0:
+            self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
         if b.ds_conv is not None:
             dc = b.ds_conv
             self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
@@ -626,8 +646,14 @@ class ResNetProgram:
                                   mean2=pb.ds_bn.mean if pb.ds_conv is not None else None,
                                   inv2=pb.ds_bn.invstd if pb.ds_conv is not None else None,
                                   stats2=pb.ds_bn.bstats if pb.ds_conv is not None else None)
-        K.conv_dgrad(b.dys[0], c0.wt16, b.dx, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad,
-                     addsrc=addsrc, add_sub=sub, epilogue=epi)
+        K.conv_dgrad(src0, c0.wt16, b.dx, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad,
+                     addsrc=addsrc, add_sub=sub, epilogue=epi, **kw0)
+        if kw0:
+            self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
+
+    def _fold(self, cv) -> bool:
+        """Fold the BN-backward apply of cv's output BN into cv's dgrad (1x1 stride-1 convs)."""
+        return self.fuse_bwd_apply and not cv.stem and K.tail_supported(cv.OC, cv.R, cv.S, cv.stride, cv.pad)
 
     def _bwd_stem(self):
         st, sbn = self.stem, self.stem_bn

@@ -208,13 +208,16 @@ class BNBwdEpilogue:
 
 @_dispatch
 def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, addsrc=None, add_sub=1,
-               epilogue: "BNBwdEpilogue" = None):
+               epilogue: "BNBwdEpilogue" = None, bwd_y=None, bwd_coeff=None, dy_out=None):
     """dX = conv_transpose(dY, W): dy [N,P,Q,K], wt16 [C, R*S*K] (CRSK), dx [N,H,W,C].
 
     Stride > 1 runs one dense launch per output phase (``dgrad_phases``): no MFMA work on the
     (stride^2 - 1)/stride^2 taps that a masked gather would multiply by zero.
     ``accumulate``: dx += result (addsrc=None) or dx = result + addsrc (addsrc at 1/add_sub
     resolution, e.g. the dense dgrad of a strided 1x1 downsample); ``epilogue``: fused BN backward.
+    ``bwd_y``/``bwd_coeff`` (1x1 stride-1 only): ``dy`` is the raw BN-output gradient g and the
+    operand is the BN-backward apply k1*g + k2*bwd_y + k3 (coeff [3, K]) computed while staging;
+    it is also stored to ``dy_out`` (for the weight gradient) -- bn_bwd_apply folded in.
     """
     N, P, Q, K = dy.shape
     _, H, W, Cc = dx.shape
@@ -248,6 +251,16 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         act_ptr = _p(e.act_out)
     else:
         act_ptr = 0
+    bwd = (0, 0, 0, 0, 0, 0)  # in_scale, in_shift, res, res_scale, res_shift, tail_out
+    if bwd_y is not None:
+        if not tail_supported(K, R, S, stride, pad):
+            raise ValueError("BN-backward prologue needs a 1x1 stride-1 dgrad with <= 1024 channels")
+        _chk(bwd_y, torch.bfloat16, "bwd_y", dy.numel())
+        _chk(bwd_coeff, torch.float32, "bwd_coeff", 3 * K)
+        if dy_out is not None:
+            _chk(dy_out, torch.bfloat16, "dy_out", dy.numel())
+        c0 = bwd_coeff.data_ptr()
+        bwd = (c0, c0 + 8 * K, bwd_y.data_ptr(), c0 + 4 * K, 0, _p(dy_out))
     phases = dgrad_phases(H, W, R, S, stride, pad)
     if not accumulate and any(ph[5] == 0 or ph[7] == 0 for ph in phases):
         if epilogue is not None:
@@ -260,10 +273,10 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
                 raise ValueError("strided dgrad with empty phases cannot carry an epilogue / addend")
             continue
         bm, bn = tile or pick_tile(N * ohs * ows, Cc, f"dgrad{epilogue.mode if epilogue else 0}", K, R, stride)
-        C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
+        C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), bwd[0], bwd[1], 0, 0, NSHARD,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,
-                       _p(addsrc), add_sub, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr())
+                       _p(addsrc), add_sub, *epi, act_ptr, bwd[2], bwd[3], bwd[4], bwd[5], 0, stream_ptr())
     return dx
 
 

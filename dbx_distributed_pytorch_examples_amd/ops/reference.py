@@ -65,7 +65,11 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
 
 
 def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, addsrc=None, add_sub=1,
-               epilogue=None):
+               epilogue=None, bwd_y=None, bwd_coeff=None, dy_out=None):
+    if bwd_y is not None:  # the operand is the BN-backward apply of (dy, bwd_y)
+        d = dy_out if dy_out is not None else torch.empty_like(dy)
+        bn_bwd_apply(dy, bwd_y, bwd_coeff, d, mask_mode=MASK_NONE)
+        dy = d
     N, P, Q, Kc = dy.shape
     _, H, W, Cc = dx.shape
     w = wt16.float().view(Cc, R, S, Kc).permute(3, 0, 1, 2)  # [K, C, R, S]

@@ -615,3 +615,49 @@ def test_conv_fwd_tail_prologue(case, tile):
         assert relerr(y, y_ref) < 2e-3
     s, s_ref = st.view(-1, 2, OC).sum(0), st_ref.view(-1, 2, OC).sum(0)
     assert ((s - s_ref).abs() / (s_ref.abs() + N * H * W)).max().item() < 1e-2
+
+
+@pytest.mark.parametrize("tile", [(64, 64), (128, 64), (128, 128), (256, 64), (256, 128), (128, 256)])
+@pytest.mark.parametrize("variant", ["epi2", "epi1_acc", "acc"])
+def test_dgrad_bwd_apply_prologue(variant, tile):
+    """1x1 dgrad whose operand is the BN-backward apply k1*g + k2*y + k3 computed while staging ==
+    bn_bwd_apply followed by the plain dgrad (same epilogue); the applied operand is stored."""
+    k = K()
+    N, H, W, Kc, Cc = 2, 14, 14, 256, 128
+    if Cc % tile[1]:
+        pytest.skip("tile wider than C")
+    torch.manual_seed(31)
+    g = torch.randn(N, H, W, Kc, device=dev).bfloat16()
+    y = torch.randn(N, H, W, Kc, device=dev).bfloat16()
+    coeff = torch.randn(3 * Kc, device=dev) * 0.5
+    wt = (torch.randn(Cc, Kc, device=dev) / math.sqrt(Kc)).bfloat16()
+    ybn = torch.randn(N, H, W, Cc, device=dev).bfloat16()
+    mean, inv = torch.randn(Cc, device=dev) * 0.1, torch.rand(Cc, device=dev) + 0.5
+    sc, sh = torch.rand(Cc, device=dev) + 0.5, torch.randn(Cc, device=dev) * 0.1
+    add = torch.randn(N, H, W, Cc, device=dev).bfloat16()
+    mbits = k.pack_mask_bits(torch.randn(N, H, W, Cc, device=dev).bfloat16())
+
+    def run(dy_in, **kw):
+        st1 = k.new_stats(Cc, dev)
+        dx = torch.empty(N, H, W, Cc, device=dev, dtype=torch.bfloat16)
+        if variant == "epi2":
+            e = k.BNBwdEpilogue(k.MASK_Y, ybn, mean, inv, st1, scale=sc, shift=sh)
+            k.conv_dgrad(dy_in, wt, dx, R=1, S=1, stride=1, pad=0, tile=tile, epilogue=e, **kw)
+        elif variant == "epi1_acc":
+            e = k.BNBwdEpilogue(k.MASK_OUT, ybn, mean, inv, st1, mbits=mbits)
+            k.conv_dgrad(dy_in, wt, dx, R=1, S=1, stride=1, pad=0, tile=tile, epilogue=e, addsrc=add, **kw)
+        else:
+            k.conv_dgrad(dy_in, wt, dx, R=1, S=1, stride=1, pad=0, tile=tile, addsrc=add, **kw)
+        return dx, st1
+
+    dy_ref = torch.empty_like(g)
+    k.bn_bwd_apply(g, y, coeff, dy_ref, mask_mode=k.MASK_NONE)
+    dx_ref, st_ref = run(dy_ref)
+    dy_out = torch.full_like(g, float("nan"))
+    dx, st = run(g, bwd_y=y, bwd_coeff=coeff, dy_out=dy_out)
+    torch.cuda.synchronize()
+    assert (dy_out.float() - dy_ref.float()).abs().max().item() <= 0.02 * dy_ref.float().abs().max().item()
+    assert relerr(dx, dx_ref) < 1e-2
+    if variant != "acc":
+        a, b = st.view(-1, 2, Cc).sum(0), st_ref.view(-1, 2, Cc).sum(0)
+        assert ((a - b).abs() / (b.abs() + N * H * W * 0.01)).max().item() < 2e-2
