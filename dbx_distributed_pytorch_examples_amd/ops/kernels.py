@@ -105,8 +105,8 @@ def pick_tile(M: int, OC: int, mode: str = "fwd", K_in: int = 0, R: int = 0, str
     heuristic: biggest tile that still puts >= ~2 workgroups on each of the 256 CUs."""
     if use_table:
         t = _tune_table().get(tune_key(mode, M, OC, K_in, R, stride))
-        if t is None and mode == "fwdt":  # tail-prologue fwd: the plain fwd winner if not tuned apart
-            t = _tune_table().get(tune_key("fwd", M, OC, K_in, R, stride))
+        if t is None and (mode == "fwdt" or mode.endswith("b")):  # prologue variants: the plain winner
+            t = _tune_table().get(tune_key("fwd" if mode == "fwdt" else mode[:-1], M, OC, K_in, R, stride))
         if t is not None and OC % t[1] == 0:
             return t
     if OC % 128 == 0 and ((M + 127) // 128) * (OC // 128) >= 512:
@@ -272,7 +272,8 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             if epilogue is not None or addsrc is not None:
                 raise ValueError("strided dgrad with empty phases cannot carry an epilogue / addend")
             continue
-        bm, bn = tile or pick_tile(N * ohs * ows, Cc, f"dgrad{epilogue.mode if epilogue else 0}", K, R, stride)
+        bm, bn = tile or pick_tile(N * ohs * ows, Cc, f"dgrad{epilogue.mode if epilogue else 0}"
+                                   + ("b" if bwd_y is not None else ""), K, R, stride)
         C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), bwd[0], bwd[1], 0, 0, NSHARD,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,

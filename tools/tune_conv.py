@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--out", default=os.path.join(ROOT, "dbx_distributed_pytorch_examples_amd", "ops", "tune_table.json"))
     ap.add_argument("--report", default=None)
-    ap.add_argument("--modes", default="fwd,fwdt,dgrad0,dgrad1,dgrad2,wgrad")
+    ap.add_argument("--modes", default="fwd,fwdt,dgrad0,dgrad1,dgrad2,dgrad1b,dgrad2b,wgrad")
     a = ap.parse_args()
     dev = "cuda"
     N = a.batch
@@ -111,6 +111,15 @@ def main():
                                                                             tile=t, addsrc=add, epilogue=e1)))
             jobs.append(("dgrad2", Md, C, Kc, R, st, lambda t: K.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad,
                                                                             tile=t, epilogue=e2)))
+            if K.tail_supported(Kc, R, R, st, pad):  # 1x1 dgrads with the BN-backward apply prologue
+                by, bc, bo = torch.randn_like(dy), torch.randn(3 * Kc, device=dev) * 0.5, torch.empty_like(dy)
+                bk = dict(bwd_y=by, bwd_coeff=bc, dy_out=bo)
+                jobs.append(("dgrad1b", Md, C, Kc, R, st,
+                             lambda t: K.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad, tile=t, addsrc=add,
+                                                    epilogue=e1, **bk)))
+                jobs.append(("dgrad2b", Md, C, Kc, R, st,
+                             lambda t: K.conv_dgrad(dy, wt, dx, R=R, S=R, stride=st, pad=pad, tile=t, epilogue=e2,
+                                                    **bk)))
         ws = torch.empty(max(64 * Kc * R * R * C, 16 << 20), device=dev)
         dw = torch.empty(Kc * R * R * C, device=dev)
         # wgrads read stored activations (no BN prologue) since the dgrad-epilogue write-back
