@@ -886,6 +886,7 @@ static int dispatch_dgrad(const IGemmArgs& a, bool accum, int epi, hipStream_t s
       return -11;
     }
     if (epi == 2) return launch_igemm_t<TM, TN, DGRAD, true, false, false, 2, true>(a, st);
+    if (epi == 0) return launch_igemm_t<TM, TN, DGRAD, true, false, false, 0, true>(a, st);
     return -11;
   }
   if (accum) {

@@ -568,6 +568,7 @@ class ResNetProgram:
         lc, lbn = b.convs[-1], b.bns[-1]
         cnt_last = N * lc.OH * lc.OW
         pend, gin = None, None  # BN-backward apply deferred into the next dgrad's prologue
+        ds_fold = None  # ... and the downsample BN's, into the downsample dgrad
         if last:
             # g = dlast * (out > 0) -> self.g_last ; tail BN reductions (and ds BN) from dlast
             K.bn_bwd_reduce(self.dlast, b.ys[-1], lbn.mean, lbn.invstd, lbn.bstats, mask_mode=K.MASK_OUT, mref=b.out)
@@ -587,6 +588,11 @@ class ResNetProgram:
                            dbn.dbeta)
             if last:
                 K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE)
+            elif self._fold(lc) and self._fold(dc, dense=True):
+                # both tail BN applies folded into the dgrads of conv3 and of the downsample conv
+                pend = dict(bwd_y=b.ys[-1], bwd_coeff=lbn.coeff, dy_out=b.dys[-1])
+                gin = g
+                ds_fold = dict(bwd_y=b.yd, bwd_coeff=dbn.coeff, dy_out=b.dyd)
             else:  # both tail BNs from one read of the block-output gradient
                 K.bn_bwd_apply2(g, b.ys[-1], lbn.coeff, b.dys[-1], b.yd, dbn.coeff, b.dyd)
         elif not last:
@@ -631,9 +637,13 @@ class ResNetProgram:
             self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
         if b.ds_conv is not None:
             dc = b.ds_conv
-            self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
-            # 1x1 strided downsample: its dgrad is a dense GEMM onto the stride-subsampled pixels
-            K.conv_dgrad(b.dyd, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0)
+            if ds_fold is None:
+                self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
+                # 1x1 strided downsample: its dgrad is a dense GEMM onto the stride-subsampled pixels
+                K.conv_dgrad(b.dyd, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0)
+            else:  # the dgrad computes (and stores) dyd from g; the wgrad follows it
+                K.conv_dgrad(g, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0, **ds_fold)
+                self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
             addsrc, sub = b.dsbuf, dc.stride
         else:
             addsrc, sub = g, 1
@@ -651,9 +661,11 @@ class ResNetProgram:
         if kw0:
             self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
 
-    def _fold(self, cv) -> bool:
-        """Fold the BN-backward apply of cv's output BN into cv's dgrad (1x1 stride-1 convs)."""
-        return self.fuse_bwd_apply and not cv.stem and K.tail_supported(cv.OC, cv.R, cv.S, cv.stride, cv.pad)
+    def _fold(self, cv, dense: bool = False) -> bool:
+        """Fold the BN-backward apply of cv's output BN into cv's dgrad (1x1 stride-1 convs;
+        ``dense``: the strided 1x1 downsample, whose dgrad runs as a dense 1x1 stride-1 GEMM)."""
+        stride = 1 if dense else cv.stride
+        return self.fuse_bwd_apply and not cv.stem and K.tail_supported(cv.OC, cv.R, cv.S, stride, cv.pad)
 
     def _bwd_stem(self):
         st, sbn = self.stem, self.stem_bn

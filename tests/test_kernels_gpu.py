@@ -618,7 +618,7 @@ def test_conv_fwd_tail_prologue(case, tile):
 
 
 @pytest.mark.parametrize("tile", [(64, 64), (128, 64), (128, 128), (256, 64), (256, 128), (128, 256)])
-@pytest.mark.parametrize("variant", ["epi2", "epi1_acc", "acc"])
+@pytest.mark.parametrize("variant", ["epi2", "epi1_acc", "acc", "plain"])
 def test_dgrad_bwd_apply_prologue(variant, tile):
     """1x1 dgrad whose operand is the BN-backward apply k1*g + k2*y + k3 computed while staging ==
     bn_bwd_apply followed by the plain dgrad (same epilogue); the applied operand is stored."""
@@ -646,8 +646,10 @@ def test_dgrad_bwd_apply_prologue(variant, tile):
         elif variant == "epi1_acc":
             e = k.BNBwdEpilogue(k.MASK_OUT, ybn, mean, inv, st1, mbits=mbits)
             k.conv_dgrad(dy_in, wt, dx, R=1, S=1, stride=1, pad=0, tile=tile, epilogue=e, addsrc=add, **kw)
-        else:
+        elif variant == "acc":
             k.conv_dgrad(dy_in, wt, dx, R=1, S=1, stride=1, pad=0, tile=tile, addsrc=add, **kw)
+        else:
+            k.conv_dgrad(dy_in, wt, dx, R=1, S=1, stride=1, pad=0, tile=tile, **kw)
         return dx, st1
 
     dy_ref = torch.empty_like(g)
@@ -658,6 +660,6 @@ def test_dgrad_bwd_apply_prologue(variant, tile):
     torch.cuda.synchronize()
     assert (dy_out.float() - dy_ref.float()).abs().max().item() <= 0.02 * dy_ref.float().abs().max().item()
     assert relerr(dx, dx_ref) < 1e-2
-    if variant != "acc":
+    if variant in ("epi2", "epi1_acc"):
         a, b = st.view(-1, 2, Cc).sum(0), st_ref.view(-1, 2, Cc).sum(0)
         assert ((a - b).abs() / (b.abs() + N * H * W * 0.01)).max().item() < 2e-2
