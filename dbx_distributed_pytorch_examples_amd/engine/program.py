@@ -144,6 +144,9 @@ class ResNetProgram:
         self.pool_reduce = os.environ.get("DBX_POOL_REDUCE", "1") == "1"
         # BN-backward apply of a 1x1 conv's output BN computed in that conv's dgrad prologue
         self.fuse_bwd_apply = os.environ.get("DBX_FUSE_BWD_APPLY", "1") == "1"
+        # ... only for large operands: folding orders the wgrad after the dgrad (no overlap), which
+        # costs more than the saved pass when the kernels are too small to fill the GPU
+        self.fold_min = int(os.environ.get("DBX_FOLD_MIN_ELEMS", str(1 << 25)))
         self._wstream = None
         self._side_pending = False
         self._build_layers()
@@ -665,7 +668,8 @@ class ResNetProgram:
         """Fold the BN-backward apply of cv's output BN into cv's dgrad (1x1 stride-1 convs;
         ``dense``: the strided 1x1 downsample, whose dgrad runs as a dense 1x1 stride-1 GEMM)."""
         stride = 1 if dense else cv.stride
-        return self.fuse_bwd_apply and not cv.stem and K.tail_supported(cv.OC, cv.R, cv.S, stride, cv.pad)
+        return (self.fuse_bwd_apply and not cv.stem and self.N * cv.OH * cv.OW * cv.OC >= self.fold_min
+                and K.tail_supported(cv.OC, cv.R, cv.S, stride, cv.pad))
 
     def _bwd_stem(self):
         st, sbn = self.stem, self.stem_bn

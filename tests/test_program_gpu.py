@@ -21,8 +21,11 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-20)).item()
 
 
-@pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 8), ("resnet18", 32, 16), ("cifar_resnet18", 32, 8)])
-def test_program_matches_autograd(arch, size, batch):
+@pytest.mark.parametrize("arch,size,batch,fold", [("resnet50", 64, 8, 0), ("resnet50", 64, 8, 1 << 40),
+                                                  ("resnet18", 32, 16, 0), ("cifar_resnet18", 32, 8, 0)])
+def test_program_matches_autograd(arch, size, batch, fold, monkeypatch):
+    # fold: DBX_FOLD_MIN_ELEMS -- 0 folds every foldable BN-backward apply into its dgrad, 2^40 none
+    monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(fold))
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
 
