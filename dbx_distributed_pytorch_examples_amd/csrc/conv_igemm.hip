@@ -856,9 +856,11 @@ using namespace dbx;
 template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI, bool TAIL = false>
 static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
   // tile shape -> wave layout: 128x128, 128x64, 64x64 on 2x2 waves (256 threads, 2 blocks/CU);
-  // 256x128 on 4x2 and 128x256 on 2x4 waves (512 threads, 1 block/CU, 96 KB LDS)
+  // 256x128 on 4x2 and 128x256 on 2x4 waves (512 threads, 1 block/CU, 96 KB LDS); 256x64 on 4x1
+  // waves (64x64 per wave like 128x128: 2/3 of the LDS bytes per MFMA of 64x32 wave tiles, for
+  // the 64-channel layers)
   constexpr int WM = (BM == 256) ? 4 : 2;
-  constexpr int WN = (BN == 256) ? 4 : 2;
+  constexpr int WN = (BN == 256) ? 4 : (BM == 256 && BN == 64) ? 1 : 2;
   const int nwg = (a.OC / BN) * ((a.M + BM - 1) / BM);
   hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI, TAIL>), dim3(nwg), dim3(64 * WM * WN), 0, st, a);
   return (int)hipGetLastError();
