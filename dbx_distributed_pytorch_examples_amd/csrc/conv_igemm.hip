@@ -62,30 +62,42 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   float* sPro = reinterpret_cast<float*>(lds + LDS_MAIN);  // [2 or 4][PRO_MAXC]: scale, shift (, rs, rh)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
-  const int ntn = a.OC / BN, ntm = (a.M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, ntn * ntm);
-  const int tm = bid / ntn, tn = bid - tm * ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int ntn = a.OC / BN, ntm = (a.M + BM - 1) / BM, ntile = ntn * ntm;
+  // Persistent tiles: workgroup b computes tiles b, b + G, b + 2G, ... (G = gridDim.x, a multiple
+  // of 8 sized by the host to the resident capacity, so tile t stays on XCD t % 8 and xcd_remap
+  // still groups A-sharing tiles per L2). The next tile's first K block is loaded while this
+  // tile's epilogue runs: short-K (1x1) convs no longer leave the CU idle during load latency.
+  // The "l" indices are the LOADER's tile (the one being staged), m0/n0/tm the epilogue's.
+  int ltm = 0, ltn = 0, lm0 = 0, ln0 = 0;
+  int lk = 0, lcb = 0, lts = 0, ltr = 0;  // next K block to load (see advance())
 
-  // ---- per-thread A rows: decompose output pixel once ------------------------------
+  // ---- per-thread A rows: decompose output pixel once per tile ---------------------
   const int ach = tid & 7;
   const bf16* abase[A_CH];   // STEM mode: image base
   int ahb[A_CH], awb[A_CH];  // top-left input coordinate of the row's receptive field
   unsigned apix[A_CH];       // byte offset of (n, ahb, awb, ach*8) in x (host: bytes < kOOB)
+  auto set_tile = [&](int t) __attribute__((always_inline)) {
+    const int bid = xcd_remap(t, ntile);
+    ltm = bid / ntn; ltn = bid - ltm * ntn;
+    lm0 = ltm * BM; ln0 = ltn * BN;
+    lk = lcb = lts = ltr = 0;
 #pragma unroll
-  for (int i = 0; i < A_CH; ++i) {
-    const int m = m0 + (tid >> 3) + RPP * i;
-    const int ohw = a.OH * a.OW;
-    int n = m / ohw;
-    const int pq = m - n * ohw;
-    const int oh = pq / a.OW, ow = pq - (pq / a.OW) * a.OW;
-    if (m >= a.M) { n = 0; }
-    abase[i] = a.x + (size_t)n * a.IH * a.IW * a.IC;
-    if (MODE == DGRAD) { ahb[i] = oh + a.dh0; awb[i] = ow + a.dw0; }
-    else { ahb[i] = oh * a.stride - a.pad; awb[i] = ow * a.stride - a.pad; }
-    apix[i] = 2u * (unsigned)(((n * a.IH + ahb[i]) * a.IW + awb[i]) * a.IC + ach * 8);
-    if (m >= a.M) ahb[i] = -(1 << 28);
-  }
+    for (int i = 0; i < A_CH; ++i) {
+      const int m = lm0 + (tid >> 3) + RPP * i;
+      const int ohw = a.OH * a.OW;
+      int n = m / ohw;
+      const int pq = m - n * ohw;
+      const int oh = pq / a.OW, ow = pq - (pq / a.OW) * a.OW;
+      if (m >= a.M) { n = 0; }
+      abase[i] = a.x + (size_t)n * a.IH * a.IW * a.IC;
+      if (MODE == DGRAD) { ahb[i] = oh + a.dh0; awb[i] = ow + a.dw0; }
+      else { ahb[i] = oh * a.stride - a.pad; awb[i] = ow * a.stride - a.pad; }
+      apix[i] = 2u * (unsigned)(((n * a.IH + ahb[i]) * a.IW + awb[i]) * a.IC + ach * 8);
+      if (m >= a.M) ahb[i] = -(1 << 28);
+    }
+  };
+  int tcur = blockIdx.x;
+  set_tile(tcur);
   const rsrc_t xr = make_rsrc(a.x, 2ull * a.N * a.IH * a.IW * a.IC);
   const int KTOT = (MODE == STEM) ? 256 : a.R * a.S * a.IC;  // weight row length
   const rsrc_t wr = make_rsrc(a.w, 2ull * a.OC * KTOT);
@@ -121,7 +133,6 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // by one per load instead of dividing kb (wave-uniform scalars). The pipeline's unconditional
   // prefetch runs two blocks past the end: those loads use an out-of-range offset for every lane,
   // so they cost an instruction issue but no memory traffic (short-K 1x1 convs: KB = 1..4)
-  int lk = 0, lcb = 0, lts = 0, ltr = 0;
   auto advance = [&]() __attribute__((always_inline)) {
     ++lk;
     if (++lcb == cpt) { lcb = 0; if (++lts == a.ns) { lts = 0; ++ltr; } }
@@ -152,7 +163,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       const int cb = lcb * BK;
       const int r = a.r0 + a.tstep * ltr, s = a.s0 + a.tstep * lts;
       if constexpr (PRO) pcb[S] = cb;
-      if constexpr (TAIL) { wlive[S] = lk < KB && tn == 0; wtoff[S] = 2u * (unsigned)cb; }
+      if constexpr (TAIL) { wlive[S] = lk < KB && ltn == 0; wtoff[S] = 2u * (unsigned)cb; }
       // tap displacement, the same for all of this thread's rows (uniform, bytes)
       const int dh = (MODE == DGRAD) ? -ltr : r, dw = (MODE == DGRAD) ? -lts : s;
       const unsigned toff = 2u * (unsigned)((dh * a.IW + dw) * a.IC + cb);
@@ -230,7 +241,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     const bool live = lk < KB;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      const int n = n0 + (tid >> 3) + RPP * i;
+      const int n = ln0 + (tid >> 3) + RPP * i;
       rb[S][i] = buf_load16(wr, live ? 2u * (unsigned)(n * KTOT + koff) : kOOB);
     }
   };
@@ -248,10 +259,6 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   };
 
   f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto mma = [&](int buf) __attribute__((always_inline)) {
     const bf16* cA = sA + buf * BM * BK;
@@ -296,12 +303,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   load_a(0);
   load_b(0);
   advance();
+  for (;;) {  // persistent tile loop (exit: every wave of the workgroup leaves after the same tile)
   load_a(1);
   load_b(1);
   advance();
   pro_a(0);
   store_ab(0, 0);
   __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   int kb = 0;
   for (; kb + 1 < KB; kb += 2) {
     step(kb, 1);
@@ -310,6 +322,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   if (kb < KB) {
     mma(kb & 1);
     __syncthreads();  // the epilogue's sC staging aliases the operand buffers
+  }
+  // this tile's indices for the epilogue; then stage the next tile's first K block (register set
+  // 0) so its loads are in flight during the epilogue
+  // (PF: plain / forward-stats epilogues; the BN-backward epilogues hold too many registers to
+  // keep a staged block alive across them, so those stage the next tile after the epilogue)
+  // Only those run persistent (PF); the rest leave the loop after one tile (the host launches
+  // one workgroup per tile for them), which compiles to the straight-line single-tile kernel.
+  constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64);  // (+: register room)
+  const int m0 = lm0, n0 = ln0, tm = ltm;
+  tcur += gridDim.x;
+  const bool more = PF && tcur < ntile;  // workgroup-uniform
+  if (more) {  // A (activations, HBM latency) now; B (weights, L2-resident) after the epilogue
+    set_tile(tcur);
+    load_a(0);
   }
 
   // ---- epilogue ------------------------------------------------------------------------
@@ -364,7 +390,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // consumed after a store is issued and no load sits under divergent control flow, so hipcc waits
   // with counted vmcnt instead of draining the queue (stores count in vmcnt too) once per row.
   constexpr int NIT = BM * CPR / NT;
-  constexpr int EGMAX = (EPI != 0 || TAIL) ? 4 : 8;  // BN epilogues hold 4-5 vectors per row: stay clear of spills
+  constexpr int EGMAX = 4;  // BN epilogues hold 4-5 vectors per row: stay clear of spills
   constexpr int EG = NIT < EGMAX ? NIT : EGMAX;
   const bool sub_geom = MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1));  // wave-uniform
   const bool tail = m0 + BM > a.M;                                                  // wave-uniform
@@ -558,6 +584,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
         atomicAdd(st2 + a.OC + n0 + tid, (double)q2);
       }
     }
+  }
+  if (!more) break;
+  load_b(0);
+  advance();
+  __syncthreads();  // the epilogue's LDS reads are done before the next tile's staging writes
   }
 }
 
@@ -861,7 +892,21 @@ static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
   // the 64-channel layers)
   constexpr int WM = (BM == 256) ? 4 : 2;
   constexpr int WN = (BN == 256) ? 4 : (BM == 256 && BN == 64) ? 1 : 2;
-  const int nwg = (a.OC / BN) * ((a.M + BM - 1) / BM);
+  const int ntile = (a.OC / BN) * ((a.M + BM - 1) / BM);
+  // persistent grid: the resident capacity (occupancy x CUs), a multiple of 8 (XCD round-robin)
+  static const int cap = [] {
+    int per_cu = 0, dev = 0, cus = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI, TAIL>),
+        64 * WM * WN, 0);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const char* e = getenv("DBX_PERSIST");
+    if ((e && e[0] == '0') || per_cu <= 0 || cus <= 0) return 1 << 30;
+    return (per_cu * cus) & ~7;
+  }();
+  constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64);  // persistent (see the kernel)
+  const int nwg = (!PF || ntile <= cap) ? ntile : cap;
   hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI, TAIL>), dim3(nwg), dim3(64 * WM * WN), 0, st, a);
   return (int)hipGetLastError();
 }

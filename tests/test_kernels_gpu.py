@@ -663,3 +663,26 @@ def test_dgrad_bwd_apply_prologue(variant, tile):
     if variant in ("epi2", "epi1_acc"):
         a, b = st.view(-1, 2, Cc).sum(0), st_ref.view(-1, 2, Cc).sum(0)
         assert ((a - b).abs() / (b.abs() + N * H * W * 0.01)).max().item() < 2e-2
+
+
+@pytest.mark.parametrize("tile", [(128, 128), (128, 256), (256, 128), (128, 64), (64, 64)])
+@pytest.mark.parametrize("R", [1, 3])
+def test_conv_fwd_persistent_many_tiles(tile, R):
+    """Far more tiles than resident workgroups (each workgroup walks several tiles, staging the
+    next tile's first block during the epilogue): output and BN statistics vs fp32 torch."""
+    k = K()
+    N, H, W, IC, OC = 24, 56, 56, 64, 256
+    torch.manual_seed(41)
+    x = torch.randn(N, H, W, IC, device=dev).bfloat16()
+    sc, sh = torch.rand(IC, device=dev) + 0.5, torch.randn(IC, device=dev) * 0.1
+    w = (torch.randn(OC, R, R, IC, device=dev) / math.sqrt(IC * R * R)).bfloat16()
+    y = torch.empty(N, H, W, OC, device=dev, dtype=torch.bfloat16)
+    st = k.new_stats(OC, dev)
+    k.conv_fwd(x, w.view(OC, -1), y, R=R, S=R, stride=1, pad=R // 2, stats=st, in_scale=sc, in_shift=sh, tile=tile)
+    act = torch.relu(x.float() * sc + sh).bfloat16().float()
+    ref = F.conv2d(nchw(act), w.float().permute(0, 3, 1, 2), padding=R // 2)
+    assert relerr(y, nhwc(ref)) < 1e-2
+    s = st.view(-1, 2, OC).sum(0)
+    yf = y.float().view(-1, OC)
+    assert ((s[0] - yf.sum(0)).abs() / (yf.abs().sum(0) + 1)).max().item() < 1e-3
+    assert ((s[1] - (yf * yf).sum(0)).abs() / ((yf * yf).sum(0) + 1)).max().item() < 1e-3
