@@ -48,6 +48,9 @@ struct IGemmArgs {
   const float* res_shift;
   bf16* tail_out;
   unsigned char* tail_bits;
+  // magic divisors (common.h mdiv) for pixel -> (n, oh, ow): ceil(2^40 / (OH*OW)), ceil(2^40 / OW);
+  // 0 = not exact for this size (plain division)
+  unsigned long long mag_ohw, mag_ow;
 };
 struct WgradArgs {
   const bf16* dy;        // [M][OC]

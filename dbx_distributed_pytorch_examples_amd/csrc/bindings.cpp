@@ -87,7 +87,14 @@ PYBIND11_MODULE(_C, m) {
                      P<const bf16*>(ybn2), P<const float*>(bsc), P<const float*>(bsh), P<const float*>(mean1),
                      P<const float*>(inv1), P<const float*>(mean2), P<const float*>(inv2), P<double*>(bstats1),
                      P<double*>(bstats2), P<bf16*>(a_out), P<const bf16*>(res), P<const float*>(res_scale),
-                     P<const float*>(res_shift), P<bf16*>(tail_out), P<unsigned char*>(tail_bits)};
+                     P<const float*>(res_shift), P<bf16*>(tail_out), P<unsigned char*>(tail_bits), 0ull, 0ull};
+    {  // magic divisors when exact: m < N*OH*OW, so m * OH*OW < 2^40 suffices
+      const unsigned long long two40 = 1ull << 40, ohw = (unsigned long long)OH * OW;
+      if (ohw > 0 && (unsigned long long)N * ohw * ohw < two40) {
+        a.mag_ohw = (two40 + ohw - 1) / ohw;
+        a.mag_ow = (two40 + OW - 1) / OW;
+      }
+    }
     check(dbx_conv_igemm(mode, bm, bn, &a, in_scale != 0, stats != 0, accum, epi, S(st)), "conv_igemm");
   });
   m.def("conv_wgrad", [](int mode, int bm, int bn, uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t in_scale,

@@ -9,6 +9,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 #define DBX_LDS __attribute__((address_space(3)))
@@ -51,6 +52,10 @@ __device__ __forceinline__ u32x4 relu_bf16x8(const u32x4 v) {
 // floor(x / d) for 0 <= x, x * d < 2^40 with mag = ceil(2^40 / d) (host: div_magic)
 __device__ __forceinline__ int mdiv(int x, unsigned long long mag) {
   return (int)(((unsigned long long)(unsigned)x * mag) >> 40);
+}
+// x / d via the magic when the host provided one (uniform branch), else a plain division
+__device__ __forceinline__ int mdiv_or(int x, unsigned long long mag, int d) {
+  return mag ? mdiv(x, mag) : x / d;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -85,9 +85,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     for (int i = 0; i < A_CH; ++i) {
       const int m = lm0 + (tid >> 3) + RPP * i;
       const int ohw = a.OH * a.OW;
-      int n = m / ohw;
+      int n = mdiv_or(m, a.mag_ohw, ohw);
       const int pq = m - n * ohw;
-      const int oh = pq / a.OW, ow = pq - (pq / a.OW) * a.OW;
+      const int oh = mdiv_or(pq, a.mag_ow, a.OW), ow = pq - oh * a.OW;
       if (m >= a.M) { n = 0; }
       abase[i] = a.x + (size_t)n * a.IH * a.IW * a.IC;
       if (MODE == DGRAD) { ahb[i] = oh + a.dh0; awb[i] = ow + a.dw0; }
@@ -380,9 +380,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 #pragma unroll
     for (int j = 0; j < 8; ++j) bs[j] = bq1[j] = bq2[j] = 0.f;
   }
+  // forward statistics in packed fp32 (v_pk_add_f32 / v_pk_fma_f32: 2 channels per instruction)
+  f32x2 ps2[4], pq2[4];
   if constexpr (STATS) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bs[j] = bq1[j] = 0.f;
+    for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = f32x2{0.f, 0.f};
   }
   // Epilogue in groups of EG rows per thread, in three straight-line phases: (1) every global load
   // of the group (residual addend, mask reference, BN inputs) — rows past M and absent addends read
@@ -411,8 +413,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       int ph = 0, pw = 0, nimg = 0;
       if (sub_geom) {
         const int ohw = a.OH * a.OW;
-        const int n = mc / ohw, pq = mc - n * ohw;
-        const int i = pq / a.OW, j = pq - (pq / a.OW) * a.OW;
+        const int n = mdiv_or(mc, a.mag_ohw, ohw), pq = mc - n * ohw;
+        const int i = mdiv_or(pq, a.mag_ow, a.OW), j = pq - i * a.OW;
         ph = i * a.osub + a.oph; pw = j * a.osub + a.opw;
         nimg = n;
         pix = ((size_t)n * a.FH + ph) * a.FW + pw;
@@ -487,16 +489,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
         }
       }
       if constexpr (STATS) {  // statistics of the stored values (ACCUM never combines with STATS)
-        float f[8];
-        unpack8(v, f);
-        if (tail && !ok[k]) {
+        const u32x4 vs = (tail && !ok[k]) ? zero4 : v;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          bs[j] += f[j];
-          bq1[j] += f[j] * f[j];
+        for (int h = 0; h < 4; ++h) {  // bf16 pair -> 2 floats: the bits shifted / masked in place
+          const f32x2 pr = {__uint_as_float(vs[h] << 16), __uint_as_float(vs[h] & 0xFFFF0000u)};
+          ps2[h] += pr;
+          pq2[h] = __builtin_elementwise_fma(pr, pr, pq2[h]);
         }
       }
       vv[k] = v;
@@ -513,6 +511,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     }
   }
   if constexpr (STATS) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      bs[2 * h] = ps2[h].x; bs[2 * h + 1] = ps2[h].y;
+      bq1[2 * h] = pq2[h].x; bq1[2 * h + 1] = pq2[h].y;
+    }
     // per-channel sum / sum of squares: in-wave lanes with the same chunk column by xor-shuffles,
     // then the waves through LDS, then one fp64 atomic pair per channel into shard tm % nshard
 #pragma unroll
