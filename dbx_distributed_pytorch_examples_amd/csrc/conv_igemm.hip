@@ -359,6 +359,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // per-thread partial sums of this thread's 8 channels: STATS: sum y, sum y^2 of the stored
   // (bf16-rounded) outputs; EPI: BN-backward raw moments
   float bs[8], bq1[8], bq2[8];
+  // accumulated in packed fp32 (v_pk_add_f32 / v_pk_fma_f32: 2 channels per instruction):
+  // ps2 = sum, pq2 = sum of squares (STATS) or sum g*y (EPI), pr2 = sum g*y2 (EPI)
+  f32x2 ps2[4], pq2[4], pr2[4];
   f32x4 e_m1[2], e_i1[2], e_m2[2], e_i2[2], e_sc[2], e_sh[2];
   const bool has2 = EPI > 0 && a.ybn2 != nullptr;  // wave-uniform: second BN (downsample branch)
   if constexpr (EPI > 0) {
@@ -378,10 +381,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       e_sh[h] = *reinterpret_cast<const f32x4*>(sh + c0 + 4 * h);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bs[j] = bq1[j] = bq2[j] = 0.f;
+    for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = pr2[h] = f32x2{0.f, 0.f};
   }
-  // forward statistics in packed fp32 (v_pk_add_f32 / v_pk_fma_f32: 2 channels per instruction)
-  f32x2 ps2[4], pq2[4];
   if constexpr (STATS) {
 #pragma unroll
     for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = f32x2{0.f, 0.f};
@@ -466,23 +467,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
             va2[k] = relu_bf16x8(pack8(t));  // the BN output itself (a.a_out write-back)
           }
           v = pack8(f);
-          unpack8(v, f);  // statistics of the values actually stored (bf16-rounded)
-          if (tail && !ok[k]) {  // rows past M contribute nothing (wave-uniform guard: last tile only)
+          // raw moments of the values actually stored (bf16-rounded): sum g, sum g*y (and g*y2);
+          // the centring/scaling by (mean, invstd) is applied once per channel after the
+          // reduction: sum g*xhat = inv * (sum g*y - mean * sum g). Rows past M contribute nothing.
+          const u32x4 vs = (tail && !ok[k]) ? zero4 : v;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = 0.f;
-          }
-          // raw moments: sum g, sum g*y (and g*y2); the centring/scaling by (mean, invstd) is
-          // applied once per channel after the reduction: sum g*xhat = inv * (sum g*y - mean * sum g)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            bs[j] += f[j];
-            bq1[j] += f[j] * yv[j];
-          }
-          if (has2) {
-            float y2[8];
-            unpack8(vy2[k], y2);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) bq2[j] += f[j] * y2[j];
+          for (int h = 0; h < 4; ++h) {
+            const f32x2 gr = {__uint_as_float(vs[h] << 16), __uint_as_float(vs[h] & 0xFFFF0000u)};
+            const f32x2 yr = {__uint_as_float(vy[k][h] << 16), __uint_as_float(vy[k][h] & 0xFFFF0000u)};
+            ps2[h] += gr;
+            pq2[h] = __builtin_elementwise_fma(gr, yr, pq2[h]);
+            if (has2) {
+              const f32x2 zr = {__uint_as_float(vy2[k][h] << 16), __uint_as_float(vy2[k][h] & 0xFFFF0000u)};
+              pr2[h] = __builtin_elementwise_fma(gr, zr, pr2[h]);
+            }
           }
         } else {
           v = pack8(f);
@@ -546,6 +544,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     }
   }
   if constexpr (EPI > 0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      bs[2 * h] = ps2[h].x; bs[2 * h + 1] = ps2[h].y;
+      bq1[2 * h] = pq2[h].x; bq1[2 * h + 1] = pq2[h].y;
+      bq2[2 * h] = pr2[h].x; bq2[2 * h + 1] = pr2[h].y;
+    }
     // reduce the per-thread partials over threads with the same chunk column: in-wave lanes
     // l, l+CPR, ... by xor-shuffles, then the 4 waves through LDS, then one atomic per channel
 #pragma unroll
