@@ -73,14 +73,14 @@ class SchedulerConfig:
 
 @dataclass
 class ZeroConfig:
-    stage: int = 0                     # 0 = plain DDP, 1 = sharded optimizer state, 2 = + sharded grads
+    stage: int = 0                     # 0 = plain DDP, 1 = sharded optimizer state, 2 = + sharded grads, 3 = + sharded params
     reduce_bucket_size: int = 500_000_000
     allgather_bucket_size: int = 500_000_000
     overlap_comm: bool = True
     contiguous_gradients: bool = True
     reduce_scatter: bool = True
-    offload_optimizer: bool = False    # accepted for config parity; documented non-goal (288 GB HBM)
-    offload_param: bool = False
+    offload_optimizer: bool = False    # fp32 master shard + moments in pinned host memory, CPU step (stage 3 path)
+    offload_param: bool = False        # + no persistent device parameter shard
 
 
 @dataclass

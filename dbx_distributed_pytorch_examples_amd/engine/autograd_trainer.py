@@ -55,12 +55,20 @@ def soft_cross_entropy(logits: torch.Tensor, target: torch.Tensor, smoothing: fl
 class AutogradTrainer:
     def __init__(self, model: nn.Module, device: torch.device, optim, label_smoothing: float = 0.0,
                  bucket_cap_mb: float = 64.0, channels_last: bool = True, zero_stage: int = 0,
-                 cutmix_alpha: float = 0.0, grad_accum: int = 1, allreduce_dtype=torch.float32):
+                 cutmix_alpha: float = 0.0, grad_accum: int = 1, allreduce_dtype=torch.float32,
+                 offload_optimizer: bool = False, offload_param: bool = False):
         self.dev = device
         self.model = model.to(device)
         if device.type == "cuda" and channels_last:
             self.model = self.model.to(memory_format=torch.channels_last)
-        self.ddp = DistributedDataParallel(self.model, bucket_cap_mb=bucket_cap_mb, allreduce_dtype=allreduce_dtype)
+        self.sharded = zero_stage == 3 or offload_optimizer or offload_param
+        if self.sharded:  # ZeRO-3: parameters, gradients and optimizer state sharded (parallel/fsdp.py)
+            from ..parallel.fsdp import ShardedDataParallel
+            self.ddp = ShardedDataParallel(self.model, optim, offload_optimizer=offload_optimizer,
+                                           offload_param=offload_param)
+            zero_stage = 0
+        else:
+            self.ddp = DistributedDataParallel(self.model, bucket_cap_mb=bucket_cap_mb, allreduce_dtype=allreduce_dtype)
         self.world = self.ddp.world
         self.o = optim
         self.smoothing = label_smoothing
@@ -69,7 +77,9 @@ class AutogradTrainer:
         self.num_classes = getattr(unwrap(model), "num_classes", None)
         self.zero = None
         params = [p for p in self.model.parameters() if p.requires_grad]
-        if zero_stage and params:
+        if self.sharded:
+            self.opt = None
+        elif zero_stage and params:
             from ..parallel.zero import ZeroShardedOptimizer
             # ZeRO over the DDP flat gradient buffer: master = flat copy of params in the same order
             self._zero_master = torch.zeros_like(self.ddp.flat.buffer)
@@ -125,6 +135,10 @@ class AutogradTrainer:
         if not last_micro:
             return
         self.ddp.finish_gradient_sync()
+        if self.sharded:
+            self.ddp.optimizer_step()
+            self.ddp.zero_grad()
+            return
         if self.o.grad_clip and self.zero is None:
             torch.nn.utils.clip_grad_norm_([p for p in self.model.parameters() if p.grad is not None], self.o.grad_clip)
         if self.zero is not None:
@@ -137,6 +151,8 @@ class AutogradTrainer:
         self.ddp.zero_grad()
 
     def read_metrics(self, reset: bool = True) -> Tuple[float, float]:
+        if self.sharded:  # epoch end (all ranks): full parameters for evaluation / rank-0 checkpoints
+            self.ddp.gather_full_params()
         loss, corr = float(self.loss_sum.item()), float(self.correct.item())
         if reset:
             self.loss_sum.zero_()

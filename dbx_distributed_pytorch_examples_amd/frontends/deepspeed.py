@@ -5,8 +5,9 @@ WarmupLR over 100 steps, gradient clipping 0.3, micro-batch 4, ZeRO-1/2/3/3-offl
 passes them (`01_cifar_deepspeed_resnet.py:108` is commented out) and never calls
 ``deepspeed.initialize``. Here ``train_func(..., deepspeed_config=zero_1)`` (or a
 ``DeepspeedTorchDistributor(deepspeedConfig=...)``) maps the dict onto the engine: bf16 compute,
-AdamW/SGD, WarmupLR, global-norm clipping, and ZeRO stage 1/2 sharded optimizer state
-(``parallel.zero``); stage 3 / offload are accepted and documented non-goals.
+AdamW/SGD, WarmupLR, global-norm clipping, ZeRO stage 1/2 sharded optimizer state
+(``parallel.zero``) and stage 3 parameter sharding with optional CPU offload of the optimizer /
+parameters (``parallel.fsdp``, autograd engine).
 """
 from __future__ import annotations
 

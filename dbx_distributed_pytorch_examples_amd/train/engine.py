@@ -201,6 +201,7 @@ class _Autograd:
         self.tr = AutogradTrainer(model, dev, cfg.optim, label_smoothing=cfg.data.label_smoothing,
                                   bucket_cap_mb=cfg.bucket_cap_mb, zero_stage=cfg.zero.stage,
                                   cutmix_alpha=cfg.data.cutmix_alpha, grad_accum=cfg.grad_accum,
+                                  offload_optimizer=cfg.zero.offload_optimizer, offload_param=cfg.zero.offload_param,
                                   allreduce_dtype=torch.bfloat16 if cfg.allreduce_dtype == "bf16" else torch.float32)
         self.loader, self.sampler = make_loader(ds, cfg.batch_size, cfg.data.shuffle, cfg.seed,
                                                 num_workers=cfg.data.num_workers if dev.type == "cuda" else 0,
@@ -246,6 +247,8 @@ def _pick_engine(cfg: TrainConfig, model, ds, dev) -> str:
     from ..models.wrappers import FrozenBackboneClassifier
     if cfg.engine in ("native", "autograd"):
         return cfg.engine
+    if cfg.zero.stage == 3 or cfg.zero.offload_optimizer or cfg.zero.offload_param:
+        return "autograd"  # parameter sharding / offload: parallel/fsdp.py on the autograd engine
     frozen = isinstance(model, FrozenBackboneClassifier) and supports(model.resnet) and \
         not any(p.requires_grad for p in model.resnet.parameters() if p is not None and
                 not any(p is q for q in model.resnet.fc.parameters()))

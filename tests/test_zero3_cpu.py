@@ -1,0 +1,169 @@
+"""ZeRO-3 (parameter sharding) and CPU offload on CPU/gloo: the sharded trainer must follow plain
+single-process training with the same optimizer step for step (`parallel/fsdp.py`; DeepSpeed
+``zero_3`` / ``zero_3_offload`` dicts of `/root/reference/02_deepspeed/deepspeed_config.py:74-105`)."""
+import pytest
+import torch
+import torch.nn as nn
+
+from dbx_distributed_pytorch_examples_amd.launch import Launcher
+
+pytestmark = pytest.mark.timeout(600)
+
+
+class Blk(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv = nn.Conv2d(c, c, 3, padding=1)
+        self.gn = nn.GroupNorm(2, c)
+
+    def forward(self, x):
+        return torch.relu(x + self.gn(self.conv(x)))
+
+
+class ResNetish(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.stem = nn.Conv2d(3, 8, 3, padding=1)
+        self.stem.bias.requires_grad_(False)           # mixed frozen / trainable root unit
+        self.layers = nn.Sequential(Blk(8), Blk(8), Blk(8))
+        self.head = nn.Linear(8, 5)
+
+    def forward(self, x):
+        return self.head(self.layers(torch.relu(self.stem(x))).mean((2, 3)))
+
+
+def _batches(steps=3, n=8):
+    g = torch.Generator().manual_seed(3)
+    return [(torch.randn(n, 3, 8, 8, generator=g), torch.randint(0, 5, (n,), generator=g)) for _ in range(steps)]
+
+
+def _optim(name):
+    from dbx_distributed_pytorch_examples_amd.config import OptimizerConfig
+    if name == "sgd":
+        return OptimizerConfig(name="sgd", lr=0.05, momentum=0.9, weight_decay=1e-3, grad_clip=0.3)
+    return OptimizerConfig(name="adamw", lr=1e-2, weight_decay=0.01, grad_clip=0.3)
+
+
+def _reference(name, steps=3):
+    torch.manual_seed(0)
+    m = ResNetish()
+    params = [p for p in m.parameters() if p.requires_grad]
+    o = _optim(name)
+    opt = torch.optim.SGD(params, lr=o.lr, momentum=o.momentum, weight_decay=o.weight_decay) if name == "sgd" \
+        else torch.optim.AdamW(params, lr=o.lr, weight_decay=o.weight_decay)
+    for x, y in _batches(steps):
+        opt.zero_grad()
+        nn.functional.cross_entropy(m(x), y).backward()
+        torch.nn.utils.clip_grad_norm_(params, o.grad_clip)
+        opt.step()
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def _zero3_run(name, offload):
+    from dbx_distributed_pytorch_examples_amd.engine.autograd_trainer import AutogradTrainer
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    ddist.init_distributed(device="cpu")
+    r, w = ddist.get_rank(), ddist.get_world_size()
+    torch.manual_seed(0)
+    model = ResNetish()
+    tr = AutogradTrainer(model, torch.device("cpu"), _optim(name), zero_stage=3, channels_last=False,
+                         offload_optimizer=offload, offload_param=offload)
+    sdp = tr.ddp
+    full = sum(p.numel() for p in model.parameters())
+    owned = sum(u.per for u in sdp._all())
+    for x, y in _batches():
+        b = x.shape[0] // w
+        tr.step(x[r * b:(r + 1) * b], y[r * b:(r + 1) * b])
+        assert sdp.materialised_bytes() == 0  # nothing stays gathered between steps
+    tr.read_metrics()  # epoch end: gathers full parameters on every rank
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    n_units = len(sdp.units)
+    ddist.destroy()
+    return sd, owned, full, n_units
+
+
+@pytest.mark.parametrize("name,offload", [("adamw", False), ("sgd", False), ("adamw", True)])
+def test_zero3_matches_single_process(name, offload):
+    sd, owned, full, n_units = Launcher(2, use_gpu=False).run(_zero3_run, name, offload)
+    assert n_units == 3                     # the three residual blocks; stem + head form the root unit
+    assert owned < full * 0.6               # each rank holds about half of the parameters
+    ref = _reference(name)
+    assert set(sd) == set(ref)
+    for k in ref:
+        assert torch.allclose(sd[k], ref[k], atol=2e-5, rtol=1e-4), (k, (sd[k] - ref[k]).abs().max())
+    assert torch.equal(sd["stem.bias"], ref["stem.bias"])  # frozen parameter untouched
+
+
+def test_zero3_single_rank_grad_accum_and_state_dict_roundtrip():
+    from dbx_distributed_pytorch_examples_amd.engine.autograd_trainer import AutogradTrainer
+    torch.manual_seed(0)
+    model = ResNetish()
+    tr = AutogradTrainer(model, torch.device("cpu"), _optim("adamw"), zero_stage=3, channels_last=False,
+                         grad_accum=2)
+    for x, y in _batches():
+        tr.step(x[:4], y[:4])
+        tr.step(x[4:], y[4:])
+    tr.read_metrics()
+    ref = _reference("adamw")
+    sd = model.state_dict()
+    for k in ref:
+        assert torch.allclose(sd[k], ref[k], atol=2e-5, rtol=1e-4), k
+    # load a checkpoint into a fresh sharded model: its shards follow the loaded values
+    torch.manual_seed(1)
+    m2 = ResNetish()
+    tr2 = AutogradTrainer(m2, torch.device("cpu"), _optim("adamw"), zero_stage=3, channels_last=False)
+    m2.load_state_dict(sd)
+    x, _ = _batches(1)[0]
+    with torch.no_grad():
+        assert torch.allclose(m2(x), model(x), atol=1e-6)
+    assert tr2.ddp.materialised_bytes() == 0 or all(u.pinned for u in tr2.ddp._all() if u.gathered)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("offload", [False, True])
+def test_zero3_gpu_torchvision_resnet18(offload):
+    """One rank on cuda:0: per-block units of a torchvision-layout ResNet-18 under bf16 autocast, HIP
+    Adam kernels on the shards (or the CPU step with offload); loss decreases on a fixed batch and no
+    unit stays materialised between steps."""
+    from dbx_distributed_pytorch_examples_amd.config import OptimizerConfig
+    from dbx_distributed_pytorch_examples_amd.engine.autograd_trainer import AutogradTrainer
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    torch.manual_seed(0)
+    dev = torch.device("cuda:0")
+    model = build_model("resnet18", num_classes=10)
+    tr = AutogradTrainer(model, dev, OptimizerConfig(name="adamw", lr=1e-3, weight_decay=0.01), zero_stage=3,
+                         offload_optimizer=offload, offload_param=offload)
+    assert len(tr.ddp.units) == 8  # the eight BasicBlocks
+    g = torch.Generator().manual_seed(0)
+    x, y = torch.randn(32, 3, 32, 32, generator=g), torch.randint(0, 10, (32,), generator=g)
+    losses = []
+    for _ in range(6):
+        tr.step(x, y)
+        torch.cuda.synchronize()
+        assert tr.ddp.materialised_bytes() == 0
+        loss, _ = tr.read_metrics()
+        losses.append(loss / 32)
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert losses[-1] < losses[0]
+
+
+def _ds_zero3_offload():
+    from dbx_distributed_pytorch_examples_amd.data.datasets import build_dataset
+    from dbx_distributed_pytorch_examples_amd.frontends import deepspeed as dsf
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    ddist.init_distributed(device="cpu")
+    tr_ds = build_dataset("synthetic", image_size=32, num_classes=10, n_synthetic=32, seed=0)
+    te_ds = build_dataset("synthetic", train=False, image_size=32, num_classes=10, n_synthetic=16, seed=0)
+    m = dsf.train_func(train_dataset=tr_ds, test_dataset=te_ds, batch_size=8, num_epochs=1,
+                       deepspeed_config=dsf.zero_3_offload, arch="resnet18", frozen_backbone=False)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    ddist.destroy()
+    return sd
+
+
+def test_deepspeed_zero3_offload_config_trains_two_ranks():
+    """The reference's ``zero_3_offload`` dict end to end through the DS-notebook ``train_func``:
+    routed to the sharded engine, both ranks finish with identical full parameters."""
+    sd = Launcher(2, use_gpu=False).run(_ds_zero3_offload)
+    assert "fc.weight" in sd and "layer4.1.conv2.weight" in sd
+    assert all(torch.isfinite(v.float()).all() for v in sd.values())
