@@ -266,3 +266,33 @@ def _divergence_check():
 def test_replica_divergence_and_bucket_order_checks():
     caught, nb = Launcher(2, use_gpu=False).run(_divergence_check)
     assert caught and nb > 1
+
+
+def _two_node_fn():
+    import torch.distributed as tdist
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    ddist.init_distributed(device="cpu")
+    t = torch.tensor([float(tdist.get_rank() + 1)])
+    tdist.all_reduce(t)
+    out = (tdist.get_rank(), tdist.get_world_size(), int(os.environ["GROUP_RANK"]), int(os.environ["LOCAL_RANK"]),
+           float(t))
+    ddist.destroy()
+    return out
+
+
+def test_two_node_rendezvous_on_one_host():
+    """Multi-node plumbing without a cluster: two launchers with nnodes=2 and
+    node_rank 0/1 rendezvous on one MASTER_ADDR:PORT and form one 4-rank gloo group."""
+    import threading
+    from dbx_distributed_pytorch_examples_amd.launch import _free_port
+    port = _free_port()
+    res = {}
+
+    def node(rank):
+        res[rank] = Launcher(2, nnodes=2, node_rank=rank, master_port=port, use_gpu=False, timeout=120).run(_two_node_fn)
+    th = threading.Thread(target=node, args=(1,))
+    th.start()
+    node(0)
+    th.join(150)
+    assert res[0] == (0, 4, 0, 0, 10.0)
+    assert res[1] == (2, 4, 1, 0, 10.0)   # node 1's local rank 0 is global rank 2
