@@ -50,7 +50,7 @@ class LocalConfig:
 
 @dataclass
 class OptimizerConfig:
-    name: str = "sgd"                  # sgd | adam | adamw
+    name: str = "sgd"                  # sgd | adam | adamw | lars
     lr: float = 0.1
     momentum: float = 0.9
     nesterov: bool = False
@@ -58,6 +58,7 @@ class OptimizerConfig:
     betas: Tuple[float, float] = (0.9, 0.999)
     eps: float = 1e-8
     grad_clip: float = 0.0
+    trust_coefficient: float = 0.001   # LARS eta
 
 
 @dataclass

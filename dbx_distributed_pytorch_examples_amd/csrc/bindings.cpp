@@ -45,6 +45,8 @@ int dbx_sgd(float*, const float*, float*, bf16*, long long, const float*, float,
 int dbx_adam(float*, const float*, float*, float*, bf16*, long long, const float*, float, float, float, float, float, int,
              float, float, const float*, float, hipStream_t);
 int dbx_sumsq(const float*, long long, double*, hipStream_t);
+int dbx_lars_scale(const float*, float*, const int*, const int*, const int*, int, int, float*, float, float, float,
+                   hipStream_t);
 int dbx_clip_factor(const double*, float, float*, hipStream_t);
 int dbx_normalize_u8(const unsigned char*, bf16*, const unsigned char*, int, int, int, int, float, float, float, float,
                      float, float, hipStream_t);
@@ -207,6 +209,12 @@ PYBIND11_MODULE(_C, m) {
     check(dbx_adam(P<float*>(p), P<const float*>(g), P<float*>(mm), P<float*>(v), P<bf16*>(p16), n,
                    P<const float*>(hyper), lr, b1, b2, eps, wd, decoupled, bc1, bc2, P<const float*>(gsp), gs, S(st)),
           "adam");
+  });
+  m.def("lars_scale", [](uintptr_t p, uintptr_t g, uintptr_t off, uintptr_t len, uintptr_t adapt, int nseg, int max_len,
+                         uintptr_t norms, float gs, float eta, float wd, uintptr_t st) {
+    check(dbx_lars_scale(P<const float*>(p), P<float*>(g), P<const int*>(off), P<const int*>(len),
+                         P<const int*>(adapt), nseg, max_len, P<float*>(norms), gs, eta, wd, S(st)),
+          "lars_scale");
   });
   m.def("sumsq", [](uintptr_t x, long long n, uintptr_t out, uintptr_t st) {
     check(dbx_sumsq(P<const float*>(x), n, P<double*>(out), S(st)), "sumsq");

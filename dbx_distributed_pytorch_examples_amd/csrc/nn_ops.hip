@@ -654,6 +654,58 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, f
   }
 }
 
+// ----------------------------------------------------------------------------------------
+// LARS (layer-wise adaptive rate scaling, large-batch SGD): per parameter tensor ("segment")
+//   trust = eta * |w| / (|g| + wd * |w|)      (1 when either norm is 0)
+//   g    <- adapt ? trust * (gs * g + wd * w) : gs * g
+// followed by the plain SGD kernel with wd = 0. grid = (chunks, nseg): blockIdx.y is the segment,
+// blocks stride over it; phase 1 reduces |w|^2 and |gs*g|^2 per segment (wave shuffles, one LDS
+// step over the 4 waves, one fp32 atomic pair per block), phase 2 rescales in place.
+// ----------------------------------------------------------------------------------------
+__global__ void lars_norms_kernel(const float* __restrict__ p, const float* __restrict__ g,
+                                  const int* __restrict__ seg_off, const int* __restrict__ seg_len, float gs,
+                                  float* __restrict__ norms) {
+  const int s = blockIdx.y;
+  const int off = seg_off[s], len = seg_len[s];
+  float ww = 0.f, gg = 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
+    const float w = p[off + i], d = g[off + i] * gs;
+    ww += w * w;
+    gg += d * d;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    ww += __shfl_xor(ww, o, 64);
+    gg += __shfl_xor(gg, o, 64);
+  }
+  __shared__ float red[2][4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    red[0][wave] = ww;
+    red[1][wave] = gg;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(norms + 2 * s, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(norms + 2 * s + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+__global__ void lars_apply_kernel(const float* __restrict__ p, float* __restrict__ g, const int* __restrict__ seg_off,
+                                  const int* __restrict__ seg_len, const int* __restrict__ adapt,
+                                  const float* __restrict__ norms, float gs, float eta, float wd) {
+  const int s = blockIdx.y;
+  const int off = seg_off[s], len = seg_len[s];
+  float scale = gs, decay = 0.f;
+  if (adapt[s]) {
+    const float wn = sqrtf(norms[2 * s]), gn = sqrtf(norms[2 * s + 1]);
+    const float trust = (wn > 0.f && gn > 0.f) ? eta * wn / (gn + wd * wn) : 1.f;
+    scale = trust * gs;
+    decay = trust * wd;
+  }
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x)
+    g[off + i] = scale * g[off + i] + decay * p[off + i];
+}
+
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, bf16* __restrict__ p16, long long n, const float* __restrict__ hyper,
                             float lr, float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
@@ -988,6 +1040,18 @@ extern "C" int dbx_adam(float* p, const float* g, float* m, float* v, bf16* p16,
                         const float* gscale_ptr, float gscale, hipStream_t st) {
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, p16, n, hyper, lr, b1, b2, eps, wd,
                      decoupled, bc1, bc2, gscale_ptr, gscale);
+  RET_LAST;
+}
+extern "C" int dbx_lars_scale(const float* p, float* g, const int* seg_off, const int* seg_len, const int* adapt,
+                              int nseg, int max_len, float* norms, float gs, float eta, float wd, hipStream_t st) {
+  if (nseg <= 0) return 0;
+  int bx = (int)((max_len + 255) / 256);
+  bx = bx < 1 ? 1 : (bx > 64 ? 64 : bx);
+  hipError_t e = hipMemsetAsync(norms, 0, sizeof(float) * 2 * nseg, st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(lars_norms_kernel, dim3(bx, nseg), dim3(256), 0, st, p, g, seg_off, seg_len, gs, norms);
+  hipLaunchKernelGGL(lars_apply_kernel, dim3(bx, nseg), dim3(256), 0, st, p, g, seg_off, seg_len, adapt, norms, gs,
+                     eta, wd);
   RET_LAST;
 }
 extern "C" int dbx_sumsq(const float* x, long long n, double* out, hipStream_t st) {

@@ -19,7 +19,42 @@ import torch.nn.functional as F
 from ..parallel.ddp import DistributedDataParallel, unwrap
 
 
+class LARS(torch.optim.Optimizer):
+    """SGD-momentum with layer-wise adaptive rate scaling (You et al., large-batch ImageNet): for every
+    tensor with ndim > 1, g <- eta*|w|/(|g| + wd*|w|) * (g + wd*w); 1-d tensors (BN, biases) take the
+    plain gradient without decay. Same math as the native ``lars_scale`` + ``sgd_step`` kernels."""
+
+    def __init__(self, params, lr, momentum=0.9, weight_decay=0.0, trust_coefficient=0.001, nesterov=False):
+        super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, eta=trust_coefficient,
+                                      nesterov=nesterov))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        for grp in self.param_groups:
+            for p in grp["params"]:
+                if p.grad is None:
+                    continue
+                d = p.grad
+                if p.ndim > 1:
+                    wn, gn = p.norm(), d.norm()
+                    trust = torch.where((wn > 0) & (gn > 0), grp["eta"] * wn / (gn + grp["weight_decay"] * wn),
+                                        torch.ones_like(wn))
+                    d = (d + grp["weight_decay"] * p) * trust
+                st = self.state[p]
+                if grp["momentum"]:
+                    buf = st.get("momentum_buffer")
+                    if buf is None:
+                        buf = st["momentum_buffer"] = d.clone()
+                    else:
+                        buf.mul_(grp["momentum"]).add_(d)
+                    d = d + grp["momentum"] * buf if grp["nesterov"] else buf
+                p.add_(d, alpha=-grp["lr"])
+
+
 def build_torch_optimizer(params, o):
+    if o.name == "lars":
+        return LARS(params, lr=o.lr, momentum=o.momentum, weight_decay=o.weight_decay,
+                    trust_coefficient=getattr(o, "trust_coefficient", 0.001), nesterov=o.nesterov)
     if o.name == "sgd":
         return torch.optim.SGD(params, lr=o.lr, momentum=o.momentum, nesterov=o.nesterov, weight_decay=o.weight_decay)
     if o.name == "adam":

@@ -44,6 +44,7 @@ class OptimConfig:
     betas: Tuple[float, float] = (0.9, 0.999)
     eps: float = 1e-8
     grad_clip: float = 0.0       # global-norm clip (DeepSpeed "gradient_clipping")
+    trust_coefficient: float = 0.001  # LARS eta (name="lars")
 
 
 class NativeTrainer:
@@ -84,6 +85,11 @@ class NativeTrainer:
                                              process_group=process_group)
             self.mom = self.zero.m  # shard-sized optimizer state only
             self.mom2 = self.zero.v
+        self.lars = None
+        if optim.name == "lars":
+            if zero_stage:
+                raise ValueError("LARS runs on the full flat buffer; use zero_stage=0")
+            self.lars = self._lars_segments()
         self._build_phases()
         # broadcast initial parameters from rank 0 (DDP constructor semantics, M2)
         if self.world > 1:
@@ -123,8 +129,27 @@ class NativeTrainer:
         phases.append(("optimizer", self._optimizer_phase, None))
         self.phases = phases
 
+    def _lars_segments(self):
+        """Per-tensor segments of the flat buffer for LARS; conv / fc weights are adapted (and decayed),
+        BN affine parameters and biases are not (the usual large-batch recipe)."""
+        rs = self.prog.param_ranges
+        dev = self.dev
+        off = torch.tensor([r[1] for r in rs], dtype=torch.int32, device=dev)
+        ln = torch.tensor([r[2] for r in rs], dtype=torch.int32, device=dev)
+        bn_names = {f"{bn.name}." for bn in self.prog.bns}
+        adapt = torch.tensor([int(r[0].endswith(".weight") and not any(r[0].startswith(b) for b in bn_names))
+                              for r in rs], dtype=torch.int32, device=dev)
+        return off, ln, adapt, torch.zeros(2 * len(rs), device=dev), max(r[2] for r in rs)
+
     def _optimizer_phase(self):
         p, o = self.prog, self.opt
+        if self.lars is not None:
+            off, ln, adapt, norms, mx = self.lars
+            K.lars_scale(p.master, p.grad, off, ln, adapt, norms, grad_scale=1.0 / self.world,
+                         eta=o.trust_coefficient, weight_decay=o.weight_decay, max_len=mx)
+            K.sgd_step(p.master, p.grad, self.mom, None, lr=o.lr, momentum=o.momentum, dampening=o.dampening,
+                       weight_decay=0.0, nesterov=o.nesterov, first=False, grad_scale=1.0, hyper=self.hyper)
+            return
         if self.zero is not None:
             # ZeRO-1/2: update this rank's shard of the flat master with its shard of the
             # optimizer state, then all-gather the master (collective: runs eagerly, not captured)
@@ -167,7 +192,7 @@ class NativeTrainer:
         o = self.opt
         self.step_count += 1
         t = self.step_count
-        if o.name == "sgd":
+        if o.name in ("sgd", "lars"):
             vals = [o.lr, 1.0, 1.0, 0.0]
         else:
             vals = [o.lr, 1.0 - o.betas[0] ** t, 1.0 - o.betas[1] ** t, 0.0]

@@ -434,3 +434,14 @@ def weight_prep(master, wbuf, desc_dev, nlayers):
 
 def cast_f32_bf16(x, y):
     y.copy_(x.bfloat16())
+
+
+def lars_scale(p, g, seg_off, seg_len, adapt, norms, *, grad_scale, eta, weight_decay, max_len):
+    for s, (o, n, a) in enumerate(zip(seg_off.tolist(), seg_len.tolist(), adapt.tolist())):
+        w, d = p[o:o + n], g[o:o + n]
+        d.mul_(grad_scale)
+        wn, gn = w.norm(), d.norm()
+        norms[2 * s], norms[2 * s + 1] = wn * wn, gn * gn
+        if a:
+            trust = float(eta * wn / (gn + weight_decay * wn)) if (wn > 0 and gn > 0) else 1.0
+            d.add_(w, alpha=weight_decay).mul_(trust)

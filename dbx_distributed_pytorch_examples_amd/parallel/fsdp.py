@@ -188,6 +188,8 @@ class ShardedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, optim, process_group=None, units: Optional[List[nn.Module]] = None,
                  offload_optimizer: bool = False, offload_param: bool = False, reshard_after_forward: bool = True):
         super().__init__()
+        if optim.name not in ("sgd", "adam", "adamw"):
+            raise ValueError(f"ZeRO-3 supports sgd / adam / adamw, not {optim.name!r}")
         self.module = module
         self.o = optim
         self.pg = process_group

@@ -53,6 +53,8 @@ class ZeroShardedOptimizer:
                  grad_scale: Optional[float] = None):
         if stage not in (1, 2, 3):
             raise ValueError("ZeRO stage must be 1, 2 or 3")
+        if optim.name not in ("sgd", "adam", "adamw"):
+            raise ValueError(f"sharded optimizer supports sgd / adam / adamw, not {optim.name!r}")
         if stage == 3:
             warnings.warn("flat-buffer ZeRO: stage 3 runs as stage 2 here; parameter sharding is parallel.fsdp.ShardedDataParallel")
             stage = 2

@@ -132,7 +132,8 @@ class _Native:
         else:
             self.tr = NativeTrainer(model, cfg.batch_size, (s, s), dev,
                                     optim=OptimConfig(o.name, o.lr, o.momentum, 0.0, o.nesterov, o.weight_decay,
-                                                      tuple(o.betas), o.eps, o.grad_clip),
+                                                      tuple(o.betas), o.eps, o.grad_clip,
+                                                      trust_coefficient=o.trust_coefficient),
                                     label_smoothing=cfg.data.label_smoothing, use_graphs=cfg.graphs,
                                     bucket_cap_mb=cfg.bucket_cap_mb, allreduce_dtype=ar,
                                     src_hw=(h, w), mean=mean, std=std, zero_stage=cfg.zero.stage)
