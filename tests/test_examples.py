@@ -35,3 +35,15 @@ def test_native_example_cli_prints_config():
                         os.path.join(ROOT, "configs", "resnet50_imagenet_8192.yaml"), "--print-config"],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and '"batch_size": 1024' in r.stdout
+
+
+@pytest.mark.timeout(600)
+def test_deepspeed_example_zero3_offload_cpu(tmp_path):
+    """The DS CIFAR example with the reference's ``zero_3_offload`` dict (frozen backbone: the
+    sharded blocks are gathered for forward only; the trainable head sits in the root unit)."""
+    env = dict(os.environ, DBX_MLRUNS=str(tmp_path / "mlruns"), PYTHONWARNINGS="ignore")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "02_deepspeed", "01_cifar_deepspeed.py"),
+                        "--cpu", "--samples", "32", "--batch-size", "8", "--out", str(tmp_path), "--zero", "3-offload"],
+                       env=env, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "engine=autograd" in r.stdout + r.stderr
