@@ -313,6 +313,7 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
             model.load_state_dict(st["model"])
             _restore_trainer_state(runner, st.get("trainer"))
             start_epoch, step = int(st.get("epoch", 0)), int(st.get("step", 0))
+            _restore_shard_state(runner, cfg.checkpoint_dir, start_epoch)
             res.history = list(st.get("history", []))
             _log(f"[train] resumed from {path} (epoch {start_epoch}, step {step})")
     elif cfg.resume and cfg.resume != "latest":
@@ -364,6 +365,8 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
                 mlflow.log_metrics({k: v for k, v in rec.items() if k != "epoch"}, step=epoch + 1)
         for cb in callbacks or []:
             cb(epoch + 1, rec, runner)
+        if cfg.checkpoint_dir and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
+            _save_shard_state(runner, cfg.checkpoint_dir, epoch + 1)  # every rank: its ZeRO shard
         if cfg.checkpoint_dir and is_main and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
             ckpt.save_checkpoint(cfg.checkpoint_dir, runner.model, None, epoch + 1, step=step,
                                  trainer=_trainer_state(runner), history=res.history, config=json.dumps(to_dict(cfg)))
@@ -405,6 +408,41 @@ def _trainer_state(runner) -> Dict[str, Any]:
     if getattr(tr, "opt", None) is not None:
         return {"kind": "torch", "optimizer": ckpt.clean_state_dict(tr.opt.state_dict())}
     return {}
+
+
+def _shard_path(d: str, epoch: int) -> str:
+    return os.path.join(d, f"zero_shard-{epoch}-rank{ddist.get_rank()}-of{ddist.get_world_size()}.pt")
+
+
+def _sharded(runner):
+    """(save, load) of this rank's sharded optimizer state (ZeRO-1/2 or ZeRO-3), if any."""
+    tr = runner.tr
+    if getattr(tr, "sharded", False):
+        return tr.ddp.optim_state_dict, tr.ddp.load_optim_state_dict
+    z = getattr(tr, "zero", None)
+    if z is not None:
+        return z.state_dict, z.load_state_dict
+    return None
+
+
+def _save_shard_state(runner, d: str, epoch: int) -> None:
+    sh = _sharded(runner)
+    if sh is None:
+        return
+    os.makedirs(d, exist_ok=True)
+    torch.save(sh[0](), _shard_path(d, epoch))
+
+
+def _restore_shard_state(runner, d: str, epoch: int) -> None:
+    """Each rank reloads its own optimizer shard (the rank-0 checkpoint holds only rank 0's)."""
+    sh = _sharded(runner)
+    if sh is None:
+        return
+    p = _shard_path(d, epoch)
+    if not os.path.exists(p):
+        _log(f"[train] warning: no optimizer shard {p}; sharded optimizer state starts fresh")
+        return
+    sh[1](torch.load(p, map_location="cpu", weights_only=True))
 
 
 def _restore_trainer_state(runner, st):
