@@ -56,7 +56,7 @@ def parse_args(argv=None):
     p.add_argument("--num-classes", type=int, default=1000)
     p.add_argument("--channels-last", type=int, default=1, help="torch impl only")
     p.add_argument("--lr", type=float, default=None, help="default: 0.1 (sgd) / 2e-4 (adamw)")
-    p.add_argument("--optim", default="sgd", choices=["sgd", "adamw"])
+    p.add_argument("--optim", default="sgd", choices=["sgd", "adamw", "lars"])
     p.add_argument("--zero", type=int, default=0, choices=[0, 1, 2], help="native impl: ZeRO stage")
     p.add_argument("--preset", default="", choices=[""] + sorted(PRESETS),
                    help="one of BASELINE.json's other configs (sets model/size/classes/batch/optim)")
@@ -65,7 +65,7 @@ def parse_args(argv=None):
     for k, v in PRESETS.get(a.preset, {}).items():
         setattr(a, k, v)
     if a.lr is None:
-        a.lr = 0.1 if a.optim == "sgd" else 2e-4
+        a.lr = {"sgd": 0.1, "lars": 9.0}.get(a.optim, 2e-4)
     return a
 
 
@@ -120,8 +120,9 @@ def main(argv=None) -> int:
             "seq_len": None,
             "parallelism": f"dp{n}",
             "impl": args.impl,
-            "optimizer": ("SGD momentum 0.9 nesterov=False wd 5e-5" if args.optim == "sgd"
-                          else "AdamW wd 0.01") + (f", ZeRO-{args.zero}" if args.zero else ""),
+            "optimizer": {"sgd": "SGD momentum 0.9 nesterov=False wd 5e-5",
+                          "lars": "LARS (eta 1e-3) + SGD momentum 0.9 wd 5e-5"}.get(args.optim, "AdamW wd 0.01")
+                         + (f", ZeRO-{args.zero}" if args.zero else ""),
             **meta,
         },
     }

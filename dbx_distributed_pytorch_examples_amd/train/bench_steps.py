@@ -29,6 +29,9 @@ def build_torch_step(args, info) -> Tuple[Callable[[], None], Dict]:
                                                           bucket_cap_mb=25, gradient_as_bucket_view=True)
     if getattr(args, "optim", "sgd") == "adamw":
         opt = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=0.01)
+    elif getattr(args, "optim", "sgd") == "lars":
+        from ..engine.autograd_trainer import LARS
+        opt = LARS(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5, trust_coefficient=0.001)
     else:
         opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5)
     x8, y = synthetic_uint8_batch(args.batch, args.image_size, args.num_classes, dev, seed=info.rank)

@@ -15,6 +15,8 @@ def build_native_step(args, info):
     model = build_model(args.model, num_classes=args.num_classes)
     if getattr(args, "optim", "sgd") == "adamw":
         opt = OptimConfig(name="adamw", lr=args.lr, weight_decay=0.01)
+    elif getattr(args, "optim", "sgd") == "lars":
+        opt = OptimConfig(name="lars", lr=args.lr, momentum=0.9, weight_decay=5e-5, trust_coefficient=0.001)
     else:
         opt = OptimConfig(name="sgd", lr=args.lr, momentum=0.9, weight_decay=5e-5)
     use_graphs = os.environ.get("DBX_GRAPHS", "1") == "1"
