@@ -152,3 +152,36 @@ def test_frozen_backbone_native_gpu():
     assert not torch.equal(w0, m.resnet.fc[1].weight.detach())
     loss, _ = tr.read_metrics()
     assert math.isfinite(loss) and loss > 0
+
+
+# SURVEY.md §7.4 "50-step loss-decrease smoke per BASELINE config": each BASELINE.json config's
+# architecture / resolution / optimizer family, at a small per-GPU batch, trained 50 steps on one
+# fixed synthetic batch through the graph-captured native step. A correct forward/backward/optimizer
+# memorises the batch; a broken kernel anywhere in the chain stalls or diverges.
+@pytest.mark.parametrize("arch,size,classes,batch,optim,clip,zero", [
+    ("resnet50", 224, 1000, 16, "sgd", 0.0, 0),       # headline ImageNet-1K large-batch (SGD)
+    ("resnet50", 224, 1000, 16, "lars", 0.0, 0),      # large-batch LARS variant
+    ("resnet50", 224, 1000, 16, "adamw", 0.3, 1),     # DeepSpeed ImageNet config: AdamW, clip 0.3, ZeRO-1
+    ("resnet18", 32, 10, 64, "adam", 0.0, 0),         # CIFAR-10 TorchDistributor (Adam 1e-3)
+    ("resnet50", 64, 200, 32, "adam", 0.0, 0),        # TinyImageNet TorchDistributor (Adam 1e-3)
+])
+def test_baseline_config_loss_decreases(arch, size, classes, batch, optim, clip, zero):
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+
+    torch.manual_seed(0)
+    model = build_model(arch, num_classes=classes)
+    lr = {"sgd": 0.05, "lars": 9.0, "adamw": 2e-4, "adam": 1e-3}[optim]
+    oc = OptimConfig(name=optim, lr=lr, grad_clip=clip, weight_decay=0.0 if optim != "lars" else 5e-5)
+    tr = NativeTrainer(model, batch, (size, size), dev, optim=oc, use_graphs=True, zero_stage=zero)
+    g = torch.Generator().manual_seed(3)
+    img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).to(dev)
+    lab = torch.randint(0, classes, (batch,), generator=g).to(dev)
+    losses = []
+    for _ in range(50):
+        tr.step(img, lab)
+        losses.append(tr.read_metrics()[0] / batch)
+    print(f"[loss50] {arch} {size} {optim}: " + " ".join(f"{v:.3f}" for v in losses[::7]))
+    assert all(math.isfinite(v) for v in losses), losses
+    first, last = sum(losses[:3]) / 3, sum(losses[-3:]) / 3
+    assert last < 0.5 * first, (arch, optim, losses[:3], losses[-3:])
