@@ -75,8 +75,13 @@ class NativeTrainer:
         self.graphs: List[Optional[torch.cuda.CUDAGraph]] = []
         self.bucket_cap = int(bucket_cap_mb * (1 << 20) // 4)
         self.ar_dtype = allreduce_dtype
+        # segmented = per-segment graphs + side-stream bucket all-reduces. Always on for world > 1;
+        # DBX_SEGMENTED_GRAPHS=1 forces it at world 1 (with an initialised process group) so the
+        # RCCL + capture interplay can be rehearsed on a one-GPU box.
+        self.segmented = self.world > 1 or (os.environ.get("DBX_SEGMENTED_GRAPHS", "0") == "1"
+                                            and dist.is_available() and dist.is_initialized())
         self.comm_stream = (torch.cuda.Stream(device=device, priority=-1)
-                            if self.world > 1 and device.type == "cuda" else None)
+                            if self.segmented and device.type == "cuda" else None)
         self.flip = None
         self.zero = None
         if zero_stage:
@@ -126,8 +131,38 @@ class NativeTrainer:
         phases.append(("fwd+" + first_name, lambda: (fwd_phase(), first_fn()), self.seg_ranges[0]))
         for (name, fn), rg in zip(segs[1:], self.seg_ranges[1:]):
             phases.append((name, fn, rg))
+        if self.segmented:
+            phases = self._merge_phases(phases)
         phases.append(("optimizer", self._optimizer_phase, None))
         self.phases = phases
+
+    def _merge_phases(self, phases):
+        """Optional coarser graph segmentation of the multi-rank path: DBX_SEG_GROUPS="3,3" merges
+        the six backward segments into two graphs (one all-reduce cut after layer3). Default: one
+        graph per backward segment. Measured over RCCL on one MI355X (world-1 process group with
+        DBX_SEGMENTED_GRAPHS=1, ResNet-50 b1024): 6 segments 13.89k img/s, 2 segments 13.85k,
+        single graph 14.33k (profiles/r1s4_revalidate/rccl_rehearsal.txt) -- boundaries are not
+        what the segmented path costs, so the finer split (more overlap, smallest exposed tail)
+        stays. Groups merge only when their gradient ranges are adjacent."""
+        spec = os.environ.get("DBX_SEG_GROUPS", "")
+        if not spec:
+            return phases
+        sizes = [int(x) for x in spec.split(",") if x.strip()]
+        sizes = [x for x in sizes if x > 0]
+        if sum(sizes) != len(phases):
+            raise ValueError(f"DBX_SEG_GROUPS={spec!r} does not cover {len(phases)} backward segments")
+        merged, pos = [], 0
+        for sz in sizes:
+            grp = phases[pos:pos + sz]
+            pos += sz
+            rgs = sorted(rg for _, _, rg in grp if rg is not None)
+            if any(a[1] != b[0] for a, b in zip(rgs, rgs[1:])):
+                return phases  # non-adjacent gradient ranges: keep one segment per phase
+            fns = [fn for _, fn, _ in grp]
+            merged.append(("+".join(nm for nm, _, _ in grp),
+                           (lambda fns=fns: [f() for f in fns]),
+                           (rgs[0][0], rgs[-1][1]) if rgs else None))
+        return merged
 
     def _lars_segments(self):
         """Per-tensor segments of the flat buffer for LARS; conv / fc weights are adapted (and decayed),
@@ -206,19 +241,19 @@ class NativeTrainer:
         if self.dev.type != "cuda":  # CPU (reference ops; gloo all-reduce, synchronous)
             for name, fn, rg in self.phases:
                 fn()
-                if rg is not None and self.world > 1:
+                if rg is not None and self.segmented:
                     self._allreduce_range(*rg)
             return
         cur = torch.cuda.current_stream(self.dev)
         for name, fn, rg in self.phases:
-            if name == "optimizer" and self.world > 1:
+            if name == "optimizer" and self.segmented:
                 cur.wait_stream(self.comm_stream)
             if self.phase_timer is not None:
                 with self.phase_timer.phase(name):
                     fn()
             else:
                 fn()
-            if rg is not None and self.world > 1:
+            if rg is not None and self.segmented:
                 self.comm_stream.wait_stream(cur)
                 with torch.cuda.stream(self.comm_stream):
                     self._allreduce_range(*rg)
@@ -228,23 +263,26 @@ class NativeTrainer:
         return [ph for ph in self.phases if not (ph[0] == "optimizer" and self.zero is not None and self.world > 1)]
 
     def _capture(self):
-        """Capture each phase (or the whole step when world == 1) into HIP graphs."""
+        """Capture each phase (or the whole step when not segmented) into HIP graphs."""
         torch.cuda.synchronize(self.dev)
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         pool = torch.cuda.graph_pool_handle()
         self.graphs = []
         with torch.cuda.stream(s):
-            if self.world == 1:
+            if not self.segmented:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool, stream=s):
                     for _, fn, _ in self.phases:
                         fn()
                 self.graphs = [g]
             else:
+                # thread-local capture: the process group's watchdog thread keeps polling the
+                # completion events of earlier collectives while we capture; under the default
+                # global mode such a query from another thread invalidates the capture
                 for _, fn, _ in self._graph_phases():
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=pool, stream=s):
+                    with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode="thread_local"):
                         fn()
                     self.graphs.append(g)
         torch.cuda.current_stream(self.dev).wait_stream(s)
@@ -252,7 +290,7 @@ class NativeTrainer:
 
     def _replay(self):
         cur = torch.cuda.current_stream(self.dev)
-        if self.world == 1:
+        if not self.segmented:
             self.graphs[0].replay()
             return
         for (name, _, rg), g in zip(self._graph_phases(), self.graphs):

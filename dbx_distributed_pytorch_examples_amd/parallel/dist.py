@@ -74,7 +74,10 @@ def init_distributed(backend: Optional[str] = None, device: Optional[str] = None
         # DBX_DIST_BACKEND=gloo lets several ranks share one GPU (RCCL refuses duplicate devices),
         # which is how the multi-rank GPU path is exercised on a single-GPU box
         backend = os.environ.get("DBX_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
-    if world > 1:
+    # DBX_FORCE_PG=1 (under a launcher) creates the process group even at world 1: a one-GPU box
+    # can then rehearse the RCCL code path (tools/gpu_rccl_rehearsal.sh)
+    force_pg = os.environ.get("DBX_FORCE_PG", "0") == "1" and "MASTER_PORT" in os.environ
+    if world > 1 or force_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         if not dist.is_initialized():

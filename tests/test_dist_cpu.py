@@ -154,8 +154,11 @@ def _native_dist():
     return out
 
 
-def test_native_program_bucket_allreduce():
-    """world-2 native step (CPU reference ops): grads are summed over ranks in every segment bucket."""
+@pytest.mark.parametrize("seg_groups", ["", "3,3", "2,4"])
+def test_native_program_bucket_allreduce(seg_groups, monkeypatch):
+    """world-2 native step (CPU reference ops): grads are summed over ranks in every segment bucket,
+    with one all-reduce cut per backward segment (default) or merged segments (DBX_SEG_GROUPS)."""
+    monkeypatch.setenv("DBX_SEG_GROUPS", seg_groups)
     g2, m2 = Launcher(2, use_gpu=False).run(_native_dist)
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
