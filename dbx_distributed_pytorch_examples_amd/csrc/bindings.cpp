@@ -45,7 +45,7 @@ int dbx_sgd(float*, const float*, float*, bf16*, long long, const float*, float,
 int dbx_adam(float*, const float*, float*, float*, bf16*, long long, const float*, float, float, float, float, float, int,
              float, float, const float*, float, hipStream_t);
 int dbx_sumsq(const float*, long long, double*, hipStream_t);
-int dbx_lars_scale(const float*, float*, const int*, const int*, const int*, int, int, float*, float, float, float,
+int dbx_lars_scale(const float*, float*, const int*, const int*, const int*, int, int, double*, float, float, float,
                    hipStream_t);
 int dbx_clip_factor(const double*, float, float*, hipStream_t);
 int dbx_normalize_u8(const unsigned char*, bf16*, const unsigned char*, int, int, int, int, float, float, float, float,
@@ -213,7 +213,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lars_scale", [](uintptr_t p, uintptr_t g, uintptr_t off, uintptr_t len, uintptr_t adapt, int nseg, int max_len,
                          uintptr_t norms, float gs, float eta, float wd, uintptr_t st) {
     check(dbx_lars_scale(P<const float*>(p), P<float*>(g), P<const int*>(off), P<const int*>(len),
-                         P<const int*>(adapt), nseg, max_len, P<float*>(norms), gs, eta, wd, S(st)),
+                         P<const int*>(adapt), nseg, max_len, P<double*>(norms), gs, eta, wd, S(st)),
           "lars_scale");
   });
   m.def("sumsq", [](uintptr_t x, long long n, uintptr_t out, uintptr_t st) {

@@ -660,11 +660,12 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, f
 //   g    <- adapt ? trust * (gs * g + wd * w) : gs * g
 // followed by the plain SGD kernel with wd = 0. grid = (chunks, nseg): blockIdx.y is the segment,
 // blocks stride over it; phase 1 reduces |w|^2 and |gs*g|^2 per segment (wave shuffles, one LDS
-// step over the 4 waves, one fp32 atomic pair per block), phase 2 rescales in place.
+// step over the 4 waves, one fp64 atomic pair per block: fp64 sums of fp32 partials are exact
+// for any block order here, so the trust ratios are bit-reproducible), phase 2 rescales in place.
 // ----------------------------------------------------------------------------------------
 __global__ void lars_norms_kernel(const float* __restrict__ p, const float* __restrict__ g,
                                   const int* __restrict__ seg_off, const int* __restrict__ seg_len, float gs,
-                                  float* __restrict__ norms) {
+                                  double* __restrict__ norms) {
   const int s = blockIdx.y;
   const int off = seg_off[s], len = seg_len[s];
   float ww = 0.f, gg = 0.f;
@@ -685,19 +686,19 @@ __global__ void lars_norms_kernel(const float* __restrict__ p, const float* __re
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(norms + 2 * s, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    atomicAdd(norms + 2 * s + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    atomicAdd(norms + 2 * s, (double)(red[0][0] + red[0][1] + red[0][2] + red[0][3]));
+    atomicAdd(norms + 2 * s + 1, (double)(red[1][0] + red[1][1] + red[1][2] + red[1][3]));
   }
 }
 
 __global__ void lars_apply_kernel(const float* __restrict__ p, float* __restrict__ g, const int* __restrict__ seg_off,
                                   const int* __restrict__ seg_len, const int* __restrict__ adapt,
-                                  const float* __restrict__ norms, float gs, float eta, float wd) {
+                                  const double* __restrict__ norms, float gs, float eta, float wd) {
   const int s = blockIdx.y;
   const int off = seg_off[s], len = seg_len[s];
   float scale = gs, decay = 0.f;
   if (adapt[s]) {
-    const float wn = sqrtf(norms[2 * s]), gn = sqrtf(norms[2 * s + 1]);
+    const float wn = (float)sqrt(norms[2 * s]), gn = (float)sqrt(norms[2 * s + 1]);
     const float trust = (wn > 0.f && gn > 0.f) ? eta * wn / (gn + wd * wn) : 1.f;
     scale = trust * gs;
     decay = trust * wd;
@@ -1043,11 +1044,11 @@ extern "C" int dbx_adam(float* p, const float* g, float* m, float* v, bf16* p16,
   RET_LAST;
 }
 extern "C" int dbx_lars_scale(const float* p, float* g, const int* seg_off, const int* seg_len, const int* adapt,
-                              int nseg, int max_len, float* norms, float gs, float eta, float wd, hipStream_t st) {
+                              int nseg, int max_len, double* norms, float gs, float eta, float wd, hipStream_t st) {
   if (nseg <= 0) return 0;
   int bx = (int)((max_len + 255) / 256);
   bx = bx < 1 ? 1 : (bx > 64 ? 64 : bx);
-  hipError_t e = hipMemsetAsync(norms, 0, sizeof(float) * 2 * nseg, st);
+  hipError_t e = hipMemsetAsync(norms, 0, sizeof(double) * 2 * nseg, st);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(lars_norms_kernel, dim3(bx, nseg), dim3(256), 0, st, p, g, seg_off, seg_len, gs, norms);
   hipLaunchKernelGGL(lars_apply_kernel, dim3(bx, nseg), dim3(256), 0, st, p, g, seg_off, seg_len, adapt, norms, gs,

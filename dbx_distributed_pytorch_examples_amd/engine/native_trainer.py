@@ -174,27 +174,34 @@ class NativeTrainer:
         bn_names = {f"{bn.name}." for bn in self.prog.bns}
         adapt = torch.tensor([int(r[0].endswith(".weight") and not any(r[0].startswith(b) for b in bn_names))
                               for r in rs], dtype=torch.int32, device=dev)
-        return off, ln, adapt, torch.zeros(2 * len(rs), device=dev), max(r[2] for r in rs)
+        return off, ln, adapt, torch.zeros(2 * len(rs), device=dev, dtype=torch.float64), max(r[2] for r in rs)
 
     def _optimizer_phase(self):
         p, o = self.prog, self.opt
-        if self.lars is not None:
-            off, ln, adapt, norms, mx = self.lars
-            K.lars_scale(p.master, p.grad, off, ln, adapt, norms, grad_scale=1.0 / self.world,
-                         eta=o.trust_coefficient, weight_decay=o.weight_decay, max_len=mx)
-            K.sgd_step(p.master, p.grad, self.mom, None, lr=o.lr, momentum=o.momentum, dampening=o.dampening,
-                       weight_decay=0.0, nesterov=o.nesterov, first=False, grad_scale=1.0, hyper=self.hyper)
-            return
         if self.zero is not None:
             # ZeRO-1/2: update this rank's shard of the flat master with its shard of the
-            # optimizer state, then all-gather the master (collective: runs eagerly, not captured)
-            self.zero.step(grads_already_reduced=(self.zero.stage == 1 or self.world == 1), lr=o.lr)
+            # optimizer state, then all-gather the master (collective: runs eagerly, not captured
+            # at world > 1). lr / bias corrections come from the device-side hyper tensor so a
+            # captured world-1 step follows set_lr() and the step count on every replay.
+            self.zero.step(grads_already_reduced=(self.zero.stage == 1 or self.world == 1), lr=o.lr,
+                           hyper=self.hyper)
             return
         gsp = None
         if o.grad_clip and o.grad_clip > 0:
             # clip on the averaged gradient: factor computed on device (no host sync)
             K.global_norm_clip_factor(p.grad, o.grad_clip * self.world, self.clip_work)
             gsp = self.clip_work[2:3]
+        if self.lars is not None:
+            # the clip factor scales the gradient before the trust ratios, as torch's
+            # clip_grad_norm_ + LARS does on the autograd engine
+            if gsp is not None:
+                p.grad.mul_(gsp)
+            off, ln, adapt, norms, mx = self.lars
+            K.lars_scale(p.master, p.grad, off, ln, adapt, norms, grad_scale=1.0 / self.world,
+                         eta=o.trust_coefficient, weight_decay=o.weight_decay, max_len=mx)
+            K.sgd_step(p.master, p.grad, self.mom, None, lr=o.lr, momentum=o.momentum, dampening=o.dampening,
+                       weight_decay=0.0, nesterov=o.nesterov, first=False, grad_scale=1.0, hyper=self.hyper)
+            return
         gscale = 1.0 / self.world
         if o.name == "sgd":
             K.sgd_step(p.master, p.grad, self.mom, None, lr=o.lr, momentum=o.momentum, dampening=o.dampening,
@@ -269,20 +276,21 @@ class NativeTrainer:
         s.wait_stream(torch.cuda.current_stream(self.dev))
         pool = torch.cuda.graph_pool_handle()
         self.graphs = []
+        # thread-local capture whenever a process group exists: its watchdog thread polls the
+        # completion events of earlier collectives while we capture, and under the default
+        # global mode such a query from another thread invalidates the capture
+        mode = "thread_local" if (dist.is_available() and dist.is_initialized()) else "global"
         with torch.cuda.stream(s):
             if not self.segmented:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool, stream=s):
+                with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode=mode):
                     for _, fn, _ in self.phases:
                         fn()
                 self.graphs = [g]
             else:
-                # thread-local capture: the process group's watchdog thread keeps polling the
-                # completion events of earlier collectives while we capture; under the default
-                # global mode such a query from another thread invalidates the capture
                 for _, fn, _ in self._graph_phases():
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode="thread_local"):
+                    with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode=mode):
                         fn()
                     self.graphs.append(g)
         torch.cuda.current_stream(self.dev).wait_stream(s)
@@ -322,6 +330,13 @@ class NativeTrainer:
         if flips is not None:
             p.flip.copy_(flips, non_blocking=True)
         self._set_hyper()
+        self._step_inner()
+        if self.zero is not None:
+            # a replayed graph does not run zero.step() in Python: keep its counter (saved in
+            # ZeRO checkpoints) on the trainer's
+            self.zero.step_count = self.step_count
+
+    def _step_inner(self):
         if not self.use_graphs:
             self._run_phases_eager()
             return

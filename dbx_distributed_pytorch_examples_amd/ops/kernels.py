@@ -555,14 +555,14 @@ def sgd_step(p, g, v, p16=None, *, lr, momentum, dampening=0.0, weight_decay=0.0
 def lars_scale(p, g, seg_off, seg_len, adapt, norms, *, grad_scale, eta, weight_decay, max_len):
     """LARS pre-scaling of the flat gradient in place (then ``sgd_step`` with wd=0): per segment
     trust = eta*|w|/(|gs*g| + wd*|w|); adapted segments get g = trust*(gs*g + wd*w), the others gs*g.
-    ``seg_off`` / ``seg_len`` / ``adapt``: int32 device tensors [nseg]; ``norms``: fp32 [2*nseg] scratch."""
+    ``seg_off`` / ``seg_len`` / ``adapt``: int32 device tensors [nseg]; ``norms``: fp64 [2*nseg] scratch."""
     n = p.numel()
     _chk(p, torch.float32, "p")
     _chk(g, torch.float32, "g", n)
     nseg = seg_off.numel()
     for t, nm in ((seg_off, "seg_off"), (seg_len, "seg_len"), (adapt, "adapt")):
         _chk(t, torch.int32, nm, nseg)
-    _chk(norms, torch.float32, "norms", 2 * nseg)
+    _chk(norms, torch.float64, "norms", 2 * nseg)
     C().lars_scale(p.data_ptr(), g.data_ptr(), seg_off.data_ptr(), seg_len.data_ptr(), adapt.data_ptr(), nseg,
                    int(max_len), norms.data_ptr(), float(grad_scale), float(eta), float(weight_decay), stream_ptr())
 

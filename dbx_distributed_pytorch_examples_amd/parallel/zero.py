@@ -89,7 +89,11 @@ class ZeroShardedOptimizer:
         return out
 
     @torch.no_grad()
-    def step(self, grads_already_reduced: bool = True, lr: Optional[float] = None):
+    def step(self, grads_already_reduced: bool = True, lr: Optional[float] = None,
+             hyper: Optional[torch.Tensor] = None):
+        """``hyper``: optional fp32 device tensor (lr, 1-b1^t, 1-b2^t) read by the kernels at run
+        time. The native trainer passes its own so a graph-captured step follows LR schedules and
+        Adam bias correction on every replay (host scalars would be frozen at capture)."""
         o = self.o
         self.step_count += 1
         n_own = self.hi - self.lo
@@ -126,11 +130,11 @@ class ZeroShardedOptimizer:
         if o.name == "sgd":
             K.sgd_step(p, g, self.m, None, lr=lr, momentum=o.momentum, dampening=getattr(o, "dampening", 0.0),
                        weight_decay=o.weight_decay, nesterov=o.nesterov, first=False, grad_scale_ptr=gsp,
-                       grad_scale=self.grad_scale)
+                       grad_scale=self.grad_scale, hyper=hyper)
         else:
             K.adam_step(p, g, self.m, self.v, None, lr=lr, beta1=o.betas[0], beta2=o.betas[1], eps=o.eps,
                         weight_decay=o.weight_decay, decoupled=(o.name == "adamw"), step=self.step_count,
-                        grad_scale_ptr=gsp, grad_scale=self.grad_scale)
+                        grad_scale_ptr=gsp, grad_scale=self.grad_scale, hyper=hyper)
         if self.world == 1:
             self.master[self.lo:self.hi].copy_(p[:n_own])
             return

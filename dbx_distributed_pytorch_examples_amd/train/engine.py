@@ -167,6 +167,10 @@ class _Native:
         img, lab, boxes, flips = batch
         self.tr.step(img, lab, boxes, flips)
 
+    @staticmethod
+    def batch_samples(batch) -> int:
+        return int(batch[1].shape[0])
+
     def set_lr(self, lr):
         self.tr.set_lr(lr)
 
@@ -221,6 +225,10 @@ class _Autograd:
 
     def step(self, batch):
         self.tr.step(*batch)
+
+    @staticmethod
+    def batch_samples(batch) -> int:
+        return int(batch[1].shape[0])
 
     def set_lr(self, lr):
         self.tr.set_lr(lr)
@@ -336,6 +344,7 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
     stop = False
     for epoch in range(start_epoch, epochs):
         t0 = time.perf_counter()
+        n_local = 0  # samples actually stepped this epoch (early stop / short final batch)
         for bi, batch in enumerate(runner.epoch_batches(epoch)):
             if step >= total:
                 break
@@ -345,11 +354,11 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
                 raise FloatingPointError(f"injected NaN loss at step {step}")
             runner.step(batch)
             step += 1
+            n_local += runner.batch_samples(batch)
             imgs += cfg.batch_size * ddist.get_world_size()
             if cfg.log_every and step % cfg.log_every == 0 and is_main:
                 print(f"[TRAINING] [RANK {ddist.get_rank()}] step {step}/{total} (epoch {epoch + 1})", flush=True)
         loss_sum, correct = runner.read_metrics()
-        n_local = spe * cfg.batch_size
         loss_sum, correct, n = ddist.all_reduce_sum([loss_sum, correct, float(n_local)])
         if not fault.check_finite(loss_sum):
             raise FloatingPointError(f"non-finite training loss in epoch {epoch + 1}")

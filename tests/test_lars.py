@@ -47,13 +47,15 @@ def test_reference_lars_matches_torch_optimizer():
         assert torch.allclose(q.detach().reshape(-1), pm[o:o + n], atol=1e-6, rtol=1e-5)
 
 
-def test_native_lars_step_matches_autograd_lars_cpu():
+@pytest.mark.parametrize("clip", [0.0, 0.5])
+def test_native_lars_step_matches_autograd_lars_cpu(clip):
     """One native-program LARS step (CPU reference ops) moves every parameter like torch LARS on the
-    autograd gradients of the same batch (cosine of the updates)."""
+    autograd gradients of the same batch (cosine of the updates). With grad_clip the global-norm
+    clip applies before the trust ratios on both engines (clip_grad_norm_ + LARS)."""
     torch.manual_seed(0)
     model = build_model("resnet18", num_classes=10)
     ref = copy.deepcopy(model).train()
-    o = OptimConfig(name="lars", lr=2.0, momentum=0.9, weight_decay=1e-4, trust_coefficient=0.02)
+    o = OptimConfig(name="lars", lr=2.0, momentum=0.9, weight_decay=1e-4, trust_coefficient=0.02, grad_clip=clip)
     tr = NativeTrainer(model, 8, (32, 32), torch.device("cpu"), optim=o, use_graphs=False)
     before = {k: v.detach().clone() for k, v in model.named_parameters()}
     gen = torch.Generator().manual_seed(1)
@@ -63,22 +65,28 @@ def test_native_lars_step_matches_autograd_lars_cpu():
     x = tr.prog.x4[..., :3].float().permute(0, 3, 1, 2).contiguous()
     opt = LARS(ref.parameters(), lr=2.0, momentum=0.9, weight_decay=1e-4, trust_coefficient=0.02)
     F.cross_entropy(ref(x), lab).backward()
+    if clip:
+        torch.nn.utils.clip_grad_norm_(ref.parameters(), clip)
     opt.step()
     nr = dict(ref.named_parameters())
+    ratios = []  # update-norm ratios of the non-adapted (BN / bias) parameters: scaled by the clip
     for name, prm in model.named_parameters():
         d_nat = (prm.detach() - before[name]).flatten()
         d_ref = (nr[name].detach() - before[name]).flatten()
+        if prm.dim() == 1:
+            ratios.append((d_nat.norm() / d_ref.norm()).item())
         cos = (d_nat @ d_ref / (d_nat.norm() * d_ref.norm() + 1e-20)).item()
         assert cos > (0.85 if prm.dim() > 1 else 0.75), (name, cos)  # bf16 program vs fp32 autograd grads
         if prm.dim() > 1:  # the trust ratio fixes the update norm: eta * lr * |w| (up to wd)
             assert 0.8 < d_nat.norm() / d_ref.norm() < 1.25, name
+    assert 0.9 < sorted(ratios)[len(ratios) // 2] < 1.1, ratios  # global norm ~109: clip 0.5 is active
 
 
 @pytest.mark.gpu
 def test_lars_kernel_matches_reference_gpu():
     p, g, off, ln, ad, mx = _segments(SHAPES, dev="cuda")
     pr, gr = p.cpu(), g.cpu()
-    K.lars_scale(p, g, off, ln, ad, torch.zeros(2 * len(SHAPES), device="cuda"), grad_scale=0.125, eta=0.001,
+    K.lars_scale(p, g, off, ln, ad, torch.zeros(2 * len(SHAPES), device="cuda", dtype=torch.float64), grad_scale=0.125, eta=0.001,
                  weight_decay=5e-5, max_len=mx)
     R.lars_scale(pr, gr, off.cpu(), ln.cpu(), ad.cpu(), torch.zeros(2 * len(SHAPES)), grad_scale=0.125, eta=0.001,
                  weight_decay=5e-5, max_len=mx)
@@ -103,3 +111,25 @@ def test_native_lars_resnet50_graph_step_gpu():
         tr.step(img, lab)
         losses.append(tr.read_metrics()[0] / 32)
     assert all(l == l for l in losses) and losses[-1] < losses[0], losses
+
+
+@pytest.mark.gpu
+def test_lars_scale_bit_reproducible():
+    """fp64 atomics for the per-segment norms: two launches give identical trust ratios."""
+    import torch
+    from dbx_distributed_pytorch_examples_amd.ops import kernels as K
+    torch.manual_seed(0)
+    n = [300000, 4096, 65536]
+    p0 = torch.randn(sum(n), device="cuda")
+    g0 = torch.randn(sum(n), device="cuda")
+    off = torch.tensor([0, n[0], n[0] + n[1]], dtype=torch.int32, device="cuda")
+    ln = torch.tensor(n, dtype=torch.int32, device="cuda")
+    ad = torch.tensor([1, 0, 1], dtype=torch.int32, device="cuda")
+    outs = []
+    for _ in range(3):
+        g = g0.clone()
+        norms = torch.zeros(6, device="cuda", dtype=torch.float64)
+        K.lars_scale(p0, g, off, ln, ad, norms, grad_scale=0.25, eta=1e-3, weight_decay=1e-4, max_len=max(n))
+        outs.append((g, norms))
+    for g, nm in outs[1:]:
+        assert torch.equal(g, outs[0][0]) and torch.equal(nm, outs[0][1])
