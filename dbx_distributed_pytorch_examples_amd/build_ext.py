@@ -59,7 +59,7 @@ def build(verbose: bool = False, jobs: int = 8, variant: str = "", defines=()) -
         objs.append(o)
         if _newer(o, [s] + headers):
             if s.endswith(".hip"):
-                cmd = [_hipcc(), f"--offload-arch={arch}", "-munsafe-fp-atomics", "-c", s, "-o", o] + common
+                cmd = [_hipcc(), f"--offload-arch={arch}", "-munsafe-fp-atomics", "-Wno-inline-asm", "-c", s, "-o", o] + common
             else:
                 cmd = [_hipcc(), "-c", s, "-o", o] + common + ["-fvisibility=hidden"]
             cmds.append(cmd)

@@ -15,7 +15,8 @@ namespace py = pybind11;
 extern "C" {
 int dbx_conv_igemm(int mode, int bm, int bn, const dbx::IGemmArgs* a, int pro, int stats, int accum, int epi,
                    hipStream_t st);
-int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, hipStream_t st, unsigned lds_pad);
+int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, hipStream_t st, unsigned lds_pad,
+                   int dma);
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
 int dbx_bn_finalize(const double*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
                     float*, float*, float*, hipStream_t);
@@ -102,14 +103,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_wgrad", [](int mode, int bm, int bn, uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t in_scale,
                          uintptr_t in_shift, int relu_in, int N, int IH, int IW, int IC, int OH, int OW, int OC, int R,
                          int S_, int stride, int pad, int KTOT, int nsplit, int m_per_split, uintptr_t st,
-                         unsigned lds_pad) {
+                         unsigned lds_pad, int dma) {
     const unsigned long long two40 = 1ull << 40;
     const unsigned long long ohw = (unsigned long long)OH * OW;
     if ((unsigned long long)N * ohw * ohw >= two40) throw std::runtime_error("conv_wgrad: batch too large for mdiv");
     dbx::WgradArgs a{P<const bf16*>(dy), P<const bf16*>(x), P<float*>(ws), P<const float*>(in_scale),
                      P<const float*>(in_shift), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad, N * OH * OW, KTOT,
                      nsplit, m_per_split, relu_in, (two40 + OW - 1) / OW, (two40 + ohw - 1) / ohw};
-    check(dbx_conv_wgrad(mode, bm, bn, &a, in_scale != 0, S(st), lds_pad), "conv_wgrad");
+    check(dbx_conv_wgrad(mode, bm, bn, &a, in_scale != 0, S(st), lds_pad, dma), "conv_wgrad");
   });
   m.def("wgrad_reduce", [](uintptr_t ws, uintptr_t dw, long long n, int nsplit, float scale, int acc, uintptr_t st) {
     check(dbx_wgrad_reduce(P<const float*>(ws), P<float*>(dw), n, nsplit, scale, acc, S(st)), "wgrad_reduce");

@@ -100,3 +100,39 @@ __device__ __forceinline__ void buf_store8(rsrc_t r, unsigned off, unsigned char
 __device__ __forceinline__ void buf_store16(rsrc_t r, unsigned off, u32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r, off, 0, 0);
 }
+
+// ---- LDS-DMA (gfx950 buffer_load_dwordx4 ... lds) ----------------------------------------------
+// 16 bytes per lane go from a raw buffer straight into LDS at m0 + 16*lane: 1 KiB per
+// wave-instruction, no VGPR staging and no ds_write (the LDS write path of a register-staged
+// tile costs ~13 cycles per ds_write_b128 and was the largest LDS consumer of the conv loops).
+// Out-of-range offsets land zeros, like buf_load16. Issued through inline asm: hipcc's waitcnt
+// pass treats its own LDS-DMA builtin as an LDS store of unknown address and inserts vmcnt(0)
+// before every later ds_read, which would drain the prefetch pipeline; the caller instead waits
+// with dma_wait<N>() (counted vmcnt) + a barrier before it reads a filled buffer. The asm is
+// invisible to that pass, so its own vmcnt waits count fewer loads than are in flight: they
+// only ever over-wait, never under-wait.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 make_srd(const void* p, unsigned long long bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned n = bytes < (unsigned long long)kOOB ? (unsigned)bytes : kOOB;
+  return i32x4{(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xFFFFu), (int)n, 0x00020000};
+}
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void lds_dma16(const i32x4 srd, unsigned voff, unsigned lds_byte) {
+  // m0 = the wave's 1 KiB destination (wave-uniform by construction; readfirstlane makes it SGPR)
+  const unsigned m = __builtin_amdgcn_readfirstlane(lds_byte);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(srd)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(unsigned long long)(const DBX_LDS void*)p;
+}
+// wait until at most N vector-memory operations of this wave are outstanding (loads, stores and
+// LDS-DMA count together, in issue order); expcnt / lgkmcnt left unconstrained
+template <int N>
+__device__ __forceinline__ void dma_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}

@@ -855,6 +855,157 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const WgradArgs 
       }
 }
 
+// Weight gradient without a BN prologue, operands moved by LDS-DMA (common.h lds_dma16): each
+// wave-instruction fills 1 KiB of a tile image straight from memory, so the K loop has no
+// register staging and no ds_write -- only the transposed fragment reads and the MFMAs touch
+// the LDS port. The swizzle moves to the source side: LDS position p of a tile image (row =
+// pixel p / NC, position p % NC) receives chunk tr_swz(row, p % NC) of that pixel (tr_swz is an
+// XOR, its own inverse), so the fragment reads are those of wgrad_kernel unchanged.
+// NBUF-deep ring: block kb+NBUF-1 is issued while block kb is computed; at the top of each step
+// the wave waits until only the younger blocks' DMAs are in flight, then one barrier publishes
+// every wave's part of block kb and retires the buffer the next issue overwrites.
+template <int BM, int BN, int WM, int WN, int NBUF>
+__global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_dma_kernel(const WgradArgs a) {
+  constexpr int NT = 64 * WM * WN, NW = WM * WN;
+  constexpr int BKM = 64;
+  constexpr int NCA = BM / 8, NCB = BN / 8;
+  constexpr int DA = BKM * NCA / NT, DB = BKM * NCB / NT;  // DMA instructions per wave and block
+  constexpr int ND = DA + DB;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  constexpr int IMG = BKM * (BM + BN);  // bf16 elements per ring slot
+  static_assert(DA >= 1 && DB >= 1 && (NBUF - 1) * ND < 64, "tile / ring shape");
+  __shared__ __attribute__((aligned(1024))) bf16 lds[NBUF * IMG];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int ntn = a.KTOT / BN;
+  const int ntile = (a.OC / BM) * ntn;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / ntile;
+  const int tile = bid - split * ntile;
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int k0 = tm * BM, kk0 = tn * BN;
+  const int mbeg = split * a.m_per_split;
+  const int mend = min(a.M, mbeg + a.m_per_split);
+  const int nkb = (mend - mbeg + BKM - 1) / BKM;
+
+  // per DMA instruction j: the pixel row inside the block and the source chunk (swizzle inverse)
+  int a_row[DA], a_cc[DA], b_row[DB], b_off[DB], b_th[DB], b_tw[DB];
+#pragma unroll
+  for (int j = 0; j < DA; ++j) {
+    const int p = (j * NW + wid) * 64 + lane;
+    a_row[j] = p / NCA;
+    a_cc[j] = tr_swz(a_row[j], p % NCA, NCA);
+  }
+#pragma unroll
+  for (int j = 0; j < DB; ++j) {
+    const int p = (j * NW + wid) * 64 + lane;
+    b_row[j] = p / NCB;
+    const int kk = kk0 + tr_swz(b_row[j], p % NCB, NCB) * 8;
+    const int tap = kk / a.IC, ch = kk - (kk / a.IC) * a.IC;
+    b_th[j] = tap / a.S;
+    b_tw[j] = tap - b_th[j] * a.S;
+    b_off[j] = (b_th[j] * a.IW + b_tw[j]) * a.IC + ch;
+  }
+  const i32x4 dyr = make_srd(a.dy, 2ull * a.M * a.OC);
+  const i32x4 xr = make_srd(a.x, 2ull * a.N * a.IH * a.IW * a.IC);
+  const unsigned lbase = lds_addr(lds);
+  const int ohw = a.OH * a.OW;
+
+  // issue block kb into ring slot s (rows past the split / blocks past the end read out of range:
+  // zeros, no traffic). Branch-free: every address is computed, the validity only selects kOOB.
+  auto issue = [&](int kb, int s) __attribute__((always_inline)) {
+    const unsigned sa = lbase + 2u * (unsigned)(s * IMG);
+    const unsigned sb = sa + 2u * (unsigned)(BKM * BM);
+    const int m0 = mbeg + kb * BKM;
+    const int mlim = kb < nkb ? mend : 0;  // wave-uniform
+#pragma unroll
+    for (int j = 0; j < DA; ++j) {
+      const int ma = m0 + a_row[j];
+      const unsigned off = ma < mlim ? 2u * (unsigned)(ma * a.OC + k0 + a_cc[j] * 8) : kOOB;
+      lds_dma16(dyr, off, sa + 1024u * (unsigned)(j * NW + wid));
+    }
+#pragma unroll
+    for (int j = 0; j < DB; ++j) {
+      const int mb = m0 + b_row[j];
+      const int n = mdiv(mb, a.mag_ohw);  // mb < 2^31: any value decomposes (n >= N reads nothing)
+      const int pq = mb - n * ohw;
+      const int oh = mdiv(pq, a.mag_ow), ow = pq - oh * a.OW;
+      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+      const bool v = mb < mlim && (unsigned)(ih0 + b_th[j]) < (unsigned)a.IH &&
+                     (unsigned)(iw0 + b_tw[j]) < (unsigned)a.IW;
+      const unsigned off = v ? 2u * (unsigned)(((n * a.IH + ih0) * a.IW + iw0) * a.IC + b_off[j]) : kOOB;
+      lds_dma16(xr, off, sb + 1024u * (unsigned)(j * NW + wid));
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  auto mma = [&](int s) __attribute__((always_inline)) {
+    const bf16* cA = lds + s * IMG;
+    const bf16* cB = cA + BKM * BM;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+      const int row = ks * 32 + 8 * g + q, row2 = row + 4;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * (BM / WM) + i * 16 + 4 * p;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DBX_LDS s16x4*)(cA + row * BM + (tr_swz(row, col >> 3, NCA) << 3) + (col & 7)));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DBX_LDS s16x4*)(cA + row2 * BM + (tr_swz(row2, col >> 3, NCA) << 3) + (col & 7)));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / WN) + j * 16 + 4 * p;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DBX_LDS s16x4*)(cB + row * BN + (tr_swz(row, col >> 3, NCB) << 3) + (col & 7)));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DBX_LDS s16x4*)(cB + row2 * BN + (tr_swz(row2, col >> 3, NCB) << 3) + (col & 7)));
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // prologue: blocks 0 .. NBUF-2 in flight
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s) issue(s, s);
+  int cur = 0;  // ring slot of block kb; block kb + NBUF - 1 goes to slot (cur + NBUF - 1) % NBUF
+  for (int kb = 0; kb < nkb; ++kb) {
+    dma_wait<(NBUF - 2) * ND>();  // this wave's part of block kb has landed
+    __syncthreads();              // ... every wave's; and slot cur-1 is no longer read
+    const int nxt = cur == 0 ? NBUF - 1 : cur - 1;
+    issue(kb + NBUF - 1, nxt);
+    mma(cur);
+    cur = cur + 1 == NBUF ? 0 : cur + 1;
+  }
+  dma_wait<0>();  // no DMA may still be writing LDS when the wave ends
+
+  // partial slab write: ws[split][k][kk]
+  float* out = a.ws + (size_t)split * a.OC * a.KTOT;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
+        const int kk = kk0 + wn * (BN / WN) + j * 16 + (lane & 15);
+        out[(size_t)k * a.KTOT + kk] = acc[i][j][r];
+      }
+}
+
 // Deterministic 2-level split-K reduction. Level 1 (G > 1): thread (i, g) sums the fixed split
 // range of group g into ws2[g][i]; level 2 sums the G group partials in order, scales, and writes
 // (or accumulates into) the fp32 gradient. Both levels are wide (n4 x G threads), so a 1024-split
@@ -1004,10 +1155,20 @@ static void launch_wgrad_t(const WgradArgs& a, int nblk, hipStream_t st, unsigne
   hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, FWD, PRO, DEPTH>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
 }
 
+template <int BM, int BN>
+static void launch_wgrad_dma_t(const WgradArgs& a, int nblk, hipStream_t st, unsigned lds_pad, int nbuf) {
+  constexpr int WM = (BM == 256) ? 4 : 2;
+  constexpr int WN = (BN == 256) ? 4 : 2;
+  if (nbuf == 2)
+    hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 2>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
+  else
+    hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 3>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
+}
+
 // lds_pad: extra dynamic LDS per workgroup (bytes) -- an occupancy cap, so that a weight gradient
 // running on the side stream leaves room on each CU for the main stream's memory-bound kernels
 extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, int pro, hipStream_t st,
-                              unsigned lds_pad) {
+                              unsigned lds_pad, int dma_req) {
   const WgradArgs& a = *args;
   if (pro && !a.relu_in) return -7;  // the BN prologue always ends in ReLU (ResNet dataflow)
   if (a.OC % bm != 0 || a.KTOT % bn != 0) return -1;
@@ -1018,11 +1179,22 @@ extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, i
     return (int)hipGetLastError();
   }
   if (a.IC % bn != 0) return -4;  // a column tile must stay inside one tap
-#define WG(BM_, BN_)                                                  \
-  if (bm == BM_ && bn == BN_) {                                       \
-    if (pro) launch_wgrad_t<BM_, BN_, true>(a, nblk, st, lds_pad);    \
-    else launch_wgrad_t<BM_, BN_, false>(a, nblk, st, lds_pad);       \
-    return (int)hipGetLastError();                                    \
+  // LDS-DMA operand path for the prologue-free weight gradients: ring depth 2 or 3, 0 = the
+  // register-staged wgrad_kernel; dma_req < 0 = DBX_WGRAD_DMA, unset = auto: 3 slots for the
+  // 8-wave 256-wide tiles (one workgroup per CU either way), 2 for the 4-wave tiles (keeps two
+  // workgroups per CU)
+  static const int dma_env = [] {
+    const char* e = getenv("DBX_WGRAD_DMA");
+    return e ? atoi(e) : -1;
+  }();
+  const int dreq = dma_req >= 0 ? dma_req : dma_env >= 0 ? dma_env : ((bm == 256 || bn == 256) ? 3 : 2);
+  const int dma = (dreq == 2 || dreq == 3) ? dreq : 0;
+#define WG(BM_, BN_)                                                                             \
+  if (bm == BM_ && bn == BN_) {                                                                  \
+    if (pro) launch_wgrad_t<BM_, BN_, true>(a, nblk, st, lds_pad);                               \
+    else if (dma) launch_wgrad_dma_t<BM_, BN_>(a, nblk, st, lds_pad, dma);                       \
+    else launch_wgrad_t<BM_, BN_, false>(a, nblk, st, lds_pad);                                  \
+    return (int)hipGetLastError();                                                               \
   }
   WG(128, 128)
   WG(128, 64)

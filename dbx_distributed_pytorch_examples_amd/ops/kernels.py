@@ -318,8 +318,10 @@ def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int
 
 @_dispatch
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True,
-               scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0):
-    """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace."""
+               scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1):
+    """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace.
+    ``dma``: operand path of the prologue-free kernels -- LDS-DMA ring depth 2 / 3, 0 = register
+    staged, -1 = the tune table's choice, else DBX_WGRAD_DMA, else 3 for 256-wide tiles / 2."""
     N, OH, OW, OC = dy.shape
     _, IH, IW, IC = x.shape
     KTOT = 256 if stem else R * S * IC
@@ -339,7 +341,9 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         else:
             t = _tune_table().get(tune_key("wgrad", N * OH * OW, OC, IC, R, stride))
             if t is not None and OC % t[0] == 0 and IC % t[1] == 0:
-                bm, bn = t
+                bm, bn = t[0], t[1]
+                if len(t) > 2 and dma < 0:  # measured operand path (tools/tune_conv.py)
+                    dma = int(t[2])
             else:
                 bm = 128 if OC % 128 == 0 else 64
                 bn = 128 if IC % 128 == 0 else 64
@@ -352,7 +356,7 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         raise ValueError("wgrad workspace too small")
     C().conv_wgrad(STEM if stem else FWD, bm, bn, dy.data_ptr(), x.data_ptr(), ws.data_ptr(), _p(in_scale),
                    _p(in_shift), int(relu_in), N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, KTOT, nsplit, ms,
-                   stream_ptr(), int(lds_pad))
+                   stream_ptr(), int(lds_pad), int(dma))
     C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsplit, float(scale), int(accumulate), stream_ptr())
     return dw
 

@@ -98,8 +98,8 @@ def test_conv_dgrad(case):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("prologue", [False, True])
-def test_conv_wgrad(case, prologue):
+@pytest.mark.parametrize("prologue,dma", [(False, -1), (False, 0), (False, 2), (True, -1)])
+def test_conv_wgrad(case, prologue, dma):
     k = K()
     N, H, W, IC, OC, R, st, pad = case
     torch.manual_seed(2)
@@ -118,7 +118,8 @@ def test_conv_wgrad(case, prologue):
     for tile in [None, (128, 128), (128, 64), (64, 128), (64, 64), (256, 128), (128, 256)]:
         if tile and (OC % tile[0] or IC % tile[1]):
             continue
-        k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, in_scale=sc, in_shift=sh, tile=tile)
+        dw.fill_(float("nan"))
+        k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, in_scale=sc, in_shift=sh, tile=tile, dma=dma)
         assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2, tile
 
 
@@ -439,8 +440,10 @@ def test_conv_wgrad_split(shape):
     for tile in [None, (256, 128), (128, 256)]:
         if tile and (OC % tile[0] or IC % tile[1]):
             continue
-        k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, tile=tile)
-        assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2, tile
+        for dma in (3, 2, 0):  # LDS-DMA rings of depth 3 / 2, register-staged
+            dw.fill_(float("nan"))
+            k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, tile=tile, dma=dma)
+            assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2, (tile, dma)
 
 
 def test_stem_wgrad_split():

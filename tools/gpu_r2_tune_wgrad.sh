@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python tools/tune_conv.py --modes wgrad --batch 1024 --verbose --out gpurun_out/tune_tmp.json > gpurun_out/tune_wgrad_all.log 2>&1 || { echo "tune FAILED"; tail -20 gpurun_out/tune_wgrad_all.log; exit 1; }
+grep "^  wgrad" gpurun_out/tune_wgrad_all.log

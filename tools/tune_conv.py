@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--out", default=os.path.join(ROOT, "dbx_distributed_pytorch_examples_amd", "ops", "tune_table.json"))
     ap.add_argument("--report", default=None)
+    ap.add_argument("--verbose", action="store_true", help="print every candidate's median time")
     ap.add_argument("--modes", default="fwd,fwdt,dgrad0,dgrad1,dgrad2,dgrad1b,dgrad2b,wgrad")
     a = ap.parse_args()
     dev = "cuda"
@@ -124,12 +125,12 @@ def main():
         dw = torch.empty(Kc * R * R * C, device=dev)
         # wgrads read stored activations (no BN prologue) since the dgrad-epilogue write-back
         jobs.append(("wgrad", N * OH * OH, Kc, C, R, st,
-                     lambda t: K.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, tile=t)))
+                     lambda t: K.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, tile=t[:2], dma=t[2])))
         for mode, M, OCm, Kin, Rk, sk, make in jobs:
             if mode not in a.modes.split(","):
                 continue
-            if mode == "wgrad":
-                cands = [t for t in WGRAD_TILES if Kc % t[0] == 0 and C % t[1] == 0]
+            if mode == "wgrad":  # tile x operand path (LDS-DMA ring depth 3 / 2, 0 = register staged)
+                cands = [t + (d,) for t in WGRAD_TILES if Kc % t[0] == 0 and C % t[1] == 0 for d in (3, 2, 0)]
             else:
                 cands = [t for t in TILES if OCm % t[1] == 0]
             res = {t: [] for t in cands}
@@ -138,11 +139,14 @@ def main():
                     res[t].append(timeit(lambda t=t: make(t), a.iters))
             med = {t: sorted(v)[len(v) // 2] for t, v in res.items()}
             best = min(med, key=med.get)
+            if a.verbose:
+                print(f"  {mode} {C}->{Kc} {R}x{R} s{st} @{H}: " + "  ".join(
+                    f"{'x'.join(map(str, t))}={v:.3f}" for t, v in sorted(med.items())), flush=True)
             default = (K.pick_tile(M, OCm, use_table=False) if mode != "wgrad" else
-                       (128 if Kc % 128 == 0 else 64, 128 if C % 128 == 0 else 64))
+                       (128 if Kc % 128 == 0 else 64, 128 if C % 128 == 0 else 64, 0))
             key = K.tune_key(mode, M, OCm, Kin, Rk, sk)
             table[key] = list(best)
-            lines.append(f"| {C}→{Kc} | {R}x{R} s{st} | {H} | {cnt} | {mode} | {best[0]}x{best[1]} | {med[best]:.3f} | "
+            lines.append(f"| {C}→{Kc} | {R}x{R} s{st} | {H} | {cnt} | {mode} | {'x'.join(map(str, best))} | {med[best]:.3f} | "
                          f"{gf / med[best]:.0f} | {med.get(default, float('nan')):.3f} |")
             print(lines[-1], flush=True)
     with open(a.out, "w") as f:
