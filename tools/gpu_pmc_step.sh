@@ -13,5 +13,8 @@ timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 echo "pass a ok"
 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE TCC_HIT_sum TCC_MISS_sum -d $R/gpurun_out/pmc_step/b -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --batch $B > $R/gpurun_out/pmc_step/b.log 2>&1 || { echo "pmc b failed"; tail -5 $R/gpurun_out/pmc_step/b.log; exit 1; }
 echo "pass b ok"
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $R/gpurun_out/pmc_step/c -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --batch $B > $R/gpurun_out/pmc_step/c.log 2>&1 || { echo "pmc c failed"; tail -5 $R/gpurun_out/pmc_step/c.log; exit 1; }
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $R/gpurun_out/pmc_step/d -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --batch $B > $R/gpurun_out/pmc_step/d.log 2>&1 || { echo "pmc d failed"; tail -5 $R/gpurun_out/pmc_step/d.log; exit 1; }
+echo "passes c, d ok"
 python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_step > $R/gpurun_out/pmc_step/summary.txt 2>&1 || echo "summary failed (raw CSVs kept)"
 head -60 $R/gpurun_out/pmc_step/summary.txt
