@@ -82,6 +82,13 @@ class NativeTrainer:
                                             and dist.is_available() and dist.is_initialized())
         self.comm_stream = (torch.cuda.Stream(device=device, priority=-1)
                             if self.segmented and device.type == "cuda" else None)
+        if self.segmented and os.environ.get("DBX_OVERLAP_WGRAD") is None:
+            # Next to the comm stream and RCCL's own stream, the wgrad side stream costs more than
+            # it overlaps: measured over a world-1 RCCL process group on one MI355X (ResNet-50
+            # b1024, 2 interleaved rounds) segmented step 14.03k / 14.06k img/s with the side
+            # stream vs 14.43k / 14.40k without; the plain single graph is 14.53-14.56k either way
+            # (profiles/r2s2_multirank/). Weight gradients then run in order on the main stream.
+            self.prog.overlap_wgrad = False
         self.flip = None
         self.zero = None
         if zero_stage:
@@ -140,10 +147,12 @@ class NativeTrainer:
         """Optional coarser graph segmentation of the multi-rank path: DBX_SEG_GROUPS="3,3" merges
         the six backward segments into two graphs (one all-reduce cut after layer3). Default: one
         graph per backward segment. Measured over RCCL on one MI355X (world-1 process group with
-        DBX_SEGMENTED_GRAPHS=1, ResNet-50 b1024): 6 segments 13.89k img/s, 2 segments 13.85k,
-        single graph 14.33k (profiles/r1s4_revalidate/rccl_rehearsal.txt) -- boundaries are not
-        what the segmented path costs, so the finer split (more overlap, smallest exposed tail)
-        stays. Groups merge only when their gradient ranges are adjacent."""
+        DBX_SEGMENTED_GRAPHS=1, ResNet-50 b1024, wgrad side stream on): 6 segments 13.98k / 14.03k
+        img/s, 2 segments 14.05k / 14.07k, one backward graph 13.99k / 14.00k, plain single graph
+        14.45k / 14.43k (profiles/r2s2_multirank/step_layout_ab.txt) -- boundaries are not what
+        the segmented path cost: the wgrad side stream next to the comm streams was (now off in
+        this mode, see __init__). The finer split (more overlap, smallest exposed tail) stays.
+        Groups merge only when their gradient ranges are adjacent."""
         spec = os.environ.get("DBX_SEG_GROUPS", "")
         if not spec:
             return phases
