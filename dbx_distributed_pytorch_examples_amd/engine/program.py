@@ -147,6 +147,9 @@ class ResNetProgram:
         # ... only for large operands: folding orders the wgrad after the dgrad (no overlap), which
         # costs more than the saved pass when the kernels are too small to fill the GPU
         self.fold_min = int(os.environ.get("DBX_FOLD_MIN_ELEMS", str(1 << 25)))
+        # ... and only where the dgrad's output channels (N) are at most this multiple of its
+        # reduction channels: every N tile of a folded dgrad re-reads and re-applies the operand
+        self.fold_max_ratio = float(os.environ.get("DBX_FOLD_MAX_RATIO", "inf"))
         self._wstream = None
         self._side_pending = False
         self._build_layers()
@@ -669,6 +672,7 @@ class ResNetProgram:
         ``dense``: the strided 1x1 downsample, whose dgrad runs as a dense 1x1 stride-1 GEMM)."""
         stride = 1 if dense else cv.stride
         return (self.fuse_bwd_apply and not cv.stem and self.N * cv.OH * cv.OW * cv.OC >= self.fold_min
+                and cv.IC <= self.fold_max_ratio * cv.OC
                 and K.tail_supported(cv.OC, cv.R, cv.S, stride, cv.pad))
 
     def _bwd_stem(self):

@@ -24,11 +24,14 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-20)).item()
 
 
-@pytest.mark.parametrize("arch,size,batch,fold", [("resnet18", 32, 8, 0), ("cifar_resnet18", 32, 4, 0),
-                                                  ("resnet50", 64, 8, 0), ("resnet50", 64, 8, 1 << 40)])
-def test_program_grads_match_autograd(arch, size, batch, fold, monkeypatch):
-    # fold: DBX_FOLD_MIN_ELEMS -- 0 folds every foldable BN-backward apply into its dgrad, 2^40 none
+@pytest.mark.parametrize("arch,size,batch,fold,ratio", [("resnet18", 32, 8, 0, "inf"), ("cifar_resnet18", 32, 4, 0, "inf"),
+                                                        ("resnet50", 64, 8, 0, "inf"), ("resnet50", 64, 8, 1 << 40, "inf"),
+                                                        ("resnet50", 64, 8, 0, "1")])
+def test_program_grads_match_autograd(arch, size, batch, fold, ratio, monkeypatch):
+    # fold: DBX_FOLD_MIN_ELEMS -- 0 folds every foldable BN-backward apply into its dgrad, 2^40 none;
+    # ratio: DBX_FOLD_MAX_RATIO -- 1 keeps the bottleneck conv1 dgrads (N = 4K) unfolded (mixed schedule)
     monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(fold))
+    monkeypatch.setenv("DBX_FOLD_MAX_RATIO", ratio)
     torch.manual_seed(0)
     model = build_model(arch, num_classes=10)
     _damp(model, arch)
