@@ -14,7 +14,7 @@ namespace py = pybind11;
 
 extern "C" {
 int dbx_conv_igemm(int mode, int bm, int bn, const dbx::IGemmArgs* a, int pro, int stats, int accum, int epi,
-                   hipStream_t st);
+                   hipStream_t st, int dma);
 int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, hipStream_t st, unsigned lds_pad,
                    int dma);
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
@@ -82,7 +82,7 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t bsc, uintptr_t bsh, uintptr_t mean1, uintptr_t inv1, uintptr_t mean2,
                          uintptr_t inv2, uintptr_t bstats1, uintptr_t bstats2, uintptr_t a_out, uintptr_t res,
                          uintptr_t res_scale, uintptr_t res_shift, uintptr_t tail_out, uintptr_t tail_bits,
-                         uintptr_t st) {
+                         uintptr_t st, int dma) {
     dbx::IGemmArgs a{P<const bf16*>(x), P<const bf16*>(w), P<bf16*>(y), P<const float*>(in_scale),
                      P<const float*>(in_shift), P<double*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
                      N * OH * OW, nshard > 0 ? nshard : 1, relu_in, nr, ns, r0, s0, tstep, dh0, dw0, osub, oph, opw,
@@ -98,7 +98,7 @@ PYBIND11_MODULE(_C, m) {
         a.mag_ow = (two40 + OW - 1) / OW;
       }
     }
-    check(dbx_conv_igemm(mode, bm, bn, &a, in_scale != 0, stats != 0, accum, epi, S(st)), "conv_igemm");
+    check(dbx_conv_igemm(mode, bm, bn, &a, in_scale != 0, stats != 0, accum, epi, S(st), dma), "conv_igemm");
   });
   m.def("conv_wgrad", [](int mode, int bm, int bn, uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t in_scale,
                          uintptr_t in_shift, int relu_in, int N, int IH, int IW, int IC, int OH, int OW, int OC, int R,

@@ -1,603 +1,9 @@
-// NHWC bf16 implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16).
-//
-// Replaces the cuDNN/MIOpen conv kernels the reference reaches through torchvision
-// (SURVEY.md §2.4 K1-K5). One kernel family, three problem mappings:
-//
-//   FWD    Y[m=(n,oh,ow)][k]  = sum_{r,s,c} X[n][oh*st-pad+r][ow*st-pad+s][c] * W[k][r][s][c]
-//   DGRAD  dX[m=(n,h,w)][c]   = sum_{r,s,k} dY[n][(h+pad-r)/st][(w+pad-s)/st][k] * Wt[c][r][s][k]
-//          (transposed gather: a tap contributes only where (h+pad-r) % st == 0)
-//   STEM   the 7x7 C=3 stem with the image padded to 4 channels: a "tap" is one filter row r
-//          and its 8 pixels x 4 channels (64 contiguous bytes of an input row); K = 8 x 32.
-//
-// GEMM view: M = output pixels, N = output channels, K = taps x input channels. Both operands are
-// K-contiguous (NHWC activations, KRSC weights), so every lane loads 16 contiguous bytes and the
-// MFMA fragments come straight out of LDS with ds_read_b128 (XOR-swizzled: conflict-free).
-//
-// Fusions (the reason this exists rather than MIOpen — the reference profile spends more time
-// in BatchNorm/ReLU/add passes than in the convolutions, profiles/r1_torch_reference):
-//   * prologue: BN-apply (+ReLU) of the PREVIOUS layer on the A operand while staging it
-//     (y_prev * scale[c] + shift[c], max 0), so BN outputs are never materialised;
-//   * epilogue: per-output-channel sum / sum-of-squares for THIS layer's BN, from the fp32
-//     accumulators: fp32 per-tile partials added into sharded fp64 slabs (fp64 atomics: the
-//     sum of fp32 partials is exact in fp64 for any realistic spread, so the result does not
-//     depend on the order the tiles finish in -> bit-reproducible training);
-//   * epilogue: accumulate into the existing output (dX of a block = dgrad(conv1) + dgrad(ds)).
-//
-// Tiles: BM x BN x 64, 256 threads = 2x2 waves, double-buffered LDS with register staging
-// (the prologue needs the data in registers anyway), one barrier per K block, XCD-aware
-// tile order (A-sharing tiles adjacent -> same XCD L2).
-#include "common.h"
-#include "abi.h"
+// Implicit-GEMM conv entry points: forward / stem dispatch, weight gradients, split-K reduction.
+// The igemm_kernel template lives in conv_igemm_kernel.h; the dgrad instantiations are compiled
+// in conv_dgrad.hip (a separate translation unit, so the two compile in parallel).
+#include "conv_igemm_kernel.h"
 
 namespace dbx {
-
-enum ConvMode { FWD = 0, DGRAD = 1, STEM = 2 };
-
-
-// TAIL (with PRO), A = x*s + h + (res*rs + rh) computed while staging; the first N tile writes A
-// back (tail_out). FWD: the previous residual block's output relu(bn3(x) + shortcut) -- no separate
-// bn_apply pass, no re-read of the block output, ReLU mask written too. DGRAD (1x1 stride-1): the
-// BN-backward apply dy = k1*g + k2*y + k3 (x = g, res = y, no ReLU) -- the BN-backward apply pass
-// is gone and its output is still stored for the weight gradient.
-template <int BM, int BN, int WM, int WN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI, bool TAIL = false>
-__global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs a) {
-  constexpr int NT = 64 * WM * WN;        // threads; WM x WN waves, each owns a (BM/WM) x (BN/WN) tile
-  constexpr int NW = WM * WN;
-  constexpr int BK = 64;
-  constexpr int RPP = NT / 8;             // tile rows covered per staging pass (8 x 16B per 64-wide row)
-  constexpr int A_CH = BM * BK / 8 / NT;  // 16-byte chunks per thread (A)
-  constexpr int B_CH = BN * BK / 8 / NT;
-  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);  // 16x16 MFMA tiles per wave
-  constexpr int LDS_AB = 2 * (BM + BN) * BK;  // bf16 elements
-  constexpr int LDS_C = BM * (BN + 8);
-  constexpr int LDS_RED = 2 * (3 * NW * BN);  // fp32 reduction scratch (in bf16 units)
-  constexpr int PRO_MAXC = TAIL ? 1024 : 512;              // prologue channels held in LDS (host-checked)
-  constexpr int LDS_PRO = (PRO && MODE != STEM) ? (TAIL ? 8 : 4) * PRO_MAXC : 0;  // fp32 arrays (bf16 units)
-  constexpr int LDS_MAIN = (LDS_AB > LDS_C + LDS_RED) ? LDS_AB : (LDS_C + LDS_RED);
-  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_MAIN + LDS_PRO];
-  bf16* sA = lds;                  // [2][BM][BK]
-  bf16* sB = lds + 2 * BM * BK;    // [2][BN][BK]
-  // prologue affine of ALL input channels, staged once: the per-block coefficients are read from
-  // LDS at transform time instead of living in registers across the pipeline
-  float* sPro = reinterpret_cast<float*>(lds + LDS_MAIN);  // [2 or 4][PRO_MAXC]: scale, shift (, rs, rh)
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
-  const int ntn = a.OC / BN, ntm = (a.M + BM - 1) / BM, ntile = ntn * ntm;
-  // Persistent tiles: workgroup b computes tiles b, b + G, b + 2G, ... (G = gridDim.x, a multiple
-  // of 8 sized by the host to the resident capacity, so tile t stays on XCD t % 8 and xcd_remap
-  // still groups A-sharing tiles per L2). The next tile's first K block is loaded while this
-  // tile's epilogue runs: short-K (1x1) convs no longer leave the CU idle during load latency.
-  // The "l" indices are the LOADER's tile (the one being staged), m0/n0/tm the epilogue's.
-  int ltm = 0, ltn = 0, lm0 = 0, ln0 = 0;
-  int lk = 0, lcb = 0, lts = 0, ltr = 0;  // next K block to load (see advance())
-
-  // ---- per-thread A rows: decompose output pixel once per tile ---------------------
-  const int ach = tid & 7;
-  const bf16* abase[A_CH];   // STEM mode: image base
-  int ahb[A_CH], awb[A_CH];  // top-left input coordinate of the row's receptive field
-  unsigned apix[A_CH];       // byte offset of (n, ahb, awb, ach*8) in x (host: bytes < kOOB)
-  auto set_tile = [&](int t) __attribute__((always_inline)) {
-    const int bid = xcd_remap(t, ntile);
-    ltm = bid / ntn; ltn = bid - ltm * ntn;
-    lm0 = ltm * BM; ln0 = ltn * BN;
-    lk = lcb = lts = ltr = 0;
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const int m = lm0 + (tid >> 3) + RPP * i;
-      const int ohw = a.OH * a.OW;
-      int n = mdiv_or(m, a.mag_ohw, ohw);
-      const int pq = m - n * ohw;
-      const int oh = mdiv_or(pq, a.mag_ow, a.OW), ow = pq - oh * a.OW;
-      if (m >= a.M) { n = 0; }
-      abase[i] = a.x + (size_t)n * a.IH * a.IW * a.IC;
-      if (MODE == DGRAD) { ahb[i] = oh + a.dh0; awb[i] = ow + a.dw0; }
-      else { ahb[i] = oh * a.stride - a.pad; awb[i] = ow * a.stride - a.pad; }
-      apix[i] = 2u * (unsigned)(((n * a.IH + ahb[i]) * a.IW + awb[i]) * a.IC + ach * 8);
-      if (m >= a.M) ahb[i] = -(1 << 28);
-    }
-  };
-  int tcur = blockIdx.x;
-  set_tile(tcur);
-  const rsrc_t xr = make_rsrc(a.x, 2ull * a.N * a.IH * a.IW * a.IC);
-  const int KTOT = (MODE == STEM) ? 256 : a.R * a.S * a.IC;  // weight row length
-  const rsrc_t wr = make_rsrc(a.w, 2ull * a.OC * KTOT);
-  const int cpt = (MODE == STEM) ? 1 : a.IC / BK;              // K blocks per tap
-  const int KB = (MODE == STEM) ? 4 : a.nr * a.ns * cpt;
-
-  // Two register staging sets: the loads of block kb+2 are issued while block kb+1's data (set
-  // issued one iteration earlier) is still landing, so each global load has two blocks of MFMA
-  // work to hide its latency instead of one. The K loop is unrolled by two so S is a constant.
-  u32x4 ra[2][A_CH], rb[2][B_CH];
-  u32x4 rr[2][TAIL ? A_CH : 1];           // TAIL: staged shortcut chunks
-  const u32x4 zero4 = {0u, 0u, 0u, 0u};
-  unsigned avalid[2] = {0u, 0u};          // bit i: chunk i is a real (non-padding) tap
-  int pcb[2] = {0, 0};                    // channel block of the staged set (prologue coefficients)
-  if constexpr (PRO && MODE != STEM) {
-    for (int c = tid; c < a.IC; c += NT) {
-      sPro[c] = a.in_scale[c];
-      sPro[PRO_MAXC + c] = a.in_shift[c];
-      if constexpr (TAIL) {
-        sPro[2 * PRO_MAXC + c] = a.res_scale ? a.res_scale[c] : 1.f;
-        sPro[3 * PRO_MAXC + c] = a.res_shift ? a.res_shift[c] : 0.f;
-      }
-    }
-    __syncthreads();
-  }
-  // TAIL write-back: wave-uniform per staged set (first N tile, live block)
-  bool wlive[2] = {false, false};
-  unsigned wtoff[2] = {0u, 0u};
-  const rsrc_t rresr = make_rsrc(a.res, TAIL ? 2ull * a.N * a.IH * a.IW * a.IC : 0ull);
-  const rsrc_t toutr = make_rsrc(a.tail_out, (TAIL && a.tail_out) ? 2ull * a.N * a.IH * a.IW * a.IC : 0ull);
-  const rsrc_t tbitr = make_rsrc(a.tail_bits, (TAIL && a.tail_bits) ? 1ull * a.N * a.IH * a.IW * a.IC / 8 : 0ull);
-  // decomposition of the NEXT block to load (kb -> channel block, tap row, tap column), advanced
-  // by one per load instead of dividing kb (wave-uniform scalars). The pipeline's unconditional
-  // prefetch runs two blocks past the end: those loads use an out-of-range offset for every lane,
-  // so they cost an instruction issue but no memory traffic (short-K 1x1 convs: KB = 1..4)
-  auto advance = [&]() __attribute__((always_inline)) {
-    ++lk;
-    if (++lcb == cpt) { lcb = 0; if (++lts == a.ns) { lts = 0; ++ltr; } }
-  };
-
-  auto load_a = [&](int S) __attribute__((always_inline)) {
-    if constexpr (MODE == STEM) {
-      // k block lk covers filter rows r = 2lk, 2lk+1; chunk ach: r = 2lk + (ach>>2), pixels
-      // s = 2*(ach&3), +1, 4 channels (8 bytes) each.
-      const int r = 2 * (lk < KB ? lk : KB - 1) + (ach >> 2);
-      const int s0 = 2 * (ach & 3);
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        const int ih = ahb[i] + r;
-        const bool rv = (r < a.R) && ih >= 0 && ih < a.IH;
-        unsigned int w4[4];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          // branch-free: an out-of-image pixel loads the image base and is zeroed by the select
-          const int s = s0 + p, iw = awb[i] + s;
-          const bool v = rv && s < a.S && (unsigned)iw < (unsigned)a.IW;
-          const uint2 t = *reinterpret_cast<const uint2*>(abase[i] + (v ? (ih * a.IW + iw) * 4 : 0));
-          w4[2 * p] = v ? t.x : 0u; w4[2 * p + 1] = v ? t.y : 0u;
-        }
-        ra[S][i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
-      }
-    } else {
-      const int cb = lcb * BK;
-      const int r = a.r0 + a.tstep * ltr, s = a.s0 + a.tstep * lts;
-      if constexpr (PRO) pcb[S] = cb;
-      if constexpr (TAIL) { wlive[S] = lk < KB && ltn == 0; wtoff[S] = 2u * (unsigned)cb; }
-      // tap displacement, the same for all of this thread's rows (uniform, bytes)
-      const int dh = (MODE == DGRAD) ? -ltr : r, dw = (MODE == DGRAD) ? -lts : s;
-      const unsigned toff = 2u * (unsigned)((dh * a.IW + dw) * a.IC + cb);
-      const bool live = lk < KB;  // wave-uniform: false for the prefetches past the last block
-      avalid[S] = 0;
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        const bool v = live && (unsigned)(ahb[i] + dh) < (unsigned)a.IH && (unsigned)(awb[i] + dw) < (unsigned)a.IW;
-        // padding taps / rows past M read out of the buffer's range: the hardware returns zeros
-        ra[S][i] = buf_load16(xr, v ? apix[i] + toff : kOOB);
-        if constexpr (TAIL) rr[S][i] = buf_load16(rresr, v ? apix[i] + toff : kOOB);
-        if constexpr (PRO) avalid[S] |= (v ? 1u : 0u) << i;
-      }
-    }
-  };
-  // BN-apply (+ReLU) prologue on the staged A chunks. Kept apart from load_a so the global loads
-  // of block kb+1 stay in flight across block kb's MFMAs (the transform waits on the data).
-  auto pro_a = [&](int S) __attribute__((always_inline)) {
-    if constexpr (PRO && MODE != STEM) {
-      const int c0 = pcb[S] + ach * 8;  // this thread's 8 channels (the same for all its rows)
-      const f32x4 ps0 = *reinterpret_cast<const f32x4*>(sPro + c0);
-      const f32x4 ps1 = *reinterpret_cast<const f32x4*>(sPro + c0 + 4);
-      const f32x4 ph0 = *reinterpret_cast<const f32x4*>(sPro + PRO_MAXC + c0);
-      const f32x4 ph1 = *reinterpret_cast<const f32x4*>(sPro + PRO_MAXC + c0 + 4);
-      f32x4 pr0, pr1, pq0, pq1;
-      if constexpr (TAIL) {
-        pr0 = *reinterpret_cast<const f32x4*>(sPro + 2 * PRO_MAXC + c0);
-        pr1 = *reinterpret_cast<const f32x4*>(sPro + 2 * PRO_MAXC + c0 + 4);
-        pq0 = *reinterpret_cast<const f32x4*>(sPro + 3 * PRO_MAXC + c0);
-        pq1 = *reinterpret_cast<const f32x4*>(sPro + 3 * PRO_MAXC + c0 + 4);
-      }
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        float f[8];
-        unpack8(ra[S][i], f);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f[j] = f[j] * ps0[j] + ph0[j];
-          f[j + 4] = f[j + 4] * ps1[j] + ph1[j];
-        }
-        if constexpr (TAIL) {  // + shortcut (identity: rs = 1, rh = 0), as bn_apply computes it
-          float g[8];
-          unpack8(rr[S][i], g);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            f[j] += g[j] * pr0[j] + pq0[j];
-            f[j + 4] += g[j + 4] * pr1[j] + pq1[j];
-          }
-        }
-        u32x4 t = pack8(f);
-        if constexpr (MODE != DGRAD) t = relu_bf16x8(t);  // forward PRO implies ReLU (host-checked)
-        const bool vi = (avalid[S] >> i) & 1u;
-        ra[S][i] = vi ? t : zero4;  // padding taps stay exactly zero
-        if constexpr (TAIL) {
-          // block output + 1-bit mask (bit j: element j > 0) written back by the first N tile
-          const unsigned off = (wlive[S] && vi) ? apix[i] + wtoff[S] : kOOB;
-          buf_store16(toutr, off, t);
-          if constexpr (MODE == DGRAD) continue;
-          unsigned bits = 0;
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            bits |= (((t[q] & 0xFFFFu) ? 1u : 0u) << (2 * q)) | (((t[q] >> 16) ? 1u : 0u) << (2 * q + 1));
-          buf_store8(tbitr, off == kOOB ? kOOB : (off >> 4), (unsigned char)bits);
-        }
-      }
-    }
-  };
-  auto load_b = [&](int S) __attribute__((always_inline)) {
-    int koff;
-    if constexpr (MODE == STEM) {
-      koff = lk * BK + ach * 8;
-    } else {
-      koff = ((a.r0 + a.tstep * ltr) * a.S + a.s0 + a.tstep * lts) * a.IC + lcb * BK + ach * 8;
-    }
-    const bool live = lk < KB;
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int n = ln0 + (tid >> 3) + RPP * i;
-      rb[S][i] = buf_load16(wr, live ? 2u * (unsigned)(n * KTOT + koff) : kOOB);
-    }
-  };
-  auto store_ab = [&](int buf, int S) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const int row = (tid >> 3) + RPP * i;
-      *reinterpret_cast<u32x4*>(sA + buf * BM * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = ra[S][i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int row = (tid >> 3) + RPP * i;
-      *reinterpret_cast<u32x4*>(sB + buf * BN * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = rb[S][i];
-    }
-  };
-
-  f32x4 acc[TM][TN];
-
-  auto mma = [&](int buf) __attribute__((always_inline)) {
-    const bf16* cA = sA + buf * BM * BK;
-    const bf16* cB = sB + buf * BN * BK;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[TM], bfr[TN];
-      const int ch = ks * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / WM) + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(cA + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * (BN / WN) + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(cB + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          // operands swapped (C^T = W X^T): a lane's 4 accumulators are 4 consecutive output
-          // channels of one pixel, so the epilogue stages them with one 8-byte LDS write
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-  };
-  // one pipeline step on block kb (LDS buffer kb&1, register set S holds block kb+1)
-  // The prefetch is issued unconditionally (past the end it re-reads the last block, data unused)
-  // and the loop body is branch-free, so hipcc's waitcnt pass sees the same in-flight loads on
-  // every path and waits only for the older set (counted vmcnt) instead of draining to vmcnt(0).
-  auto step = [&](int kb, int S) __attribute__((always_inline)) {
-    load_a(S ^ 1);  // block min(kb + 2, KB - 1)
-    load_b(S ^ 1);
-    advance();
-    mma(kb & 1);
-    pro_a(S);
-    store_ab((kb + 1) & 1, S);  // past the last block this fills the idle buffer, never read
-    __syncthreads();
-  };
-
-  load_a(0);
-  load_b(0);
-  advance();
-  for (;;) {  // persistent tile loop (exit: every wave of the workgroup leaves after the same tile)
-  load_a(1);
-  load_b(1);
-  advance();
-  pro_a(0);
-  store_ab(0, 0);
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int kb = 0;
-  for (; kb + 1 < KB; kb += 2) {
-    step(kb, 1);
-    step(kb + 1, 0);
-  }
-  if (kb < KB) {
-    mma(kb & 1);
-    __syncthreads();  // the epilogue's sC staging aliases the operand buffers
-  }
-  // this tile's indices for the epilogue; then stage the next tile's first K block (register set
-  // 0) so its loads are in flight during the epilogue
-  // (PF: plain / forward-stats epilogues; the BN-backward epilogues hold too many registers to
-  // keep a staged block alive across them, so those stage the next tile after the epilogue)
-  // Only those run persistent (PF); the rest leave the loop after one tile (the host launches
-  // one workgroup per tile for them), which compiles to the straight-line single-tile kernel.
-  constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64);  // (+: register room)
-  const int m0 = lm0, n0 = ln0, tm = ltm;
-  tcur += gridDim.x;
-  const bool more = PF && tcur < ntile;  // workgroup-uniform
-  if (more) {  // A (activations, HBM latency) now; B (weights, L2-resident) after the epilogue
-    set_tile(tcur);
-    load_a(0);
-  }
-
-  // ---- epilogue ------------------------------------------------------------------------
-  // acc[i][j][r] (C^T): pixel row = wm*BM/WM + i*16 + (lane&15), channel = wn*BN/WN + j*16 + (lane>>4)*4 + r
-  // staged bf16 through LDS ([BM][BN+8]: the 8-byte writes of a wave hit each bank 4 times, the
-  // minimum for 512 B) and re-read as 16-byte row chunks for coalesced global stores
-  static_assert(!(STATS && EPI), "forward BN statistics and BN-backward epilogues are exclusive");
-  bf16* sC = lds;  // [BM][BN+8]
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int row = wm * (BM / WM) + i * 16 + (lane & 15);
-      const int col = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
-      *reinterpret_cast<uint2*>(sC + row * (BN + 8) + col) =
-          uint2{pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3])};
-    }
-  __syncthreads();
-  constexpr int CPR = BN / 8;  // 16B chunks per output row; a thread's chunk column is fixed
-  const int ccol = tid % CPR;
-  // per-thread partial sums of this thread's 8 channels: STATS: sum y, sum y^2 of the stored
-  // (bf16-rounded) outputs; EPI: BN-backward raw moments
-  float bs[8], bq1[8], bq2[8];
-  // accumulated in packed fp32 (v_pk_add_f32 / v_pk_fma_f32: 2 channels per instruction):
-  // ps2 = sum, pq2 = sum of squares (STATS) or sum g*y (EPI), pr2 = sum g*y2 (EPI)
-  f32x2 ps2[4], pq2[4], pr2[4];
-  f32x4 e_m1[2], e_i1[2], e_m2[2], e_i2[2], e_sc[2], e_sh[2];
-  const bool has2 = EPI > 0 && a.ybn2 != nullptr;  // wave-uniform: second BN (downsample branch)
-  if constexpr (EPI > 0) {
-    // vector loads of the per-channel coefficients; absent ones read a valid stand-in (no branch)
-    const int c0 = n0 + ccol * 8;
-    const float* m2 = has2 ? a.mean2 : a.mean1;
-    const float* i2 = has2 ? a.inv2 : a.inv1;
-    const float* sc = (EPI == 2) ? a.bsc : a.mean1;
-    const float* sh = (EPI == 2) ? a.bsh : a.inv1;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      e_m1[h] = *reinterpret_cast<const f32x4*>(a.mean1 + c0 + 4 * h);
-      e_i1[h] = *reinterpret_cast<const f32x4*>(a.inv1 + c0 + 4 * h);
-      e_m2[h] = *reinterpret_cast<const f32x4*>(m2 + c0 + 4 * h);
-      e_i2[h] = *reinterpret_cast<const f32x4*>(i2 + c0 + 4 * h);
-      e_sc[h] = *reinterpret_cast<const f32x4*>(sc + c0 + 4 * h);
-      e_sh[h] = *reinterpret_cast<const f32x4*>(sh + c0 + 4 * h);
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = pr2[h] = f32x2{0.f, 0.f};
-  }
-  if constexpr (STATS) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = f32x2{0.f, 0.f};
-  }
-  // Epilogue in groups of EG rows per thread, in three straight-line phases: (1) every global load
-  // of the group (residual addend, mask reference, BN inputs) — rows past M and absent addends read
-  // a valid stand-in address instead of branching; (2) all arithmetic; (3) all stores. No load is
-  // consumed after a store is issued and no load sits under divergent control flow, so hipcc waits
-  // with counted vmcnt instead of draining the queue (stores count in vmcnt too) once per row.
-  constexpr int NIT = BM * CPR / NT;
-  constexpr int EGMAX = 4;  // BN epilogues hold 4-5 vectors per row: stay clear of spills
-  constexpr int EG = NIT < EGMAX ? NIT : EGMAX;
-  const bool sub_geom = MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1));  // wave-uniform
-  const bool tail = m0 + BM > a.M;                                                  // wave-uniform
-#pragma unroll
-  for (int g0 = 0; g0 < NIT; g0 += EG) {
-    u32x4 vv[EG], va[EG], vy[EG], vy2[EG], va2[EG];
-    unsigned vm[EG];  // EPI 1: this chunk's 8 mask bits
-    size_t ee[EG];
-    bool ok[EG], has_add[EG];
-#pragma unroll
-    for (int k = 0; k < EG; ++k) {
-      const int row = (tid + (g0 + k) * NT) / CPR;
-      const int m = m0 + row;
-      ok[k] = m < a.M;
-      const int mc = ok[k] ? m : m0;  // m0 < M for every launched tile
-      vv[k] = *reinterpret_cast<const u32x4*>(sC + row * (BN + 8) + ccol * 8);
-      size_t pix = (size_t)mc;
-      int ph = 0, pw = 0, nimg = 0;
-      if (sub_geom) {
-        const int ohw = a.OH * a.OW;
-        const int n = mdiv_or(mc, a.mag_ohw, ohw), pq = mc - n * ohw;
-        const int i = mdiv_or(pq, a.mag_ow, a.OW), j = pq - i * a.OW;
-        ph = i * a.osub + a.oph; pw = j * a.osub + a.opw;
-        nimg = n;
-        pix = ((size_t)n * a.FH + ph) * a.FW + pw;
-      }
-      const size_t e = pix * a.OC + n0 + ccol * 8;
-      ee[k] = e;
-      if constexpr (ACCUM) {
-        size_t ae = e;
-        bool hv = true;
-        if (a.add_sub > 1) {
-          hv = (ph % a.add_sub) == 0 && (pw % a.add_sub) == 0;
-          const int hh = a.FH / a.add_sub, ww = a.FW / a.add_sub;
-          ae = hv ? (((size_t)nimg * hh + ph / a.add_sub) * ww + pw / a.add_sub) * a.OC + n0 + ccol * 8 : 0;
-        }
-        has_add[k] = hv;
-        va[k] = *reinterpret_cast<const u32x4*>((a.addsrc ? a.addsrc : a.y) + ae);
-      }
-      if constexpr (EPI > 0) {
-        vy[k] = *reinterpret_cast<const u32x4*>(a.ybn + e);
-        if constexpr (EPI == 1) vm[k] = a.mbits[e >> 3];
-        vy2[k] = *reinterpret_cast<const u32x4*>((has2 ? a.ybn2 : a.ybn) + e);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < EG; ++k) {
-      u32x4 v = vv[k];
-      if constexpr (ACCUM || EPI > 0) {
-        float f[8];
-        unpack8(v, f);
-        if constexpr (ACCUM) {
-          float g[8];
-          unpack8(va[k], g);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] += has_add[k] ? g[j] : 0.f;
-        }
-        if constexpr (EPI > 0) {
-          float yv[8];
-          unpack8(vy[k], yv);
-          if constexpr (EPI == 1) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = ((vm[k] >> j) & 1u) ? f[j] : 0.f;
-          } else {
-            float t[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              t[j] = yv[j] * e_sc[j >> 2][j & 3] + e_sh[j >> 2][j & 3];
-              f[j] = t[j] > 0.f ? f[j] : 0.f;
-            }
-            va2[k] = relu_bf16x8(pack8(t));  // the BN output itself (a.a_out write-back)
-          }
-          v = pack8(f);
-          // raw moments of the values actually stored (bf16-rounded): sum g, sum g*y (and g*y2);
-          // the centring/scaling by (mean, invstd) is applied once per channel after the
-          // reduction: sum g*xhat = inv * (sum g*y - mean * sum g). Rows past M contribute nothing.
-          const u32x4 vs = (tail && !ok[k]) ? zero4 : v;
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const f32x2 gr = {__uint_as_float(vs[h] << 16), __uint_as_float(vs[h] & 0xFFFF0000u)};
-            const f32x2 yr = {__uint_as_float(vy[k][h] << 16), __uint_as_float(vy[k][h] & 0xFFFF0000u)};
-            ps2[h] += gr;
-            pq2[h] = __builtin_elementwise_fma(gr, yr, pq2[h]);
-            if (has2) {
-              const f32x2 zr = {__uint_as_float(vy2[k][h] << 16), __uint_as_float(vy2[k][h] & 0xFFFF0000u)};
-              pr2[h] = __builtin_elementwise_fma(gr, zr, pr2[h]);
-            }
-          }
-        } else {
-          v = pack8(f);
-        }
-      }
-      if constexpr (STATS) {  // statistics of the stored values (ACCUM never combines with STATS)
-        const u32x4 vs = (tail && !ok[k]) ? zero4 : v;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {  // bf16 pair -> 2 floats: the bits shifted / masked in place
-          const f32x2 pr = {__uint_as_float(vs[h] << 16), __uint_as_float(vs[h] & 0xFFFF0000u)};
-          ps2[h] += pr;
-          pq2[h] = __builtin_elementwise_fma(pr, pr, pq2[h]);
-        }
-      }
-      vv[k] = v;
-    }
-#pragma unroll
-    for (int k = 0; k < EG; ++k)
-      if (ok[k]) *reinterpret_cast<u32x4*>(a.y + ee[k]) = vv[k];
-    if constexpr (EPI == 2) {
-      if (a.a_out) {  // wave-uniform
-#pragma unroll
-        for (int k = 0; k < EG; ++k)
-          if (ok[k]) *reinterpret_cast<u32x4*>(a.a_out + ee[k]) = va2[k];
-      }
-    }
-  }
-  if constexpr (STATS) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      bs[2 * h] = ps2[h].x; bs[2 * h + 1] = ps2[h].y;
-      bq1[2 * h] = pq2[h].x; bq1[2 * h + 1] = pq2[h].y;
-    }
-    // per-channel sum / sum of squares: in-wave lanes with the same chunk column by xor-shuffles,
-    // then the waves through LDS, then one fp64 atomic pair per channel into shard tm % nshard
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int o = CPR; o < 64; o <<= 1) {
-        bs[j] += __shfl_xor(bs[j], o, 64);
-        bq1[j] += __shfl_xor(bq1[j], o, 64);
-      }
-    }
-    __syncthreads();  // sC reuse
-    float* red = reinterpret_cast<float*>(lds);  // [NW waves][2][BN]
-    if (lane < CPR) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[(wid * 2 + 0) * BN + ccol * 8 + j] = bs[j];
-        red[(wid * 2 + 1) * BN + ccol * 8 + j] = bq1[j];
-      }
-    }
-    __syncthreads();
-    if (tid < BN) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) { s += red[(w * 2) * BN + tid]; q += red[(w * 2 + 1) * BN + tid]; }
-      double* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
-      atomicAdd(st + n0 + tid, (double)s);
-      atomicAdd(st + a.OC + n0 + tid, (double)q);
-    }
-  }
-  if constexpr (EPI > 0) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      bs[2 * h] = ps2[h].x; bs[2 * h + 1] = ps2[h].y;
-      bq1[2 * h] = pq2[h].x; bq1[2 * h + 1] = pq2[h].y;
-      bq2[2 * h] = pr2[h].x; bq2[2 * h + 1] = pr2[h].y;
-    }
-    // reduce the per-thread partials over threads with the same chunk column: in-wave lanes
-    // l, l+CPR, ... by xor-shuffles, then the 4 waves through LDS, then one atomic per channel
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int o = CPR; o < 64; o <<= 1) {
-        bs[j] += __shfl_xor(bs[j], o, 64);
-        bq1[j] += __shfl_xor(bq1[j], o, 64);
-        bq2[j] += __shfl_xor(bq2[j], o, 64);
-      }
-    }
-    __syncthreads();  // sC / sStat reuse
-    float* red = reinterpret_cast<float*>(lds);  // [NW waves][3][BN]
-    if (lane < CPR) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[(wid * 3 + 0) * BN + ccol * 8 + j] = bs[j];
-        red[(wid * 3 + 1) * BN + ccol * 8 + j] = bq1[j];
-        red[(wid * 3 + 2) * BN + ccol * 8 + j] = bq2[j];
-      }
-    }
-    __syncthreads();
-    if (tid < BN) {
-      float s = 0.f, q1 = 0.f, q2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        s += red[(w * 3 + 0) * BN + tid]; q1 += red[(w * 3 + 1) * BN + tid]; q2 += red[(w * 3 + 2) * BN + tid];
-      }
-      const int c = n0 + tid;  // raw moments -> sum g*xhat
-      q1 = a.inv1[c] * (q1 - a.mean1[c] * s);
-      if (has2) q2 = a.inv2[c] * (q2 - a.mean2[c] * s);
-      const int shard = (blockIdx.x % a.nshard);
-      double* st1 = a.bstats1 + (size_t)shard * 2 * a.OC;
-      atomicAdd(st1 + n0 + tid, (double)s);
-      atomicAdd(st1 + a.OC + n0 + tid, (double)q1);
-      if (a.bstats2) {
-        double* st2 = a.bstats2 + (size_t)shard * 2 * a.OC;
-        atomicAdd(st2 + n0 + tid, (double)s);
-        atomicAdd(st2 + a.OC + n0 + tid, (double)q2);
-      }
-    }
-  }
-  if (!more) break;
-  load_b(0);
-  advance();
-  __syncthreads();  // the epilogue's LDS reads are done before the next tile's staging writes
-  }
-}
 
 // ======================================================================================
 // Weight gradient: dW[k][kk] = sum_m dY[m][k] * Xcol[m][kk]   (kk = (r, s, c), KRSC order)
@@ -1037,83 +443,29 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
 
 }  // namespace dbx
 
-// ======================================================================================
-// host launchers (C ABI; raw pointers + stream, called from bindings.cpp)
-// ======================================================================================
 using namespace dbx;
 
-template <int BM, int BN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI, bool TAIL = false>
-static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
-  // tile shape -> wave layout: 128x128, 128x64, 64x64 on 2x2 waves (256 threads, 2 blocks/CU);
-  // 256x128 on 4x2 and 128x256 on 2x4 waves (512 threads, 1 block/CU, 96 KB LDS); 256x64 on 4x1
-  // waves (64x64 per wave like 128x128: 2/3 of the LDS bytes per MFMA of 64x32 wave tiles, for
-  // the 64-channel layers)
-  constexpr int WM = (BM == 256) ? 4 : 2;
-  constexpr int WN = (BN == 256) ? 4 : (BM == 256 && BN == 64) ? 1 : 2;
-  const int ntile = (a.OC / BN) * ((a.M + BM - 1) / BM);
-  // persistent grid: the resident capacity (occupancy x CUs), a multiple of 8 (XCD round-robin)
-  static const int cap = [] {
-    int per_cu = 0, dev = 0, cus = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(&igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI, TAIL>),
-        64 * WM * WN, 0);
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const char* e = getenv("DBX_PERSIST");
-    if ((e && e[0] == '0') || per_cu <= 0 || cus <= 0) return 1 << 30;
-    return (per_cu * cus) & ~7;
-  }();
-  constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64);  // persistent (see the kernel)
-  const int nwg = (!PF || ntile <= cap) ? ntile : cap;
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI, TAIL>), dim3(nwg), dim3(64 * WM * WN), 0, st, a);
-  return (int)hipGetLastError();
-}
+int dbx_dispatch_dgrad(int bm, int bn, const IGemmArgs& a, bool accum, int epi, int dma, hipStream_t st);  // conv_dgrad.hip
 
 template <int BM, int BN>
-static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, hipStream_t st) {
+static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, int dma, hipStream_t st) {
   if (a.res) {
     // the staged shortcut chunks push the 128x256 tile past 256 VGPRs: same-area 256x128 instead
     constexpr int TM = (BM == 128 && BN == 256) ? 256 : BM, TN = (BM == 128 && BN == 256) ? 128 : BN;
-    return stats ? launch_igemm_t<TM, TN, FWD, true, true, false, 0, true>(a, st)
-                 : launch_igemm_t<TM, TN, FWD, true, false, false, 0, true>(a, st);
+    if (stats) DBX_DMA_PRO(launch_igemm_t, TM, TN, FWD, true, true, false, 0, true);
+    DBX_DMA_PRO(launch_igemm_t, TM, TN, FWD, true, false, false, 0, true);
   }
-  if (pro) return stats ? launch_igemm_t<BM, BN, FWD, true, true, false, 0>(a, st) : launch_igemm_t<BM, BN, FWD, true, false, false, 0>(a, st);
-  return stats ? launch_igemm_t<BM, BN, FWD, false, true, false, 0>(a, st) : launch_igemm_t<BM, BN, FWD, false, false, false, 0>(a, st);
+  if (pro) {
+    if (stats) DBX_DMA_PRO(launch_igemm_t, BM, BN, FWD, true, true, false, 0, false);
+    DBX_DMA_PRO(launch_igemm_t, BM, BN, FWD, true, false, false, 0, false);
+  }
+  if (stats) DBX_DMA_PLAIN(launch_igemm_t, BM, BN, FWD, false, true, false, 0, false);
+  DBX_DMA_PLAIN(launch_igemm_t, BM, BN, FWD, false, false, false, 0, false);
 }
 
-template <int BM, int BN>
-static int dispatch_dgrad(const IGemmArgs& a, bool accum, int epi, hipStream_t st) {
-  if (a.res) {  // BN-backward apply prologue (1x1 stride-1 dgrads of the bottleneck)
-    constexpr int TM = (BM == 128 && BN == 256) ? 256 : BM, TN = (BM == 128 && BN == 256) ? 128 : BN;
-    if (accum) {
-      if (epi == 1) return launch_igemm_t<TM, TN, DGRAD, true, false, true, 1, true>(a, st);
-      if (epi == 0) return launch_igemm_t<TM, TN, DGRAD, true, false, true, 0, true>(a, st);
-      return -11;
-    }
-    if (epi == 2) return launch_igemm_t<TM, TN, DGRAD, true, false, false, 2, true>(a, st);
-    if (epi == 0) return launch_igemm_t<TM, TN, DGRAD, true, false, false, 0, true>(a, st);
-    return -11;
-  }
-  if (accum) {
-    if (epi == 1) return launch_igemm_t<BM, BN, DGRAD, false, false, true, 1>(a, st);
-    if (epi == 2) return launch_igemm_t<BM, BN, DGRAD, false, false, true, 2>(a, st);
-    return launch_igemm_t<BM, BN, DGRAD, false, false, true, 0>(a, st);
-  }
-  if (epi == 1) return launch_igemm_t<BM, BN, DGRAD, false, false, false, 1>(a, st);
-  if (epi == 2) return launch_igemm_t<BM, BN, DGRAD, false, false, false, 2>(a, st);
-  return launch_igemm_t<BM, BN, DGRAD, false, false, false, 0>(a, st);
-}
-
-#define DBX_TILES(F, ...)                                                         \
-  if (bm == 128 && bn == 128) return F<128, 128>(__VA_ARGS__);                    \
-  if (bm == 128 && bn == 64) return F<128, 64>(__VA_ARGS__);                      \
-  if (bm == 64 && bn == 64) return F<64, 64>(__VA_ARGS__);                        \
-  if (bm == 256 && bn == 128) return F<256, 128>(__VA_ARGS__);                    \
-  if (bm == 128 && bn == 256) return F<128, 256>(__VA_ARGS__);                    \
-  if (bm == 256 && bn == 64) return F<256, 64>(__VA_ARGS__);
 
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
-                              int accum, int epi, hipStream_t st) {
+                              int accum, int epi, hipStream_t st, int dma) {
   const IGemmArgs& a = *args;
   if (pro && mode == FWD && !a.relu_in) return -7;  // the forward BN prologue always ends in ReLU
   if (pro && a.IC > (a.res ? 1024 : 512)) return -8;  // prologue coefficients staged in LDS (PRO_MAXC)
@@ -1131,7 +483,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
   if (a.IC % 64 != 0) return -4;
   if (mode == FWD) {
     if (accum || epi) return -2;
-    DBX_TILES(dispatch_fwd, a, pro, stats, st)
+    DBX_TILES(dispatch_fwd, a, pro, stats, dma, st)
     return -3;
   }
   if (mode == DGRAD) {
@@ -1139,8 +491,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
     if (epi && (a.ybn == nullptr || a.bstats1 == nullptr || a.mean1 == nullptr || a.inv1 == nullptr)) return -6;
     if (epi == 1 && a.mbits == nullptr) return -6;
     if (epi == 2 && (a.bsc == nullptr || a.bsh == nullptr)) return -6;
-    DBX_TILES(dispatch_dgrad, a, accum, epi, st)
-    return -3;
+    return dbx_dispatch_dgrad(bm, bn, a, accum, epi, dma, st);
   }
   return -5;
 }

@@ -149,7 +149,9 @@ class ResNetProgram:
         self.fold_min = int(os.environ.get("DBX_FOLD_MIN_ELEMS", str(1 << 25)))
         # ... and only where the dgrad's output channels (N) are at most this multiple of its
         # reduction channels: every N tile of a folded dgrad re-reads and re-applies the operand
-        self.fold_max_ratio = float(os.environ.get("DBX_FOLD_MAX_RATIO", "inf"))
+        # (default 1: the bottleneck conv1 dgrads, N = 4K, stay unfolded -- 14.39-14.41k vs
+        # 14.22-14.27k img/s folded, ResNet-50 b1024, profiles/r2s3_fold/fold_ratio_ab.txt)
+        self.fold_max_ratio = float(os.environ.get("DBX_FOLD_MAX_RATIO", "1"))
         self._wstream = None
         self._side_pending = False
         self._build_layers()

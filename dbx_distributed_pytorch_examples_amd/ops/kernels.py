@@ -108,12 +108,28 @@ def pick_tile(M: int, OC: int, mode: str = "fwd", K_in: int = 0, R: int = 0, str
         if t is None and (mode == "fwdt" or mode.endswith("b")):  # prologue variants: the plain winner
             t = _tune_table().get(tune_key("fwd" if mode == "fwdt" else mode[:-1], M, OC, K_in, R, stride))
         if t is not None and OC % t[1] == 0:
-            return t
+            return t  # (bm, bn) or (bm, bn, dma): a measured operand path (tools/tune_conv.py)
     if OC % 128 == 0 and ((M + 127) // 128) * (OC // 128) >= 512:
         return 128, 128
     if ((M + 127) // 128) * (OC // 64) >= 384:
         return 128, 64
     return 64, 64
+
+
+_DMA_ENV = None
+
+
+def _tile_dma(t) -> Tuple[int, int, int]:
+    """(bm, bn[, dma]) -> (bm, bn, dma). ``dma`` is the conv operand path (conv_igemm_kernel.h):
+    0 register-staged, 1 weights by LDS-DMA (prologue convs), 2 / 3 both operands by LDS-DMA
+    through a 2- / 3-slot ring. DBX_CONV_DMA overrides every choice (A/B runs)."""
+    global _DMA_ENV
+    if _DMA_ENV is None:
+        import os
+        _DMA_ENV = int(os.environ.get("DBX_CONV_DMA", "-1"))
+    if _DMA_ENV >= 0:
+        return int(t[0]), int(t[1]), _DMA_ENV
+    return int(t[0]), int(t[1]), int(t[2]) if len(t) > 2 else 0
 
 
 # --------------------------------------------------------------------------------------
@@ -152,11 +168,11 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
             _chk(tail_out, torch.bfloat16, "tail_out", x.numel())
         if tail_bits is not None:
             _chk(tail_bits, torch.uint8, "tail_bits", x.numel() // 8)
-    bm, bn = tile or pick_tile(N * OH * OW, OC, "fwd" if tail_res is None else "fwdt", IC, R, stride)
+    bm, bn, dma = _tile_dma(tile or pick_tile(N * OH * OW, OC, "fwd" if tail_res is None else "fwdt", IC, R, stride))
     C().conv_igemm(FWD, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
                    R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
-                   _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr())
+                   _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma)
     return out
 
 
@@ -272,12 +288,12 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             if epilogue is not None or addsrc is not None:
                 raise ValueError("strided dgrad with empty phases cannot carry an epilogue / addend")
             continue
-        bm, bn = tile or pick_tile(N * ohs * ows, Cc, f"dgrad{epilogue.mode if epilogue else 0}"
-                                   + ("b" if bwd_y is not None else ""), K, R, stride)
+        bm, bn, dma = _tile_dma(tile or pick_tile(N * ohs * ows, Cc, f"dgrad{epilogue.mode if epilogue else 0}"
+                                                  + ("b" if bwd_y is not None else ""), K, R, stride))
         C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), bwd[0], bwd[1], 0, 0, NSHARD,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,
-                       _p(addsrc), add_sub, *epi, act_ptr, bwd[2], bwd[3], bwd[4], bwd[5], 0, stream_ptr())
+                       _p(addsrc), add_sub, *epi, act_ptr, bwd[2], bwd[3], bwd[4], bwd[5], 0, stream_ptr(), dma)
     return dx
 
 
@@ -298,7 +314,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
         raise ValueError("stem kernel supports R,S <= 8")
     C().conv_igemm(STEM, 128, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
-                   *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr())
+                   *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr(), 0)
     return out
 
 

@@ -35,17 +35,22 @@ def est(name, args, kw):
         N, IH, IW, IC = x.shape
         OC = w.shape[0]
         fl = 2 * out.numel() * w.shape[1]
-        return f"fwd {IC}->{OC} {kw['R']}x{kw['S']} s{kw['stride']} @{IH}", fl, _b(x) + _b(w) + _b(out)
+        by = _b(x) + _b(w) + _b(out) + _b(kw.get("tail_res")) + _b(kw.get("tail_out")) + _b(kw.get("tail_bits"))
+        tag = " tail" if kw.get("tail_res") is not None else (" pro" if kw.get("in_scale") is not None else "")
+        return f"fwd {IC}->{OC} {kw['R']}x{kw['S']} s{kw['stride']} @{IH}{tag}", fl, by
     if name == "conv_dgrad":
         dy, wt, dx = args[:3]
         N, P, Q, Kc = dy.shape
         fl = 2 * dy.numel() * wt.shape[0] * kw["R"] * kw["S"]
         epi = kw.get("epilogue")
-        by = _b(dy) + _b(wt) + _b(dx) + _b(kw.get("addsrc"))
-        tag = ""
+        by = _b(dy) + _b(wt) + _b(dx) + _b(kw.get("addsrc")) + _b(kw.get("bwd_y")) + _b(kw.get("dy_out"))
+        if kw.get("accumulate") and kw.get("addsrc") is None:
+            by += _b(dx)  # dx += result
+        tag = " fold" if kw.get("bwd_y") is not None else ""
         if epi is not None:
             by += _b(epi.ybn) + _b(epi.ybn2) + _b(epi.mbits)
-            tag = f" epi{epi.mode}"
+            by += _b(epi.act_out)
+            tag += f" epi{epi.mode}"
         return f"dgrad {Kc}->{dx.shape[3]} {kw['R']}x{kw['S']} s{kw['stride']} @{dx.shape[1]}{tag}", fl, by
     if name == "conv_wgrad":
         dy, x, dw = args[:3]

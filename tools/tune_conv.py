@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--report", default=None)
     ap.add_argument("--verbose", action="store_true", help="print every candidate's median time")
     ap.add_argument("--modes", default="fwd,fwdt,dgrad0,dgrad1,dgrad2,dgrad1b,dgrad2b,wgrad")
+    ap.add_argument("--dma", type=int, default=1,
+                    help="also time the LDS-DMA operand paths of the fwd / dgrad kernels (tile x path)")
     a = ap.parse_args()
     dev = "cuda"
     N = a.batch
@@ -131,8 +133,10 @@ def main():
                 continue
             if mode == "wgrad":  # tile x operand path (LDS-DMA ring depth 3 / 2, 0 = register staged)
                 cands = [t + (d,) for t in WGRAD_TILES if Kc % t[0] == 0 and C % t[1] == 0 for d in (3, 2, 0)]
-            else:
-                cands = [t for t in TILES if OCm % t[1] == 0]
+            else:  # tile x operand path: prologue convs 0 / 1 (weights by DMA), plain 0 / 2 / 3 (ring)
+                pro = mode in ("fwdt", "dgrad1b", "dgrad2b") or (mode == "fwd" and psc is not None)
+                dmas = ((0, 1) if pro else (0, 2, 3)) if a.dma else (0,)
+                cands = [t + (d,) for t in TILES if OCm % t[1] == 0 for d in dmas]
             res = {t: [] for t in cands}
             for _ in range(a.rounds):
                 for t in cands:
@@ -142,10 +146,10 @@ def main():
             if a.verbose:
                 print(f"  {mode} {C}->{Kc} {R}x{R} s{st} @{H}: " + "  ".join(
                     f"{'x'.join(map(str, t))}={v:.3f}" for t, v in sorted(med.items())), flush=True)
-            default = (K.pick_tile(M, OCm, use_table=False) if mode != "wgrad" else
+            default = (K.pick_tile(M, OCm, use_table=False) + (0,) if mode != "wgrad" else
                        (128 if Kc % 128 == 0 else 64, 128 if C % 128 == 0 else 64, 0))
             key = K.tune_key(mode, M, OCm, Kin, Rk, sk)
-            table[key] = list(best)
+            table[key] = list(best) if (mode == "wgrad" or best[2]) else list(best[:2])
             lines.append(f"| {C}→{Kc} | {R}x{R} s{st} | {H} | {cnt} | {mode} | {'x'.join(map(str, best))} | {med[best]:.3f} | "
                          f"{gf / med[best]:.0f} | {med.get(default, float('nan')):.3f} |")
             print(lines[-1], flush=True)
