@@ -27,13 +27,288 @@
 // (the prologue needs the data in registers anyway), one barrier per K block, XCD-aware
 // tile order (A-sharing tiles adjacent -> same XCD L2).
 #pragma once
+#include <type_traits>
 #include "common.h"
 #include "abi.h"
 
 namespace dbx {
 
-enum ConvMode { FWD = 0, DGRAD = 1, STEM = 2 };
+enum ConvMode { FWD = 0, DGRAD = 1, STEM = 2, FWD_PATCH = 3, DGRAD_PATCH = 4 };
 
+
+// ---- epilogue (shared by igemm_kernel and the 3x3 patch kernel) ---------------------------------
+// acc: this wave's (BM/WM) x (BN/WN) accumulators of the tile starting at output row m0 / channel n0;
+// lds: >= BM*(BN+8) bf16 + the reduction scratch; tm: the tile's M index (statistics shard);
+// shard: the BN-backward statistics shard selector. Ends with the LDS free for reuse after a barrier.
+template <int BM, int BN, int WM, int WN, int MODE, bool STATS, bool ACCUM, int EPI, int EGMAX = 4>
+__device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x4 (&acc)[BM / (16 * WM)][BN / (16 * WN)],
+                                               bf16* lds, const int m0, const int n0, const int tm,
+                                               const int shard) {
+  constexpr int NT = 64 * WM * WN, NW = WM * WN;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const u32x4 zero4 = {0u, 0u, 0u, 0u};
+  // acc[i][j][r] (C^T): pixel row = wm*BM/WM + i*16 + (lane&15), channel = wn*BN/WN + j*16 + (lane>>4)*4 + r
+  // staged bf16 through LDS ([BM][BN+8]: the 8-byte writes of a wave hit each bank 4 times, the
+  // minimum for 512 B) and re-read as 16-byte row chunks for coalesced global stores
+  static_assert(!(STATS && EPI), "forward BN statistics and BN-backward epilogues are exclusive");
+  bf16* sC = lds;  // [BM][BN+8]
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wm * (BM / WM) + i * 16 + (lane & 15);
+      const int col = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
+      *reinterpret_cast<uint2*>(sC + row * (BN + 8) + col) =
+          uint2{pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3])};
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 16B chunks per output row; a thread's chunk column is fixed
+  const int ccol = tid % CPR;
+  // per-thread partial sums of this thread's 8 channels: STATS: sum y, sum y^2 of the stored
+  // (bf16-rounded) outputs; EPI: BN-backward raw moments
+  float bs[8], bq1[8], bq2[8];
+  // accumulated in packed fp32 (v_pk_add_f32 / v_pk_fma_f32: 2 channels per instruction):
+  // ps2 = sum, pq2 = sum of squares (STATS) or sum g*y (EPI), pr2 = sum g*y2 (EPI)
+  f32x2 ps2[4], pq2[4], pr2[4];
+  f32x4 e_m1[2], e_i1[2], e_m2[2], e_i2[2], e_sc[2], e_sh[2];
+  const bool has2 = EPI > 0 && a.ybn2 != nullptr;  // wave-uniform: second BN (downsample branch)
+  if constexpr (EPI > 0) {
+    // vector loads of the per-channel coefficients; absent ones read a valid stand-in (no branch)
+    int c0 = n0 + ccol * 8;
+    // opaque to the optimiser: in a persistent caller these tile-invariant loads would otherwise be
+    // hoisted out of its tile loop and hold 48 VGPRs across the MFMA loop
+    asm volatile("" : "+v"(c0));
+    const float* m2 = has2 ? a.mean2 : a.mean1;
+    const float* i2 = has2 ? a.inv2 : a.inv1;
+    const float* sc = (EPI == 2) ? a.bsc : a.mean1;
+    const float* sh = (EPI == 2) ? a.bsh : a.inv1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      e_m1[h] = *reinterpret_cast<const f32x4*>(a.mean1 + c0 + 4 * h);
+      e_i1[h] = *reinterpret_cast<const f32x4*>(a.inv1 + c0 + 4 * h);
+      e_m2[h] = *reinterpret_cast<const f32x4*>(m2 + c0 + 4 * h);
+      e_i2[h] = *reinterpret_cast<const f32x4*>(i2 + c0 + 4 * h);
+      e_sc[h] = *reinterpret_cast<const f32x4*>(sc + c0 + 4 * h);
+      e_sh[h] = *reinterpret_cast<const f32x4*>(sh + c0 + 4 * h);
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = pr2[h] = f32x2{0.f, 0.f};
+  }
+  if constexpr (STATS) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = f32x2{0.f, 0.f};
+  }
+  // Epilogue in groups of EG rows per thread, in three straight-line phases: (1) every global load
+  // of the group (residual addend, mask reference, BN inputs) — rows past M and absent addends read
+  // a valid stand-in address instead of branching; (2) all arithmetic; (3) all stores. No load is
+  // consumed after a store is issued and no load sits under divergent control flow, so hipcc waits
+  // with counted vmcnt instead of draining the queue (stores count in vmcnt too) once per row.
+  constexpr int NIT = BM * CPR / NT;
+  // EGMAX (default 4): BN epilogues hold 4-5 vectors per row: stay clear of spills
+  constexpr int EG = NIT < EGMAX ? NIT : EGMAX;
+  const bool sub_geom = MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1));  // wave-uniform
+  const bool tail = m0 + BM > a.M;                                                  // wave-uniform
+  // one group of G rows per thread (G = EG, and a final NIT % EG group when EG does not tile NIT)
+  auto group = [&](const int g0, auto gcount) __attribute__((always_inline)) {
+    constexpr int G = decltype(gcount)::value;
+    u32x4 vv[G], va[G], vy[G], vy2[G], va2[G];
+    unsigned vm[G];  // EPI 1: this chunk's 8 mask bits
+    size_t ee[G];
+    bool ok[G], has_add[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int row = (tid + (g0 + k) * NT) / CPR;
+      const int m = m0 + row;
+      ok[k] = m < a.M;
+      const int mc = ok[k] ? m : m0;  // m0 < M for every launched tile
+      vv[k] = *reinterpret_cast<const u32x4*>(sC + row * (BN + 8) + ccol * 8);
+      size_t pix = (size_t)mc;
+      int ph = 0, pw = 0, nimg = 0;
+      if (sub_geom) {
+        const int ohw = a.OH * a.OW;
+        const int n = mdiv_or(mc, a.mag_ohw, ohw), pq = mc - n * ohw;
+        const int i = mdiv_or(pq, a.mag_ow, a.OW), j = pq - i * a.OW;
+        ph = i * a.osub + a.oph; pw = j * a.osub + a.opw;
+        nimg = n;
+        pix = ((size_t)n * a.FH + ph) * a.FW + pw;
+      }
+      const size_t e = pix * a.OC + n0 + ccol * 8;
+      ee[k] = e;
+      if constexpr (ACCUM) {
+        size_t ae = e;
+        bool hv = true;
+        if (a.add_sub > 1) {
+          hv = (ph % a.add_sub) == 0 && (pw % a.add_sub) == 0;
+          const int hh = a.FH / a.add_sub, ww = a.FW / a.add_sub;
+          ae = hv ? (((size_t)nimg * hh + ph / a.add_sub) * ww + pw / a.add_sub) * a.OC + n0 + ccol * 8 : 0;
+        }
+        has_add[k] = hv;
+        va[k] = *reinterpret_cast<const u32x4*>((a.addsrc ? a.addsrc : a.y) + ae);
+      }
+      if constexpr (EPI > 0) {
+        vy[k] = *reinterpret_cast<const u32x4*>(a.ybn + e);
+        if constexpr (EPI == 1) vm[k] = a.mbits[e >> 3];
+        vy2[k] = *reinterpret_cast<const u32x4*>((has2 ? a.ybn2 : a.ybn) + e);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      u32x4 v = vv[k];
+      if constexpr (ACCUM || EPI > 0) {
+        float f[8];
+        unpack8(v, f);
+        if constexpr (ACCUM) {
+          float g[8];
+          unpack8(va[k], g);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] += has_add[k] ? g[j] : 0.f;
+        }
+        if constexpr (EPI > 0) {
+          float yv[8];
+          unpack8(vy[k], yv);
+          if constexpr (EPI == 1) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = ((vm[k] >> j) & 1u) ? f[j] : 0.f;
+          } else {
+            float t[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              t[j] = yv[j] * e_sc[j >> 2][j & 3] + e_sh[j >> 2][j & 3];
+              f[j] = t[j] > 0.f ? f[j] : 0.f;
+            }
+            va2[k] = relu_bf16x8(pack8(t));  // the BN output itself (a.a_out write-back)
+          }
+          v = pack8(f);
+          // raw moments of the values actually stored (bf16-rounded): sum g, sum g*y (and g*y2);
+          // the centring/scaling by (mean, invstd) is applied once per channel after the
+          // reduction: sum g*xhat = inv * (sum g*y - mean * sum g). Rows past M contribute nothing.
+          const u32x4 vs = (tail && !ok[k]) ? zero4 : v;
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const f32x2 gr = {__uint_as_float(vs[h] << 16), __uint_as_float(vs[h] & 0xFFFF0000u)};
+            const f32x2 yr = {__uint_as_float(vy[k][h] << 16), __uint_as_float(vy[k][h] & 0xFFFF0000u)};
+            ps2[h] += gr;
+            pq2[h] = __builtin_elementwise_fma(gr, yr, pq2[h]);
+            if (has2) {
+              const f32x2 zr = {__uint_as_float(vy2[k][h] << 16), __uint_as_float(vy2[k][h] & 0xFFFF0000u)};
+              pr2[h] = __builtin_elementwise_fma(gr, zr, pr2[h]);
+            }
+          }
+        } else {
+          v = pack8(f);
+        }
+      }
+      if constexpr (STATS) {  // statistics of the stored values (ACCUM never combines with STATS)
+        const u32x4 vs = (tail && !ok[k]) ? zero4 : v;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {  // bf16 pair -> 2 floats: the bits shifted / masked in place
+          const f32x2 pr = {__uint_as_float(vs[h] << 16), __uint_as_float(vs[h] & 0xFFFF0000u)};
+          ps2[h] += pr;
+          pq2[h] = __builtin_elementwise_fma(pr, pr, pq2[h]);
+        }
+      }
+      vv[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+      if (ok[k]) *reinterpret_cast<u32x4*>(a.y + ee[k]) = vv[k];
+    if constexpr (EPI == 2) {
+      if (a.a_out) {  // wave-uniform
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+          if (ok[k]) *reinterpret_cast<u32x4*>(a.a_out + ee[k]) = va2[k];
+      }
+    }
+  };
+#pragma unroll
+  for (int g0 = 0; g0 + EG <= NIT; g0 += EG) group(g0, std::integral_constant<int, EG>{});
+  if constexpr (NIT % EG != 0) group(NIT - NIT % EG, std::integral_constant<int, NIT % EG>{});
+  if constexpr (STATS) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      bs[2 * h] = ps2[h].x; bs[2 * h + 1] = ps2[h].y;
+      bq1[2 * h] = pq2[h].x; bq1[2 * h + 1] = pq2[h].y;
+    }
+    // per-channel sum / sum of squares: in-wave lanes with the same chunk column by xor-shuffles,
+    // then the waves through LDS, then one fp64 atomic pair per channel into shard tm % nshard
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        bs[j] += __shfl_xor(bs[j], o, 64);
+        bq1[j] += __shfl_xor(bq1[j], o, 64);
+      }
+    }
+    __syncthreads();  // sC reuse
+    float* red = reinterpret_cast<float*>(lds);  // [NW waves][2][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wid * 2 + 0) * BN + ccol * 8 + j] = bs[j];
+        red[(wid * 2 + 1) * BN + ccol * 8 + j] = bq1[j];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) { s += red[(w * 2) * BN + tid]; q += red[(w * 2 + 1) * BN + tid]; }
+      double* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
+      atomicAdd(st + n0 + tid, (double)s);
+      atomicAdd(st + a.OC + n0 + tid, (double)q);
+    }
+  }
+  if constexpr (EPI > 0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      bs[2 * h] = ps2[h].x; bs[2 * h + 1] = ps2[h].y;
+      bq1[2 * h] = pq2[h].x; bq1[2 * h + 1] = pq2[h].y;
+      bq2[2 * h] = pr2[h].x; bq2[2 * h + 1] = pr2[h].y;
+    }
+    // reduce the per-thread partials over threads with the same chunk column: in-wave lanes
+    // l, l+CPR, ... by xor-shuffles, then the 4 waves through LDS, then one atomic per channel
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        bs[j] += __shfl_xor(bs[j], o, 64);
+        bq1[j] += __shfl_xor(bq1[j], o, 64);
+        bq2[j] += __shfl_xor(bq2[j], o, 64);
+      }
+    }
+    __syncthreads();  // sC / sStat reuse
+    float* red = reinterpret_cast<float*>(lds);  // [NW waves][3][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wid * 3 + 0) * BN + ccol * 8 + j] = bs[j];
+        red[(wid * 3 + 1) * BN + ccol * 8 + j] = bq1[j];
+        red[(wid * 3 + 2) * BN + ccol * 8 + j] = bq2[j];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float s = 0.f, q1 = 0.f, q2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        s += red[(w * 3 + 0) * BN + tid]; q1 += red[(w * 3 + 1) * BN + tid]; q2 += red[(w * 3 + 2) * BN + tid];
+      }
+      const int c = n0 + tid;  // raw moments -> sum g*xhat
+      q1 = a.inv1[c] * (q1 - a.mean1[c] * s);
+      if (has2) q2 = a.inv2[c] * (q2 - a.mean2[c] * s);
+      const int shard = (shard % a.nshard);
+      double* st1 = a.bstats1 + (size_t)shard * 2 * a.OC;
+      atomicAdd(st1 + n0 + tid, (double)s);
+      atomicAdd(st1 + a.OC + n0 + tid, (double)q1);
+      if (a.bstats2) {
+        double* st2 = a.bstats2 + (size_t)shard * 2 * a.OC;
+        atomicAdd(st2 + n0 + tid, (double)s);
+        atomicAdd(st2 + a.OC + n0 + tid, (double)q2);
+      }
+    }
+  }
+}
 
 // TAIL (with PRO), A = x*s + h + (res*rs + rh) computed while staging; the first N tile writes A
 // back (tail_out). FWD: the previous residual block's output relu(bn3(x) + shortcut) -- no separate
@@ -458,260 +733,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     load_a(0);
   }
 
-  // ---- epilogue ------------------------------------------------------------------------
-  // acc[i][j][r] (C^T): pixel row = wm*BM/WM + i*16 + (lane&15), channel = wn*BN/WN + j*16 + (lane>>4)*4 + r
-  // staged bf16 through LDS ([BM][BN+8]: the 8-byte writes of a wave hit each bank 4 times, the
-  // minimum for 512 B) and re-read as 16-byte row chunks for coalesced global stores
-  static_assert(!(STATS && EPI), "forward BN statistics and BN-backward epilogues are exclusive");
-  bf16* sC = lds;  // [BM][BN+8]
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int row = wm * (BM / WM) + i * 16 + (lane & 15);
-      const int col = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
-      *reinterpret_cast<uint2*>(sC + row * (BN + 8) + col) =
-          uint2{pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3])};
-    }
-  __syncthreads();
-  constexpr int CPR = BN / 8;  // 16B chunks per output row; a thread's chunk column is fixed
-  const int ccol = tid % CPR;
-  // per-thread partial sums of this thread's 8 channels: STATS: sum y, sum y^2 of the stored
-  // (bf16-rounded) outputs; EPI: BN-backward raw moments
-  float bs[8], bq1[8], bq2[8];
-  // accumulated in packed fp32 (v_pk_add_f32 / v_pk_fma_f32: 2 channels per instruction):
-  // ps2 = sum, pq2 = sum of squares (STATS) or sum g*y (EPI), pr2 = sum g*y2 (EPI)
-  f32x2 ps2[4], pq2[4], pr2[4];
-  f32x4 e_m1[2], e_i1[2], e_m2[2], e_i2[2], e_sc[2], e_sh[2];
-  const bool has2 = EPI > 0 && a.ybn2 != nullptr;  // wave-uniform: second BN (downsample branch)
-  if constexpr (EPI > 0) {
-    // vector loads of the per-channel coefficients; absent ones read a valid stand-in (no branch)
-    const int c0 = n0 + ccol * 8;
-    const float* m2 = has2 ? a.mean2 : a.mean1;
-    const float* i2 = has2 ? a.inv2 : a.inv1;
-    const float* sc = (EPI == 2) ? a.bsc : a.mean1;
-    const float* sh = (EPI == 2) ? a.bsh : a.inv1;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      e_m1[h] = *reinterpret_cast<const f32x4*>(a.mean1 + c0 + 4 * h);
-      e_i1[h] = *reinterpret_cast<const f32x4*>(a.inv1 + c0 + 4 * h);
-      e_m2[h] = *reinterpret_cast<const f32x4*>(m2 + c0 + 4 * h);
-      e_i2[h] = *reinterpret_cast<const f32x4*>(i2 + c0 + 4 * h);
-      e_sc[h] = *reinterpret_cast<const f32x4*>(sc + c0 + 4 * h);
-      e_sh[h] = *reinterpret_cast<const f32x4*>(sh + c0 + 4 * h);
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = pr2[h] = f32x2{0.f, 0.f};
-  }
-  if constexpr (STATS) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = f32x2{0.f, 0.f};
-  }
-  // Epilogue in groups of EG rows per thread, in three straight-line phases: (1) every global load
-  // of the group (residual addend, mask reference, BN inputs) — rows past M and absent addends read
-  // a valid stand-in address instead of branching; (2) all arithmetic; (3) all stores. No load is
-  // consumed after a store is issued and no load sits under divergent control flow, so hipcc waits
-  // with counted vmcnt instead of draining the queue (stores count in vmcnt too) once per row.
-  constexpr int NIT = BM * CPR / NT;
-  constexpr int EGMAX = 4;  // BN epilogues hold 4-5 vectors per row: stay clear of spills
-  constexpr int EG = NIT < EGMAX ? NIT : EGMAX;
-  const bool sub_geom = MODE == DGRAD && (a.osub > 1 || (ACCUM && a.add_sub > 1));  // wave-uniform
-  const bool tail = m0 + BM > a.M;                                                  // wave-uniform
-#pragma unroll
-  for (int g0 = 0; g0 < NIT; g0 += EG) {
-    u32x4 vv[EG], va[EG], vy[EG], vy2[EG], va2[EG];
-    unsigned vm[EG];  // EPI 1: this chunk's 8 mask bits
-    size_t ee[EG];
-    bool ok[EG], has_add[EG];
-#pragma unroll
-    for (int k = 0; k < EG; ++k) {
-      const int row = (tid + (g0 + k) * NT) / CPR;
-      const int m = m0 + row;
-      ok[k] = m < a.M;
-      const int mc = ok[k] ? m : m0;  // m0 < M for every launched tile
-      vv[k] = *reinterpret_cast<const u32x4*>(sC + row * (BN + 8) + ccol * 8);
-      size_t pix = (size_t)mc;
-      int ph = 0, pw = 0, nimg = 0;
-      if (sub_geom) {
-        const int ohw = a.OH * a.OW;
-        const int n = mdiv_or(mc, a.mag_ohw, ohw), pq = mc - n * ohw;
-        const int i = mdiv_or(pq, a.mag_ow, a.OW), j = pq - i * a.OW;
-        ph = i * a.osub + a.oph; pw = j * a.osub + a.opw;
-        nimg = n;
-        pix = ((size_t)n * a.FH + ph) * a.FW + pw;
-      }
-      const size_t e = pix * a.OC + n0 + ccol * 8;
-      ee[k] = e;
-      if constexpr (ACCUM) {
-        size_t ae = e;
-        bool hv = true;
-        if (a.add_sub > 1) {
-          hv = (ph % a.add_sub) == 0 && (pw % a.add_sub) == 0;
-          const int hh = a.FH / a.add_sub, ww = a.FW / a.add_sub;
-          ae = hv ? (((size_t)nimg * hh + ph / a.add_sub) * ww + pw / a.add_sub) * a.OC + n0 + ccol * 8 : 0;
-        }
-        has_add[k] = hv;
-        va[k] = *reinterpret_cast<const u32x4*>((a.addsrc ? a.addsrc : a.y) + ae);
-      }
-      if constexpr (EPI > 0) {
-        vy[k] = *reinterpret_cast<const u32x4*>(a.ybn + e);
-        if constexpr (EPI == 1) vm[k] = a.mbits[e >> 3];
-        vy2[k] = *reinterpret_cast<const u32x4*>((has2 ? a.ybn2 : a.ybn) + e);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < EG; ++k) {
-      u32x4 v = vv[k];
-      if constexpr (ACCUM || EPI > 0) {
-        float f[8];
-        unpack8(v, f);
-        if constexpr (ACCUM) {
-          float g[8];
-          unpack8(va[k], g);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] += has_add[k] ? g[j] : 0.f;
-        }
-        if constexpr (EPI > 0) {
-          float yv[8];
-          unpack8(vy[k], yv);
-          if constexpr (EPI == 1) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = ((vm[k] >> j) & 1u) ? f[j] : 0.f;
-          } else {
-            float t[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              t[j] = yv[j] * e_sc[j >> 2][j & 3] + e_sh[j >> 2][j & 3];
-              f[j] = t[j] > 0.f ? f[j] : 0.f;
-            }
-            va2[k] = relu_bf16x8(pack8(t));  // the BN output itself (a.a_out write-back)
-          }
-          v = pack8(f);
-          // raw moments of the values actually stored (bf16-rounded): sum g, sum g*y (and g*y2);
-          // the centring/scaling by (mean, invstd) is applied once per channel after the
-          // reduction: sum g*xhat = inv * (sum g*y - mean * sum g). Rows past M contribute nothing.
-          const u32x4 vs = (tail && !ok[k]) ? zero4 : v;
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const f32x2 gr = {__uint_as_float(vs[h] << 16), __uint_as_float(vs[h] & 0xFFFF0000u)};
-            const f32x2 yr = {__uint_as_float(vy[k][h] << 16), __uint_as_float(vy[k][h] & 0xFFFF0000u)};
-            ps2[h] += gr;
-            pq2[h] = __builtin_elementwise_fma(gr, yr, pq2[h]);
-            if (has2) {
-              const f32x2 zr = {__uint_as_float(vy2[k][h] << 16), __uint_as_float(vy2[k][h] & 0xFFFF0000u)};
-              pr2[h] = __builtin_elementwise_fma(gr, zr, pr2[h]);
-            }
-          }
-        } else {
-          v = pack8(f);
-        }
-      }
-      if constexpr (STATS) {  // statistics of the stored values (ACCUM never combines with STATS)
-        const u32x4 vs = (tail && !ok[k]) ? zero4 : v;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {  // bf16 pair -> 2 floats: the bits shifted / masked in place
-          const f32x2 pr = {__uint_as_float(vs[h] << 16), __uint_as_float(vs[h] & 0xFFFF0000u)};
-          ps2[h] += pr;
-          pq2[h] = __builtin_elementwise_fma(pr, pr, pq2[h]);
-        }
-      }
-      vv[k] = v;
-    }
-#pragma unroll
-    for (int k = 0; k < EG; ++k)
-      if (ok[k]) *reinterpret_cast<u32x4*>(a.y + ee[k]) = vv[k];
-    if constexpr (EPI == 2) {
-      if (a.a_out) {  // wave-uniform
-#pragma unroll
-        for (int k = 0; k < EG; ++k)
-          if (ok[k]) *reinterpret_cast<u32x4*>(a.a_out + ee[k]) = va2[k];
-      }
-    }
-  }
-  if constexpr (STATS) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      bs[2 * h] = ps2[h].x; bs[2 * h + 1] = ps2[h].y;
-      bq1[2 * h] = pq2[h].x; bq1[2 * h + 1] = pq2[h].y;
-    }
-    // per-channel sum / sum of squares: in-wave lanes with the same chunk column by xor-shuffles,
-    // then the waves through LDS, then one fp64 atomic pair per channel into shard tm % nshard
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int o = CPR; o < 64; o <<= 1) {
-        bs[j] += __shfl_xor(bs[j], o, 64);
-        bq1[j] += __shfl_xor(bq1[j], o, 64);
-      }
-    }
-    __syncthreads();  // sC reuse
-    float* red = reinterpret_cast<float*>(lds);  // [NW waves][2][BN]
-    if (lane < CPR) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[(wid * 2 + 0) * BN + ccol * 8 + j] = bs[j];
-        red[(wid * 2 + 1) * BN + ccol * 8 + j] = bq1[j];
-      }
-    }
-    __syncthreads();
-    if (tid < BN) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) { s += red[(w * 2) * BN + tid]; q += red[(w * 2 + 1) * BN + tid]; }
-      double* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
-      atomicAdd(st + n0 + tid, (double)s);
-      atomicAdd(st + a.OC + n0 + tid, (double)q);
-    }
-  }
-  if constexpr (EPI > 0) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      bs[2 * h] = ps2[h].x; bs[2 * h + 1] = ps2[h].y;
-      bq1[2 * h] = pq2[h].x; bq1[2 * h + 1] = pq2[h].y;
-      bq2[2 * h] = pr2[h].x; bq2[2 * h + 1] = pr2[h].y;
-    }
-    // reduce the per-thread partials over threads with the same chunk column: in-wave lanes
-    // l, l+CPR, ... by xor-shuffles, then the 4 waves through LDS, then one atomic per channel
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int o = CPR; o < 64; o <<= 1) {
-        bs[j] += __shfl_xor(bs[j], o, 64);
-        bq1[j] += __shfl_xor(bq1[j], o, 64);
-        bq2[j] += __shfl_xor(bq2[j], o, 64);
-      }
-    }
-    __syncthreads();  // sC / sStat reuse
-    float* red = reinterpret_cast<float*>(lds);  // [NW waves][3][BN]
-    if (lane < CPR) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[(wid * 3 + 0) * BN + ccol * 8 + j] = bs[j];
-        red[(wid * 3 + 1) * BN + ccol * 8 + j] = bq1[j];
-        red[(wid * 3 + 2) * BN + ccol * 8 + j] = bq2[j];
-      }
-    }
-    __syncthreads();
-    if (tid < BN) {
-      float s = 0.f, q1 = 0.f, q2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        s += red[(w * 3 + 0) * BN + tid]; q1 += red[(w * 3 + 1) * BN + tid]; q2 += red[(w * 3 + 2) * BN + tid];
-      }
-      const int c = n0 + tid;  // raw moments -> sum g*xhat
-      q1 = a.inv1[c] * (q1 - a.mean1[c] * s);
-      if (has2) q2 = a.inv2[c] * (q2 - a.mean2[c] * s);
-      const int shard = (blockIdx.x % a.nshard);
-      double* st1 = a.bstats1 + (size_t)shard * 2 * a.OC;
-      atomicAdd(st1 + n0 + tid, (double)s);
-      atomicAdd(st1 + a.OC + n0 + tid, (double)q1);
-      if (a.bstats2) {
-        double* st2 = a.bstats2 + (size_t)shard * 2 * a.OC;
-        atomicAdd(st2 + n0 + tid, (double)s);
-        atomicAdd(st2 + a.OC + n0 + tid, (double)q2);
-      }
-    }
-  }
+  igemm_epilogue<BM, BN, WM, WN, MODE, STATS, ACCUM, EPI>(a, acc, lds, m0, n0, tm, blockIdx.x);
   if (!more) break;
   load_b(0);
   advance();

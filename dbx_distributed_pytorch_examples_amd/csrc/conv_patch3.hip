@@ -1,0 +1,217 @@
+// 3x3 stride-1 convolutions of the 64-channel ResNet stage as a weights-stationary "patch" kernel.
+//
+// The implicit-GEMM kernel (conv_igemm_kernel.h) stages one (pixel x 64-channel) block of A per
+// filter tap, so every input element is gathered, BN-transformed (forward prologue) and written to
+// LDS nine times. For the 64 -> 64 3x3 convs at 56x56 (N = 64: little MFMA work per staged byte)
+// that made them VALU- and latency-bound at ~18 % MFMA (profiles/r2s3_patch/). Here a workgroup
+// owns TR full output rows of one image (BM = TR * W pixels) and
+//   * keeps ALL 9 x 64 x 64 weights resident in LDS (loaded once per workgroup: persistent grid),
+//   * stages the input patch (TR + 2 rows x W + 2 columns x 64 channels, halo zero-filled) ONCE
+//     per tile, applying the BN prologue once per element,
+//   * runs the 9 taps straight out of the patch (tap = an address offset; no barrier inside the
+//     K loop), the next tile's patch loads in flight in registers meanwhile,
+//   * finishes with the shared igemm epilogue (BN statistics / BN-backward MASK_Y epilogue).
+// FWD:   Y[n,h,w,k]  = sum_{r,s,c} act(X[n,h-1+r,w-1+s,c]) W[k][r][s][c]
+// DGRAD: dX[n,h,w,c] = sum_{r,s,k} dY[n,h+1-r,w+1-s,k] Wt[c][r][s][k]     (3x3, pad 1, stride 1)
+// Weight rows use the conv kernels' XOR swizzle (chunk ^ ((row >> 1) & 7)). The patch swizzle is a
+// function of the OUTPUT-linear index x = p - 2 * (p / PC) (= q + dr*W + ds for the pixel a tap reads):
+// chunk ^ (x & 6). A tap shifts the 16 pixels of a fragment by an arbitrary (often odd) amount, and
+// (x & 6) is the swizzle under which every lane group of a ds_read_b128 fragment read hits 16
+// distinct 16-byte bank groups for every shift (found by exhaustive search over the gfx950 lane
+// groups; the row swizzle (x >> 1) & 7 gave 2-way conflicts on odd shifts).
+#include "conv_igemm_kernel.h"
+
+namespace dbx {
+
+template <int MODE, bool PRO, bool STATS, int EPI, int TR, int WIDTH>
+__global__ __launch_bounds__(512, 1) void patch3_kernel(const IGemmArgs a) {
+  constexpr int C = 64, BN = 64;          // input / output channels of the patch convs
+  constexpr int WM = 4, WN = 2, NT = 512;  // 8 waves: each (BM/4) pixels x 32 channels
+  constexpr int BM = TR * WIDTH;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  static_assert(BM % (16 * WM) == 0, "tile rows must split into 16-row MFMA blocks per wave");
+  constexpr int PC = WIDTH + 2, PR = TR + 2, PPIX = PR * PC;
+  constexpr int PCH = PPIX * 8;               // 16-byte chunks of one patch image
+  constexpr int PU = (PCH + NT - 1) / NT;     // patch chunks per thread
+  constexpr int WCH = 9 * BN * 8;             // weight chunks (9 taps x 64 rows x 8)
+  static_assert(WCH % NT == 0, "weight staging");
+  constexpr int LDS_W = 9 * BN * C;           // bf16 elements
+  constexpr int LDS_P = PPIX * C;
+  static_assert(LDS_P >= BM * (BN + 8), "the epilogue stages its tile through the patch image");
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_W + LDS_P];
+  bf16* sW = lds;
+  bf16* sP = lds + LDS_W;
+  __shared__ float sPro[2 * C];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int H = a.OH;  // stride 1, pad 1: output rows == input rows
+  const int ntile = a.N * H / TR;
+
+  // ---- resident weights: B[tap][n][k] (FWD: W[n][tap*64 + k]; DGRAD: Wt[n][tap*64 + k]) --------
+#pragma unroll
+  for (int u = 0; u < WCH / NT; ++u) {
+    const int e = tid + NT * u;           // chunk: (tap, row n, chunk ch)
+    const int ch = e & 7, n = (e >> 3) & 63, tap = e >> 9;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(a.w + (size_t)n * (9 * C) + tap * C + ch * 8);
+    *reinterpret_cast<u32x4*>(sW + tap * BN * C + n * C + ((ch ^ ((n >> 1) & 7)) << 3)) = v;
+  }
+  if constexpr (PRO) {
+    for (int c = tid; c < C; c += NT) { sPro[c] = a.in_scale[c]; sPro[C + c] = a.in_shift[c]; }
+  }
+
+  // ---- patch staging: chunk e = tid + NT*u -> patch pixel p = e / 8 (row p / PC, col p % PC) -------
+  const rsrc_t xr = make_rsrc(a.x, 2ull * a.N * H * WIDTH * C);
+  u32x4 pv[PU];
+  unsigned pval = 0;  // bit u: chunk u is an in-image pixel (padding stays exactly zero after PRO)
+  auto load_patch = [&](int t) __attribute__((always_inline)) {
+    const int g0 = t * TR, n = g0 / H, h0 = g0 - n * H;
+    pval = 0;
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const int e = tid + NT * u;
+      const int p = e >> 3, ch = e & 7;
+      const int pr = p / PC, pc = p - pr * PC;
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const bool v = e < PCH && t < ntile && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)WIDTH;
+      pv[u] = buf_load16(xr, v ? 2u * (unsigned)((((n * H + h) * WIDTH) + w) * C + ch * 8) : kOOB);
+      pval |= (v ? 1u : 0u) << u;
+    }
+  };
+  auto store_patch = [&]() __attribute__((always_inline)) {
+    // this thread's 8 channels are the same for every chunk (NT % 8 == 0): coefficients read once
+    f32x4 s0, s1, h0, h1;
+    if constexpr (PRO) {
+      s0 = *reinterpret_cast<const f32x4*>(sPro + (tid & 7) * 8);
+      s1 = *reinterpret_cast<const f32x4*>(sPro + (tid & 7) * 8 + 4);
+      h0 = *reinterpret_cast<const f32x4*>(sPro + C + (tid & 7) * 8);
+      h1 = *reinterpret_cast<const f32x4*>(sPro + C + (tid & 7) * 8 + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const int e = tid + NT * u;
+      if (PCH % NT != 0 && e >= PCH) break;  // (only the last chunk set can be partial)
+      const int p = e >> 3, ch = e & 7;
+      u32x4 v = pv[u];
+      if constexpr (PRO) {
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f[j] = f[j] * s0[j] + h0[j];
+          f[j + 4] = f[j + 4] * s1[j] + h1[j];
+        }
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        v = ((pval >> u) & 1u) ? relu_bf16x8(pack8(f)) : z;
+      }
+      const int x = p - 2 * (p / PC);
+      *reinterpret_cast<u32x4*>(sP + p * C + ((ch ^ (x & 6)) << 3)) = v;
+    }
+  };
+
+  // ---- per-lane fragment geometry ------------------------------------------------------------
+  // A: output pixel q = wm*(BM/WM) + i*16 + (lane & 15) of the tile -> patch pixel of tap (0, 0)
+  int pbase[TM], qbase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int q = wm * (BM / WM) + i * 16 + (lane & 15);
+    const int oi = q / WIDTH, oj = q - oi * WIDTH;
+    pbase[i] = oi * PC + oj;
+    qbase[i] = q;
+  }
+  const int kq = lane >> 4;  // chunk within a 32-wide K step: ks*4 + kq
+
+  int t = blockIdx.x;
+  load_patch(t);
+  __syncthreads();  // sPro
+  store_patch();
+  f32x4 acc[TM][TN];
+  for (;;) {
+    __syncthreads();  // patch(t) (and on the first tile the weights) visible
+    const int tn = t + gridDim.x;
+    if (tn < ntile) load_patch(tn);  // in flight during the MFMAs (workgroup-uniform branch)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // Fragment reads are software-pipelined one half-tap ahead (two register sets: the reads of
+    // step k+1 are in flight while step k's 14 MFMAs issue). Taps are not unrolled: per-tap
+    // fragment addresses are computed in the loop instead of being hoisted out of the persistent
+    // loop by the compiler (7 x 9 x 2 live addresses would spill).
+    bf16x8 afA[TM], bfA[TN], afB[TM], bfB[TN];
+    auto frags = [&](int tap, int ks, bf16x8 (&af)[TM], bf16x8 (&bf)[TN]) __attribute__((always_inline)) {
+      const int r = tap / 3, s = tap - 3 * r;
+      // FWD reads input (h - 1 + r, w - 1 + s) = patch (oi + r, oj + s); DGRAD reads dY at
+      // (h + 1 - r, w + 1 - s) = patch (oi + 2 - r, oj + 2 - s)
+      const int dr = (MODE == DGRAD) ? 2 - r : r, ds = (MODE == DGRAD) ? 2 - s : s;
+      const int doff = dr * PC + ds, dx = dr * WIDTH + ds;
+      const int ch = ks * 4 + kq;
+      const bf16* cB = sW + tap * BN * C;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (BN / WN) + j * 16 + (lane & 15);
+        bf[j] = *reinterpret_cast<const bf16x8*>(cB + row * C + ((ch ^ ((row >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int p = pbase[i] + doff, x = qbase[i] + dx;
+        af[i] = *reinterpret_cast<const bf16x8*>(sP + p * C + ((ch ^ (x & 6)) << 3));
+      }
+    };
+    auto mma = [&](const bf16x8 (&af)[TM], const bf16x8 (&bf)[TN]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    };
+    frags(0, 0, afA, bfA);
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      frags(tap, 1, afB, bfB);
+      mma(afA, bfA);
+      frags(tap < 8 ? tap + 1 : 8, 0, afA, bfA);  // (past the last tap: a harmless re-read)
+      mma(afB, bfB);
+    }
+    __syncthreads();  // every wave is done with patch(t): the epilogue stages through it
+    // (row groups of 2 in the BN-backward epilogue: the next patch's registers stay live across it)
+    igemm_epilogue<BM, BN, WM, WN, MODE, STATS, false, EPI, (EPI ? 2 : 4)>(a, acc, sP, t * BM, 0, t, blockIdx.x);
+    if (tn >= ntile) break;
+    __syncthreads();  // the epilogue's LDS reads are done
+    store_patch();
+    t = tn;
+  }
+}
+
+}  // namespace dbx
+
+using namespace dbx;
+
+// Geometry the patch kernel covers: 3x3, stride 1, pad 1, 64 -> 64 channels, width 56, H % 8 == 0.
+extern "C" int dbx_conv_patch3(int mode, const IGemmArgs* args, int pro, int stats, int epi, hipStream_t st) {
+  const IGemmArgs& a = *args;
+  if (a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1 || a.IC != 64 || a.OC != 64) return -20;
+  if (a.OW != 56 || a.IW != 56 || a.OH != a.IH || a.OH % 8 != 0) return -21;
+  const int ntile = a.N * a.OH / 8;
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  const int nwg = ntile < cus ? ntile : cus;
+  if (mode == FWD) {
+    if (epi) return -22;
+    if (pro && stats) hipLaunchKernelGGL((patch3_kernel<FWD, true, true, 0, 8, 56>), dim3(nwg), dim3(512), 0, st, a);
+    else if (pro) hipLaunchKernelGGL((patch3_kernel<FWD, true, false, 0, 8, 56>), dim3(nwg), dim3(512), 0, st, a);
+    else if (stats) hipLaunchKernelGGL((patch3_kernel<FWD, false, true, 0, 8, 56>), dim3(nwg), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((patch3_kernel<FWD, false, false, 0, 8, 56>), dim3(nwg), dim3(512), 0, st, a);
+  } else if (mode == DGRAD) {
+    if (pro || stats || epi == 1) return -22;
+    if (a.osub != 1 || a.addsrc) return -23;
+    if (epi == 2) hipLaunchKernelGGL((patch3_kernel<DGRAD, false, false, 2, 8, 56>), dim3(nwg), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((patch3_kernel<DGRAD, false, false, 0, 8, 56>), dim3(nwg), dim3(512), 0, st, a);
+  } else {
+    return -24;
+  }
+  return (int)hipGetLastError();
+}

@@ -20,7 +20,7 @@ from ..utils import debug as _debug
 from . import reference as _ref
 from ._ext import C, stream_ptr, use_native
 
-FWD, DGRAD, STEM = 0, 1, 2
+FWD, DGRAD, STEM, FWD_PATCH, DGRAD_PATCH = 0, 1, 2, 3, 4
 # addsrc, add_sub, epi, mbits, ybn, ybn2, bsc, bsh, mean1, inv1, mean2, inv2, bstats1, bstats2
 _NO_EPI = (0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
 MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
@@ -132,6 +132,30 @@ def _tile_dma(t) -> Tuple[int, int, int]:
     return int(t[0]), int(t[1]), int(t[2]) if len(t) > 2 else 0
 
 
+_PATCH3 = None
+
+
+def patch3_supported(IC: int, OC: int, R: int, S: int, stride: int, pad: int, H: int, W: int) -> bool:
+    """Geometry of the weights-stationary 3x3 patch kernel (csrc/conv_patch3.hip)."""
+    return (R == 3 and S == 3 and stride == 1 and pad == 1 and IC == 64 and OC == 64 and W == 56
+            and H % 8 == 0)
+
+
+def _use_patch3(tile, mode: str) -> bool:
+    """tile == "patch" forces the patch kernel, an explicit (bm, bn[, dma]) the implicit GEMM;
+    otherwise DBX_PATCH3 decides: "fwd" (default: the forward convs; their data gradients stay on
+    the implicit GEMM, which overlaps the BN-backward epilogue's loads better), "all", or "0"."""
+    global _PATCH3
+    if isinstance(tile, str):
+        return tile == "patch"
+    if tile is not None:
+        return False
+    if _PATCH3 is None:
+        import os
+        _PATCH3 = os.environ.get("DBX_PATCH3", "fwd")
+    return _PATCH3 == "all" or _PATCH3 == mode
+
+
 # --------------------------------------------------------------------------------------
 # convolutions
 # --------------------------------------------------------------------------------------
@@ -168,8 +192,15 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
             _chk(tail_out, torch.bfloat16, "tail_out", x.numel())
         if tail_bits is not None:
             _chk(tail_bits, torch.uint8, "tail_bits", x.numel() // 8)
-    bm, bn, dma = _tile_dma(tile or pick_tile(N * OH * OW, OC, "fwd" if tail_res is None else "fwdt", IC, R, stride))
-    C().conv_igemm(FWD, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
+    mode = FWD
+    if tail_res is None and patch3_supported(IC, OC, R, S, stride, pad, IH, IW) and _use_patch3(tile, "fwd"):
+        mode, bm, bn, dma = FWD_PATCH, 0, 0, 0
+    else:
+        if isinstance(tile, str):
+            raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 conv at width 56")
+        bm, bn, dma = _tile_dma(tile or pick_tile(N * OH * OW, OC, "fwd" if tail_res is None else "fwdt", IC, R,
+                                                  stride))
+    C().conv_igemm(mode, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
                    R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
                    _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma)
@@ -277,6 +308,14 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             _chk(dy_out, torch.bfloat16, "dy_out", dy.numel())
         c0 = bwd_coeff.data_ptr()
         bwd = (c0, c0 + 8 * K, bwd_y.data_ptr(), c0 + 4 * K, 0, _p(dy_out))
+    if (not accumulate and bwd_y is None and (epilogue is None or epilogue.mode == MASK_Y)
+            and patch3_supported(K, Cc, R, S, stride, pad, H, W) and _use_patch3(tile, "dgrad")):
+        C().conv_igemm(DGRAD_PATCH, 0, 0, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
+                       N, P, Q, K, H, W, Cc, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, H, W,
+                       0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), 0)
+        return dx
+    if isinstance(tile, str):
+        raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 dgrad at width 56 (no addend / fold)")
     phases = dgrad_phases(H, W, R, S, stride, pad)
     if not accumulate and any(ph[5] == 0 or ph[7] == 0 for ph in phases):
         if epilogue is not None:
@@ -318,12 +357,20 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
     return out
 
 
+_WG_ROUNDS = None
+
+
 def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int) -> Tuple[int, int]:
     """Split the pixel reduction so that ~1024 workgroups stream (>= 8 K-blocks each); the
     workspace holds nsplit slabs + up to 64 level-1 partial slabs of the reduction."""
+    global _WG_ROUNDS
+    if _WG_ROUNDS is None:
+        import os
+        _WG_ROUNDS = float(os.environ.get("DBX_WGRAD_ROUNDS", "2"))
     tiles = (OC // bm) * (KTOT // bn)
-    # ~4 rounds of workgroups over the 256 CUs: 8-wave (256-wide) tiles run one per CU, 4-wave two
-    target = max(1, (512 if max(bm, bn) >= 256 else 1024) // tiles)
+    # _WG_ROUNDS rounds of workgroups over the 256 CUs (8-wave (256-wide) tiles run one per CU,
+    # 4-wave two): fewer rounds = longer workgroups and proportionally smaller fp32 partial slabs
+    target = max(1, int(_WG_ROUNDS * (256 if max(bm, bn) >= 256 else 512)) // tiles)
     ms = max(512, ((M + target - 1) // target + 63) // 64 * 64)
     nsplit = (M + ms - 1) // ms
     while (nsplit + min(64, nsplit)) * OC * KTOT > max_ws_elems and nsplit > 1:

@@ -1,0 +1,95 @@
+"""Weights-stationary 3x3 patch kernel (csrc/conv_patch3.hip) vs the implicit-GEMM path.
+
+Same tap order, same MFMA operand roles and fp32 accumulation order as the implicit GEMM, so the
+conv outputs (and the MASK_Y epilogue's masked gradient / BN-output write-back) must be
+bit-identical; the BN statistics are sums of different per-tile fp32 partials (448-row tiles
+instead of 128) and are compared with a tolerance. The implicit GEMM itself is checked against
+fp32 PyTorch in test_kernels_gpu.py.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def K():
+    from dbx_distributed_pytorch_examples_amd.ops import kernels
+    return kernels
+
+
+def _close_stats(a, b, count):
+    a, b = a.view(-1, 2, 64).sum(0), b.view(-1, 2, 64).sum(0)
+    return ((a - b).abs() / (b.abs() + count * 1e-3)).max().item()
+
+
+@pytest.mark.parametrize("N,H", [(2, 56), (3, 16), (1, 8)])
+@pytest.mark.parametrize("prologue", [True, False])
+def test_patch3_fwd_matches_igemm(N, H, prologue):
+    k = K()
+    torch.manual_seed(7)
+    W, C = 56, 64
+    assert k.patch3_supported(C, C, 3, 3, 1, 1, H, W)
+    x = torch.randn(N, H, W, C, device=dev).bfloat16()
+    w = (torch.randn(C, 9 * C, device=dev) / math.sqrt(9 * C)).bfloat16()
+    sc = sh = None
+    if prologue:
+        sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    outs = []
+    for tile in ((128, 64), "patch"):
+        y = torch.full((N, H, W, C), float("nan"), device=dev, dtype=torch.bfloat16)
+        st = k.new_stats(C, dev)
+        k.conv_fwd(x, w, y, R=3, S=3, stride=1, pad=1, stats=st, in_scale=sc, in_shift=sh, tile=tile)
+        outs.append((y, st))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert _close_stats(outs[1][1], outs[0][1], N * H * W) < 1e-5
+
+
+@pytest.mark.parametrize("N,H", [(2, 56), (3, 16)])
+@pytest.mark.parametrize("epi", [None, "mask_y"])
+def test_patch3_dgrad_matches_igemm(N, H, epi):
+    k = K()
+    torch.manual_seed(8)
+    W, C = 56, 64
+    w = (torch.randn(C, 3, 3, C, device=dev) / math.sqrt(9 * C)).bfloat16()
+    wt = w.permute(3, 1, 2, 0).contiguous().view(C, -1)
+    dy = torch.randn(N, H, W, C, device=dev).bfloat16()
+    ybn = torch.randn(N, H, W, C, device=dev).bfloat16()
+    sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    mean, inv = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    outs = []
+    for tile in ((256, 64), "patch"):
+        dx = torch.full((N, H, W, C), float("nan"), device=dev, dtype=torch.bfloat16)
+        st = k.new_stats(C, dev)
+        act = torch.full_like(dx, float("nan"))
+        e = None
+        if epi:
+            e = k.BNBwdEpilogue(k.MASK_Y, ybn, mean, inv, st, scale=sc, shift=sh, act_out=act)
+        k.conv_dgrad(dy, wt, dx, R=3, S=3, stride=1, pad=1, epilogue=e, tile=tile)
+        outs.append((dx, st, act))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    if epi:
+        assert torch.equal(outs[0][2], outs[1][2])
+        assert _close_stats(outs[1][1], outs[0][1], N * H * W) < 1e-5
+
+
+def test_patch3_default_routing_and_fallbacks():
+    """Eligible convs take the patch kernel by default; an addend / stride / other width falls back."""
+    k = K()
+    assert not k.patch3_supported(64, 64, 3, 3, 2, 1, 56, 56)
+    assert not k.patch3_supported(128, 128, 3, 3, 1, 1, 28, 28)
+    assert not k.patch3_supported(64, 64, 3, 3, 1, 1, 12, 56)
+    torch.manual_seed(9)
+    x = torch.randn(1, 8, 56, 64, device=dev).bfloat16()
+    w = (torch.randn(64, 9 * 64, device=dev) / 24).bfloat16()
+    y1, y2 = torch.empty_like(x), torch.empty_like(x)
+    k.conv_fwd(x, w, y1, R=3, S=3, stride=1, pad=1)
+    k.conv_fwd(x, w, y2, R=3, S=3, stride=1, pad=1, tile="patch")
+    assert torch.equal(y1, y2)
+    with pytest.raises(ValueError):
+        k.conv_fwd(torch.randn(1, 8, 28, 64, device=dev).bfloat16(), w, torch.empty(1, 8, 28, 64, device=dev).bfloat16(),
+                   R=3, S=3, stride=1, pad=1, tile="patch")

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Patch kernel: correctness vs the implicit GEMM, single-conv timing, headline bench A/B.
+set -o pipefail
+mkdir -p gpurun_out/r2s3
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_conv_patch3_gpu.py > gpurun_out/r2s3/t_patch.log 2>&1 || { echo "patch tests FAILED"; tail -30 gpurun_out/r2s3/t_patch.log; exit 1; }
+tail -1 gpurun_out/r2s3/t_patch.log
+for c in "fwd3x3_64 128,64,1" "fwd3x3_64 patch" "dgrad3x3_64 256,64,2" "dgrad3x3_64 patch"; do
+  set -- $c
+  timeout -k 10 60 python tools/conv_probe.py --case $1 --tile $2 --iters 9
+done
+for r in 1 2; do
+  for v in 0 1; do
+    DBX_PATCH3=$v timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/r2s3/patch_$v.log 2>&1 || { echo "bench $v FAILED"; tail -20 gpurun_out/r2s3/patch_$v.log; exit 1; }
+    echo "patch3=$v: $(tail -1 gpurun_out/r2s3/patch_$v.log | cut -c80-140)"
+  done
+done
+bash tools/gpu_r2s3_rounds.sh
