@@ -446,7 +446,8 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
 using namespace dbx;
 
 int dbx_dispatch_dgrad(int bm, int bn, const IGemmArgs& a, bool accum, int epi, int dma, hipStream_t st);  // conv_dgrad.hip
-extern "C" int dbx_conv_patch3(int mode, const IGemmArgs* args, int pro, int stats, int epi, hipStream_t st);
+extern "C" int dbx_conv_patch3(int mode, const IGemmArgs* args, int pro, int stats, int epi, hipStream_t st,
+                               int streamed);
 
 template <int BM, int BN>
 static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, int dma, hipStream_t st) {
@@ -470,7 +471,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
   const IGemmArgs& a = *args;
   if (mode == FWD_PATCH || mode == DGRAD_PATCH) {  // 3x3 weights-stationary patch kernel (conv_patch3.hip)
     if (pro && !a.relu_in) return -7;
-    return dbx_conv_patch3(mode == FWD_PATCH ? FWD : DGRAD, args, pro, stats, epi, st);
+    return dbx_conv_patch3(mode == FWD_PATCH ? FWD : DGRAD, args, pro, stats, epi, st, dma);  // dma: 1 = streamed
   }
   if (pro && mode == FWD && !a.relu_in) return -7;  // the forward BN prologue always ends in ReLU
   if (pro && a.IC > (a.res ? 1024 : 512)) return -8;  // prologue coefficients staged in LDS (PRO_MAXC)

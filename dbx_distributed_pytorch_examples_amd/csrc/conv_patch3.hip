@@ -182,15 +182,191 @@ __global__ __launch_bounds__(512, 1) void patch3_kernel(const IGemmArgs a) {
   }
 }
 
+
+// Streamed-weights variant: 4 waves, one tile of TR rows per workgroup (not persistent), the patch
+// by LDS-DMA (no prologue) or register-staged (BN prologue), the 9 per-tap weight blocks by
+// LDS-DMA through a 3-slot ring. ~68 KB of LDS instead of ~148 KB: two workgroups share a CU, so
+// one's epilogue (the BN-backward MASK_Y epilogue streams three tensors) overlaps the other's MFMAs
+// -- which the single resident-weights workgroup per CU cannot do.
+template <int MODE, bool PRO, bool STATS, int EPI, int TR, int WIDTH>
+__global__ __launch_bounds__(256, 2) void patch3s_kernel(const IGemmArgs a) {
+  constexpr int C = 64, BN = 64;
+  constexpr int WM = 2, WN = 2, NT = 256, NW = 4;
+  constexpr int BM = TR * WIDTH;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  static_assert(BM % (16 * WM) == 0, "tile rows must split into 16-row MFMA blocks per wave");
+  constexpr int PC = WIDTH + 2, PR = TR + 2, PPIX = PR * PC;
+  constexpr int PCH = PPIX * 8;                      // 16-byte chunks of the patch image
+  constexpr int PDI = (PCH + 64 * NW - 1) / (64 * NW);  // patch DMA instructions per wave
+  constexpr int LDS_P = PDI * NW * 64 * 8;           // bf16 elements (whole 1 KiB DMA pieces)
+  constexpr int NB = 3;                              // weight ring slots
+  constexpr int WSLOT = BN * C;                      // one tap's weights
+  static_assert(LDS_P >= BM * (BN + 8), "the epilogue stages its tile through the patch image");
+  __shared__ __attribute__((aligned(1024))) bf16 lds[LDS_P + NB * WSLOT];
+  bf16* sP = lds;
+  bf16* sW = lds + LDS_P;
+  __shared__ float sPro[2 * C];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int H = a.OH;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int g0 = t * TR, n = g0 / H, h0 = g0 - n * H;
+  const unsigned lbase = lds_addr(lds);
+  const i32x4 wsrd = make_srd(a.w, 2ull * BN * 9 * C);
+
+  // weights of tap k -> ring slot k % NB: lane fills row wr = 8*(wid + NW*i) + lane/8, slot lane%8
+  // with source chunk slot ^ ((row >> 1) & 7) (the row swizzle, inverted at the source)
+  auto dma_w = [&](int tap) __attribute__((always_inline)) {
+    const unsigned dst = lbase + 2u * (unsigned)(LDS_P + (tap % NB) * WSLOT) + 1024u * (unsigned)wid;
+#pragma unroll
+    for (int i = 0; i < WSLOT / 8 / (64 * NW); ++i) {
+      const int row = 8 * (wid + NW * i) + (lane >> 3);
+      const int src = (lane & 7) ^ ((row >> 1) & 7);
+      const unsigned off = tap < 9 ? 2u * (unsigned)(row * 9 * C + tap * C + src * 8) : kOOB;
+      lds_dma16(wsrd, off, dst + 1024u * (unsigned)(NW * i));
+    }
+  };
+  constexpr int WDI = WSLOT / 8 / (64 * NW);  // weight DMA instructions per wave and tap
+
+  // ---- patch ------------------------------------------------------------------------------
+  if constexpr (!PRO) {
+    const i32x4 xsrd = make_srd(a.x, 2ull * a.N * H * WIDTH * C);
+#pragma unroll
+    for (int i = 0; i < PDI; ++i) {
+      const int e = 64 * (wid + NW * i) + lane;  // LDS chunk position
+      const int p = e >> 3;
+      const int pr = p / PC, pc = p - pr * PC;
+      const int x = p - 2 * pr;
+      const int ch = (lane & 7) ^ (x & 6);
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const bool v = e < PCH && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)WIDTH;
+      lds_dma16(xsrd, v ? 2u * (unsigned)((((n * H + h) * WIDTH) + w) * C + ch * 8) : kOOB,
+                lbase + 1024u * (unsigned)(wid + NW * i));
+    }
+    dma_w(0);
+    dma_w(1);
+  } else {
+    dma_w(0);
+    dma_w(1);
+    for (int c = tid; c < C; c += NT) { sPro[c] = a.in_scale[c]; sPro[C + c] = a.in_shift[c]; }
+    __syncthreads();
+    const rsrc_t xr = make_rsrc(a.x, 2ull * a.N * H * WIDTH * C);
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(sPro + (tid & 7) * 8);
+    const f32x4 s1 = *reinterpret_cast<const f32x4*>(sPro + (tid & 7) * 8 + 4);
+    const f32x4 f0 = *reinterpret_cast<const f32x4*>(sPro + C + (tid & 7) * 8);
+    const f32x4 f1 = *reinterpret_cast<const f32x4*>(sPro + C + (tid & 7) * 8 + 4);
+    constexpr int PU = (PCH + NT - 1) / NT;
+    u32x4 pv[PU];
+    unsigned pval = 0;
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const int e = tid + NT * u;
+      const int p = e >> 3, ch = e & 7;
+      const int pr = p / PC, pc = p - pr * PC;
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const bool v = e < PCH && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)WIDTH;
+      pv[u] = buf_load16(xr, v ? 2u * (unsigned)((((n * H + h) * WIDTH) + w) * C + ch * 8) : kOOB);
+      pval |= (v ? 1u : 0u) << u;
+    }
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const int e = tid + NT * u;
+      if (PCH % NT != 0 && e >= PCH) break;
+      const int p = e >> 3, ch = e & 7;
+      float f[8];
+      unpack8(pv[u], f);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[j] = f[j] * s0[j] + f0[j];
+        f[j + 4] = f[j + 4] * s1[j] + f1[j];
+      }
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      const int x = p - 2 * (p / PC);
+      *reinterpret_cast<u32x4*>(sP + p * C + ((ch ^ (x & 6)) << 3)) = ((pval >> u) & 1u) ? relu_bf16x8(pack8(f)) : z;
+    }
+  }
+
+  // ---- MFMAs: 9 taps out of the patch, weights through the ring -----------------------------
+  int pbase[TM], qbase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int q = wm * (BM / WM) + i * 16 + (lane & 15);
+    const int oi = q / WIDTH, oj = q - oi * WIDTH;
+    pbase[i] = oi * PC + oj;
+    qbase[i] = q;
+  }
+  const int kq = lane >> 4;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int tap = 0; tap < 9; ++tap) {
+    // this wave's share of tap's weights (and, at tap 0, of the patch) has landed; the barrier
+    // publishes every wave's and retires the slot the next issue overwrites
+    dma_wait<WDI>();
+    __syncthreads();
+    dma_w(tap + 2);
+    const int r = tap / 3, s = tap - 3 * r;
+    const int dr = (MODE == DGRAD) ? 2 - r : r, ds = (MODE == DGRAD) ? 2 - s : s;
+    const int doff = dr * PC + ds, dx = dr * WIDTH + ds;
+    const bf16* cB = sW + (tap % NB) * WSLOT;
+    bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + kq;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (BN / WN) + j * 16 + (lane & 15);
+        bfr[ks][j] = *reinterpret_cast<const bf16x8*>(cB + row * C + ((ch ^ ((row >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int p = pbase[i] + doff, x = qbase[i] + dx;
+        af[ks][i] = *reinterpret_cast<const bf16x8*>(sP + p * C + ((ch ^ (x & 6)) << 3));
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+  }
+  dma_wait<0>();
+  __syncthreads();  // every wave is done with the patch: the epilogue stages through it
+  igemm_epilogue<BM, BN, WM, WN, MODE, STATS, false, EPI>(a, acc, sP, t * BM, 0, t, blockIdx.x);
+}
+
 }  // namespace dbx
 
 using namespace dbx;
 
 // Geometry the patch kernel covers: 3x3, stride 1, pad 1, 64 -> 64 channels, width 56, H % 8 == 0.
-extern "C" int dbx_conv_patch3(int mode, const IGemmArgs* args, int pro, int stats, int epi, hipStream_t st) {
+extern "C" int dbx_conv_patch3(int mode, const IGemmArgs* args, int pro, int stats, int epi, hipStream_t st,
+                               int streamed) {
   const IGemmArgs& a = *args;
   if (a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1 || a.IC != 64 || a.OC != 64) return -20;
   if (a.OW != 56 || a.IW != 56 || a.OH != a.IH || a.OH % 8 != 0) return -21;
+  if (streamed) {  // patch3s_kernel: 4-row tiles, one per workgroup, two workgroups per CU
+    const dim3 g(a.N * a.OH / 4), b(256);
+    if (mode == FWD) {
+      if (epi) return -22;
+      if (pro && stats) hipLaunchKernelGGL((patch3s_kernel<FWD, true, true, 0, 4, 56>), g, b, 0, st, a);
+      else if (pro) hipLaunchKernelGGL((patch3s_kernel<FWD, true, false, 0, 4, 56>), g, b, 0, st, a);
+      else if (stats) hipLaunchKernelGGL((patch3s_kernel<FWD, false, true, 0, 4, 56>), g, b, 0, st, a);
+      else hipLaunchKernelGGL((patch3s_kernel<FWD, false, false, 0, 4, 56>), g, b, 0, st, a);
+    } else if (mode == DGRAD) {
+      if (pro || stats || epi == 1 || a.osub != 1 || a.addsrc) return -22;
+      if (epi == 2) hipLaunchKernelGGL((patch3s_kernel<DGRAD, false, false, 2, 4, 56>), g, b, 0, st, a);
+      else hipLaunchKernelGGL((patch3s_kernel<DGRAD, false, false, 0, 4, 56>), g, b, 0, st, a);
+    } else {
+      return -24;
+    }
+    return (int)hipGetLastError();
+  }
   const int ntile = a.N * a.OH / 8;
   static const int cus = [] {
     int dev = 0, n = 0;

@@ -141,19 +141,23 @@ def patch3_supported(IC: int, OC: int, R: int, S: int, stride: int, pad: int, H:
             and H % 8 == 0)
 
 
-def _use_patch3(tile, mode: str) -> bool:
-    """tile == "patch" forces the patch kernel, an explicit (bm, bn[, dma]) the implicit GEMM;
-    otherwise DBX_PATCH3 decides: "fwd" (default: the forward convs; their data gradients stay on
-    the implicit GEMM, which overlaps the BN-backward epilogue's loads better), "all", or "0"."""
+def _use_patch3(tile, mode: str) -> int:
+    """0 = implicit GEMM, 1 = patch kernel with resident weights (one workgroup per CU), 2 = patch
+    kernel with streamed weights (two workgroups per CU). tile "patch" / "patch_r" / "patch_s"
+    forces one, an explicit (bm, bn[, dma]) the implicit GEMM; otherwise DBX_PATCH3 ("all" default,
+    "fwd", "dgrad" or "0") picks the convs and DBX_PATCH3_STREAM ("dgrad" default, "fwd", "all",
+    "0") the ones on the streamed-weights variant."""
     global _PATCH3
-    if isinstance(tile, str):
-        return tile == "patch"
-    if tile is not None:
-        return False
     if _PATCH3 is None:
         import os
-        _PATCH3 = os.environ.get("DBX_PATCH3", "fwd")
-    return _PATCH3 == "all" or _PATCH3 == mode
+        _PATCH3 = (os.environ.get("DBX_PATCH3", "all"), os.environ.get("DBX_PATCH3_STREAM", "dgrad"))
+    use, stream = _PATCH3
+    kind = 2 if stream in ("all", mode) else 1
+    if isinstance(tile, str):
+        return {"patch": kind, "patch_r": 1, "patch_s": 2}.get(tile, 0)
+    if tile is not None:
+        return 0
+    return kind if use in ("all", mode) else 0
 
 
 # --------------------------------------------------------------------------------------
@@ -193,8 +197,9 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
         if tail_bits is not None:
             _chk(tail_bits, torch.uint8, "tail_bits", x.numel() // 8)
     mode = FWD
-    if tail_res is None and patch3_supported(IC, OC, R, S, stride, pad, IH, IW) and _use_patch3(tile, "fwd"):
-        mode, bm, bn, dma = FWD_PATCH, 0, 0, 0
+    kind = _use_patch3(tile, "fwd") if tail_res is None and patch3_supported(IC, OC, R, S, stride, pad, IH, IW) else 0
+    if kind:
+        mode, bm, bn, dma = FWD_PATCH, 0, 0, kind - 1
     else:
         if isinstance(tile, str):
             raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 conv at width 56")
@@ -308,11 +313,12 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             _chk(dy_out, torch.bfloat16, "dy_out", dy.numel())
         c0 = bwd_coeff.data_ptr()
         bwd = (c0, c0 + 8 * K, bwd_y.data_ptr(), c0 + 4 * K, 0, _p(dy_out))
-    if (not accumulate and bwd_y is None and (epilogue is None or epilogue.mode == MASK_Y)
-            and patch3_supported(K, Cc, R, S, stride, pad, H, W) and _use_patch3(tile, "dgrad")):
+    kind = (_use_patch3(tile, "dgrad") if not accumulate and bwd_y is None and (epilogue is None or epilogue.mode == MASK_Y)
+            and patch3_supported(K, Cc, R, S, stride, pad, H, W) else 0)
+    if kind:
         C().conv_igemm(DGRAD_PATCH, 0, 0, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
                        N, P, Q, K, H, W, Cc, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, H, W,
-                       0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), 0)
+                       0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), kind - 1)
         return dx
     if isinstance(tile, str):
         raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 dgrad at width 56 (no addend / fold)")

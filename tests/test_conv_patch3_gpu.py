@@ -38,14 +38,15 @@ def test_patch3_fwd_matches_igemm(N, H, prologue):
     if prologue:
         sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
     outs = []
-    for tile in ((128, 64), "patch"):
+    for tile in ((128, 64), "patch_r", "patch_s"):
         y = torch.full((N, H, W, C), float("nan"), device=dev, dtype=torch.bfloat16)
         st = k.new_stats(C, dev)
         k.conv_fwd(x, w, y, R=3, S=3, stride=1, pad=1, stats=st, in_scale=sc, in_shift=sh, tile=tile)
         outs.append((y, st))
     torch.cuda.synchronize()
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert _close_stats(outs[1][1], outs[0][1], N * H * W) < 1e-5
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        assert _close_stats(o[1], outs[0][1], N * H * W) < 1e-5
 
 
 @pytest.mark.parametrize("N,H", [(2, 56), (3, 16)])
@@ -61,7 +62,7 @@ def test_patch3_dgrad_matches_igemm(N, H, epi):
     sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
     mean, inv = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
     outs = []
-    for tile in ((256, 64), "patch"):
+    for tile in ((256, 64), "patch_r", "patch_s"):
         dx = torch.full((N, H, W, C), float("nan"), device=dev, dtype=torch.bfloat16)
         st = k.new_stats(C, dev)
         act = torch.full_like(dx, float("nan"))
@@ -71,10 +72,11 @@ def test_patch3_dgrad_matches_igemm(N, H, epi):
         k.conv_dgrad(dy, wt, dx, R=3, S=3, stride=1, pad=1, epilogue=e, tile=tile)
         outs.append((dx, st, act))
     torch.cuda.synchronize()
-    assert torch.equal(outs[0][0], outs[1][0])
-    if epi:
-        assert torch.equal(outs[0][2], outs[1][2])
-        assert _close_stats(outs[1][1], outs[0][1], N * H * W) < 1e-5
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        if epi:
+            assert torch.equal(outs[0][2], o[2])
+            assert _close_stats(o[1], outs[0][1], N * H * W) < 1e-5
 
 
 def test_patch3_default_routing_and_fallbacks():

@@ -33,7 +33,7 @@ def main():
     kind, ch = a.case.split("3x3_")
     C, H = GEOM[ch]
     N, dev = a.batch, "cuda"
-    tile = (a.tile if a.tile == "patch" else tuple(int(v) for v in a.tile.split(","))) if a.tile else None
+    tile = (a.tile if a.tile.startswith("patch") else tuple(int(v) for v in a.tile.split(","))) if a.tile else None
     torch.manual_seed(0)
     x = torch.randn(N, H, H, C, device=dev).bfloat16()
     w = (torch.randn(C, 9 * C, device=dev) / math.sqrt(9 * C)).bfloat16()
