@@ -448,6 +448,7 @@ using namespace dbx;
 int dbx_dispatch_dgrad(int bm, int bn, const IGemmArgs& a, bool accum, int epi, int dma, hipStream_t st);  // conv_dgrad.hip
 extern "C" int dbx_conv_patch3(int mode, const IGemmArgs* args, int pro, int stats, int epi, hipStream_t st,
                                int streamed);
+extern "C" int dbx_stem_patch(const IGemmArgs* args, int stats, hipStream_t st);
 
 template <int BM, int BN>
 static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, int dma, hipStream_t st) {
@@ -482,6 +483,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
   if (a.OC % bn != 0) return -1;
   if (mode == STEM) {
     if (pro || accum || epi) return -2;
+    if (bm == 0) return dbx_stem_patch(args, stats, st);  // conv_patch3.hip
     if (bm == 128 && bn == 64) return stats ? launch_igemm_t<128, 64, STEM, false, true, false, 0>(a, st)
                                             : launch_igemm_t<128, 64, STEM, false, false, false, 0>(a, st);
     return -3;

@@ -340,6 +340,115 @@ __global__ __launch_bounds__(256, 2) void patch3s_kernel(const IGemmArgs a) {
   igemm_epilogue<BM, BN, WM, WN, MODE, STATS, false, EPI>(a, acc, sP, t * BM, 0, t, blockIdx.x);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// The 7x7 stride-2 stem on the NHWC4 image as a patch kernel. A tile is TR output rows x 112 (448
+// pixels); its input patch (2TR+5 rows x 232 columns x 4 channels, 16-byte chunks = pixel pairs,
+// columns -4..227 so a pair never straddles the image border) arrives by LDS-DMA, double-buffered
+// (the next tile's patch lands during this tile's MFMAs and epilogue). A K step is one filter row
+// r: 8 taps x 4 channels; the weights are shifted by one tap (s' = s + 1, s' = 0 is zero) so that
+// every fragment read is one aligned pixel pair: patch chunk (2*oi + r) * 116 + oj + kq. Filter row
+// 7 does not exist, so 7 K steps of 32 (224 padded K for 147 real; the implicit GEMM used 256).
+// All offsets of a fragment read are immediates off two per-lane bases; no per-step VALU.
+template <bool STATS, int TR>
+__global__ __launch_bounds__(512, 1) void stem_patch_kernel(const IGemmArgs a) {
+  constexpr int OW = 112, IW = 224, BN = 64;
+  constexpr int WM = 4, WN = 2, NT = 512, NW = 8;
+  constexpr int BM = TR * OW;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  static_assert(BM % (16 * WM) == 0, "tile rows");
+  constexpr int PCC = 116;                             // 16-byte chunks per patch row (232 pixels)
+  constexpr int PROWS = 2 * TR + 5;
+  constexpr int PCH = PROWS * PCC;
+  constexpr int PDI = (PCH + 64 * NW - 1) / (64 * NW);  // DMA instructions per wave per patch
+  constexpr int PBUF = PDI * NW * 64 * 8;              // bf16 elements per patch buffer
+  constexpr int WP = 240;                              // weight row pitch (224 + 16: conflict-free)
+  constexpr int LDS_C = BM * (BN + 8);
+  __shared__ __attribute__((aligned(1024))) bf16 lds[2 * PBUF + BN * WP + LDS_C];
+  bf16* sP = lds;                  // [2][PBUF]
+  bf16* sW = lds + 2 * PBUF;       // [64][WP]
+  bf16* sC = sW + BN * WP;         // epilogue staging (its own region: the patches stay live)
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int ntile = a.N * (a.OH / TR);
+  constexpr int TPI = 112 / TR;  // tiles per image
+
+  // shifted weights: W'[n][r*32 + s'*4 + c] = W[n][r*32 + (s'-1)*4 + c] (s' = 0: zero), r < 7
+  for (int e = tid; e < BN * 28; e += NT) {
+    const int n = e / 28, q = e - n * 28, r = q >> 2, j = q & 3;  // chunk j of filter row r: s' = 2j, 2j+1
+    const bf16* src = a.w + n * 256 + r * 32 + 8 * j;  // taps s = 2j (hi half); s = 2j - 1 (lo half)
+    const uint2 hi = *reinterpret_cast<const uint2*>(src);
+    uint2 lo = *reinterpret_cast<const uint2*>(src - (j ? 4 : 0));  // (j = 0: an in-range stand-in)
+    if (j == 0) lo = uint2{0u, 0u};
+    *reinterpret_cast<u32x4*>(sW + n * WP + r * 32 + j * 8) = u32x4{lo.x, lo.y, hi.x, hi.y};
+  }
+
+  const i32x4 xsrd = make_srd(a.x, 2ull * a.N * a.IH * IW * 4);
+  const unsigned lbase = lds_addr(lds);
+  auto dma_patch = [&](int t, int buf) __attribute__((always_inline)) {
+    const int n = t / TPI, oh0 = (t - n * TPI) * TR;
+    const int ih0 = 2 * oh0 - 3;
+#pragma unroll
+    for (int i = 0; i < PDI; ++i) {
+      const int e = 64 * (wid + NW * i) + lane;
+      const int pr = e / PCC, pc = e - pr * PCC;
+      const int ih = ih0 + pr, iw = 2 * pc - 4;
+      const bool v = e < PCH && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)IW;
+      lds_dma16(xsrd, v ? 8u * (unsigned)((n * a.IH + ih) * IW + iw) : kOOB,
+                lbase + 2u * (unsigned)(buf * PBUF) + 1024u * (unsigned)(wid + NW * i));
+    }
+  };
+
+  // per-lane fragment bases (bytes): A = pixel pair of output pixel q at filter row 0, B = row n
+  unsigned abase[TM], bbase[TN];
+  const int kq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int q = wm * (BM / WM) + i * 16 + (lane & 15);
+    const int oi = q / OW, oj = q - oi * OW;
+    abase[i] = 16u * (unsigned)(2 * oi * PCC + oj + kq);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bbase[j] = 2u * (unsigned)((wn * (BN / WN) + j * 16 + (lane & 15)) * WP + kq * 8);
+
+  int t = blockIdx.x;
+  dma_patch(t, 0);
+  f32x4 acc[TM][TN];
+  // vector-memory ops a thread issues after a patch DMA: the epilogue's NIT row stores (and, for the
+  // first 64 threads, 2 statistics atomics): waiting for that many younger ops retires the DMA
+  constexpr int NST = BM * (BN / 8) / NT;
+  for (int it = 0;; ++it) {
+    if (it == 0) dma_wait<0>();
+    else dma_wait<NST>();
+    __syncthreads();  // patch(t) landed for every wave; (first tile) the weights are visible
+    const int tn = t + gridDim.x;
+    if (tn < ntile) dma_patch(tn, (it + 1) & 1);  // into the buffer tile t-1 read
+    const char* cP = reinterpret_cast<const char*>(sP + (it & 1) * PBUF);
+    const char* cW = reinterpret_cast<const char*>(sW);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(cW + bbase[j] + 64 * r);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(cP + abase[i] + 16 * PCC * r);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    igemm_epilogue<BM, BN, WM, WN, FWD, STATS, false, 0>(a, acc, sC, t * BM, 0, t, blockIdx.x);
+    if (tn >= ntile) break;
+    t = tn;
+  }
+  dma_wait<0>();
+}
+
 }  // namespace dbx
 
 using namespace dbx;
@@ -389,5 +498,23 @@ extern "C" int dbx_conv_patch3(int mode, const IGemmArgs* args, int pro, int sta
   } else {
     return -24;
   }
+  return (int)hipGetLastError();
+}
+
+// Stem (7x7 s2 p3, NHWC4 image of width 224 -> 64 channels at 112x112): the patch kernel above.
+extern "C" int dbx_stem_patch(const IGemmArgs* args, int stats, hipStream_t st) {
+  const IGemmArgs& a = *args;
+  if (a.R != 7 || a.S != 7 || a.stride != 2 || a.pad != 3 || a.IC != 4 || a.OC != 64) return -30;
+  if (a.IW != 224 || a.OW != 112 || a.OH % 4 != 0 || a.OH != (a.IH + 6 - 7) / 2 + 1) return -31;
+  const int ntile = a.N * a.OH / 4;
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  const int nwg = ntile < cus ? ntile : cus;
+  if (stats) hipLaunchKernelGGL((stem_patch_kernel<true, 4>), dim3(nwg), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((stem_patch_kernel<false, 4>), dim3(nwg), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }

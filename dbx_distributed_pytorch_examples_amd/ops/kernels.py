@@ -342,9 +342,16 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
     return dx
 
 
+def stem_patch_supported(IH: int, IW: int, OC: int, R: int, S: int, stride: int, pad: int) -> bool:
+    """Geometry of the stem patch kernel (csrc/conv_patch3.hip): the ResNet 7x7/2 stem at 224."""
+    OH, OW = conv_out_hw(IH, IW, R, S, stride, pad)
+    return (R, S, stride, pad, IW, OC) == (7, 7, 2, 3, 224, 64) and OH % 4 == 0
+
+
 @_dispatch
-def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
-    """Stem conv on the NHWC4 image: w16s [OC, 256] = (8 rows x 8 pixels x 4 channels)."""
+def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch=None):
+    """Stem conv on the NHWC4 image: w16s [OC, 256] = (8 rows x 8 pixels x 4 channels).
+    ``patch``: the patch kernel (224-wide images) -- None = DBX_STEM_PATCH (default on)."""
     N, IH, IW, C4 = x4.shape
     if C4 != 4:
         raise ValueError("stem expects NHWC4 input")
@@ -357,7 +364,11 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
         _chk(stats, torch.float64, "stats", NSHARD * 2 * OC)
     if R > 8 or S > 8:
         raise ValueError("stem kernel supports R,S <= 8")
-    C().conv_igemm(STEM, 128, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
+    if patch is None:
+        import os
+        patch = os.environ.get("DBX_STEM_PATCH", "1") == "1"
+    bm = 0 if patch and stem_patch_supported(IH, IW, OC, R, S, stride, pad) else 128  # bm 0: patch kernel
+    C().conv_igemm(STEM, bm, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
                    *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr(), 0)
     return out

@@ -106,7 +106,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
     return dx
 
 
-def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None):
+def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch=None):
     OC = w16s.shape[0]
     w = w16s.float().view(OC, 8, 8, 4)[:, :R, :S, :].permute(0, 3, 1, 2)
     y = _nhwc(F.conv2d(_nchw(x4.float()), w, stride=stride, padding=pad)).bfloat16()

@@ -10,6 +10,7 @@ import math
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -95,3 +96,39 @@ def test_patch3_default_routing_and_fallbacks():
     with pytest.raises(ValueError):
         k.conv_fwd(torch.randn(1, 8, 28, 64, device=dev).bfloat16(), w, torch.empty(1, 8, 28, 64, device=dev).bfloat16(),
                    R=3, S=3, stride=1, pad=1, tile="patch")
+
+
+@pytest.mark.parametrize("N,H", [(2, 224), (1, 96)])
+def test_stem_patch_vs_fp32(N, H):
+    """Stem patch kernel (7x7/2 on the NHWC4 image, width 224) vs fp32 torch, and vs the implicit
+    GEMM stem (same products, different order inside a K step: close, not bit-exact)."""
+    k = K()
+    W = 224
+    torch.manual_seed(10)
+    img = torch.randn(N, H, W, 3, device=dev)
+    x4 = torch.zeros(N, H, W, 4, device=dev)
+    x4[..., :3] = img
+    x4 = x4.bfloat16()
+    w = torch.randn(64, 7, 7, 3, device=dev) * 0.05
+    ws_ = torch.zeros(64, 8, 8, 4, device=dev)
+    ws_[:, :7, :7, :3] = w
+    w16s = ws_.bfloat16().view(64, 256)
+    OH, OW = k.conv_out_hw(H, W, 7, 7, 2, 3)
+    assert k.stem_patch_supported(H, W, 64, 7, 7, 2, 3)
+    outs = []
+    for patch in (True, False):
+        out = torch.full((N, OH, OW, 64), float("nan"), device=dev, dtype=torch.bfloat16)
+        st = k.new_stats(64, dev)
+        k.conv_stem_fwd(x4, w16s, out, stats=st, patch=patch)
+        outs.append((out, st))
+    torch.cuda.synchronize()
+    ref = F.conv2d(x4[..., :3].float().permute(0, 3, 1, 2), ws_.bfloat16().float()[:, :7, :7, :3].permute(0, 3, 1, 2),
+                   stride=2, padding=3).permute(0, 2, 3, 1)
+    out, st = outs[0]
+    assert not torch.isnan(out.float()).any()
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 1e-2
+    assert (out.float() - outs[1][0].float()).abs().max().item() <= 0.02 * ref.abs().max().item()
+    s = st.view(-1, 2, 64).sum(0)
+    o = out.float().view(-1, 64)
+    assert ((s[0] - o.sum(0)).abs() / (o.abs().sum(0) + 1)).max().item() < 1e-3
+    assert ((s[1] - (o * o).sum(0)).abs() / ((o * o).sum(0) + 1)).max().item() < 1e-3
