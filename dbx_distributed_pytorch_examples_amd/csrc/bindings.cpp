@@ -18,6 +18,7 @@ int dbx_conv_igemm(int mode, int bm, int bn, const dbx::IGemmArgs* a, int pro, i
 int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, hipStream_t st, unsigned lds_pad,
                    int dma);
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
+int dbx_wgrad_patch3(const dbx::WgradArgs* a, hipStream_t st);
 int dbx_bn_finalize(const double*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
                     float*, float*, float*, hipStream_t);
 int dbx_bn_eval_coeff(int, const float*, const float*, float, const float*, const float*, float*, float*, hipStream_t);
@@ -111,6 +112,15 @@ PYBIND11_MODULE(_C, m) {
                      P<const float*>(in_shift), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad, N * OH * OW, KTOT,
                      nsplit, m_per_split, relu_in, (two40 + OW - 1) / OW, (two40 + ohw - 1) / ohw};
     check(dbx_conv_wgrad(mode, bm, bn, &a, in_scale != 0, S(st), lds_pad, dma), "conv_wgrad");
+  });
+  m.def("wgrad_patch3", [](uintptr_t dy, uintptr_t x, uintptr_t ws, int N, int IH, int IW, int IC, int OH, int OW,
+                           int OC, int R, int S_, int stride, int pad, uintptr_t st) {
+    // 3x3 patch weight gradient (conv_patch3.hip): one fp32 slab per workgroup; returns the count
+    dbx::WgradArgs a{P<const bf16*>(dy), P<const bf16*>(x), P<float*>(ws), nullptr, nullptr, N, IH, IW, IC, OH, OW,
+                     OC, R, S_, stride, pad, N * OH * OW, R * S_ * IC, 0, 0, 0, 0ull, 0ull};
+    const int n = dbx_wgrad_patch3(&a, S(st));
+    if (n <= 0) check(n ? n : -1, "wgrad_patch3");
+    return n;
   });
   m.def("wgrad_reduce", [](uintptr_t ws, uintptr_t dw, long long n, int nsplit, float scale, int acc, uintptr_t st) {
     check(dbx_wgrad_reduce(P<const float*>(ws), P<float*>(dw), n, nsplit, scale, acc, S(st)), "wgrad_reduce");

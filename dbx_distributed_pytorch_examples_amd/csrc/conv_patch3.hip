@@ -449,6 +449,133 @@ __global__ __launch_bounds__(512, 1) void stem_patch_kernel(const IGemmArgs a) {
   dma_wait<0>();
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradient of the 64 -> 64 3x3 stride-1 convs as a patch kernel:
+//   dW[k][tap][c] = sum_q dY[q][k] * X[q (+) tap][c]        (X = the stored BN output, zero halo)
+// A workgroup (4 waves, one per CU, persistent) walks tiles of TR output rows; per tile the dY rows
+// and the (TR+2) x (W+2) input patch arrive by LDS-DMA (double-buffered: the next tile lands during
+// this one). Wave w owns channels c = 16w..16w+15 of ALL 9 taps x 64 k (36 accumulator blocks), so
+// per 32-pixel K step it reads 4 dY fragments and 9 patch fragments for 36 MFMAs; the tap is a row
+// offset into the patch (transposed reads, ds_read_b64_tr_b16). Both images use the wgrad tr_swz
+// chunk swizzle keyed on the OUTPUT-linear pixel index (for the patch x = p - 2 * (p / PC)), which
+// keeps the shifted transposed reads conflict-free for every tap (exhaustive check over shifts).
+// Each workgroup writes one fp32 partial slab of dW; wgrad_reduce sums them in a fixed order.
+__device__ __forceinline__ int trx(int x) {  // tr_swz(row, ., 8) XOR term (conv_igemm.hip)
+  return ((((x & 1) << 2) ^ (x & 2) ^ (((x >> 3) & 1) << 2)) & 7);
+}
+
+template <int TR, int WIDTH>
+__global__ __launch_bounds__(256, 1) void wgrad_patch3_kernel(const WgradArgs a) {
+  constexpr int C = 64, NW = 4;
+  constexpr int BMP = TR * WIDTH;                    // pixels per tile (K of the tile's GEMM)
+  static_assert(BMP % 32 == 0, "tile pixels must be whole 32-pixel K steps");
+  constexpr int KS = BMP / 32;
+  constexpr int PC = WIDTH + 2, PR = TR + 2, PPIX = PR * PC;
+  constexpr int DYI = (BMP * 8 + 64 * NW - 1) / (64 * NW);   // dY DMA instructions per wave
+  constexpr int PAI = (PPIX * 8 + 64 * NW - 1) / (64 * NW);  // patch DMA instructions per wave
+  constexpr int DYE = DYI * NW * 64 * 8, PAE = PAI * NW * 64 * 8;  // bf16 elements per image
+  constexpr int BUF = DYE + PAE;
+  __shared__ __attribute__((aligned(1024))) bf16 lds[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int H = a.OH;
+  const int ntile = a.N * H / TR;
+  const i32x4 dysrd = make_srd(a.dy, 2ull * a.M * C);
+  const i32x4 xsrd = make_srd(a.x, 2ull * a.N * H * WIDTH * C);
+  const unsigned lbase = lds_addr(lds);
+
+  auto dma_tile = [&](int t, int buf) __attribute__((always_inline)) {
+    const int g0 = t * TR, n = g0 / H, h0 = g0 - n * H;
+    const unsigned dst = lbase + 2u * (unsigned)(buf * BUF);
+#pragma unroll
+    for (int i = 0; i < DYI; ++i) {
+      const int e = 64 * (wid + NW * i) + lane;
+      const int row = e >> 3, src = (lane & 7) ^ trx(row);
+      const unsigned off = row < BMP ? 2u * (unsigned)((g0 * WIDTH + row) * C + src * 8) : kOOB;
+      lds_dma16(dysrd, off, dst + 1024u * (unsigned)(wid + NW * i));
+    }
+#pragma unroll
+    for (int i = 0; i < PAI; ++i) {
+      const int e = 64 * (wid + NW * i) + lane;
+      const int pp = e >> 3, pr = pp / PC, pc = pp - pr * PC;
+      const int src = (lane & 7) ^ trx(pp - 2 * pr);
+      const int h = h0 - 1 + pr, w = pc - 1;
+      const bool v = pp < PPIX && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)WIDTH;
+      lds_dma16(xsrd, v ? 2u * (unsigned)(((n * H + h) * WIDTH + w) * C + src * 8) : kOOB,
+                dst + 2u * (unsigned)DYE + 1024u * (unsigned)(wid + NW * i));
+    }
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) acc[kb][tp] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  int t = blockIdx.x;
+  dma_tile(t, 0);
+  for (int it = 0;; ++it) {
+    dma_wait<0>();
+    __syncthreads();  // tile t landed (every wave's part); the other buffer is no longer read
+    const int tn = t + gridDim.x;
+    if (tn < ntile) dma_tile(tn, (it + 1) & 1);
+    const bf16* cA = lds + (it & 1) * BUF;
+    const bf16* cP = cA + DYE;
+#pragma unroll 1
+    for (int js = 0; js < KS; ++js) {
+      s16x4 va[2][4], vb[2][9];  // [lo / hi: pixel rows +0 / +4]
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int row = js * 32 + 8 * g + q4 + 4 * h2;
+        const int oi = row / WIDTH, oj = row - oi * WIDTH;
+        const int pp0 = oi * PC + oj;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          const int col = kb * 16 + 4 * p4;
+          va[h2][kb] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (DBX_LDS s16x4*)(cA + row * C + (((col >> 3) ^ trx(row)) << 3) + (col & 7)));
+        }
+        const int colb = wid * 16 + 4 * p4;
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          const int r = tp / 3, sx = tp - 3 * (tp / 3);
+          const int pp = pp0 + r * PC + sx, x = row + r * WIDTH + sx;
+          vb[h2][tp] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (DBX_LDS s16x4*)(cP + pp * C + (((colb >> 3) ^ trx(x)) << 3) + (colb & 7)));
+        }
+      }
+      bf16x8 af[4], bfr[9];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+        af[kb] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(va[0][kb], va[1][kb], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp)
+        bfr[tp] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(vb[0][tp], vb[1][tp], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp)
+          acc[kb][tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kb], bfr[tp], acc[kb][tp], 0, 0, 0);
+    }
+    if (tn >= ntile) break;
+    t = tn;
+  }
+  dma_wait<0>();
+  // partial slab: ws[blockIdx][k][tap*64 + c]
+  float* out = a.ws + (size_t)blockIdx.x * C * 9 * C;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = kb * 16 + (lane >> 4) * 4 + r;
+        out[(size_t)k * (9 * C) + tp * C + wid * 16 + (lane & 15)] = acc[kb][tp][r];
+      }
+}
+
 }  // namespace dbx
 
 using namespace dbx;
@@ -517,4 +644,23 @@ extern "C" int dbx_stem_patch(const IGemmArgs* args, int stats, hipStream_t st) 
   if (stats) hipLaunchKernelGGL((stem_patch_kernel<true, 4>), dim3(nwg), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((stem_patch_kernel<false, 4>), dim3(nwg), dim3(512), 0, st, a);
   return (int)hipGetLastError();
+}
+
+// Weight gradient of the 64 -> 64 3x3 stride-1 convs at width 56: the patch kernel above writes
+// one fp32 slab per workgroup into ws; returns the slab count (the caller reduces), < 0 on error.
+extern "C" int dbx_wgrad_patch3(const WgradArgs* args, hipStream_t st) {
+  const WgradArgs& a = *args;
+  if (a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1 || a.IC != 64 || a.OC != 64) return -40;
+  if (a.OW != 56 || a.IW != 56 || a.OH != a.IH || a.OH % 4 != 0) return -41;
+  const int ntile = a.N * a.OH / 4;
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  const int nwg = ntile < cus ? ntile : cus;
+  hipLaunchKernelGGL((wgrad_patch3_kernel<4, 56>), dim3(nwg), dim3(256), 0, st, a);
+  const int e = (int)hipGetLastError();
+  return e ? -e : nwg;
 }

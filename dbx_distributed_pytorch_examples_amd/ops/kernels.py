@@ -157,7 +157,7 @@ def _use_patch3(tile, mode: str) -> int:
         return {"patch": kind, "patch_r": 1, "patch_s": 2}.get(tile, 0)
     if tile is not None:
         return 0
-    return kind if use in ("all", mode) else 0
+    return kind if (use == "all" or mode in use.split(",")) else 0
 
 
 # --------------------------------------------------------------------------------------
@@ -411,6 +411,18 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
     _chk(ws, torch.float32, "ws")
     if conv_out_hw(IH, IW, R, S, stride, pad) != (OH, OW):
         raise ValueError("conv_wgrad: shapes inconsistent with the conv geometry")
+    if (not stem and in_scale is None and tile in (None, "patch")
+            and patch3_supported(IC, OC, R, S, stride, pad, IH, IW) and IH % 4 == 0
+            and (tile == "patch" or _use_patch3(None, "wgrad"))):
+        # 3x3 patch kernel (csrc/conv_patch3.hip): one fp32 slab per persistent workgroup
+        if 320 * OC * R * S * IC > ws.numel():  # 256 slabs + the two-level reduction's partials
+            raise ValueError("wgrad workspace too small for the patch kernel")
+        nsl = C().wgrad_patch3(dy.data_ptr(), x.data_ptr(), ws.data_ptr(), N, IH, IW, IC, OH, OW, OC, R, S, stride,
+                               pad, stream_ptr())
+        C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsl, float(scale), int(accumulate), stream_ptr())
+        return dw
+    if isinstance(tile, str):
+        raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 wgrad at width 56 without a prologue")
     if stem:
         bm, bn = 64, 128
     else:
