@@ -152,6 +152,10 @@ class ResNetProgram:
         # (default 1: the bottleneck conv1 dgrads, N = 4K, stay unfolded -- 14.39-14.41k vs
         # 14.22-14.27k img/s folded, ResNet-50 b1024, profiles/r2s3_fold/fold_ratio_ab.txt)
         self.fold_max_ratio = float(os.environ.get("DBX_FOLD_MAX_RATIO", "1"))
+        # ... except at feature maps >= this size (the ratio limit is about the N-tile repeats of
+        # the operand prologue: at 56x56 the conv1 dgrads have only 1-2 N tiles; 15.19k / 15.21k vs
+        # 15.17k / 15.13k img/s with the limit everywhere, profiles/r2s3_fold/fold_ratio_ab.txt)
+        self.fold_ratio_min_hw = int(os.environ.get("DBX_FOLD_RATIO_MIN_HW", "56"))
         self._wstream = None
         self._side_pending = False
         self._build_layers()
@@ -674,7 +678,7 @@ class ResNetProgram:
         ``dense``: the strided 1x1 downsample, whose dgrad runs as a dense 1x1 stride-1 GEMM)."""
         stride = 1 if dense else cv.stride
         return (self.fuse_bwd_apply and not cv.stem and self.N * cv.OH * cv.OW * cv.OC >= self.fold_min
-                and cv.IC <= self.fold_max_ratio * cv.OC
+                and (cv.IC <= self.fold_max_ratio * cv.OC or cv.OH >= self.fold_ratio_min_hw)
                 and K.tail_supported(cv.OC, cv.R, cv.S, stride, cv.pad))
 
     def _bwd_stem(self):
