@@ -62,4 +62,20 @@ struct WgradArgs {
   int M, KTOT, nsplit, m_per_split, relu_in;
   unsigned long long mag_ow, mag_ohw;  // ceil(2^40 / OW), ceil(2^40 / (OH*OW)): pixel -> (n, oh, ow)
 };
+// Fused backward of a bottleneck conv3 (1x1 stride-1, C -> K channels), conv_dwfused.hip
+struct DwFusedArgs {
+  const bf16* g;         // [M][K] gradient of the BN3 output (block-output gradient, ReLU-masked)
+  const bf16* y3;        // [M][K] BN3 input (conv3 raw output)
+  const float* coeff;    // [3][K] BN3-backward apply: dy3 = k1*g + k2*y3 + k3
+  const bf16* wt;        // [C][K] dgrad weights (CRSK, 1x1)
+  const bf16* y2;        // [M][C] BN2 input (conv2 raw output)
+  const float* bsc;      // BN2 forward scale / shift: a2 = relu(y2*bsc + bsh)
+  const float* bsh;
+  const float* mean2;    // BN2 batch mean / invstd (backward moments)
+  const float* inv2;
+  bf16* da;              // [M][C] out: relu-masked data gradient of a2
+  double* bstats;        // [nshard][2][C] BN2-backward moments (sum g, sum g*xhat)
+  float* ws;             // [grid][K][C] fp32 weight-gradient partial slabs
+  int M, K, C, nshard;
+};
 }  // namespace dbx

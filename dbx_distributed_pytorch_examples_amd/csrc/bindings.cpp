@@ -19,6 +19,7 @@ int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, h
                    int dma);
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
 int dbx_wgrad_patch3(const dbx::WgradArgs* a, hipStream_t st);
+int dbx_conv_dwfused(const dbx::DwFusedArgs* a, long long ws_cap, hipStream_t st);
 int dbx_bn_finalize(const double*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
                     float*, float*, float*, hipStream_t);
 int dbx_bn_eval_coeff(int, const float*, const float*, float, const float*, const float*, float*, float*, hipStream_t);
@@ -120,6 +121,18 @@ PYBIND11_MODULE(_C, m) {
                      OC, R, S_, stride, pad, N * OH * OW, R * S_ * IC, 0, 0, 0, 0ull, 0ull};
     const int n = dbx_wgrad_patch3(&a, S(st));
     if (n <= 0) check(n ? n : -1, "wgrad_patch3");
+    return n;
+  });
+  m.def("conv_dwfused", [](uintptr_t g, uintptr_t y3, uintptr_t coeff, uintptr_t wt, uintptr_t y2, uintptr_t bsc,
+                           uintptr_t bsh, uintptr_t mean2, uintptr_t inv2, uintptr_t da, uintptr_t bstats, uintptr_t ws,
+                           long long ws_cap, int M, int K, int C, int nshard, uintptr_t st) {
+    // fused bottleneck-conv3 backward (conv_dwfused.hip): returns the number of dW partial slabs
+    dbx::DwFusedArgs a{P<const bf16*>(g), P<const bf16*>(y3), P<const float*>(coeff), P<const bf16*>(wt),
+                       P<const bf16*>(y2), P<const float*>(bsc), P<const float*>(bsh), P<const float*>(mean2),
+                       P<const float*>(inv2), P<bf16*>(da), P<double*>(bstats), P<float*>(ws), M, K, C,
+                       nshard > 0 ? nshard : 1};
+    const int n = dbx_conv_dwfused(&a, ws_cap, S(st));
+    if (n <= 0) check(n ? n : -1, "conv_dwfused");
     return n;
   });
   m.def("wgrad_reduce", [](uintptr_t ws, uintptr_t dw, long long n, int nsplit, float scale, int acc, uintptr_t st) {

@@ -136,3 +136,14 @@ __device__ __forceinline__ void dma_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
+
+// XOR swizzle of a [rows][nch x 16B] LDS tile image read by ds_read_b64_tr_b16 (weight gradients):
+__device__ __forceinline__ int tr_swz(int row, int ch, int nch) {
+  // conflict-free for BOTH the ds_write_b128 staging stores (8-lane groups: the two rows a group
+  // covers must land on different 64-B halves of the 128-B bank window) and the
+  // ds_read_b64_tr_b16 fragment reads (32-lane groups over 8 rows); model: tools/lds_banks.py
+  if (nch == 32) return ch ^ (((row & 1) << 1) | ((row & 2) << 1) | (row & 8));  // 256-wide tiles
+  if (nch == 16) return ch ^ ((((row & 1) << 2) | (row & 2) | (row & 8)) & 15);
+  return ch ^ ((((row & 1) << 2) ^ (row & 2) ^ (((row >> 3) & 1) << 2)) & 7);
+}
+

@@ -14,15 +14,6 @@ namespace dbx {
 // and wgrad_reduce sums the slabs in a fixed order (deterministic).
 // ======================================================================================
 
-__device__ __forceinline__ int tr_swz(int row, int ch, int nch) {
-  // conflict-free for BOTH the ds_write_b128 staging stores (8-lane groups: the two rows a group
-  // covers must land on different 64-B halves of the 128-B bank window) and the
-  // ds_read_b64_tr_b16 fragment reads (32-lane groups over 8 rows); model: tools/lds_banks.py
-  if (nch == 32) return ch ^ (((row & 1) << 1) | ((row & 2) << 1) | (row & 8));  // 256-wide tiles
-  if (nch == 16) return ch ^ ((((row & 1) << 2) | (row & 2) | (row & 8)) & 15);
-  return ch ^ ((((row & 1) << 2) ^ (row & 2) ^ (((row >> 3) & 1) << 2)) & 7);
-}
-
 // WM x WN waves (64*WM*WN threads), each owning a (BM/WM) x (BN/WN) block of dW.
 template <int BM, int BN, int WM, int WN, int MODE, bool PRO, int DEPTH = 2>
 __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const WgradArgs a) {

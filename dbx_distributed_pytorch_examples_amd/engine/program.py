@@ -156,6 +156,9 @@ class ResNetProgram:
         # the operand prologue: at 56x56 the conv1 dgrads have only 1-2 N tiles; 15.19k / 15.21k vs
         # 15.17k / 15.13k img/s with the limit everywhere, profiles/r2s3_fold/fold_ratio_ab.txt)
         self.fold_ratio_min_hw = int(os.environ.get("DBX_FOLD_RATIO_MIN_HW", "56"))
+        # bottleneck conv3 backward as ONE kernel (BN3-backward apply + dgrad + MASK_Y epilogue +
+        # weight gradient, K.conv_dwfused): dy3 and the BN2 output a2 never reach HBM
+        self.fuse_dw = os.environ.get("DBX_FUSE_DW", "1") == "1"
         self._wstream = None
         self._side_pending = False
         self._build_layers()
@@ -380,6 +383,11 @@ class ResNetProgram:
             wsmax = max(wsmax, cv.OC * ktot)
         # split-K wgrad workspace: up to 64 splits of the largest layer, >= 64 MiB
         self.ws = torch.empty(max(64 * wsmax, 16 << 20), device=dev, dtype=torch.float32)
+        # the fused conv3 backward runs on the main stream while side-stream weight gradients use
+        # self.ws: its per-workgroup slabs get their own workspace (<= 1024 slabs + 64 partials)
+        fused = [b.convs[-1] for i, b in enumerate(self.blocks) if self._fuse3(b, i == len(self.blocks) - 1)]
+        self.ws_dw = (torch.empty((1024 + 64) * max(c.OC * c.IC for c in fused), device=dev, dtype=torch.float32)
+                      if fused else None)
         fh, fw = self.feat_hw
         self.dfeat = self.blocks[-1].out  # placeholder name; real grad buffer below
         self.dlast = E(N, fh, fw, self.feat_c)
@@ -581,6 +589,7 @@ class ResNetProgram:
         cnt_last = N * lc.OH * lc.OW
         pend, gin = None, None  # BN-backward apply deferred into the next dgrad's prologue
         ds_fold = None  # ... and the downsample BN's, into the downsample dgrad
+        fuse3 = self._fuse3(b, last)  # conv3's BN-backward apply + dgrad + wgrad in one kernel
         if last:
             # g = dlast * (out > 0) -> self.g_last ; tail BN reductions (and ds BN) from dlast
             K.bn_bwd_reduce(self.dlast, b.ys[-1], lbn.mean, lbn.invstd, lbn.bstats, mask_mode=K.MASK_OUT, mref=b.out)
@@ -600,15 +609,19 @@ class ResNetProgram:
                            dbn.dbeta)
             if last:
                 K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE)
-            elif self._fold(lc) and self._fold(dc, dense=True):
+            elif (fuse3 or self._fold(lc)) and self._fold(dc, dense=True):
                 # both tail BN applies folded into the dgrads of conv3 and of the downsample conv
                 pend = dict(bwd_y=b.ys[-1], bwd_coeff=lbn.coeff, dy_out=b.dys[-1])
                 gin = g
                 ds_fold = dict(bwd_y=b.yd, bwd_coeff=dbn.coeff, dy_out=b.dyd)
+            elif fuse3:  # conv3's inside the fused kernel, the downsample BN's as its own pass
+                K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE)
+                pend = dict(bwd_y=b.ys[-1], bwd_coeff=lbn.coeff, dy_out=b.dys[-1])
+                gin = g
             else:  # both tail BNs from one read of the block-output gradient
                 K.bn_bwd_apply2(g, b.ys[-1], lbn.coeff, b.dys[-1], b.yd, dbn.coeff, b.dyd)
         elif not last:
-            if self._fold(lc):  # folded into conv3's dgrad prologue (it stores dys[-1] for the wgrad)
+            if fuse3 or self._fold(lc):  # folded into conv3's dgrad prologue (it stores dys[-1] for the wgrad)
                 pend = dict(bwd_y=b.ys[-1], bwd_coeff=lbn.coeff, dy_out=b.dys[-1])
                 gin = g
             else:
@@ -622,16 +635,22 @@ class ResNetProgram:
             act = b.acts[j - 1]
             kw, src = (pend, gin) if pend else ({}, b.dys[j])
             pend = None
-            pre = act is None and not kw  # wgrad re-applies BN+ReLU to its staged input tiles (BN prologue)
+            if fuse3 and j == nconv - 1:
+                # one pass: dy3 = BN3-bwd apply(g, y3) -> da2 (+ BN2 moments) and dW3 = dy3^T relu(bn2(y2))
+                K.conv_dwfused(src, kw["bwd_y"], kw["bwd_coeff"], cv.wt16, b.ys[j - 1], pbn.scale, pbn.shift,
+                               pbn.mean, pbn.invstd, pbn.bstats, b.das[j - 1], cv.grad, self.ws_dw)
+                act, kw = None, None
+            pre = act is None and kw == {}  # wgrad re-applies BN+ReLU to its staged input tiles (BN prologue)
             if pre:
                 self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                             in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
-            K.conv_dgrad(src, cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
-                         epilogue=K.BNBwdEpilogue(K.MASK_Y, b.ys[j - 1], pbn.mean, pbn.invstd, pbn.bstats,
-                                                  scale=pbn.scale, shift=pbn.shift, act_out=act), **kw)
+            if kw is not None:
+                K.conv_dgrad(src, cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                             epilogue=K.BNBwdEpilogue(K.MASK_Y, b.ys[j - 1], pbn.mean, pbn.invstd, pbn.bstats,
+                                                      scale=pbn.scale, shift=pbn.shift, act_out=act), **kw)
             if act is not None:
                 self._wgrad(b.dys[j], act, cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad)
-            elif not pre:
+            elif kw and not pre:
                 self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                             in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
             K.bn_bwd_coeff(pbn.bstats, N * pc.OH * pc.OW, pbn.gamma, pbn.mean, pbn.invstd, pbn.coeff, pbn.dgamma,
@@ -672,6 +691,15 @@ class ResNetProgram:
                      addsrc=addsrc, add_sub=sub, epilogue=epi, **kw0)
         if kw0:
             self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
+
+    def _fuse3(self, b: BlockL, last: bool) -> bool:
+        """Run block b's conv3 backward through K.conv_dwfused (the 64 -> 256 conv3 of the 56x56
+        stage: its weight-gradient accumulators fit a workgroup's registers)."""
+        if not self.fuse_dw or last or b.kind != "bottleneck":
+            return False
+        c3 = b.convs[-1]
+        return ((c3.R, c3.S, c3.stride, c3.pad) == (1, 1, 1, 0)
+                and K.dwfused_supported(c3.IC, c3.OC, self.N * c3.OH * c3.OW))
 
     def _fold(self, cv, dense: bool = False) -> bool:
         """Fold the BN-backward apply of cv's output BN into cv's dgrad (1x1 stride-1 convs;

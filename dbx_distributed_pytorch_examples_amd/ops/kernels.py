@@ -453,6 +453,42 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
     return dw
 
 
+def dwfused_supported(C: int, K: int, M: int) -> bool:
+    """Geometry of the fused bottleneck-conv3 backward kernel (csrc/conv_dwfused.hip): the 64 -> 256
+    channel conv3 of the 56x56 stage, whole 128-pixel tiles, 32-bit buffer offsets."""
+    return C == 64 and K == 256 and M % 128 == 0 and 2 * M * K < 0xFFFFFF00
+
+
+@_dispatch
+def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2, da, dw, ws):
+    """Backward of a bottleneck conv3 (1x1 stride 1, C -> K) in one pass (csrc/conv_dwfused.hip):
+    dy3 = k1*g + k2*y3 + k3 (BN3-backward apply, ``coeff`` [3, K]) -> data gradient
+    ``da`` = [a2 > 0] * conv_transpose(dy3) with the BN2-backward moments into ``bstats2`` (the MASK_Y
+    epilogue, a2 = relu(y2*scale2 + shift2)), and weight gradient ``dw`` [K, C] = dy3^T a2 (fp32,
+    per-workgroup slabs in ``ws`` + the deterministic split reduction). dy3 and a2 never reach HBM."""
+    N, H, W, Kc = g.shape
+    Cc = y2.shape[-1]
+    M = N * H * W
+    _chk(g, torch.bfloat16, "g")
+    _chk(y3, torch.bfloat16, "y3", g.numel())
+    _chk(coeff, torch.float32, "coeff", 3 * Kc)
+    _chk(wt16, torch.bfloat16, "wt16", Cc * Kc)
+    _chk(y2, torch.bfloat16, "y2", M * Cc)
+    _chk(da, torch.bfloat16, "da", M * Cc)
+    _chk(dw, torch.float32, "dw", Kc * Cc)
+    _chk(ws, torch.float32, "ws")
+    _chk(bstats2, torch.float64, "bstats2", NSHARD * 2 * Cc)
+    for t, nm in ((scale2, "scale2"), (shift2, "shift2"), (mean2, "mean2"), (invstd2, "invstd2")):
+        _chk(t, torch.float32, nm, Cc)
+    if not dwfused_supported(Cc, Kc, M):
+        raise ValueError(f"conv_dwfused: unsupported geometry C={Cc} K={Kc} M={M}")
+    n = C().conv_dwfused(g.data_ptr(), y3.data_ptr(), coeff.data_ptr(), wt16.data_ptr(), y2.data_ptr(),
+                         scale2.data_ptr(), shift2.data_ptr(), mean2.data_ptr(), invstd2.data_ptr(), da.data_ptr(),
+                         bstats2.data_ptr(), ws.data_ptr(), ws.numel(), M, Kc, Cc, NSHARD, stream_ptr())
+    C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), Kc * Cc, n, 1.0, 0, stream_ptr())
+    return da
+
+
 # --------------------------------------------------------------------------------------
 # batch norm / elementwise
 # --------------------------------------------------------------------------------------

@@ -134,6 +134,19 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
     return dw
 
 
+def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2, da, dw, ws):
+    """Fused bottleneck-conv3 backward = BN3-backward apply -> MASK_Y dgrad + weight gradient."""
+    from types import SimpleNamespace
+    dy = torch.empty_like(g)
+    bn_bwd_apply(g, y3, coeff, dy, mask_mode=MASK_NONE)
+    act = torch.relu(y2.float() * scale2 + shift2).bfloat16()
+    epi = SimpleNamespace(mode=MASK_Y, ybn=y2, mean1=mean2, inv1=invstd2, stats1=bstats2, mbits=None, scale=scale2,
+                          shift=shift2, ybn2=None, mean2=None, inv2=None, stats2=None, act_out=None)
+    conv_dgrad(dy, wt16, da, R=1, S=1, stride=1, pad=0, epilogue=epi)
+    conv_wgrad(dy, act, dw, ws, R=1, S=1, stride=1, pad=0)
+    return da
+
+
 def bn_finalize(stats, count, gamma, beta, eps, momentum, running_mean, running_var, scale, shift, save_mean,
                 save_invstd):
     C = scale.numel()

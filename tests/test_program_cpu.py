@@ -141,3 +141,27 @@ def test_frozen_backbone_native_features_and_head_step():
     assert any(not torch.equal(a, b) for a, b in zip(head_before, m.resnet.fc.parameters()))
     after = [p.detach() for n, p in m.resnet.named_parameters() if not n.startswith("fc")]
     assert all(torch.equal(a, b) for a, b in zip(backbone_before, after))
+
+
+@pytest.mark.parametrize("fold", [0, 1 << 40])
+def test_fused_conv3_backward_schedule(fold, monkeypatch):
+    """DBX_FUSE_DW: the bottleneck conv3 backward as one op (K.conv_dwfused) gives the gradients of
+    the unfused schedule (BN-backward apply -> MASK_Y dgrad -> weight gradient), folded or not."""
+    monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(fold))
+    grads = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DBX_FUSE_DW", flag)
+        torch.manual_seed(0)
+        model = build_model("resnet50", num_classes=10)
+        _damp(model, "resnet50")
+        tr = NativeTrainer(model, 8, (64, 64), CPU, optim=OptimConfig(lr=0.0, momentum=0.0, weight_decay=0.0),
+                           use_graphs=False)
+        assert (tr.prog.ws_dw is not None) == (flag == "1")
+        assert sum(tr.prog._fuse3(b, i == len(tr.prog.blocks) - 1) for i, b in enumerate(tr.prog.blocks)) == (
+            3 if flag == "1" else 0)
+        g = torch.Generator().manual_seed(1)
+        img = torch.randint(0, 256, (8, 64, 64, 3), dtype=torch.uint8, generator=g)
+        lab = torch.randint(0, 10, (8,), generator=g)
+        tr.step(img, lab)
+        grads.append(tr.prog.grad.clone())
+    assert torch.allclose(grads[0], grads[1], rtol=1e-5, atol=1e-7)
