@@ -23,21 +23,33 @@
 
 namespace dbx {
 
-template <int C, int NKB>
-__global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
-  constexpr int BM = 128, NT = 256, K = NKB * 64;
-  constexpr int WCH = K / 8;          // 16-byte chunks per resident weight row
-  constexpr int CPR = C / 8;          // chunks per a2 / da row
-  static_assert(C == 64, "loader / epilogue mapping assumes 64 dgrad output channels");
-  __shared__ __attribute__((aligned(16))) bf16 lds[C * K + 2 * BM * 64 + BM * C];
-  bf16* sW = lds;                 // [C][K], chunk ^ (row & 15)
-  bf16* sA = lds + C * K;         // [2][BM][64] dy3 K-blocks (tr_swz)
-  bf16* sP = sA + 2 * BM * 64;    // [BM][C] a2 tile (tr_swz)
-  bf16* sC = sA;                  // epilogue staging [BM][C + 8] (aliases sA after the K loop)
+// C: dgrad output channels (conv3 input), NKB: K / 64, BM: pixels per tile, NS: register staging
+// sets (the g / y3 loads of block kb + NS are issued while block kb is computed), OCC: workgroups
+// per CU (2: 256 VGPRs per lane; 1: the LDS holds one workgroup, whose waves get all 512), Y2N:
+// prefetch the next tile's y2 into spare registers at the tile start (else during the epilogue).
+template <int C, int NKB, int BM, int NS, int OCC, bool Y2N>
+__global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) {
+  constexpr int NT = 256, K = NKB * 64;
+  constexpr int WCH = K / 8;            // 16-byte chunks per resident weight row
+  constexpr int CPR = C / 8;            // chunks per a2 / da row
+  constexpr int RPP = NT / CPR;         // a2 / da rows per thread pass
+  constexpr int NY = BM / RPP;          // y2 / da chunks per thread
+  constexpr int NG = BM / 32;           // g / y3 chunks per thread and K-block (rows lrow + 32 i)
+  constexpr int TM = BM / 32, TN = C / 32;  // dgrad: wave (wm, wn) owns BM/2 pixels x C/2 channels
+  constexpr int TNW = C / 32;               // wgrad: wave owns 32 k x C/2 channels of each K-block
+  static_assert(NKB % NS == 0 && C % 64 == 0 && BM % 32 == 0 && BM % RPP == 0, "tile shape");
+  constexpr int LDS_W = C * K, LDS_A = 2 * BM * 64, LDS_P = BM * C;
+  static_assert(BM * (C + 8) <= LDS_A + LDS_P, "epilogue staging must fit the dy3 + a2 images");
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_W + LDS_A + LDS_P];
+  bf16* sW = lds;              // [C][K], chunk ^ (row & 15)
+  bf16* sA = lds + LDS_W;      // [2][BM][64] dy3 K-blocks (tr_swz)
+  bf16* sP = sA + LDS_A;       // [BM][C] a2 tile (tr_swz)
+  bf16* sC = sA;               // epilogue staging [BM][C + 8] (aliases sA + sP after the K loop)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
   const int ntile = a.M / BM;
-  const int lrow = tid >> 3, lch = tid & 7;  // loader / epilogue: rows lrow + 32 i, chunk lch
+  const int lrow = tid >> 3, lch = tid & 7;      // g / y3 loader: rows lrow + 32 i, chunk lch
+  const int erow = tid / CPR, ech = tid % CPR;   // y2 / epilogue: rows erow + RPP i, chunk ech
 
   for (int q = tid; q < C * WCH; q += NT) {
     const int row = q / WCH, ch = q - (q / WCH) * WCH;
@@ -46,7 +58,7 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
   }
   // BN2 forward affine of this thread's 8 channels: re-read (L1 / L2 hits) at each use instead of
   // pinning 16 VGPRs across the K loop (the accumulators need them)
-  int cbn = lch * 8;
+  int cbn = ech * 8;
   auto bn2_affine = [&](f32x4& s0, f32x4& s1, f32x4& h0, f32x4& h1) __attribute__((always_inline)) {
     asm volatile("" : "+v"(cbn));  // opaque: keeps the loads at the use (not hoisted out of the tile loop)
     s0 = *reinterpret_cast<const f32x4*>(a.bsc + cbn);
@@ -57,32 +69,32 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
   f32x2 st_s[4], st_q[4];  // running BN2-backward raw moments of this thread's channels (packed)
 #pragma unroll
   for (int h = 0; h < 4; ++h) st_s[h] = st_q[h] = f32x2{0.f, 0.f};
-  f32x4 accw[NKB][2][2];
+  f32x4 accw[NKB][2][TNW];
 #pragma unroll
   for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) accw[kb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < TNW; ++j) accw[kb][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const rsrc_t gr = make_rsrc(a.g, 2ull * a.M * K);
   const rsrc_t yr = make_rsrc(a.y3, 2ull * a.M * K);
   const rsrc_t y2r = make_rsrc(a.y2, 2ull * a.M * C);
-  u32x4 rg[4], ry[4], ry2[4];
+  u32x4 rg[NS][NG], ry[NS][NG], ry2[NY], ry2n[Y2N ? NY : 1];
   // tiles past the end read out of range (zeros, no traffic): the prefetch is unconditional
-  auto load_k = [&](int t, int kb) __attribute__((always_inline)) {
+  auto load_k = [&](int t, int kb, int set) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NG; ++i) {
       const unsigned off = t < ntile ? 2u * (unsigned)((t * BM + lrow + 32 * i) * K + kb * 64 + lch * 8) : kOOB;
-      rg[i] = buf_load16(gr, off);
-      ry[i] = buf_load16(yr, off);
+      rg[set][i] = buf_load16(gr, off);
+      ry[set][i] = buf_load16(yr, off);
     }
   };
-  auto load_y2 = [&](int t, int i) __attribute__((always_inline)) {
-    ry2[i] = buf_load16(y2r, t < ntile ? 2u * (unsigned)((t * BM + lrow + 32 * i) * C + lch * 8) : kOOB);
+  auto y2_off = [&](int t, int i) __attribute__((always_inline)) {
+    return t < ntile ? 2u * (unsigned)((t * BM + erow + RPP * i) * C + ech * 8) : kOOB;
   };
   // BN3-backward apply of K-block kb -> dy3 image (bf16, as the unfused fold stores it)
-  auto fold_store = [&](int kb, int buf) __attribute__((always_inline)) {
+  auto fold_store = [&](int kb, int buf, int set) __attribute__((always_inline)) {
     const int c0 = kb * 64 + lch * 8;
     const f32x4 k1a = *reinterpret_cast<const f32x4*>(a.coeff + c0);
     const f32x4 k1b = *reinterpret_cast<const f32x4*>(a.coeff + c0 + 4);
@@ -91,10 +103,10 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
     const f32x4 k3a = *reinterpret_cast<const f32x4*>(a.coeff + 2 * K + c0);
     const f32x4 k3b = *reinterpret_cast<const f32x4*>(a.coeff + 2 * K + c0 + 4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NG; ++i) {
       float f[8], y[8];
-      unpack8(rg[i], f);
-      unpack8(ry[i], y);
+      unpack8(rg[set][i], f);
+      unpack8(ry[set][i], y);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         f[j] = f[j] * k1a[j] + k3a[j] + y[j] * k2a[j];
@@ -108,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
     f32x4 bsc0, bsc1, bsh0, bsh1;
     bn2_affine(bsc0, bsc1, bsh0, bsh1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NY; ++i) {
       float f[8];
       unpack8(ry2[i], f);
 #pragma unroll
@@ -116,42 +128,42 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
         f[j] = f[j] * bsc0[j] + bsh0[j];
         f[j + 4] = f[j + 4] * bsc1[j] + bsh1[j];
       }
-      const int row = lrow + 32 * i;
-      *reinterpret_cast<u32x4*>(sP + row * C + (tr_swz(row, lch, 8) << 3)) = relu_bf16x8(pack8(f));
+      const int row = erow + RPP * i;
+      *reinterpret_cast<u32x4*>(sP + row * C + (tr_swz(row, ech, CPR) << 3)) = relu_bf16x8(pack8(f));
     }
   };
 
   const int g4 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  f32x4 accd[4][2];  // dgrad: wave (wm, wn) owns pixels wm*64.. x channels wn*32..
+  f32x4 accd[TM][TN];
   auto mma = [&](int kb, int buf) __attribute__((always_inline)) {
     const bf16* cA = sA + buf * BM * 64;
     // data gradient: acc^T = W . dy3^T (a lane's 4 accumulators = 4 consecutive channels of a pixel)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + g4;
-      bf16x8 af[4], bw[2];
+      bf16x8 af[TM], bw[TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * 64 + i * 16 + (lane & 15);
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (BM / 2) + i * 16 + (lane & 15);
         af[i] = *reinterpret_cast<const bf16x8*>(cA + row * 64 + (tr_swz(row, ch, 8) << 3));
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int crow = wn * 32 + j * 16 + (lane & 15);
+      for (int j = 0; j < TN; ++j) {
+        const int crow = wn * (C / 2) + j * 16 + (lane & 15);
         bw[j] = *reinterpret_cast<const bf16x8*>(sW + crow * K + (((kb * 8 + ch) ^ (crow & 15)) << 3));
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TN; ++j)
           accd[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], accd[i][j], 0, 0, 0);
     }
     // weight gradient of this K-block: dW[k][c] += sum_m dy3[m][k] * a2[m][c]  (reduction over
-    // the tile's 128 pixels = 4 steps of 32; fragments by hardware-transposed LDS reads)
+    // the tile's pixels in steps of 32; fragments by hardware-transposed LDS reads)
 #pragma unroll
     for (int ks = 0; ks < BM / 32; ++ks) {
       const int row = ks * 32 + 8 * g4 + q4, row2 = row + 4;
-      bf16x8 af[2], bp[2];
+      bf16x8 af[2], bp[TNW];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int col = wm * 32 + i * 16 + 4 * p4;
@@ -162,52 +174,59 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
         af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = wn * 32 + j * 16 + 4 * p4;
+      for (int j = 0; j < TNW; ++j) {
+        const int col = wn * (C / 2) + j * 16 + 4 * p4;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (DBX_LDS s16x4*)(sP + row * C + (tr_swz(row, col >> 3, 8) << 3) + (col & 7)));
+            (DBX_LDS s16x4*)(sP + row * C + (tr_swz(row, col >> 3, CPR) << 3) + (col & 7)));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (DBX_LDS s16x4*)(sP + row2 * C + (tr_swz(row2, col >> 3, 8) << 3) + (col & 7)));
+            (DBX_LDS s16x4*)(sP + row2 * C + (tr_swz(row2, col >> 3, CPR) << 3) + (col & 7)));
         bp[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TNW; ++j)
           accw[kb][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bp[j], accw[kb][i][j], 0, 0, 0);
     }
   };
 
   int t = blockIdx.x;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) load_y2(t, i);
-  load_k(t, 0);
+  for (int i = 0; i < NY; ++i) ry2[i] = buf_load16(y2r, y2_off(t, i));
+#pragma unroll
+  for (int s = 0; s < NS; ++s) load_k(t, s, s);
   __syncthreads();  // resident weights visible
   for (; t < ntile; t += gridDim.x) {
+    const int tn = t + gridDim.x;
+    if constexpr (Y2N) {
+#pragma unroll
+      for (int i = 0; i < NY; ++i) ry2n[i] = buf_load16(y2r, y2_off(tn, i));
+    }
     a2_store();
-    fold_store(0, 0);
+    fold_store(0, 0, 0);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) accd[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int tn = t + gridDim.x;
+      for (int j = 0; j < TN; ++j) accd[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
-      // one register set: block kb+1 (or the next tile's block 0) loads under block kb's MFMAs
-      load_k(kb + 1 < NKB ? t : tn, kb + 1 < NKB ? kb + 1 : 0);
+      // register set kb % NS was consumed by fold_store(kb): refill it with the block NS ahead in
+      // the stream (past the tile's last block: the next tile's first blocks), under kb's MFMAs
+      const int f = kb + NS;
+      load_k(f < NKB ? t : tn, f < NKB ? f : f - NKB, kb % NS);
       mma(kb, kb & 1);
-      if (kb + 1 < NKB) fold_store(kb + 1, (kb + 1) & 1);
+      if (kb + 1 < NKB) fold_store(kb + 1, (kb + 1) & 1, (kb + 1) % NS);
       __syncthreads();
     }
     // epilogue: da = [a2 > 0] * acc, staged through LDS for 16-byte row chunks (the thread's chunks
     // are the rows / channels of its y2 registers)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = wm * 64 + i * 16 + (lane & 15);
-        const int col = wn * 32 + j * 16 + g4 * 4;
+      for (int j = 0; j < TN; ++j) {
+        const int row = wm * (BM / 2) + i * 16 + (lane & 15);
+        const int col = wn * (C / 2) + j * 16 + g4 * 4;
         *reinterpret_cast<uint2*>(sC + row * (C + 8) + col) =
             uint2{pack2(accd[i][j][0], accd[i][j][1]), pack2(accd[i][j][2], accd[i][j][3])};
       }
@@ -215,10 +234,10 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
     f32x4 bsc0, bsc1, bsh0, bsh1;
     bn2_affine(bsc0, bsc1, bsh0, bsh1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = lrow + 32 * i;
+    for (int i = 0; i < NY; ++i) {
+      const int row = erow + RPP * i;
       float f[8], y[8];
-      unpack8(*reinterpret_cast<const u32x4*>(sC + row * (C + 8) + lch * 8), f);
+      unpack8(*reinterpret_cast<const u32x4*>(sC + row * (C + 8) + ech * 8), f);
       unpack8(ry2[i], y);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -227,7 +246,7 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
         f[j + 4] = t1 > 0.f ? f[j + 4] : 0.f;
       }
       const u32x4 v = pack8(f);
-      *reinterpret_cast<u32x4*>(a.da + (size_t)(t * BM + row) * C + lch * 8) = v;
+      *reinterpret_cast<u32x4*>(a.da + (size_t)(t * BM + row) * C + ech * 8) = v;
 #pragma unroll
       for (int h = 0; h < 4; ++h) {  // raw moments of the stored (bf16) values: sum g, sum g*y2
         const f32x2 gv = {__uint_as_float(v[h] << 16), __uint_as_float(v[h] & 0xFFFF0000u)};
@@ -235,9 +254,11 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
         st_s[h] += gv;
         st_q[h] = __builtin_elementwise_fma(gv, yv, st_q[h]);
       }
-      load_y2(tn, i);  // the next tile's y2 chunk into the register just consumed
+      // the next tile's y2: prefetched at the tile start (Y2N) or now, into the register just consumed
+      if constexpr (Y2N) ry2[i] = ry2n[i];
+      else ry2[i] = buf_load16(y2r, y2_off(tn, i));
     }
-    __syncthreads();  // sC (= sA) and sP free for the next tile's staging
+    __syncthreads();  // sC (= sA + sP) free for the next tile's staging
   }
 
   // weight-gradient partial slab ws[blockIdx][k][c] (every workgroup writes one, zero if it had no tile)
@@ -247,13 +268,13 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < TNW; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int k = kb * 64 + wm * 32 + i * 16 + g4 * 4 + r;
-          out[(size_t)k * C + wn * 32 + j * 16 + (lane & 15)] = accw[kb][i][j][r];
+          out[(size_t)k * C + wn * (C / 2) + j * 16 + (lane & 15)] = accw[kb][i][j][r];
         }
-  // BN2-backward moments: threads with the same chunk column (lanes l, l^8, ...; then the 4 waves
+  // BN2-backward moments: threads with the same chunk column (lanes l, l ^ CPR, ...; then the 4 waves
   // through LDS), centred once per channel: sum g*xhat = inv * (sum g*y - mean * sum g)
   float s[8], q[8];
 #pragma unroll
@@ -264,12 +285,12 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int o = 8; o < 64; o <<= 1) {
+    for (int o = CPR; o < 64; o <<= 1) {
       s[j] += __shfl_xor(s[j], o, 64);
       q[j] += __shfl_xor(q[j], o, 64);
     }
   float* red = reinterpret_cast<float*>(sA);  // [4 waves][2][C] (the loop's last barrier freed sA)
-  if (lane < 8) {
+  if (lane < CPR) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       red[(wid * 2 + 0) * C + lane * 8 + j] = s[j];
@@ -277,14 +298,14 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
     }
   }
   __syncthreads();
-  if (tid < C) {
+  for (int c = tid; c < C; c += NT) {
     float ss = 0.f, qq = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) { ss += red[(w * 2) * C + tid]; qq += red[(w * 2 + 1) * C + tid]; }
-    qq = a.inv2[tid] * (qq - a.mean2[tid] * ss);
+    for (int w = 0; w < 4; ++w) { ss += red[(w * 2) * C + c]; qq += red[(w * 2 + 1) * C + c]; }
+    qq = a.inv2[c] * (qq - a.mean2[c] * ss);
     double* st = a.bstats + (size_t)(blockIdx.x % a.nshard) * 2 * C;
-    atomicAdd(st + tid, (double)ss);
-    atomicAdd(st + C + tid, (double)qq);
+    atomicAdd(st + c, (double)ss);
+    atomicAdd(st + C + c, (double)qq);
   }
 }
 
@@ -293,24 +314,43 @@ __global__ __launch_bounds__(256, 2) void dwfused_kernel(const DwFusedArgs a) {
 using namespace dbx;
 
 // Returns the number of partial slabs written (= workgroups), or a negative error.
-// ws_cap: floats available at a.ws (the slabs plus wgrad_reduce's level-1 partials).
-extern "C" int dbx_conv_dwfused(const DwFusedArgs* args, long long ws_cap, hipStream_t st) {
-  const DwFusedArgs& a = *args;
-  if (a.C != 64 || a.K != 256) return -30;
-  if (a.M % 128 != 0 || a.M <= 0) return -31;
-  if (2ull * a.M * a.K >= (unsigned long long)kOOB) return -32;  // 32-bit buffer offsets
+template <int C, int NKB, int BM, int NS, int OCC, bool Y2N>
+static int launch_dwfused(const DwFusedArgs& a, long long ws_cap, hipStream_t st) {
+  if (a.M % BM != 0 || a.M <= 0) return -31;
   static const int cap = [] {
     int per_cu = 0, dev = 0, cus = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&dwfused_kernel<64, 4>),
-                                                       256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&dwfused_kernel<C, NKB, BM, NS, OCC, Y2N>), 256, 0);
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return (per_cu > 0 && cus > 0) ? per_cu * cus : 256;
   }();
-  const int ntile = a.M / 128;
+  const int ntile = a.M / BM;
   const int grid = ntile < cap ? ntile : cap;
   if ((long long)(grid + (grid < 64 ? grid : 64)) * a.K * a.C > ws_cap) return -33;
-  hipLaunchKernelGGL((dwfused_kernel<64, 4>), dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((dwfused_kernel<C, NKB, BM, NS, OCC, Y2N>), dim3(grid), dim3(256), 0, st, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? grid : -(int)e - 1000;
+}
+
+// ws_cap: floats available at a.ws (the slabs plus wgrad_reduce's level-1 partials).
+// Returns the number of partial slabs written (= workgroups), or a negative error.
+extern "C" int dbx_conv_dwfused(const DwFusedArgs* args, long long ws_cap, hipStream_t st) {
+  const DwFusedArgs& a = *args;
+  if (2ull * a.M * a.K >= (unsigned long long)kOOB) return -32;  // 32-bit buffer offsets
+  // 56x56 stage: 128-pixel tiles, two workgroups per CU (32 KB resident weights)
+#ifndef DBX_DWF64
+#define DBX_DWF64 128, 1, 2, false
+#endif
+  if (a.C == 64 && a.K == 256) return launch_dwfused<64, 4, DBX_DWF64>(a, ws_cap, st);
+  // 28x28 stage: 128 KB resident weights -> one workgroup per CU with all 512 registers per lane
+  // (the 512 x 128 weight-gradient accumulators in AGPRs), 64-pixel tiles, two register sets in flight.
+  // Measured at b1024 (tools/bench_dwfused.py, profiles/r2s4_dwfused/): 0.631 ms vs 0.875 ms with
+  // 32-pixel tiles (4 or 2 sets: twice the barriers per pixel with the CU's only workgroup) and
+  // 0.811 ms for the unfused dgrad + wgrad pair
+#ifndef DBX_DWF128
+#define DBX_DWF128 64, 2, 1, false
+#endif
+  if (a.C == 128 && a.K == 512) return launch_dwfused<128, 8, DBX_DWF128>(a, ws_cap, st);
+  return -30;
 }

@@ -455,8 +455,15 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
 
 def dwfused_supported(C: int, K: int, M: int) -> bool:
     """Geometry of the fused bottleneck-conv3 backward kernel (csrc/conv_dwfused.hip): the 64 -> 256
-    channel conv3 of the 56x56 stage, whole 128-pixel tiles, 32-bit buffer offsets."""
-    return C == 64 and K == 256 and M % 128 == 0 and 2 * M * K < 0xFFFFFF00
+    conv3 of the 56x56 stage (128-pixel tiles) and the 128 -> 512 conv3 of the 28x28 stage (64-pixel
+    tiles), whole tiles, 32-bit buffer offsets."""
+    if (C, K) == (64, 256):
+        bm = 128
+    elif (C, K) == (128, 512):
+        bm = 64
+    else:
+        return False
+    return M % bm == 0 and 2 * M * K < 0xFFFFFF00
 
 
 @_dispatch

@@ -158,7 +158,7 @@ def test_fused_conv3_backward_schedule(fold, monkeypatch):
                            use_graphs=False)
         assert (tr.prog.ws_dw is not None) == (flag == "1")
         assert sum(tr.prog._fuse3(b, i == len(tr.prog.blocks) - 1) for i, b in enumerate(tr.prog.blocks)) == (
-            3 if flag == "1" else 0)
+            7 if flag == "1" else 0)  # layer1's 3 and layer2's 4 conv3s
         g = torch.Generator().manual_seed(1)
         img = torch.randint(0, 256, (8, 64, 64, 3), dtype=torch.uint8, generator=g)
         lab = torch.randint(0, 10, (8,), generator=g)

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Time the fused bottleneck-conv3 backward (K.conv_dwfused) against the unfused schedule it replaces
+(BN3-backward apply folded into the MASK_Y dgrad, which stores dy3 and a2, + the weight gradient) at
+the ResNet-50 b1024 stage shapes. Prints ms per call and effective HBM bandwidth of the fused pass."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dbx_distributed_pytorch_examples_amd.ops import kernels as k  # noqa: E402
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    a = ap.parse_args()
+    dev = "cuda"
+    for (H, Cc, Kc) in ((56, 64, 256), (28, 128, 512)):
+        N = a.batch
+        torch.manual_seed(0)
+        g = torch.randn(N, H, H, Kc, device=dev).bfloat16()
+        y3 = torch.randn(N, H, H, Kc, device=dev).bfloat16()
+        coeff = torch.randn(3 * Kc, device=dev) * 0.5
+        wt = (torch.randn(Cc, Kc, device=dev) / Kc ** 0.5).bfloat16()
+        y2 = torch.randn(N, H, H, Cc, device=dev).bfloat16()
+        sc, sh = torch.rand(Cc, device=dev) + 0.5, torch.randn(Cc, device=dev) * 0.3
+        mean, inv = torch.randn(Cc, device=dev) * 0.1, torch.rand(Cc, device=dev) + 0.5
+        da = torch.empty(N, H, H, Cc, device=dev, dtype=torch.bfloat16)
+        dw = torch.empty(Kc, Cc, device=dev)
+        st = k.new_stats(Cc, dev)
+        ws = torch.empty((512 + 64) * Kc * Cc, device=dev)
+        t_f = timeit(lambda: k.conv_dwfused(g, y3, coeff, wt, y2, sc, sh, mean, inv, st, da, dw, ws))
+        dy3, act = torch.empty_like(g), torch.empty_like(y2)
+        wsu = torch.empty(64 * Kc * Cc * 8, device=dev)
+
+        def unfused():
+            e = k.BNBwdEpilogue(k.MASK_Y, y2, mean, inv, st, scale=sc, shift=sh, act_out=act)
+            k.conv_dgrad(g, wt, da, R=1, S=1, stride=1, pad=0, epilogue=e, bwd_y=y3, bwd_coeff=coeff, dy_out=dy3)
+            k.conv_wgrad(dy3, act, dw, wsu, R=1, S=1, stride=1, pad=0)
+        t_u = timeit(unfused)
+        byts = 2 * N * H * H * (2 * Kc + 2 * Cc)
+        print(f"{H}x{H} C={Cc} K={Kc} b{N}: fused {t_f:.3f} ms ({byts / t_f / 1e9:.2f} TB/s) | "
+              f"unfused dgrad+wgrad {t_u:.3f} ms | saved {t_u - t_f:.3f} ms per conv3", flush=True)
+        del g, y3, y2, da, dy3, act
+
+
+if __name__ == "__main__":
+    main()
