@@ -700,7 +700,7 @@ class ResNetProgram:
             return False
         c3 = b.convs[-1]
         return ((c3.R, c3.S, c3.stride, c3.pad) == (1, 1, 1, 0)
-                and K.dwfused_supported(c3.IC, c3.OC, self.N * c3.OH * c3.OW))
+                and K.dwfused_preferred(c3.IC, c3.OC, self.N * c3.OH * c3.OW))
 
     def _fold(self, cv, dense: bool = False) -> bool:
         """Fold the BN-backward apply of cv's output BN into cv's dgrad (1x1 stride-1 convs;

@@ -455,15 +455,19 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
 
 def dwfused_supported(C: int, K: int, M: int) -> bool:
     """Geometry of the fused bottleneck-conv3 backward kernel (csrc/conv_dwfused.hip): the 64 -> 256
-    conv3 of the 56x56 stage (128-pixel tiles) and the 128 -> 512 conv3 of the 28x28 stage (64-pixel
-    tiles), whole tiles, 32-bit buffer offsets."""
-    if (C, K) == (64, 256):
-        bm = 128
-    elif (C, K) == (128, 512):
-        bm = 64
-    else:
-        return False
-    return M % bm == 0 and 2 * M * K < 0xFFFFFF00
+    conv3 of the 56x56 stage and the 128 -> 512 conv3 of the 28x28 stage (64-pixel tiles), whole
+    tiles, 32-bit buffer offsets."""
+    return (C, K) in ((64, 256), (128, 512)) and M % 64 == 0 and 2 * M * K < 0xFFFFFF00
+
+
+def dwfused_preferred(C: int, K: int, M: int) -> bool:
+    """Schedule policy: the fused conv3 backward only when every resident workgroup walks >=
+    DBX_FUSE_DW_MIN_TILES (default 8) tiles -- with fewer, the per-workgroup weight load and slab write
+    and the lost wgrad side-stream overlap outweigh the saved traffic (TinyImageNet b512 fused at 2-4
+    tiles per workgroup: 86.5k vs 87.2k img/s, profiles/r2s4_dwfused/)."""
+    import os
+    grid = 512 if (C, K) == (64, 256) else 256  # resident workgroups: 2 / 1 per CU
+    return dwfused_supported(C, K, M) and M >= int(os.environ.get("DBX_FUSE_DW_MIN_TILES", "8")) * grid * 64
 
 
 @_dispatch

@@ -115,6 +115,7 @@ def test_native_step_fused_vs_unfused(monkeypatch):
     img = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device=dev)
     lab = torch.randint(0, 1000, (2,), device=dev)
     grads = []
+    monkeypatch.setenv("DBX_FUSE_DW_MIN_TILES", "0")  # batch 2: fuse regardless of tiles per workgroup
     for flag in ("1", "0"):
         monkeypatch.setenv("DBX_FUSE_DW", flag)
         torch.manual_seed(0)

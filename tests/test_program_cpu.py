@@ -148,6 +148,7 @@ def test_fused_conv3_backward_schedule(fold, monkeypatch):
     """DBX_FUSE_DW: the bottleneck conv3 backward as one op (K.conv_dwfused) gives the gradients of
     the unfused schedule (BN-backward apply -> MASK_Y dgrad -> weight gradient), folded or not."""
     monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(fold))
+    monkeypatch.setenv("DBX_FUSE_DW_MIN_TILES", "0")  # small batch: fuse regardless of tiles per workgroup
     grads = []
     for flag in ("1", "0"):
         monkeypatch.setenv("DBX_FUSE_DW", flag)

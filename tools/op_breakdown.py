@@ -57,6 +57,12 @@ def est(name, args, kw):
         N, OH, OW, OC = dy.shape
         fl = 2 * dy.numel() * dw.shape[1] if not kw.get("stem") else 2 * dy.numel() * 147
         return f"wgrad {x.shape[3]}->{OC} {kw['R']}x{kw['S']} s{kw['stride']} @{x.shape[1]}", fl, _b(dy) + _b(x) + _b(dw)
+    if name == "conv_dwfused":
+        g, y3, _, wt, y2 = args[:5]
+        da, dw = args[10], args[11]
+        fl = 2 * 2 * g.numel() * y2.shape[-1]  # data + weight gradient GEMMs
+        return (f"dwfused {g.shape[3]}->{y2.shape[3]} 1x1 @{g.shape[1]}", fl,
+                _b(g) + _b(y3) + _b(y2) + _b(da) + _b(wt))
     if name == "conv_stem_fwd":
         x4, w, out = args[:3]
         return "stem fwd", 2 * out.numel() * 147, _b(x4) + _b(out)
@@ -99,7 +105,7 @@ def main():
     for _ in range(2):
         tr.step()
     torch.cuda.synchronize()
-    for n in ["conv_fwd", "conv_dgrad", "conv_wgrad", "conv_stem_fwd", "bn_apply", "bn_bwd_apply", "bn_bwd_reduce",
+    for n in ["conv_fwd", "conv_dgrad", "conv_wgrad", "conv_dwfused", "conv_stem_fwd", "bn_apply", "bn_bwd_apply", "bn_bwd_reduce",
               "bn_bwd_coeff", "bn_finalize", "maxpool_fwd", "maxpool_bwd", "avgpool_fwd", "avgpool_bwd",
               "softmax_ce", "sgd_step", "weight_prep", "augment_u8", "pool_bn_bwd_reduce", "pool_bn_bwd_apply", "bn_bwd_apply2"]:
         wrap(n)
