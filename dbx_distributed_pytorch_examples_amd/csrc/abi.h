@@ -78,4 +78,19 @@ struct DwFusedArgs {
   float* ws;             // [grid][K][C] fp32 weight-gradient partial slabs
   int M, K, C, nshard;
 };
+// Fused stem backward (max-pool backward + BN-backward apply + stem weight gradient), stem_bwd.hip
+struct StemBwdArgs {
+  const bf16* dpool;          // [N][P][Q][C] max-pool output gradient
+  const unsigned char* arg;   // [N][P][Q][C] argmax r*PK + s within each pooling window
+  const bf16* y;              // [N][H][W][C] stem conv output (the BN input)
+  const float* sc;            // stem BN forward scale / shift (the ReLU mask)
+  const float* sh;
+  const float* coeff;         // [3][C] BN-backward apply: dy = k1*g + k2*y + k3
+  const bf16* x4;             // [N][IH][IW][4] NHWC4 input image
+  float* ws;                  // [nsplit][C][256] fp32 weight-gradient partial slabs (8 x 8 x 4 taps)
+  int N, H, W, C, P, Q, PK, pstride, ppad;  // stem output / max-pool geometry
+  int IH, IW, R, S, stride, pad;             // stem conv geometry
+  int M, nsplit, m_per_split;
+  unsigned long long mag_hw, mag_w;          // ceil(2^40 / (H*W)), ceil(2^40 / W)
+};
 }  // namespace dbx

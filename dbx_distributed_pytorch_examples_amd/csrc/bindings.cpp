@@ -20,6 +20,7 @@ int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, h
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
 int dbx_wgrad_patch3(const dbx::WgradArgs* a, hipStream_t st);
 int dbx_conv_dwfused(const dbx::DwFusedArgs* a, long long ws_cap, hipStream_t st);
+int dbx_stem_bwd(dbx::StemBwdArgs* a, long long ws_cap, hipStream_t st);
 int dbx_bn_finalize(const double*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
                     float*, float*, float*, hipStream_t);
 int dbx_bn_eval_coeff(int, const float*, const float*, float, const float*, const float*, float*, float*, hipStream_t);
@@ -133,6 +134,20 @@ PYBIND11_MODULE(_C, m) {
                        nshard > 0 ? nshard : 1};
     const int n = dbx_conv_dwfused(&a, ws_cap, S(st));
     if (n <= 0) check(n ? n : -1, "conv_dwfused");
+    return n;
+  });
+  m.def("stem_bwd", [](uintptr_t dpool, uintptr_t arg, uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t coeff,
+                       uintptr_t x4, uintptr_t ws, long long ws_cap, int N, int H, int W, int C, int Pp, int Qq, int PK,
+                       int pstride, int ppad, int IH, int IW, int R, int S_, int stride, int pad, uintptr_t st) {
+    // fused stem backward (stem_bwd.hip): returns the number of dW partial slabs
+    const unsigned long long two40 = 1ull << 40, hw = (unsigned long long)H * W;
+    if ((unsigned long long)N * hw * hw >= two40) throw std::runtime_error("stem_bwd: batch too large for mdiv");
+    dbx::StemBwdArgs a{P<const bf16*>(dpool), P<const unsigned char*>(arg), P<const bf16*>(y), P<const float*>(sc),
+                       P<const float*>(sh), P<const float*>(coeff), P<const bf16*>(x4), P<float*>(ws), N, H, W, C, Pp, Qq,
+                       PK, pstride, ppad, IH, IW, R, S_, stride, pad, N * H * W, 0, 0, (two40 + hw - 1) / hw,
+                       (two40 + W - 1) / W};
+    const int n = dbx_stem_bwd(&a, ws_cap, S(st));
+    if (n <= 0) check(n ? n : -1, "stem_bwd");
     return n;
   });
   m.def("wgrad_reduce", [](uintptr_t ws, uintptr_t dw, long long n, int nsplit, float scale, int acc, uintptr_t st) {

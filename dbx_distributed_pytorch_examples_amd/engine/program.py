@@ -159,6 +159,12 @@ class ResNetProgram:
         # bottleneck conv3 backward as ONE kernel (BN3-backward apply + dgrad + MASK_Y epilogue +
         # weight gradient, K.conv_dwfused): dy3 and the BN2 output a2 never reach HBM
         self.fuse_dw = os.environ.get("DBX_FUSE_DW", "1") == "1"
+        # stem backward as ONE kernel (max-pool backward + BN-backward apply + stem weight gradient,
+        # K.stem_bwd_fused): the full-resolution stem gradient never reaches HBM. Off by default: it
+        # saves the 3.3 GB dy0 round trip at b1024 but runs 1.97 ms against 0.91 + 0.92 ms for the
+        # streaming pool/BN pass + the stem wgrad (the 4-window argmax routing per element is VALU work
+        # that the two-workgroups-per-CU MFMA kernel cannot hide; profiles/r2s4_stem/)
+        self.fuse_stem_bwd = os.environ.get("DBX_FUSE_STEM_BWD", "0") == "1"
         self._wstream = None
         self._side_pending = False
         self._build_layers()
@@ -724,6 +730,13 @@ class ResNetProgram:
                                      **pk)
             K.bn_bwd_coeff(sbn.bstats, self.N * st.OH * st.OW, sbn.gamma, sbn.mean, sbn.invstd, sbn.coeff,
                            sbn.dgamma, sbn.dbeta)
+            if self.fuse_stem_bwd and K.stem_bwd_supported(st.OC, self.pool_k, self.pool_s, st.R, st.S):
+                # dy0 = BN-backward apply of the pool backward, straight into the weight-gradient tiles
+                K.stem_bwd_fused(dp, self.parg, self.y0, sbn.scale, sbn.shift, sbn.coeff, self.x4, self.stem_grad_tmp,
+                                 self.ws, R=st.R, S=st.S, conv_stride=st.stride, conv_pad=st.pad, **pk)
+                g = self.grad[st.off:st.off + st.numel].view(st.OC, st.R, st.S, st.IC)
+                g.copy_(self.stem_grad_tmp.view(st.OC, 8, 8, 4)[:, :st.R, :st.S, :st.IC])
+                return
             K.pool_bn_bwd_apply(dp, self.parg, self.y0, sbn.scale, sbn.shift, sbn.coeff, self.dy0, **pk)
         else:
             K.maxpool_bwd(dp, self.parg, self.da0, K=self.pool_k, stride=self.pool_s, pad=self.pool_p)

@@ -650,6 +650,39 @@ def pool_bn_bwd_apply(dpool, arg, y, scale, shift, coeff, dy, *, K=3, stride=2, 
                     N, H, W, Cc, Pp, Q, K, stride, pad, 1, stream_ptr())
 
 
+def stem_bwd_supported(C: int, K: int, stride: int, R: int, S: int) -> bool:
+    """Geometry of the fused stem backward (csrc/stem_bwd.hip): 64 stem channels, <= 8x8 taps,
+    pooling windows that cover a pixel at most twice per dimension."""
+    return C == 64 and R <= 8 and S <= 8 and (K + stride - 1) // stride <= 2
+
+
+@_dispatch
+def stem_bwd_fused(dpool, arg, y, scale, shift, coeff, x4, dw, ws, *, K=3, stride=2, pad=1, R=7, S=7,
+                   conv_stride=2, conv_pad=3):
+    """Stem backward in one pass (csrc/stem_bwd.hip): dy = BN-backward apply of the max-pool
+    backward of ``dpool`` (argmax ``arg``, ReLU mask from ``y*scale + shift``) -- never stored -- and
+    the stem weight gradient ``dw`` [C, 8*8*4] fp32 (the stem's padded tap layout) = dy^T im2col(x4),
+    through per-workgroup slabs in ``ws`` + the deterministic split reduction. Replaces
+    ``pool_bn_bwd_apply`` + ``conv_wgrad(..., stem=True)``."""
+    N, H, W, Cc, Pp, Q = _pool_bn_bwd_check(dpool, arg, y, K, stride)
+    _chk(x4, torch.bfloat16, "x4")
+    _chk(coeff, torch.float32, "coeff", 3 * Cc)
+    _chk(scale, torch.float32, "scale", Cc)
+    _chk(shift, torch.float32, "shift", Cc)
+    _chk(dw, torch.float32, "dw", Cc * 256)
+    _chk(ws, torch.float32, "ws")
+    Nx, IH, IW, C4 = x4.shape
+    if Nx != N or C4 != 4 or conv_out_hw(IH, IW, R, S, conv_stride, conv_pad) != (H, W):
+        raise ValueError("stem_bwd_fused: image / stem output shapes disagree")
+    if not stem_bwd_supported(Cc, K, stride, R, S):
+        raise ValueError("stem_bwd_fused: unsupported geometry")
+    n = C().stem_bwd(dpool.data_ptr(), arg.data_ptr(), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                     coeff.data_ptr(), x4.data_ptr(), ws.data_ptr(), ws.numel(), N, H, W, Cc, Pp, Q, K, stride, pad,
+                     IH, IW, R, S, conv_stride, conv_pad, stream_ptr())
+    C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), Cc * 256, n, 1.0, 0, stream_ptr())
+    return dw
+
+
 @_dispatch
 def avgpool_fwd(x, out):
     N, H, W, Cc = x.shape

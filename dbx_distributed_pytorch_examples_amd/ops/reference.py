@@ -318,6 +318,15 @@ def pool_bn_bwd_apply(dpool, arg, y, scale, shift, coeff, dy, *, K=3, stride=2, 
     dy.copy_((k[0] * g + k[1] * y.float() + k[2]).bfloat16())
 
 
+def stem_bwd_fused(dpool, arg, y, scale, shift, coeff, x4, dw, ws, *, K=3, stride=2, pad=1, R=7, S=7,
+                   conv_stride=2, conv_pad=3):
+    """Fused stem backward = pool_bn_bwd_apply + the stem weight gradient."""
+    dy = torch.empty_like(y)
+    pool_bn_bwd_apply(dpool, arg, y, scale, shift, coeff, dy, K=K, stride=stride, pad=pad)
+    conv_wgrad(dy, x4, dw, ws, R=R, S=S, stride=conv_stride, pad=conv_pad, stem=True)
+    return dw
+
+
 def avgpool_fwd(x, out):
     out.copy_(x.float().mean((1, 2)).bfloat16())
 

@@ -63,6 +63,10 @@ def est(name, args, kw):
         fl = 2 * 2 * g.numel() * y2.shape[-1]  # data + weight gradient GEMMs
         return (f"dwfused {g.shape[3]}->{y2.shape[3]} 1x1 @{g.shape[1]}", fl,
                 _b(g) + _b(y3) + _b(y2) + _b(da) + _b(wt))
+    if name == "stem_bwd_fused":
+        dpool, arg, y = args[:3]
+        x4 = args[6]
+        return "stem bwd fused", 2 * y.numel() * 256, _b(dpool) + _b(arg) + _b(y) + _b(x4)
     if name == "conv_stem_fwd":
         x4, w, out = args[:3]
         return "stem fwd", 2 * out.numel() * 147, _b(x4) + _b(out)
@@ -105,7 +109,7 @@ def main():
     for _ in range(2):
         tr.step()
     torch.cuda.synchronize()
-    for n in ["conv_fwd", "conv_dgrad", "conv_wgrad", "conv_dwfused", "conv_stem_fwd", "bn_apply", "bn_bwd_apply", "bn_bwd_reduce",
+    for n in ["conv_fwd", "conv_dgrad", "conv_wgrad", "conv_dwfused", "stem_bwd_fused", "conv_stem_fwd", "bn_apply", "bn_bwd_apply", "bn_bwd_reduce",
               "bn_bwd_coeff", "bn_finalize", "maxpool_fwd", "maxpool_bwd", "avgpool_fwd", "avgpool_bwd",
               "softmax_ce", "sgd_step", "weight_prep", "augment_u8", "pool_bn_bwd_reduce", "pool_bn_bwd_apply", "bn_bwd_apply2"]:
         wrap(n)
