@@ -24,20 +24,25 @@
 namespace dbx {
 
 // C: dgrad output channels (conv3 input), NKB: K / 64, BM: pixels per tile, NS: register staging
-// sets (the g / y3 loads of block kb + NS are issued while block kb is computed), OCC: workgroups
-// per CU (2: 256 VGPRs per lane; 1: the LDS holds one workgroup, whose waves get all 512), Y2N:
-// prefetch the next tile's y2 into spare registers at the tile start (else during the epilogue).
-template <int C, int NKB, int BM, int NS, int OCC, bool Y2N>
-__global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) {
-  constexpr int NT = 256, K = NKB * 64;
+// sets (the g / y3 loads of block kb + NS are issued while block kb is computed), NT: threads,
+// WN: waves along the channels (grid 2 x WN: a wave owns C / WN channels of both GEMMs, so the
+// weight-gradient accumulators per lane are 64 K / NT x C), OCC: workgroups per CU, Y2N: prefetch the
+// next tile's y2 into spare registers at the tile start (else during the epilogue).
+template <int C, int NKB, int BM, int NS, int NT, int WN, int OCC, bool Y2N>
+__global__ __launch_bounds__(NT, OCC) void dwfused_kernel(const DwFusedArgs a) {
+  constexpr int K = NKB * 64;
+  constexpr int NW = NT / 64, WM = NW / WN;  // wave grid: WM x WN (WM = 2)
+  constexpr int WC = C / WN;                 // channels per wave
   constexpr int WCH = K / 8;            // 16-byte chunks per resident weight row
   constexpr int CPR = C / 8;            // chunks per a2 / da row
   constexpr int RPP = NT / CPR;         // a2 / da rows per thread pass
   constexpr int NY = BM / RPP;          // y2 / da chunks per thread
-  constexpr int NG = BM / 32;           // g / y3 chunks per thread and K-block (rows lrow + 32 i)
-  constexpr int TM = BM / 32, TN = C / 32;  // dgrad: wave (wm, wn) owns BM/2 pixels x C/2 channels
-  constexpr int TNW = C / 32;               // wgrad: wave owns 32 k x C/2 channels of each K-block
-  static_assert(NKB % NS == 0 && C % 64 == 0 && BM % 32 == 0 && BM % RPP == 0, "tile shape");
+  constexpr int LR = NT / 8;            // g / y3 rows per thread pass (8 chunks per 64-wide row)
+  constexpr int NG = BM / LR;           // g / y3 chunks per thread and K-block (rows lrow + LR i)
+  constexpr int TM = BM / (16 * WM), TN = WC / 16;  // dgrad: wave (wm, wn) owns BM/WM pixels x WC channels
+  constexpr int TNW = WC / 16;                      // wgrad: wave owns 32 k x WC channels of each K-block
+  static_assert(NKB % NS == 0 && C % 64 == 0 && WM == 2 && BM % (16 * WM) == 0 && BM % LR == 0 && BM % RPP == 0,
+                "tile shape");
   constexpr int LDS_W = C * K, LDS_A = 2 * BM * 64, LDS_P = BM * C;
   static_assert(BM * (C + 8) <= LDS_A + LDS_P, "epilogue staging must fit the dy3 + a2 images");
   __shared__ __attribute__((aligned(16))) bf16 lds[LDS_W + LDS_A + LDS_P];
@@ -46,9 +51,9 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
   bf16* sP = sA + LDS_A;       // [BM][C] a2 tile (tr_swz)
   bf16* sC = sA;               // epilogue staging [BM][C + 8] (aliases sA + sP after the K loop)
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
   const int ntile = a.M / BM;
-  const int lrow = tid >> 3, lch = tid & 7;      // g / y3 loader: rows lrow + 32 i, chunk lch
+  const int lrow = tid >> 3, lch = tid & 7;      // g / y3 loader: rows lrow + LR i, chunk lch
   const int erow = tid / CPR, ech = tid % CPR;   // y2 / epilogue: rows erow + RPP i, chunk ech
 
   for (int q = tid; q < C * WCH; q += NT) {
@@ -85,7 +90,7 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
   auto load_k = [&](int t, int kb, int set) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
-      const unsigned off = t < ntile ? 2u * (unsigned)((t * BM + lrow + 32 * i) * K + kb * 64 + lch * 8) : kOOB;
+      const unsigned off = t < ntile ? 2u * (unsigned)((t * BM + lrow + LR * i) * K + kb * 64 + lch * 8) : kOOB;
       rg[set][i] = buf_load16(gr, off);
       ry[set][i] = buf_load16(yr, off);
     }
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
         f[j] = f[j] * k1a[j] + k3a[j] + y[j] * k2a[j];
         f[j + 4] = f[j + 4] * k1b[j] + k3b[j] + y[j + 4] * k2b[j];
       }
-      const int row = lrow + 32 * i;
+      const int row = lrow + LR * i;
       *reinterpret_cast<u32x4*>(sA + buf * BM * 64 + row * 64 + (tr_swz(row, lch, 8) << 3)) = pack8(f);
     }
   };
@@ -144,12 +149,12 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
       bf16x8 af[TM], bw[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / 2) + i * 16 + (lane & 15);
+        const int row = wm * (BM / WM) + i * 16 + (lane & 15);
         af[i] = *reinterpret_cast<const bf16x8*>(cA + row * 64 + (tr_swz(row, ch, 8) << 3));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int crow = wn * (C / 2) + j * 16 + (lane & 15);
+        const int crow = wn * WC + j * 16 + (lane & 15);
         bw[j] = *reinterpret_cast<const bf16x8*>(sW + crow * K + (((kb * 8 + ch) ^ (crow & 15)) << 3));
       }
 #pragma unroll
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
       }
 #pragma unroll
       for (int j = 0; j < TNW; ++j) {
-        const int col = wn * (C / 2) + j * 16 + 4 * p4;
+        const int col = wn * WC + j * 16 + 4 * p4;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (DBX_LDS s16x4*)(sP + row * C + (tr_swz(row, col >> 3, CPR) << 3) + (col & 7)));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -225,8 +230,8 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int row = wm * (BM / 2) + i * 16 + (lane & 15);
-        const int col = wn * (C / 2) + j * 16 + g4 * 4;
+        const int row = wm * (BM / WM) + i * 16 + (lane & 15);
+        const int col = wn * WC + j * 16 + g4 * 4;
         *reinterpret_cast<uint2*>(sC + row * (C + 8) + col) =
             uint2{pack2(accd[i][j][0], accd[i][j][1]), pack2(accd[i][j][2], accd[i][j][3])};
       }
@@ -272,7 +277,7 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int k = kb * 64 + wm * 32 + i * 16 + g4 * 4 + r;
-          out[(size_t)k * C + wn * (C / 2) + j * 16 + (lane & 15)] = accw[kb][i][j][r];
+          out[(size_t)k * C + wn * WC + j * 16 + (lane & 15)] = accw[kb][i][j][r];
         }
   // BN2-backward moments: threads with the same chunk column (lanes l, l ^ CPR, ...; then the 4 waves
   // through LDS), centred once per channel: sum g*xhat = inv * (sum g*y - mean * sum g)
@@ -289,7 +294,7 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
       s[j] += __shfl_xor(s[j], o, 64);
       q[j] += __shfl_xor(q[j], o, 64);
     }
-  float* red = reinterpret_cast<float*>(sA);  // [4 waves][2][C] (the loop's last barrier freed sA)
+  float* red = reinterpret_cast<float*>(sA);  // [NW waves][2][C] (the loop's last barrier freed sA)
   if (lane < CPR) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -301,7 +306,7 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
   for (int c = tid; c < C; c += NT) {
     float ss = 0.f, qq = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) { ss += red[(w * 2) * C + c]; qq += red[(w * 2 + 1) * C + c]; }
+    for (int w = 0; w < NW; ++w) { ss += red[(w * 2) * C + c]; qq += red[(w * 2 + 1) * C + c]; }
     qq = a.inv2[c] * (qq - a.mean2[c] * ss);
     double* st = a.bstats + (size_t)(blockIdx.x % a.nshard) * 2 * C;
     atomicAdd(st + c, (double)ss);
@@ -314,13 +319,13 @@ __global__ __launch_bounds__(256, OCC) void dwfused_kernel(const DwFusedArgs a) 
 using namespace dbx;
 
 // Returns the number of partial slabs written (= workgroups), or a negative error.
-template <int C, int NKB, int BM, int NS, int OCC, bool Y2N>
+template <int C, int NKB, int BM, int NS, int NT, int WN, int OCC, bool Y2N>
 static int launch_dwfused(const DwFusedArgs& a, long long ws_cap, hipStream_t st) {
   if (a.M % BM != 0 || a.M <= 0) return -31;
   static const int cap = [] {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(&dwfused_kernel<C, NKB, BM, NS, OCC, Y2N>), 256, 0);
+        &per_cu, reinterpret_cast<const void*>(&dwfused_kernel<C, NKB, BM, NS, NT, WN, OCC, Y2N>), NT, 0);
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return (per_cu > 0 && cus > 0) ? per_cu * cus : 256;
@@ -328,7 +333,7 @@ static int launch_dwfused(const DwFusedArgs& a, long long ws_cap, hipStream_t st
   const int ntile = a.M / BM;
   const int grid = ntile < cap ? ntile : cap;
   if ((long long)(grid + (grid < 64 ? grid : 64)) * a.K * a.C > ws_cap) return -33;
-  hipLaunchKernelGGL((dwfused_kernel<C, NKB, BM, NS, OCC, Y2N>), dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((dwfused_kernel<C, NKB, BM, NS, NT, WN, OCC, Y2N>), dim3(grid), dim3(NT), 0, st, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? grid : -(int)e - 1000;
 }
@@ -341,16 +346,16 @@ extern "C" int dbx_conv_dwfused(const DwFusedArgs* args, long long ws_cap, hipSt
   // 56x56 stage: two workgroups per CU (32 KB resident weights), 64-pixel tiles, two register sets
   // (0.903 ms at b1024 vs 0.928 ms for 128-pixel tiles with one set, 1.052 ms with 64 / one set)
 #ifndef DBX_DWF64
-#define DBX_DWF64 64, 2, 2, false
+#define DBX_DWF64 64, 2, 256, 2, 2, false
 #endif
   if (a.C == 64 && a.K == 256) return launch_dwfused<64, 4, DBX_DWF64>(a, ws_cap, st);
-  // 28x28 stage: 128 KB resident weights -> one workgroup per CU with all 512 registers per lane
-  // (the 512 x 128 weight-gradient accumulators in AGPRs), 64-pixel tiles, two register sets in flight.
+  // 28x28 stage: 128 KB resident weights -> one workgroup per CU; 4 waves (2 x 2) whose lanes hold
+  // the 256 weight-gradient accumulators in AGPRs, 64-pixel tiles, two register sets in flight.
   // Measured at b1024 (tools/bench_dwfused.py, profiles/r2s4_dwfused/): 0.631 ms vs 0.875 ms with
-  // 32-pixel tiles (4 or 2 sets: twice the barriers per pixel with the CU's only workgroup) and
-  // 0.811 ms for the unfused dgrad + wgrad pair
+  // 32-pixel tiles, 0.73 / 1.03 ms with 8 waves (2 x 4, 128 accumulators per lane, 2 / 4 sets: the
+  // rest of the state still spills at 256 registers), 0.811 ms for the unfused dgrad + wgrad pair
 #ifndef DBX_DWF128
-#define DBX_DWF128 64, 2, 1, false
+#define DBX_DWF128 64, 2, 256, 2, 1, false
 #endif
   if (a.C == 128 && a.K == 512) return launch_dwfused<128, 8, DBX_DWF128>(a, ws_cap, st);
   return -30;
