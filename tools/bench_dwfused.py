@@ -43,7 +43,7 @@ def main():
         da = torch.empty(N, H, H, Cc, device=dev, dtype=torch.bfloat16)
         dw = torch.empty(Kc, Cc, device=dev)
         st = k.new_stats(Cc, dev)
-        ws = torch.empty((512 + 64) * Kc * Cc, device=dev)
+        ws = torch.empty((1024 + 64) * Kc * Cc, device=dev)
         t_f = timeit(lambda: k.conv_dwfused(g, y3, coeff, wt, y2, sc, sh, mean, inv, st, da, dw, ws))
         dy3, act = torch.empty_like(g), torch.empty_like(y2)
         wsu = torch.empty(64 * Kc * Cc * 8, device=dev)
