@@ -20,7 +20,7 @@ int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, h
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
 int dbx_wgrad_patch3(const dbx::WgradArgs* a, hipStream_t st);
 int dbx_conv_dwfused(const dbx::DwFusedArgs* a, long long ws_cap, hipStream_t st);
-int dbx_stem_bwd(dbx::StemBwdArgs* a, long long ws_cap, hipStream_t st);
+int dbx_stem_bwd(dbx::StemBwdArgs* a, long long ws_cap, int fused, hipStream_t st);
 int dbx_bn_finalize(const double*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
                     float*, float*, float*, hipStream_t);
 int dbx_bn_eval_coeff(int, const float*, const float*, float, const float*, const float*, float*, float*, hipStream_t);
@@ -138,15 +138,16 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("stem_bwd", [](uintptr_t dpool, uintptr_t arg, uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t coeff,
                        uintptr_t x4, uintptr_t ws, long long ws_cap, int N, int H, int W, int C, int Pp, int Qq, int PK,
-                       int pstride, int ppad, int IH, int IW, int R, int S_, int stride, int pad, uintptr_t st) {
-    // fused stem backward (stem_bwd.hip): returns the number of dW partial slabs
+                       int pstride, int ppad, int IH, int IW, int R, int S_, int stride, int pad, int fused,
+                       uintptr_t st) {
+    // stem backward / stem weight gradient (stem_bwd.hip): returns the number of dW partial slabs
     const unsigned long long two40 = 1ull << 40, hw = (unsigned long long)H * W;
     if ((unsigned long long)N * hw * hw >= two40) throw std::runtime_error("stem_bwd: batch too large for mdiv");
     dbx::StemBwdArgs a{P<const bf16*>(dpool), P<const unsigned char*>(arg), P<const bf16*>(y), P<const float*>(sc),
                        P<const float*>(sh), P<const float*>(coeff), P<const bf16*>(x4), P<float*>(ws), N, H, W, C, Pp, Qq,
                        PK, pstride, ppad, IH, IW, R, S_, stride, pad, N * H * W, 0, 0, (two40 + hw - 1) / hw,
                        (two40 + W - 1) / W};
-    const int n = dbx_stem_bwd(&a, ws_cap, S(st));
+    const int n = dbx_stem_bwd(&a, ws_cap, fused, S(st));
     if (n <= 0) check(n ? n : -1, "stem_bwd");
     return n;
   });

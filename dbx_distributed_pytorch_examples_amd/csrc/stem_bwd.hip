@@ -27,6 +27,10 @@ __device__ __forceinline__ u32x2 buf_load8(rsrc_t r, unsigned off) {
   return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
 
+// FUSED = false: the plain stem weight gradient from a stored dy (a.y), same tiles / pipeline: one
+// 64 x 256 tile per workgroup, so dy is read once (the generic wgrad kernel splits the 256 tap
+// columns over two workgroups that each read it).
+template <bool FUSED>
 __global__ __launch_bounds__(256, 2) void stem_bwd_kernel(const StemBwdArgs a) {
   constexpr int C = 64, KT = 256, BKM = 64;
   constexpr int TM = 2, TN = 8;  // wave (wm, wn): 32 output channels x 128 tap columns
@@ -61,6 +65,10 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_kernel(const StemBwdArgs a) {
     for (int i = 0; i < 2; ++i) {
       const int m = m0 + arow + 32 * i;
       const bool mv = m < mlim;
+      if constexpr (!FUSED) {
+        ry[i] = buf_load16(yr, mv ? 2u * (unsigned)(m * C + ach * 8) : kOOB);
+        continue;
+      }
       const int n = mdiv(m, a.mag_hw), hw = m - n * HW;
       const int h = mdiv(hw, a.mag_w), w = hw - h * a.W;
       const int p_lo = max(0, (h + a.ppad - a.PK + a.pstride) / a.pstride);
@@ -101,6 +109,13 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_kernel(const StemBwdArgs a) {
   // pinning 40 VGPRs across the MFMAs
   int cbn = ach * 8;
   auto compute_store = [&](int buf) __attribute__((always_inline)) {
+    if constexpr (!FUSED) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = arow + 32 * i;
+        *reinterpret_cast<u32x4*>(sA + buf * BKM * C + row * C + (tr_swz(row, ach, 8) << 3)) = ry[i];
+      }
+    } else {
     asm volatile("" : "+v"(cbn));
     float s_[8], h_[8], k1[8], k2[8], k3[8];
 #pragma unroll
@@ -140,6 +155,7 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_kernel(const StemBwdArgs a) {
       }
       const int row = arow + 32 * i;
       *reinterpret_cast<u32x4*>(sA + buf * BKM * C + row * C + (tr_swz(row, ach, 8) << 3)) = pack8(o);
+    }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -216,17 +232,18 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_kernel(const StemBwdArgs a) {
 
 using namespace dbx;
 
-// Returns the number of partial slabs written (= workgroups), or a negative error.
-extern "C" int dbx_stem_bwd(StemBwdArgs* args, long long ws_cap, hipStream_t st) {
+// Returns the number of partial slabs written (= workgroups), or a negative error. fused = 0: the
+// plain stem weight gradient of the stored gradient a.y (pool / BN fields unused).
+extern "C" int dbx_stem_bwd(StemBwdArgs* args, long long ws_cap, int fused, hipStream_t st) {
   StemBwdArgs& a = *args;
   if (a.C != 64 || a.R > 8 || a.S > 8) return -40;
-  if ((a.PK + a.pstride - 1) / a.pstride > 2) return -41;  // <= 2 x 2 pooling windows per pixel
+  if (fused && (a.PK + a.pstride - 1) / a.pstride > 2) return -41;  // <= 2 x 2 pooling windows per pixel
   if ((long long)a.N * a.H * a.W * a.C >= (1ll << 31) || 8ll * a.N * a.IH * a.IW >= (long long)kOOB) return -42;
   if (a.M <= 0) return -43;
   static const int cap = [] {
     int per_cu = 0, dev = 0, cus = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&stem_bwd_kernel), 256,
-                                                       0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&stem_bwd_kernel<true>),
+                                                       256, 0);
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return (per_cu > 0 && cus > 0) ? per_cu * cus : 256;
@@ -238,7 +255,8 @@ extern "C" int dbx_stem_bwd(StemBwdArgs* args, long long ws_cap, hipStream_t st)
   nsplit = (nblk + bps - 1) / bps;
   a.nsplit = nsplit;
   if ((long long)(nsplit + (nsplit < 64 ? nsplit : 64)) * a.C * 256 > ws_cap) return -44;
-  hipLaunchKernelGGL(stem_bwd_kernel, dim3(nsplit), dim3(256), 0, st, a);
+  if (fused) hipLaunchKernelGGL(stem_bwd_kernel<true>, dim3(nsplit), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(stem_bwd_kernel<false>, dim3(nsplit), dim3(256), 0, st, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? nsplit : -(int)e - 1000;
 }

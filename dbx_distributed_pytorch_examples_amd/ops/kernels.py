@@ -375,6 +375,17 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
 
 
 _WG_ROUNDS = None
+_STEM_WGRAD = None
+
+
+def _stem_wgrad_tile() -> bool:
+    """DBX_STEM_WGRAD: "tile" (default) = the 64 x 256-tile stem weight gradient (csrc/stem_bwd.hip),
+    "generic" = the wgrad kernel's STEM mode (two 128-column tiles; A/B switch)."""
+    global _STEM_WGRAD
+    if _STEM_WGRAD is None:
+        import os
+        _STEM_WGRAD = os.environ.get("DBX_STEM_WGRAD", "tile") == "tile"
+    return _STEM_WGRAD
 
 
 def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int) -> Tuple[int, int]:
@@ -423,6 +434,13 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         return dw
     if isinstance(tile, str):
         raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 wgrad at width 56 without a prologue")
+    if stem and OC == 64 and R <= 8 and S <= 8 and tile is None and _stem_wgrad_tile():
+        # one 64 x 256 tile per workgroup (csrc/stem_bwd.hip, plain mode): dy read once
+        _chk(dy, torch.bfloat16, "dy", N * OH * OW * 64)
+        n = C().stem_bwd(0, 0, dy.data_ptr(), 0, 0, 0, x.data_ptr(), ws.data_ptr(), ws.numel(), N, OH, OW, OC, 0, 0,
+                         0, 1, 0, IH, IW, R, S, stride, pad, 0, stream_ptr())
+        C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, n, float(scale), int(accumulate), stream_ptr())
+        return dw
     if stem:
         bm, bn = 64, 128
     else:
@@ -678,7 +696,7 @@ def stem_bwd_fused(dpool, arg, y, scale, shift, coeff, x4, dw, ws, *, K=3, strid
         raise ValueError("stem_bwd_fused: unsupported geometry")
     n = C().stem_bwd(dpool.data_ptr(), arg.data_ptr(), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
                      coeff.data_ptr(), x4.data_ptr(), ws.data_ptr(), ws.numel(), N, H, W, Cc, Pp, Q, K, stride, pad,
-                     IH, IW, R, S, conv_stride, conv_pad, stream_ptr())
+                     IH, IW, R, S, conv_stride, conv_pad, 1, stream_ptr())
     C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), Cc * 256, n, 1.0, 0, stream_ptr())
     return dw
 

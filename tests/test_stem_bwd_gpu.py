@@ -112,3 +112,22 @@ def test_native_step_stem_fused_vs_unfused(monkeypatch):
     a, b = grads[0][st.off:st.off + st.numel], grads[1][st.off:st.off + st.numel]
     assert relerr(a, b) < 1e-3
     assert relerr(grads[0], grads[1]) < 1e-2
+
+
+@pytest.mark.parametrize("N,HI", [(2, 32), (8, 224)])
+def test_stem_wgrad_tile_matches_generic(N, HI):
+    """The 64 x 256-tile stem weight gradient (stem_bwd.hip, plain mode; conv_wgrad's default for the
+    64-channel stem) == the generic wgrad kernel's STEM mode (tile=(64, 128))."""
+    k = K()
+    torch.manual_seed(2)
+    x4 = torch.zeros(N, HI, HI, 4, device=dev, dtype=torch.bfloat16)
+    x4[..., :3] = torch.randn(N, HI, HI, 3, device=dev).bfloat16()
+    H = (HI + 6 - 7) // 2 + 1
+    dy = torch.randn(N, H, H, 64, device=dev).bfloat16()
+    ws = torch.empty(600 * 64 * 256, device=dev)
+    a, b = torch.empty(64, 256, device=dev), torch.empty(64, 256, device=dev)
+    k.conv_wgrad(dy, x4, a, ws, R=7, S=7, stride=2, pad=3, stem=True)
+    k.conv_wgrad(dy, x4, b, ws, R=7, S=7, stride=2, pad=3, stem=True, tile=(64, 128))
+    torch.cuda.synchronize()
+    assert relerr(a, b) < 1e-4
+    assert a.view(64, 8, 8, 4)[:, :, 7].abs().max().item() == 0.0
