@@ -95,10 +95,6 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x4 (&acc)[
 #pragma unroll
     for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = pr2[h] = f32x2{0.f, 0.f};
   }
-  if constexpr (STATS) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) ps2[h] = pq2[h] = f32x2{0.f, 0.f};
-  }
   // Epilogue in groups of EG rows per thread, in three straight-line phases: (1) every global load
   // of the group (residual addend, mask reference, BN inputs) — rows past M and absent addends read
   // a valid stand-in address instead of branching; (2) all arithmetic; (3) all stores. No load is
@@ -199,15 +195,6 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x4 (&acc)[
           v = pack8(f);
         }
       }
-      if constexpr (STATS) {  // statistics of the stored values (ACCUM never combines with STATS)
-        const u32x4 vs = (tail && !ok[k]) ? zero4 : v;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {  // bf16 pair -> 2 floats: the bits shifted / masked in place
-          const f32x2 pr = {__uint_as_float(vs[h] << 16), __uint_as_float(vs[h] & 0xFFFF0000u)};
-          ps2[h] += pr;
-          pq2[h] = __builtin_elementwise_fma(pr, pr, pq2[h]);
-        }
-      }
       vv[k] = v;
     }
 #pragma unroll
@@ -225,39 +212,39 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x4 (&acc)[
   for (int g0 = 0; g0 + EG <= NIT; g0 += EG) group(g0, std::integral_constant<int, EG>{});
   if constexpr (NIT % EG != 0) group(NIT - NIT % EG, std::integral_constant<int, NIT % EG>{});
   if constexpr (STATS) {
+    // per-channel sum / sum of squares of the stored (bf16) tile on the matrix cores instead of the
+    // VALU (the statistics were 8-31 % of the expanding 1x1 forwards: profiles/r2s4_probes/): for a
+    // 16-channel column group, F = the [32 pixels][16 channels] block of sC read transposed;
+    // mfma(ones, F) accumulates the column sums, mfma(F, F) the 16x16 Gram block whose diagonal is
+    // the sums of squares. bf16 x bf16 products are exact in fp32. Rows past M are zero (their
+    // operands were zero-filled). One fp64 atomic pair per channel into shard tm % nshard.
+    constexpr int NCG = BN / 16;
+    const int gq = lane >> 4, qq = (lane & 15) >> 2, pq = lane & 3;
+    const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+    double* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
+    for (int cg = wid; cg < NCG; cg += NW) {  // wave-uniform (the transposed reads need full EXEC)
+      f32x4 dsum = {0.f, 0.f, 0.f, 0.f}, dsq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      bs[2 * h] = ps2[h].x; bs[2 * h + 1] = ps2[h].y;
-      bq1[2 * h] = pq2[h].x; bq1[2 * h + 1] = pq2[h].y;
-    }
-    // per-channel sum / sum of squares: in-wave lanes with the same chunk column by xor-shuffles,
-    // then the waves through LDS, then one fp64 atomic pair per channel into shard tm % nshard
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int o = CPR; o < 64; o <<= 1) {
-        bs[j] += __shfl_xor(bs[j], o, 64);
-        bq1[j] += __shfl_xor(bq1[j], o, 64);
+      for (int rb = 0; rb < BM; rb += 32) {
+        const int row = rb + 8 * gq + qq;
+        const int col = cg * 16 + 4 * pq;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DBX_LDS s16x4*)(sC + row * (BN + 8) + col));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DBX_LDS s16x4*)(sC + (row + 4) * (BN + 8) + col));
+        const bf16x8 f = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        dsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f, dsum, 0, 0, 0);
+        dsq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, f, dsq, 0, 0, 0);
+      }
+      // D[i][j] sits in lane (i / 4) * 16 + j, register i % 4: column sums in every row (lanes 0-15
+      // flush row 0), the diagonal D[j][j] in lane (j / 4) * 16 + j, register j % 4
+      const int c = n0 + cg * 16 + (lane & 15);
+      if (lane < 16) atomicAdd(st + c, (double)dsum[0]);
+      const int dr = (lane & 15) - 4 * gq;
+      if (dr >= 0 && dr < 4) {
+        const float q = dr == 0 ? dsq[0] : dr == 1 ? dsq[1] : dr == 2 ? dsq[2] : dsq[3];
+        atomicAdd(st + a.OC + c, (double)q);
       }
     }
-    __syncthreads();  // sC reuse
-    float* red = reinterpret_cast<float*>(lds);  // [NW waves][2][BN]
-    if (lane < CPR) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[(wid * 2 + 0) * BN + ccol * 8 + j] = bs[j];
-        red[(wid * 2 + 1) * BN + ccol * 8 + j] = bq1[j];
-      }
-    }
-    __syncthreads();
-    if (tid < BN) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) { s += red[(w * 2) * BN + tid]; q += red[(w * 2 + 1) * BN + tid]; }
-      double* st = a.stats + (size_t)(tm % a.nshard) * 2 * a.OC;
-      atomicAdd(st + n0 + tid, (double)s);
-      atomicAdd(st + a.OC + n0 + tid, (double)q);
-    }
+    __syncthreads();  // the LDS is free for reuse when the epilogue returns
   }
   if constexpr (EPI > 0) {
 #pragma unroll
