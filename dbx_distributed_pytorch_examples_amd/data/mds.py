@@ -14,11 +14,15 @@ is not installed here, so both sides are implemented from the format:
 * encodings: ``int`` (int64), ``str``/``bytes``, ``pil`` (uint32 w, h, len(mode) + mode + raw
   pixels), ``jpeg``/``png`` (file bytes), ``ndarray:<dtype>:<d0,d1,...>`` (raw).
 
-Compression: ``zstd`` needs the ``zstandard`` module, absent here — the writer emits
-uncompressed shards (raw ``pil`` pixels are what the native loader wants anyway: no decode at
-all, ImageNet-scale throughput comes from pre-resized raw shards) and the reader raises a clear
-error for compressed shards it cannot open. Parity with mosaicml-streaming's own reader is
-"unpinned" (not installed); tests pin the format round-trip (tests/test_data.py).
+Compression (``compression='gz' | 'gz:<level>' | 'bz2' | 'zstd[:<level>]'``): as in mosaicml-streaming,
+a compressed shard is stored as ``zip_data`` (``shard.00000.mds.gz`` ...) next to the uncompressed
+``raw_data`` description; the reader decompresses it once into its ``local`` directory and then
+memory-maps the raw shard (the C++ assembler always reads raw shards). ``gz`` / ``bz2`` use the
+standard library; ``zstd`` needs the ``zstandard`` module, absent here: the writer then falls back to
+uncompressed shards with a warning and the reader raises a clear error for zstd shards it cannot open.
+Raw ``pil`` pixels are what the native loader wants anyway (no image decode at all). Parity with
+mosaicml-streaming's own reader is "unpinned" (not installed); tests pin the format round-trip
+(tests/test_data.py).
 
 :class:`StreamingDataset` partitions samples over ``RANK/WORLD_SIZE`` (and DataLoader workers)
 deterministically per epoch — no shared-memory coordination.
@@ -121,6 +125,32 @@ def _fixed_size(enc: str) -> Optional[int]:
 
 
 # ---------------------------------------------------------------------------------------
+# compression codecs (mosaicml-streaming names: "gz", "gz:6", "bz2", "zstd", "zstd:7")
+# ---------------------------------------------------------------------------------------
+def _codec(spec: str, decoder: bool = False):
+    """-> (compress fn, file extension), or (extension, decompress fn) with ``decoder=True``."""
+    algo, _, lvl = spec.partition(":")
+    level = int(lvl) if lvl else None
+    if algo == "gz":
+        import gzip
+        return ("gz", gzip.decompress) if decoder else \
+            ((lambda b: gzip.compress(b, compresslevel=9 if level is None else level, mtime=0)), "gz")
+    if algo == "bz2":
+        import bz2
+        return ("bz2", bz2.decompress) if decoder else \
+            ((lambda b: bz2.compress(b, 9 if level is None else level)), "bz2")
+    if algo == "zstd":
+        try:
+            import zstandard
+        except ImportError:
+            raise RuntimeError(f"MDS compression {spec!r} needs the zstandard module (not installed)") from None
+        if decoder:
+            return "zstd", (lambda b: zstandard.ZstdDecompressor().decompress(b))
+        return (lambda b: zstandard.ZstdCompressor(level=3 if level is None else level).compress(b)), "zstd"
+    raise RuntimeError(f"unsupported MDS compression {spec!r} (gz, bz2, zstd)")
+
+
+# ---------------------------------------------------------------------------------------
 # writer
 # ---------------------------------------------------------------------------------------
 class MDSWriter:
@@ -128,10 +158,14 @@ class MDSWriter:
 
     def __init__(self, out: str, columns: Dict[str, str], compression: Optional[str] = None,
                  size_limit: int = 1 << 26, exist_ok: bool = True, **_):
+        self.compression = None
         if compression not in (None, "", "none"):
-            # zstd needs the `zstandard` module (not installed): write raw shards, say so once
-            import warnings
-            warnings.warn(f"MDS compression {compression!r} unavailable here; writing uncompressed shards")
+            try:
+                _codec(compression)
+                self.compression = compression
+            except RuntimeError as e:  # zstd without the zstandard module: raw shards, say so once
+                import warnings
+                warnings.warn(f"{e}; writing uncompressed shards")
         self.out = out
         os.makedirs(out, exist_ok=exist_ok)
         self.names = sorted(columns)
@@ -166,16 +200,23 @@ class MDSWriter:
         for r in self._samples:
             offs.append(offs[-1] + len(r))
         name = f"shard.{len(self.shards):05d}.mds"
-        with open(os.path.join(self.out, name), "wb") as f:
-            f.write(struct.pack("<I", n))
-            f.write(np.array(offs, np.uint32).tobytes())
-            for r in self._samples:
-                f.write(r)
+        raw = b"".join([struct.pack("<I", n), np.array(offs, np.uint32).tobytes()] + self._samples)
+        zip_data = None
+        if self.compression:
+            comp, ext = _codec(self.compression)
+            zname = f"{name}.{ext}"
+            blob = comp(raw)
+            with open(os.path.join(self.out, zname), "wb") as f:
+                f.write(blob)
+            zip_data = {"basename": zname, "bytes": len(blob), "hashes": {}}
+        else:
+            with open(os.path.join(self.out, name), "wb") as f:
+                f.write(raw)
         self.shards.append({
             "column_encodings": self.encs, "column_names": self.names, "column_sizes": self.sizes,
-            "compression": None, "format": "mds", "hashes": [],
+            "compression": self.compression, "format": "mds", "hashes": [],
             "raw_data": {"basename": name, "bytes": offs[-1], "hashes": {}},
-            "samples": n, "size_limit": self.size_limit, "version": 2, "zip_data": None,
+            "samples": n, "size_limit": self.size_limit, "version": 2, "zip_data": zip_data,
         })
         self._samples, self._bytes = [], 0
 
@@ -251,10 +292,20 @@ class StreamingDataset(IterableDataset):
             idx = json.load(f)
         self.shards: List[_Shard] = []
         for sh in idx["shards"]:
-            if sh.get("compression"):
-                raise RuntimeError(f"compressed MDS shard {sh['raw_data']['basename']} ({sh['compression']}) "
-                                   "cannot be read here (no zstandard module)")
-            self.shards.append(_Shard(os.path.join(self.local, sh["raw_data"]["basename"]), sh))
+            raw_path = os.path.join(self.local, sh["raw_data"]["basename"])
+            if sh.get("compression") and not (os.path.exists(raw_path)
+                                              and os.path.getsize(raw_path) == sh["raw_data"]["bytes"]):
+                _, dec = _codec(sh["compression"], decoder=True)
+                with open(os.path.join(self.local, sh["zip_data"]["basename"]), "rb") as f:
+                    data = dec(f.read())
+                if len(data) != sh["raw_data"]["bytes"]:
+                    raise ValueError(f"{sh['zip_data']['basename']}: decompressed {len(data)} bytes, "
+                                     f"index says {sh['raw_data']['bytes']}")
+                tmp = raw_path + f".tmp{os.getpid()}"
+                with open(tmp, "wb") as f:
+                    f.write(data)
+                os.replace(tmp, raw_path)  # atomic: concurrent local ranks may race to decompress
+            self.shards.append(_Shard(raw_path, sh))
         self.cum = np.cumsum([0] + [s.n for s in self.shards])
         self.num_samples = int(self.cum[-1])
         self.shuffle, self.seed, self.batch_size, self.drop_last = shuffle, shuffle_seed, batch_size, drop_last

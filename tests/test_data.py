@@ -31,6 +31,45 @@ def test_mds_roundtrip_and_shards():
         assert it["label"] == ds[i][1]
 
 
+@pytest.mark.parametrize("comp", ["gz", "gz:1", "bz2"])
+def test_mds_compressed_shards(comp):
+    """compressed shards (zip_data next to raw_data, as mosaicml-streaming writes them) are
+    decompressed once into the reader's local directory; remote keeps only the compressed files"""
+    import json
+    remote, local = tempfile.mkdtemp(), tempfile.mkdtemp()
+    ds = SyntheticImages(23, 8, 3, 10, seed=4)
+    with MDSWriter(remote, {"image": "pil", "label": "int"}, compression=comp, size_limit=1500) as w:
+        for i in range(len(ds)):
+            img, y = ds[i]
+            w.write({"image": img, "label": y})
+    idx = json.load(open(os.path.join(remote, "index.json")))
+    ext = comp.split(":")[0]
+    assert len(idx["shards"]) > 1
+    for sh in idx["shards"]:
+        assert sh["compression"] == comp and sh["zip_data"]["basename"].endswith("." + ext)
+        assert not os.path.exists(os.path.join(remote, sh["raw_data"]["basename"]))
+    sd = StreamingDataset(remote=remote, local=local)
+    assert sd.num_samples == 23
+    for i in (0, 11, 22):
+        assert np.array_equal(np.asarray(sd[i]["image"]), ds[i][0]) and sd[i]["label"] == ds[i][1]
+    sd2 = StreamingDataset(local=local)  # second open: raw shards already materialised
+    assert np.array_equal(np.asarray(sd2[5]["image"]), ds[5][0])
+
+
+def test_mds_zstd_without_module_falls_back():
+    try:
+        import zstandard  # noqa: F401
+        pytest.skip("zstandard installed: the fallback path is not taken")
+    except ImportError:
+        pass
+    d = tempfile.mkdtemp()
+    with pytest.warns(UserWarning, match="zstandard"):
+        w = MDSWriter(d, {"label": "int"}, compression="zstd")
+    w.write({"label": 3})
+    w.finish()
+    assert StreamingDataset(local=d)[0]["label"] == 3
+
+
 def test_mds_mixed_columns():
     d = tempfile.mkdtemp()
     with MDSWriter(d, {"a": "int", "s": "str", "b": "bytes", "x": "ndarray:float32:2,3"}) as w:
