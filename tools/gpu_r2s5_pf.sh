@@ -1,0 +1,18 @@
+#!/bin/bash
+# Persistent conv tiles: next tile's A and B issued before the epilogue, branch-free epilogue stores,
+# count-matching dropped stores on the loop entry (waits no longer drain the epilogue stores).
+# Kernel tests, stats probe, per-op breakdown, 3 bench runs.
+set -o pipefail
+O=gpurun_out/r2s5_pf
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_conv_dma_gpu.py tests/test_conv_patch3_gpu.py tests/test_program_gpu.py -x -q --timeout 120 --timeout-method thread > $O/test.log 2>&1 || { echo "tests FAILED"; tail -40 $O/test.log; exit 1; }
+tail -1 $O/test.log
+timeout -k 10 300 python tools/probe_stats.py > $O/probe.txt 2>&1 || { echo "probe FAILED"; tail -5 $O/probe.txt; exit 1; }
+grep -v amdgpu.ids $O/probe.txt
+for r in 1 2 3; do
+  timeout -k 10 300 python bench.py --steps 30 --warmup 10 > $O/bench_r$r.log 2>&1 || { echo "bench FAILED"; tail -20 $O/bench_r$r.log; exit 1; }
+  echo "run $r: $(tail -1 $O/bench_r$r.log | cut -c80-140)"
+done
+timeout -k 10 300 python tools/op_breakdown.py > $O/op_breakdown.txt 2>&1 || { echo "op_breakdown FAILED"; tail -5 $O/op_breakdown.txt; exit 1; }
+head -3 $O/op_breakdown.txt
