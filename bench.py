@@ -111,7 +111,8 @@ def main(argv=None) -> int:
         "scaling": "weak",
         "vs_baseline": (round(value / (base * n), 4) if base else None),
         "dtype": "bf16",
-        "data": "synthetic (uint8 NHWC 224x224 images + random labels, on-device; random-init weights)",
+        "data": f"synthetic (uint8 NHWC {args.image_size}x{args.image_size} images + random labels, on-device; "
+                "random-init weights)",
         "config": {
             "model": f"{args.model} ImageNet-1K {args.image_size}x{args.image_size} {args.num_classes} classes"
                      + (" large-batch (global 8192 at 8 GPUs)" if args.batch == 1024 else ""),
