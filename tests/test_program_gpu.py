@@ -154,6 +154,32 @@ def test_frozen_backbone_native_gpu():
     assert math.isfinite(loss) and loss > 0
 
 
+@pytest.mark.gpu
+def test_frozen_backbone_graph_replay_matches_eager():
+    """the graph-captured backbone forward (after two eager calls) follows new inputs every replay and
+    gives bit-identical features to the eager program, including a short final batch"""
+    from dbx_distributed_pytorch_examples_amd.config import OptimizerConfig
+    from dbx_distributed_pytorch_examples_amd.engine.frozen_trainer import FrozenFeatureTrainer
+    from dbx_distributed_pytorch_examples_amd.models import FrozenBackboneClassifier
+    torch.manual_seed(1)
+    m = FrozenBackboneClassifier("resnet18", num_classes=10)
+    dev = torch.device("cuda")
+    g = FrozenFeatureTrainer(m, 32, (32, 32), dev, OptimizerConfig(name="adam", lr=1e-3))
+    e = FrozenFeatureTrainer(m, 32, (32, 32), dev, OptimizerConfig(name="adam", lr=1e-3), use_graphs=False)
+    imgs = [torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, device=dev) for _ in range(5)]
+    lab = torch.randint(0, 10, (32,), device=dev)
+    for i, x in enumerate(imgs + [imgs[0][:20]]):
+        fg = g._features(x, lab[:x.shape[0]], None, None).clone()
+        fe = e._features(x, lab[:x.shape[0]], None, None).clone()
+        assert torch.equal(fg, fe), i
+    assert g._graph is not None and e._graph is None
+    for _ in range(3):
+        g.step(imgs[1], lab)
+    torch.cuda.synchronize()
+    loss, _ = g.read_metrics()
+    assert math.isfinite(loss) and loss > 0
+
+
 # SURVEY.md §7.4 "50-step loss-decrease smoke per BASELINE config": each BASELINE.json config's
 # architecture / resolution / optimizer family, at a small per-GPU batch, trained 50 steps on one
 # fixed synthetic batch through the graph-captured native step. A correct forward/backward/optimizer
