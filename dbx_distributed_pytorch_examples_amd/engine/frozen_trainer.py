@@ -13,7 +13,11 @@ The backbone forward (~150 kernels for ResNet-50; launch-bound at the reference'
 e.g. ResNet-18 on 32x32 CIFAR images) is captured as one HIP graph after two eager warm-up
 calls and replayed from then on: inputs are copied into the program's static buffers outside
 the graph, the features come back in the program's static ``pooled`` buffer. No collective runs
-inside it, so the same graph serves every world size.
+inside it, so the same graph serves every world size. At world size 1 with Adam / AdamW (every
+frozen-backbone notebook of the reference uses Adam) the WHOLE step is one graph instead: backbone,
+head forward / backward (autograd, captured), a capturable optimizer whose learning rate lives in a
+device tensor (``set_lr`` follows on every replay) and the device-side metrics. A short final
+batch runs eagerly.
 """
 from __future__ import annotations
 
@@ -56,7 +60,6 @@ class FrozenFeatureTrainer:
         self.prog.prepare_weights()  # frozen: converted once
         self.head = model.resnet.fc.to(device)
         self.ddp = DistributedDataParallel(self.head, bucket_cap_mb=bucket_cap_mb, allreduce_dtype=allreduce_dtype)
-        self.opt = build_torch_optimizer([p for p in self.head.parameters() if p.requires_grad], optim)
         self.smoothing = label_smoothing
         self.metrics = torch.zeros(2, device=device)  # loss sum, correct (device-side, no host sync)
         self.use_graphs = (use_graphs and device.type == "cuda" and not _debug.enabled()
@@ -64,6 +67,26 @@ class FrozenFeatureTrainer:
         self._graph = None
         self._feats = None
         self._warm = 0
+        params = [p for p in self.head.parameters() if p.requires_grad]
+        # whole-step graph: pays off where the step is launch-bound (measured on one MI355X,
+        # profiles/r2s5_frozen/: ResNet-18 CIFAR b256 530k vs 455k img/s with the backbone-only graph);
+        # for larger inputs the capturable optimizer costs a little more than the head launches it
+        # hides (ResNet-50 64x64 / 224x224: -2..-3 %). DBX_FROZEN_FULL_GRAPH=1 / 0 forces it.
+        mode = os.environ.get("DBX_FROZEN_FULL_GRAPH", "auto")
+        small = batch * image_hw[0] * image_hw[1] <= 256 * 32 * 32
+        self.full_graph = (self.use_graphs and self.ddp.world == 1 and optim.name in ("adam", "adamw")
+                           and (mode == "1" or (mode == "auto" and small)))
+        self.lr_t = None
+        if self.full_graph:
+            self.lr_t = torch.tensor(float(optim.lr), device=device)
+            cls = torch.optim.Adam if optim.name == "adam" else torch.optim.AdamW
+            self.opt = cls(params, lr=self.lr_t, betas=tuple(optim.betas), eps=optim.eps,
+                           weight_decay=optim.weight_decay, capturable=True)
+            self.lab = torch.zeros(batch, dtype=torch.int64, device=device)  # static labels of the graph
+        else:
+            self.opt = build_torch_optimizer(params, optim)
+        self._sgraph = None
+        self._swarm = 0
 
     def _run_backbone(self) -> torch.Tensor:
         p = self.prog
@@ -94,10 +117,46 @@ class FrozenFeatureTrainer:
         return self._feats
 
     def set_lr(self, lr: float):
+        if self.lr_t is not None:
+            self.lr_t.fill_(float(lr))  # the captured optimizer reads it on every replay
+            return
         for g in self.opt.param_groups:
             g["lr"] = float(lr)
 
     def _features(self, images_u8, labels, boxes, flips) -> torch.Tensor:
+        self._stage_inputs(images_u8, boxes, flips)
+        return self._backbone()[:images_u8.shape[0]]
+
+    def step(self, images_u8, labels, boxes=None, flips=None):
+        if self.full_graph and images_u8.shape[0] == self.prog.N:
+            self._stage_inputs(images_u8, boxes, flips)
+            self.lab.copy_(labels, non_blocking=True)
+            if self._sgraph is None:
+                cur = torch.cuda.current_stream(self.dev)
+                if self._swarm < 2:  # eager warm-up steps on a side stream (optimizer state, autograd)
+                    self._swarm += 1
+                    s = torch.cuda.Stream(device=self.dev)
+                    s.wait_stream(cur)
+                    with torch.cuda.stream(s):
+                        self._head_step(self._backbone_eager().float(), self.lab)
+                    cur.wait_stream(s)
+                    return
+                torch.cuda.synchronize(self.dev)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._head_step(self._backbone_eager().float(), self.lab)
+                torch.cuda.synchronize(self.dev)
+                self._sgraph = g
+            self._sgraph.replay()
+            return
+        feats = self._features(images_u8, labels, boxes, flips).float()
+        self._head_step(feats, labels.to(self.dev, non_blocking=True))
+
+    @torch.no_grad()
+    def _backbone_eager(self) -> torch.Tensor:
+        return self._run_backbone()
+
+    def _stage_inputs(self, images_u8, boxes, flips):
         p = self.prog
         n = images_u8.shape[0]
         p.img_u8[:n].copy_(images_u8, non_blocking=True)
@@ -107,11 +166,8 @@ class FrozenFeatureTrainer:
             p.flip[:n].copy_(flips, non_blocking=True)
         else:
             p.flip.zero_()
-        return self._backbone()[:n]
 
-    def step(self, images_u8, labels, boxes=None, flips=None):
-        feats = self._features(images_u8, labels, boxes, flips).float()
-        labels = labels.to(self.dev, non_blocking=True)
+    def _head_step(self, feats, labels):
         self.head.train()
         logits = self.ddp(feats)
         loss = F.cross_entropy(logits, labels, label_smoothing=self.smoothing)

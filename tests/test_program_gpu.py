@@ -180,6 +180,40 @@ def test_frozen_backbone_graph_replay_matches_eager():
     assert math.isfinite(loss) and loss > 0
 
 
+@pytest.mark.gpu
+def test_frozen_whole_step_graph_matches_eager():
+    """world-1 Adam: the whole frozen step (backbone + autograd head + capturable Adam + metrics) as one
+    graph tracks the eager step over 6 steps with a changing learning rate (dropout off: p=0)"""
+    import copy
+    from dbx_distributed_pytorch_examples_amd.config import OptimizerConfig
+    from dbx_distributed_pytorch_examples_amd.engine.frozen_trainer import FrozenFeatureTrainer
+    from dbx_distributed_pytorch_examples_amd.models import FrozenBackboneClassifier
+    torch.manual_seed(2)
+    m = FrozenBackboneClassifier("resnet18", num_classes=10, dropout=0.0)
+    m2 = copy.deepcopy(m)
+    dev = torch.device("cuda")
+    oc = OptimizerConfig(name="adam", lr=1e-2)
+    g = FrozenFeatureTrainer(m, 32, (32, 32), dev, oc)
+    e = FrozenFeatureTrainer(m2, 32, (32, 32), dev, OptimizerConfig(name="adam", lr=1e-2), use_graphs=False)
+    assert g.full_graph and not e.full_graph
+    gen = torch.Generator(device="cpu").manual_seed(3)
+    for i in range(6):
+        x = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, generator=gen).to(dev)
+        y = torch.randint(0, 10, (32,), generator=gen).to(dev)
+        lr = 1e-2 * (i + 1) / 6
+        g.set_lr(lr)
+        e.set_lr(lr)
+        g.step(x, y)
+        e.step(x, y)
+    torch.cuda.synchronize()
+    assert g._sgraph is not None
+    wg, we = m.resnet.fc[1].weight.detach(), m2.resnet.fc[1].weight.detach()
+    assert ((wg - we).norm() / we.norm()).item() < 1e-4
+    lg, cg = g.read_metrics()
+    le, ce = e.read_metrics()
+    assert abs(lg - le) / le < 1e-4 and abs(cg - ce) <= 1  # (an argmax near-tie may flip)
+
+
 # SURVEY.md §7.4 "50-step loss-decrease smoke per BASELINE config": each BASELINE.json config's
 # architecture / resolution / optimizer family, at a small per-GPU batch, trained 50 steps on one
 # fixed synthetic batch through the graph-captured native step. A correct forward/backward/optimizer
