@@ -5,6 +5,10 @@ this rank's GPU (channels_last), wraps it in the flat-bucket DDP, re-shards the 
 ``ShardSampler`` and returns them; ``backward(loss)`` runs autograd and finishes the bucket
 all-reduces; ``gather`` / ``reduce`` are packed collectives; ``log`` forwards to the MLflow-compat
 tracker (``log_with="mlflow"``). bf16 autocast is enabled by ``mixed_precision="bf16"``.
+
+A model already wrapped by :func:`~dbx_distributed_pytorch_examples_amd.engine.native_module.native_module`
+(the notebook's loop on the native HIP kernels) is passed through unwrapped: its backward all-reduces its
+flat gradient in one collective itself.
 """
 from __future__ import annotations
 
@@ -87,6 +91,9 @@ class Accelerator:
 
     def _prep_one(self, obj):
         if isinstance(obj, torch.nn.Module):
+            from ..engine.native_module import NativeResNet
+            if isinstance(obj, NativeResNet):
+                return obj  # on the device already; gradients all-reduced by its own backward
             m = obj.to(self.device)
             if self.device.type == "cuda":
                 m = m.to(memory_format=torch.channels_last)

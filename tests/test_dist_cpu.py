@@ -299,3 +299,35 @@ def test_two_node_rendezvous_on_one_host():
     th.join(150)
     assert res[0] == (0, 4, 0, 0, 10.0)
     assert res[1] == (2, 4, 1, 0, 10.0)   # node 1's local rank 0 is global rank 2
+
+
+def _accel_native():
+    """Accelerate-style loop on engine.native_module at world 2 (CPU reference ops, gloo): prepare()
+    passes the module through, its backward averages the flat gradient in one collective."""
+    import torch.distributed as tdist
+    from dbx_distributed_pytorch_examples_amd.engine.native_module import NativeResNet, native_module
+    from dbx_distributed_pytorch_examples_amd.frontends.accelerate import Accelerator
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    acc = Accelerator(cpu=True)
+    torch.manual_seed(0)
+    nm = native_module(build_model("resnet18", num_classes=10), 4, (32, 32), torch.device("cpu")).train()
+    opt = torch.optim.SGD(nm.parameters(), lr=0.05)
+    model, opt = acc.prepare(nm, opt)
+    g = torch.Generator().manual_seed(10 + acc.process_index)  # different data per rank
+    x, y = torch.randn(4, 3, 32, 32, generator=g), torch.randint(0, 10, (4,), generator=g)
+    loss = nn.functional.cross_entropy(model(x), y)
+    acc.backward(loss)
+    grad = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+    opt.step()
+    par = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    both = [torch.empty_like(grad) for _ in range(2)]
+    tdist.all_gather(both, grad)
+    pboth = [torch.empty_like(par) for _ in range(2)]
+    tdist.all_gather(pboth, par)
+    return (isinstance(model, NativeResNet), torch.equal(both[0], both[1]), torch.equal(pboth[0], pboth[1]),
+            float(grad.norm()))
+
+
+def test_accelerate_native_module_two_ranks():
+    is_native, grads_equal, params_equal, gnorm = Launcher(2, use_gpu=False).run(_accel_native)
+    assert is_native and grads_equal and params_equal and gnorm > 0  # averaged gradients, replicas in sync

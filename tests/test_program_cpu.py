@@ -166,3 +166,57 @@ def test_fused_conv3_backward_schedule(fold, monkeypatch):
         tr.step(img, lab)
         grads.append(tr.prog.grad.clone())
     assert torch.allclose(grads[0], grads[1], rtol=1e-5, atol=1e-7)
+
+
+def test_native_module_autograd_dropin_matches_torch():
+    """engine.native_module: the native program inside a user-written autograd loop (soft CutMix-style
+    targets + label smoothing computed by torch on the logits) gives the fp32-autograd gradients; a
+    torch optimizer steps the parameters in place; other batch sizes fall back to the torch module."""
+    from dbx_distributed_pytorch_examples_amd.engine.native_module import native_module
+    torch.manual_seed(0)
+    model = build_model("resnet18", num_classes=10)
+    _damp(model, "resnet18")
+    ref = copy.deepcopy(model).train()
+    nm = native_module(model, 8, (32, 32), CPU).train()
+    assert len(list(nm.parameters())) == len(list(ref.parameters()))
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(8, 3, 32, 32, generator=g)
+    x = x.bfloat16().float()  # the program computes on bf16 inputs
+    t = torch.softmax(torch.randn(8, 10, generator=g), 1)  # soft targets (CutMix / mixup style)
+    loss_n = torch.nn.functional.cross_entropy(nm(x), t, label_smoothing=0.1)
+    loss_n.backward()
+    loss_r = torch.nn.functional.cross_entropy(ref(x), t, label_smoothing=0.1)
+    loss_r.backward()
+    assert abs(loss_n.item() - loss_r.item()) < 2e-2 * loss_r.item()
+    nr = dict(ref.named_parameters())
+    for name, prm in nm.named_parameters():
+        assert prm.grad is not None, name
+        assert _cos(prm.grad, nr[name].grad) > (0.9 if prm.dim() > 1 else 0.75), name
+    # running statistics follow torch's
+    for (n1, b1), (n2, b2) in zip(model.named_buffers(), ref.named_buffers()):
+        if "running_mean" in n1:
+            assert _cos(b1, b2) > 0.99 or b2.abs().max() < 1e-3, n1
+    # a torch optimizer over nm.parameters() updates the program's master in place
+    opt = torch.optim.Adam(nm.parameters(), lr=1e-3)
+    before = nm.prog.master.clone()
+    opt.step()
+    assert not torch.equal(before, nm.prog.master)
+    losses = []
+    y = torch.randint(0, 10, (8,), generator=g)
+    for _ in range(6):
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(nm(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0], losses
+    # short batch: torch module on the same parameters (autograd through torch ops)
+    opt.zero_grad()
+    out = nm(x[:5])
+    assert out.shape == (5, 10)
+    out.sum().backward()
+    assert all(p.grad is not None for p in nm.parameters())
+    nm.eval()
+    with torch.no_grad():
+        ev = nm(x)
+    assert ev.shape == (8, 10) and torch.isfinite(ev).all()

@@ -1,0 +1,10 @@
+#!/bin/bash
+# engine.native_module (native HIP program inside a user-written autograd loop): GPU test + throughput vs the
+# stock torch module in the same loop (Accelerate / Ray / Composer notebook shapes).
+set -o pipefail
+O=gpurun_out/r2s5_nm
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_program_gpu.py -x -q -k native_module --timeout 120 --timeout-method thread > $O/test.log 2>&1 || { echo "tests FAILED"; tail -30 $O/test.log; exit 1; }
+tail -1 $O/test.log
+timeout -k 10 500 python -u tools/bench_native_module.py --steps 20 --warmup 5 > $O/bench.txt 2>&1 || { echo "bench FAILED"; tail -20 $O/bench.txt; exit 1; }
+grep images_per_s $O/bench.txt | cut -c1-140
