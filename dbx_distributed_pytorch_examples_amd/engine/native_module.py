@@ -18,9 +18,14 @@ already ARE views of the program's flat fp32 master, so any torch optimizer step
   accumulation across two backwards into the same view (call ``zero_grad`` between steps, the
   usual loop);
 * world size > 1: the flat gradient is all-reduced (averaged) in ONE collective at the end of
-  the backward; do not wrap the result in DDP as well (``frontends.accelerate`` knows this).
+  the backward; do not wrap the result in DDP as well (``frontends.accelerate`` knows this);
+* on the GPU the program's forward (train / eval) and backward are each captured as a HIP graph
+  after two eager calls and replayed (the user loop is otherwise launch-bound at CIFAR sizes);
+  the input / dlogits copies into the static buffers and the all-reduce stay outside the graphs.
 """
 from __future__ import annotations
+
+import os
 
 from typing import Optional, Tuple
 
@@ -53,6 +58,9 @@ class NativeResNet(nn.Module):
         self.prog = ResNetProgram(model, batch, image_hw, device)
         self.prog.build_backward()
         self.pg = process_group
+        self.use_graphs = device.type == "cuda" and os.environ.get("DBX_NATIVE_MODULE_GRAPHS", "1") != "0"
+        self._graphs = {}  # "fwd_train" / "fwd_eval" / "bwd" -> CUDAGraph
+        self._calls = {}
         # autograd needs one leaf that requires grad to route the loss back into _NativeFn
         self._anchor = nn.Parameter(torch.zeros((), device=device), requires_grad=True)
         p = self.prog
@@ -93,20 +101,45 @@ class NativeResNet(nn.Module):
                 return self._native_forward(x)
         return _NativeFn.apply(x, self._anchor, self)
 
+    def _run(self, key: str, fn) -> None:
+        """fn() eagerly for the first two calls of this kind, then as a captured graph's replay."""
+        if not self.use_graphs:
+            fn()
+            return
+        g = self._graphs.get(key)
+        if g is None:
+            n = self._calls.get(key, 0)
+            if n < 2:
+                self._calls[key] = n + 1
+                fn()
+                return
+            torch.cuda.synchronize(self.prog.dev)
+            g = torch.cuda.CUDAGraph()
+            mode = "thread_local" if (dist.is_available() and dist.is_initialized()) else "global"
+            with torch.cuda.graph(g, capture_error_mode=mode):
+                fn()
+            torch.cuda.synchronize(self.prog.dev)
+            self._graphs[key] = g
+        g.replay()
+
+    def _fwd_body(self):
+        p = self.prog
+        p.prepare_weights()
+        if p.training:
+            p.nbt.add_(1)
+        p.forward(compute_grad=False, metrics=False)
+
     def _native_forward(self, x: torch.Tensor) -> torch.Tensor:
         p = self.prog
         p.training = self.training
         p.x4[..., :p.in_ch].copy_(x.detach().permute(0, 2, 3, 1))  # NCHW float -> NHWC4 bf16
-        p.prepare_weights()
-        if self.training:
-            p.nbt.add_(1)
-        out = p.forward(compute_grad=False, metrics=False)
-        return out.float()
+        self._run("fwd_train" if self.training else "fwd_eval", self._fwd_body)
+        return p.logits.float()
 
     def _native_backward(self, dlogits: torch.Tensor) -> None:
         p = self.prog
         p.dlogits.copy_(dlogits)
-        p.backward()
+        self._run("bwd", p.backward)
         world = dist.get_world_size(self.pg) if (dist.is_available() and dist.is_initialized()) else 1
         if world > 1:
             from ..parallel.dist import host_sync_for_gloo
