@@ -107,8 +107,16 @@ def report(metrics: Dict[str, Any], checkpoint: Optional[Checkpoint] = None) -> 
         shutil.copytree(checkpoint.path, os.path.join(trial, f"checkpoint_{n:06d}"), dirs_exist_ok=True)
 
 
-def prepare_model(model: torch.nn.Module, **ddp_kw) -> torch.nn.Module:
+def prepare_model(model: torch.nn.Module, native_batch: int = 0, native_hw=(32, 32), **ddp_kw) -> torch.nn.Module:
+    """``ray.train.torch.prepare_model``. ``native_batch`` > 0 (GPU, a supported ResNet): the worker's own loop
+    runs on the native HIP program (``engine.native_module``; gradients averaged by its backward), else the
+    model is moved to the device and wrapped in the flat-bucket DDP at world > 1."""
     info = ddist.init_distributed(device="cpu" if os.environ.get("DBX_FORCE_CPU") == "1" else None)
+    if native_batch and info.device.type == "cuda":
+        from ..engine.native_module import native_module
+        from ..engine.program import supports
+        if supports(model):
+            return native_module(model, native_batch, tuple(native_hw), info.device)
     model = model.to(info.device)
     if info.device.type == "cuda":
         model = model.to(memory_format=torch.channels_last)

@@ -16,7 +16,10 @@ import _common as C  # noqa: E402
 
 
 def main():
-    args = C.parser(__doc__, procs=1, epochs=1, batch=32).parse_args()
+    ap = C.parser(__doc__, procs=1, epochs=1, batch=32)
+    ap.add_argument("--native", action="store_true",
+                    help="run this loop on the HIP kernels: engine.native_module (GPU; 2.6x at b128, profiles/r2s5_native_module)")
+    args = ap.parse_args()
     use_gpu = C.setup_env(args)
     import torch
     import torch.nn as nn
@@ -35,6 +38,11 @@ def main():
     train_loader = DataLoader(tr, batch_size=config["batch_size"], sampler=ShardSampler(tr), pin_memory=use_gpu)
     test_loader = DataLoader(te, batch_size=config["batch_size"], sampler=ShardSampler(te, shuffle=False))
     model = build_model("resnet50", num_classes=config["num_classes"])
+    if args.native and use_gpu:
+        # the same loop, forward / backward on the native program (build it BEFORE the optimizer:
+        # the parameters become views of the program's flat master)
+        from dbx_distributed_pytorch_examples_amd.engine.native_module import native_module
+        model = native_module(model, config["batch_size"], (32, 32), acc.device)
     optimizer = torch.optim.Adam(model.parameters(), lr=config["learning_rate"], weight_decay=config["weight_decay"])
     scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=config["num_epochs"])
     criterion = nn.CrossEntropyLoss()
