@@ -86,6 +86,11 @@ class NativeResNet(nn.Module):
         with torch.no_grad():
             return self.model.load_state_dict(sd, strict)
 
+    def _apply(self, fn, recurse=True):
+        # the parameters are views of the program's flat master (and its HIP buffers live on one
+        # device): .to(device / dtype / memory_format), .cuda(), .half() ... must not re-create them
+        return self
+
     def train(self, mode: bool = True):
         super().train(mode)
         self.model.train(mode)

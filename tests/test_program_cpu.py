@@ -179,6 +179,9 @@ def test_native_module_autograd_dropin_matches_torch():
     ref = copy.deepcopy(model).train()
     nm = native_module(model, 8, (32, 32), CPU).train()
     assert len(list(nm.parameters())) == len(list(ref.parameters()))
+    ptr = nm.prog.master.data_ptr()
+    assert nm.to(memory_format=torch.channels_last) is nm and nm.float() is nm  # views of master survive
+    assert all(p.data_ptr() >= ptr for p in nm.parameters())
     g = torch.Generator().manual_seed(1)
     x = torch.randn(8, 3, 32, 32, generator=g)
     x = x.bfloat16().float()  # the program computes on bf16 inputs
