@@ -2,7 +2,7 @@
 
 ``Accelerator().prepare(model, optimizer, train_loader, eval_loader, scheduler)`` moves the model to
 this rank's GPU (channels_last), wraps it in the flat-bucket DDP, re-shards the loaders with
-``ShardSampler`` and returns them; ``backward(loss)`` runs autograd and finishes the bucket
+``ShardSampler`` (their batches then arrive on the device) and returns them; ``backward(loss)`` runs autograd and finishes the bucket
 all-reduces; ``gather`` / ``reduce`` are packed collectives; ``log`` forwards to the MLflow-compat
 tracker (``log_with="mlflow"``). bf16 autocast is enabled by ``mixed_precision="bf16"``.
 
@@ -56,6 +56,33 @@ class _PreparedOptimizer:
         return self.opt.load_state_dict(sd)
 
 
+class _DeviceLoader:
+    """A prepared DataLoader: batches arrive on the accelerator's device (HF Accelerate's
+    ``DataLoaderShard`` behaviour); every other attribute is the wrapped loader's."""
+
+    def __init__(self, dl: DataLoader, device: torch.device):
+        self.dl, self.device = dl, device
+
+    def _move(self, b):
+        if isinstance(b, torch.Tensor):
+            return b.to(self.device, non_blocking=True)
+        if isinstance(b, (list, tuple)):
+            return type(b)(self._move(v) for v in b)
+        if isinstance(b, dict):
+            return {k: self._move(v) for k, v in b.items()}
+        return b
+
+    def __iter__(self):
+        for b in self.dl:
+            yield self._move(b)
+
+    def __len__(self):
+        return len(self.dl)
+
+    def __getattr__(self, k):
+        return getattr(self.dl, k)
+
+
 class Accelerator:
     def __init__(self, log_with: Optional[str] = None, mixed_precision: str = "bf16", cpu: bool = False, **_):
         self.info = ddist.init_distributed(device="cpu" if cpu else None)
@@ -103,12 +130,13 @@ class Accelerator:
         if isinstance(obj, torch.optim.Optimizer):
             return _PreparedOptimizer(obj, self)
         if isinstance(obj, DataLoader):
-            if ddist.get_world_size() == 1:
-                return obj
-            shuffle = not isinstance(obj.sampler, torch.utils.data.SequentialSampler)
-            return DataLoader(obj.dataset, batch_size=obj.batch_size, sampler=ShardSampler(obj.dataset, shuffle=shuffle),
-                              num_workers=obj.num_workers, collate_fn=obj.collate_fn, pin_memory=obj.pin_memory,
-                              drop_last=obj.drop_last)
+            dl = obj
+            if ddist.get_world_size() > 1:
+                shuffle = not isinstance(obj.sampler, torch.utils.data.SequentialSampler)
+                dl = DataLoader(obj.dataset, batch_size=obj.batch_size, sampler=ShardSampler(obj.dataset, shuffle=shuffle),
+                                num_workers=obj.num_workers, collate_fn=obj.collate_fn, pin_memory=obj.pin_memory,
+                                drop_last=obj.drop_last)
+            return _DeviceLoader(dl, self.device) if self.device.type != "cpu" else dl
         return obj  # schedulers etc.
 
     def prepare(self, *objs):
