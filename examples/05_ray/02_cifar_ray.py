@@ -15,7 +15,9 @@ def train_func(config):
     from torch.utils.data import DataLoader
     from dbx_distributed_pytorch_examples_amd.frontends import ray as rt
     from dbx_distributed_pytorch_examples_amd.models import build_model
-    model = rt.prepare_model(build_model("resnet18", num_classes=10))
+    # --native: the worker's loop on the HIP kernels (engine.native_module via prepare_model)
+    model = rt.prepare_model(build_model("resnet18", num_classes=10),
+                             native_batch=config["batch_size"] if config.get("native") else 0, native_hw=(32, 32))
     loader = rt.prepare_data_loader(DataLoader(config["train"], batch_size=config["batch_size"], shuffle=True))
     opt = torch.optim.Adam(model.parameters(), lr=config["lr"])
     for epoch in range(config["epochs"]):
@@ -33,13 +35,15 @@ def train_func(config):
 
 
 def main():
-    args = C.parser(__doc__, procs=1, epochs=1, batch=64).parse_args()
+    ap = C.parser(__doc__, procs=1, epochs=1, batch=64)
+    ap.add_argument("--native", action="store_true", help="GPU: the loop on engine.native_module")
+    args = ap.parse_args()
     use_gpu = C.setup_env(args)
     from dbx_distributed_pytorch_examples_amd.data.transforms import default_image_transforms
     from dbx_distributed_pytorch_examples_amd.frontends import ray as rt
     tr, _ = C.datasets("cifar10", args, transform=default_image_transforms(32))
     res = rt.TorchTrainer(train_func, train_loop_config={"train": tr, "batch_size": args.batch_size, "lr": 1e-5,
-                                                         "epochs": args.epochs},
+                                                         "epochs": args.epochs, "native": args.native},
                           scaling_config=rt.ScalingConfig(num_workers=args.procs, use_gpu=use_gpu),
                           run_config=rt.RunConfig(storage_path=os.path.join(args.out, "ray"), name="cifar")).fit()
     print("metrics:", res.metrics, "error:", res.error)
