@@ -73,6 +73,12 @@ class NativeResNet(nn.Module):
                 if prm.dim() == 4 else g.view(prm.shape)
             self._grad_views.append((prm, gv))
 
+    @property
+    def module(self) -> nn.Module:
+        """the wrapped torch module (``unwrap`` / ``accelerator.unwrap_model`` return it: its parameters
+        are the live weights, so it can be saved or logged as a plain model)"""
+        return self.model
+
     def parameters(self, recurse: bool = True):  # the anchor is internal: optimizers see the model's
         return self.model.parameters(recurse)
 

@@ -13,6 +13,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import _common as C  # noqa: E402
 
 
+def _local(log_dir, tr, te, epochs, device):
+    from dbx_distributed_pytorch_examples_amd.frontends import torch_distributor as td
+    td.train(log_dir, dataset=tr, epochs=epochs, device=device)
+    td.test(log_dir, dataset=te, epoch=epochs, device=device)
+
+
 def main():
     args = C.parser(__doc__, procs=2, epochs=1, batch=100).parse_args()
     use_gpu = C.setup_env(args)
@@ -23,8 +29,13 @@ def main():
     # single process (the notebook's "local" section)
     log_dir = create_log_dir(os.path.join(args.out, "mnist_local"))
     t = time.time()
-    td.train(log_dir, dataset=tr, epochs=args.epochs, device="cuda" if use_gpu else "cpu")
-    td.test(log_dir, dataset=te, epoch=args.epochs, device="cuda" if use_gpu else "cpu")
+    if use_gpu:
+        # on the GPU the local section runs in ONE child process: this process must not initialise the
+        # GPU before it spawns the distributed ranks below (the launcher refuses to spawn from it then)
+        td.TorchDistributor(num_processes=1, local_mode=True, use_gpu=True).run(_local, log_dir, tr, te, args.epochs,
+                                                                                 "cuda")
+    else:
+        _local(log_dir, tr, te, args.epochs, "cpu")
     print(f"local: {time.time() - t:.1f}s")
     # distributed (TorchDistributor(num_processes=N, local_mode=True).run(main_fn, dir))
     ddp_dir = create_log_dir(os.path.join(args.out, "mnist_ddp"))
