@@ -6,6 +6,12 @@ Algorithms map onto the engine: label smoothing -> the CE target, CutMix -> the 
 (soft-label CE), ChannelsLast -> a no-op marker (every GPU path here is NHWC end to end, K19).
 The model follows Composer's ``forward(batch)`` / ``loss(outputs, batch)`` convention
 (``models.ComposerResNet50``); plain modules work too.
+
+On one GPU a ``ComposerResNet50`` trains on the native HIP program: its inner ResNet is wrapped by
+``engine.native_module`` for the train loader's batch size and image size (CutMix's soft targets and
+label smoothing stay torch ops on the logits; other batch sizes run the torch module on the same
+parameters). ``DBX_COMPOSER_NATIVE=0`` keeps the stock module (2.5x slower at the notebook's
+b128 CIFAR shape, ``profiles/r2s5_native_module/``).
 """
 from __future__ import annotations
 
@@ -71,6 +77,8 @@ class Trainer:
         from ..engine.autograd_trainer import AutogradTrainer
         from ..config import OptimizerConfig
         self.info = ddist.init_distributed(device=device if device in ("cpu", "cuda") else None)
+        self.native = False
+        model = self._maybe_native(model, train_dataloader)
         smoothing = next((a.smoothing for a in algorithms if isinstance(a, LabelSmoothing)), 0.0)
         cut = next((a for a in algorithms if isinstance(a, CutMix)), None)
         oc = OptimizerConfig(name="adam", lr=1e-4, weight_decay=0.0)
@@ -89,6 +97,25 @@ class Trainer:
         self.loggers = list(loggers)
         self.state: Dict[str, Any] = {"epoch": 0, "batch": 0}
         self.history: List[Dict[str, float]] = []
+
+    def _maybe_native(self, model, dl):
+        import os
+        from ..engine.native_module import native_module
+        from ..engine.program import supports
+        from ..models.wrappers import ComposerResNet50
+        if (os.environ.get("DBX_COMPOSER_NATIVE", "1") == "0" or self.info.device.type != "cuda"
+                or ddist.get_world_size() > 1 or not isinstance(model, ComposerResNet50)):
+            return model
+        bs = getattr(dl, "batch_size", None)
+        try:
+            x0 = dl.dataset[0][0]
+        except Exception:
+            return model
+        if not bs or not torch.is_tensor(x0) or x0.dim() != 3 or not supports(model.model):
+            return model
+        model.model = native_module(model.model, bs, tuple(x0.shape[1:]), self.info.device)
+        self.native = True
+        return model
 
     def fit(self):
         spe = len(self.train_dl)

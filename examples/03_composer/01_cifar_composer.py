@@ -29,10 +29,15 @@ def main():
                          algorithms=[cp.LabelSmoothing(0.1), cp.CutMix(alpha=1.0, num_classes=1000), cp.ChannelsLast()],
                          loggers=[cp.MLFlowLogger(experiment_name="composer_cifar")],
                          device="cuda" if use_gpu else "cpu")
+    import time
+    t0 = time.time()
     hist = trainer.fit()
+    print(f"fit: {time.time() - t0:.1f}s ({'native HIP program' if trainer.native else 'torch module'})")
     print(hist[-1])
     img, label = C.datasets("cifar10", args)[1][0]
-    predict_image(trainer.model.cpu(), img, device="cpu", true_label=label)
+    # (on the GPU the native module's parameters stay on the device: predict there)
+    dev = "cuda" if use_gpu else "cpu"
+    predict_image(trainer.model if use_gpu else trainer.model.cpu(), img, device=dev, true_label=label)
     trainer.close()
 
 

@@ -349,3 +349,28 @@ def test_native_module_graph_replay_bit_exact():
     with torch.no_grad():
         for _ in range(3):
             assert torch.equal(a(x), b(x))
+
+
+def test_composer_trainer_runs_on_native_module():
+    """frontends.composer.Trainer on one GPU: ComposerResNet50 wrapped by native_module (CutMix soft targets
+    + label smoothing through autograd) trains 3 epochs and evaluates; the short final batch takes the
+    torch-module path."""
+    from torch.utils.data import DataLoader, TensorDataset
+    from dbx_distributed_pytorch_examples_amd.frontends.composer import CutMix, LabelSmoothing, Trainer
+    from dbx_distributed_pytorch_examples_amd.models import ComposerResNet50
+    torch.manual_seed(0)
+    n, nc = 200, 10
+    protos = torch.randn(nc, 3, 32, 32)
+    y = torch.randint(0, nc, (n,))
+    x = protos[y] + 0.3 * torch.randn(n, 3, 32, 32)
+    dl = DataLoader(TensorDataset(x, y), batch_size=64, shuffle=True)
+    model = ComposerResNet50(num_classes=nc)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    tr = Trainer(model, optimizers=opt, train_dataloader=dl, eval_dataloader=dl, max_duration="3ep",
+                 algorithms=[LabelSmoothing(0.1), CutMix(1.0)], device="cuda")
+    assert tr.native
+    w0 = model.model.model.fc.weight.detach().clone()
+    hist = tr.fit()
+    assert len(hist) == 3 and all(math.isfinite(h["train/loss"]) for h in hist), hist
+    assert not torch.equal(w0, model.model.model.fc.weight.detach())
+    assert 0.0 <= hist[-1]["metrics/eval/Accuracy"] <= 1.0
