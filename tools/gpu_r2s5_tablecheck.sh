@@ -1,7 +1,9 @@
 #!/bin/bash
-# The committed table + the ResNet-50 b256 entries: headline and ZeRO-1 preset vs the previous table
-# (git's copy shipped as gpurun_out-free file tools/tune_table_prev.json), alternating, same box.
+# The committed table + the ResNet-50 b256 entries: headline and ZeRO-1 preset vs the previous table,
+# alternating, same box. Before running, write the previous table next to this script (the box has no .git):
+#   git show 7a3c89c:dbx_distributed_pytorch_examples_amd/ops/tune_table.json > tools/tune_table_prev.json
 set -o pipefail
+[ -f tools/tune_table_prev.json ] || { echo "tools/tune_table_prev.json missing (see the header)"; exit 2; }
 O=gpurun_out/r2s5_tablecheck
 mkdir -p $O
 for r in 1 2; do
