@@ -4,8 +4,15 @@
 Metric (BASELINE.json): images/sec for the whole job, ResNet-50 ImageNet-1K, at 1/2/4/8
 MI355X, bf16, synthetic data + random-init weights, weak scaling (fixed per-GPU batch).
 
-  python bench.py --gpus N --steps K --warmup W        # N=1 runs in-process
+  python bench.py --gpus N --steps K --warmup W        # N=1 runs in-process; N>1 spawns N ranks itself
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+With ``--gpus N > 1`` and no launcher environment (no WORLD_SIZE), bench.py starts N local rank
+processes itself (the reference's ``TorchDistributor(num_processes=N, local_mode=True).run(...)``,
+`01_torch_distributor/01_basic_torch_distributor.py:360-367`) before anything touches the GPU, and
+exits with the worst rank's exit code. Under torchrun / our launcher it runs as the given rank. A
+world size that differs from ``--gpus`` is an error (exit 3), and the JSON line reports the world
+size the process group actually formed (``world_size_seen``) and its backend.
 
 Implementations (``--impl``):
   native  the framework's flagship path: NHWC bf16 ResNet program on the hand-written HIP
@@ -32,6 +39,17 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 # `python bench.py --impl torch --batch B` (eager nn.Module, channels_last, autocast bf16, MIOpen
 # convs, torch.optim.SGD; BASELINE.md, profiles/r1_torch_reference/). Keyed by per-GPU batch.
 BASELINE_IMG_PER_SEC_PER_GPU = {256: 5941.96, 1024: 6496.62}
+# ... and for BASELINE.json's other configs (same measurement method)
+PRESET_BASELINE_PER_GPU = {"resnet18_cifar10": 52051.0, "resnet50_tiny_imagenet": 17714.0,
+                           "resnet50_imagenet_zero1": 5970.0}
+HEADLINE_METRIC = "images/sec (whole node) ResNet-50 ImageNet-1K at 1/2/4/8 MI355X; top-1 acc"
+PRESET_METRIC = {
+    "resnet18_cifar10": "images/sec (whole node) ResNet-18 CIFAR-10 32x32 DDP bf16 (BASELINE.json config 2)",
+    "resnet50_tiny_imagenet": "images/sec (whole node) ResNet-50 TinyImageNet 64x64 DDP bf16 (BASELINE.json config 3)",
+    "resnet50_imagenet_zero1": "images/sec (whole node) ResNet-50 ImageNet-1K ZeRO-1 AdamW bf16 (BASELINE.json config 4)",
+    "resnet50_imagenet_8192": HEADLINE_METRIC,
+}
+DATASET_NAME = {(32, 10): "CIFAR-10", (64, 200): "TinyImageNet-200", (224, 1000): "ImageNet-1K"}
 
 # BASELINE.json's other configs (the headline default is ResNet-50 ImageNet-1K, 1024/GPU).
 PRESETS = {
@@ -62,45 +80,81 @@ def parse_args(argv=None):
                    help="one of BASELINE.json's other configs (sets model/size/classes/batch/optim)")
     p.add_argument("--json-out", default=None)
     a = p.parse_args(argv)
+    given = {t.split("=", 1)[0] for t in (sys.argv[1:] if argv is None else argv) if t.startswith("--")}
     for k, v in PRESETS.get(a.preset, {}).items():
-        setattr(a, k, v)
+        if "--" + k.replace("_", "-") not in given:  # explicit flags win over the preset's values
+            setattr(a, k, v)
     if a.lr is None:
         a.lr = {"sgd": 0.1, "lars": 9.0}.get(a.optim, 2e-4)
     return a
 
 
+def self_launch(args, argv) -> int:
+    """Spawn ``args.gpus`` local ranks of this script (no GPU call happens in this process first:
+    torch.cuda.device_count() does not initialise HIP)."""
+    backend = os.environ.get("DBX_DIST_BACKEND", "")
+    ndev = torch.cuda.device_count()
+    if backend != "gloo" and ndev < args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but {ndev} GPU(s) visible (RCCL needs one GPU per rank; "
+              f"DBX_DIST_BACKEND=gloo rehearses several ranks on one device)", file=sys.stderr)
+        return 3
+    from dbx_distributed_pytorch_examples_amd.launch import run_subprocess_ranks
+    return run_subprocess_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + list(argv))
+
+
 def main(argv=None) -> int:
-    args = parse_args(argv)
+    raw = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(raw)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args, raw)
     from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
     from dbx_distributed_pytorch_examples_amd.train.bench_steps import build_step
 
     info = ddist.init_distributed()
-    if info.world_size != args.gpus and info.rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
+    import torch.distributed as tdist
+    seen = tdist.get_world_size() if tdist.is_initialized() else 1
+    if seen != args.gpus or info.world_size != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but the process group has {seen} rank(s) "
+              f"(WORLD_SIZE={info.world_size}); refusing to report a mislabelled number", file=sys.stderr)
+        ddist.destroy()
+        return 3
     torch.manual_seed(1234 + info.rank)
     step, meta = build_step(args, info)
 
+    def sync():
+        if info.device.type == "cuda":
+            torch.cuda.synchronize()
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     ddist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     ddist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     elapsed = ddist.all_reduce_max(elapsed)
 
     n = info.world_size
     imgs = args.batch * n * args.steps
     value = imgs / elapsed
-    headline = args.model == "resnet50" and args.image_size == 224 and args.num_classes == 1000 and args.optim == "sgd"
-    base = BASELINE_IMG_PER_SEC_PER_GPU.get(args.batch) if headline else None
+    headline = (args.model == "resnet50" and args.image_size == 224 and args.num_classes == 1000
+                and args.optim == "sgd" and not args.zero)
+    if headline:
+        base = BASELINE_IMG_PER_SEC_PER_GPU.get(args.batch)
+    elif args.preset in PRESET_BASELINE_PER_GPU and args.batch == PRESETS[args.preset]["batch"]:
+        base = PRESET_BASELINE_PER_GPU[args.preset]
+    else:
+        base = None
+    metric = PRESET_METRIC.get(args.preset, HEADLINE_METRIC) if (args.preset or headline) else (
+        f"images/sec (whole node) {args.model} {args.image_size}x{args.image_size} {args.num_classes}-class bf16")
+    dname = DATASET_NAME.get((args.image_size, args.num_classes), f"{args.num_classes}-class")
     out = {
-        "metric": "images/sec (whole node) ResNet-50 ImageNet-1K at 1/2/4/8 MI355X; top-1 acc",
+        "metric": metric,
         "value": round(value, 2),
         "unit": "images/s",
         "n_gpus": n,
@@ -114,12 +168,14 @@ def main(argv=None) -> int:
         "data": f"synthetic (uint8 NHWC {args.image_size}x{args.image_size} images + random labels, on-device; "
                 "random-init weights)",
         "config": {
-            "model": f"{args.model} ImageNet-1K {args.image_size}x{args.image_size} {args.num_classes} classes"
-                     + (" large-batch (global 8192 at 8 GPUs)" if args.batch == 1024 else ""),
+            "model": f"{args.model} {dname} {args.image_size}x{args.image_size} {args.num_classes} classes"
+                     + (" large-batch (global 8192 at 8 GPUs)" if headline and args.batch == 1024 else ""),
             "global_batch": args.batch * n,
             "per_gpu_batch": args.batch,
             "seq_len": None,
-            "parallelism": f"dp{n}",
+            "parallelism": f"dp{n}" + (f"+zero{args.zero}" if args.zero else ""),
+            "world_size_seen": seen,
+            "backend": info.backend if n > 1 else "none",
             "impl": args.impl,
             "optimizer": {"sgd": "SGD momentum 0.9 nesterov=False wd 5e-5",
                           "lars": "LARS (eta 1e-3) + SGD momentum 0.9 wd 5e-5"}.get(args.optim, "AdamW wd 0.01")

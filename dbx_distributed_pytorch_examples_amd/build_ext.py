@@ -4,7 +4,10 @@ Compiles every ``csrc/*.hip`` for gfx950 with hipcc and the pybind11 bindings, l
 ``_C<EXT_SUFFIX>`` next to this file (the .so travels to the GPU box with the snapshot; the
 git history stays source-only). Incremental: objects newer than their sources are reused.
 Environment: ``DBX_ARCH`` (default gfx950), ``DBX_HIPCC`` (default /opt/rocm/bin/hipcc),
-``DBX_DEBUG=1`` adds ``-g -DDBX_DEBUG`` (bounds-checked index math in debug builds).
+``DBX_DEBUG=1`` builds the separate variant ``_C_variant_debug`` with ``-g -DDBX_DEBUG``: the
+``DBX_DCHECK`` device checks (common.h) on the conv kernels' gather / scatter offsets then print the
+failing condition, block and thread instead of letting an out-of-range offset read zeros or write
+past a tensor; load it with ``DBX_EXT_VARIANT=debug`` (the production ``_C`` is never replaced).
 """
 from __future__ import annotations
 
@@ -45,6 +48,8 @@ def _newer(target: str, deps) -> bool:
 
 def build(verbose: bool = False, jobs: int = 8, variant: str = "", defines=()) -> str:
     arch = os.environ.get("DBX_ARCH", "gfx950")
+    if os.environ.get("DBX_DEBUG") == "1" and not variant:
+        variant = "debug"
     bdir = BUILD if not variant else BUILD + "_" + variant
     os.makedirs(bdir, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "*.h"))

@@ -14,6 +14,22 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 #define DBX_LDS __attribute__((address_space(3)))
 
+// Device-side index checks of the debug build (build_ext with DBX_DEBUG=1 -> _C_variant_debug):
+// a failing condition prints itself with the block / thread; the kernel continues (no trap, so a
+// failing check cannot take the device down). Compiled out of the production build.
+#ifdef DBX_DEBUG
+#define DBX_DCHECK(cond)                                                                              \
+  do {                                                                                                \
+    if (!(cond))                                                                                      \
+      printf("[dbx] DBX_DCHECK failed: %s at %s:%d block %d thread %d\n", #cond, __FILE__, __LINE__, \
+             (int)blockIdx.x, (int)threadIdx.x);                                                      \
+  } while (0)
+#else
+#define DBX_DCHECK(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 #define HIP_CHECK_RET(expr)                                   \
   do {                                                        \
     hipError_t _e = (expr);                                   \

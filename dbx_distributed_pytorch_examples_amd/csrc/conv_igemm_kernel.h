@@ -130,6 +130,7 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x4 (&acc)[
         pix = ((size_t)n * a.FH + ph) * a.FW + pw;
       }
       const size_t e = pix * a.OC + n0 + ccol * 8;
+      DBX_DCHECK(!ok[k] || e + 8 <= (size_t)(sub_geom ? (size_t)a.N * a.FH * a.FW : (size_t)a.M) * a.OC);
       ee[k] = e;
       if constexpr (ACCUM) {
         size_t ae = e;
@@ -370,6 +371,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       if (MODE == DGRAD) { ahb[i] = oh + a.dh0; awb[i] = ow + a.dw0; }
       else { ahb[i] = oh * a.stride - a.pad; awb[i] = ow * a.stride - a.pad; }
       apix[i] = 2u * (unsigned)(((n * a.IH + ahb[i]) * a.IW + awb[i]) * a.IC + acha * 8);
+      // a live row's sample lies inside x (its taps then add in-image displacements only)
+      DBX_DCHECK(m >= a.M || (n >= 0 && n < a.N && oh >= 0 && oh < a.OH && ow >= 0 && ow < a.OW));
       if (m >= a.M) ahb[i] = -(1 << 28);
     }
   };
@@ -450,6 +453,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       for (int i = 0; i < A_CH; ++i) {
         const bool v = live && (unsigned)(ahb[i] + dh) < (unsigned)a.IH && (unsigned)(awb[i] + dw) < (unsigned)a.IW;
         // padding taps / rows past M read out of the buffer's range: the hardware returns zeros
+        DBX_DCHECK(!v || (unsigned long long)(apix[i] + toff) + 16ull <= 2ull * a.N * a.IH * a.IW * a.IC);
         ra[S][i] = buf_load16(xr, v ? apix[i] + toff : kOOB);
         if constexpr (TAIL) rr[S][i] = buf_load16(rresr, v ? apix[i] + toff : kOOB);
         if constexpr (PRO) avalid[S] |= (v ? 1u : 0u) << i;
@@ -519,6 +523,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int n = ln0 + (tid >> 3) + RPP * i;
+      DBX_DCHECK(!live || (n < a.OC && koff + 8 <= KTOT));
       rb[S][i] = buf_load16(wr, live ? 2u * (unsigned)(n * KTOT + koff) : kOOB);
     }
   };

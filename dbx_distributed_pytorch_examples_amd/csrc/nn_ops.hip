@@ -660,9 +660,11 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, f
 //   g    <- adapt ? trust * (gs * g + wd * w) : gs * g
 // followed by the plain SGD kernel with wd = 0. grid = (chunks, nseg): blockIdx.y is the segment,
 // blocks stride over it; phase 1 reduces |w|^2 and |gs*g|^2 per segment (wave shuffles, one LDS
-// step over the 4 waves, one fp64 atomic pair per block: fp64 sums of fp32 partials are exact
-// for any block order here, so the trust ratios are bit-reproducible), phase 2 rescales in place.
+// step over the 4 waves) into one fp64 partial pair per (segment, block) slot -- no atomics; phase 2
+// sums a segment's partials in block order (every block the same fixed order), so the trust ratios
+// are bit-reproducible whatever order the blocks ran in, then rescales in place.
 // ----------------------------------------------------------------------------------------
+constexpr int kLarsMaxBlocks = 64;  // blocks per segment (dbx_lars_scale clamps to this)
 __global__ void lars_norms_kernel(const float* __restrict__ p, const float* __restrict__ g,
                                   const int* __restrict__ seg_off, const int* __restrict__ seg_len, float gs,
                                   double* __restrict__ norms) {
@@ -685,9 +687,10 @@ __global__ void lars_norms_kernel(const float* __restrict__ p, const float* __re
     red[1][wave] = gg;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    atomicAdd(norms + 2 * s, (double)(red[0][0] + red[0][1] + red[0][2] + red[0][3]));
-    atomicAdd(norms + 2 * s + 1, (double)(red[1][0] + red[1][1] + red[1][2] + red[1][3]));
+  if (threadIdx.x == 0) {  // slot (s, block): norms is [nseg][kLarsMaxBlocks][2]
+    double* o = norms + 2 * ((size_t)s * kLarsMaxBlocks + blockIdx.x);
+    o[0] = (double)(red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    o[1] = (double)(red[1][0] + red[1][1] + red[1][2] + red[1][3]);
   }
 }
 
@@ -698,7 +701,10 @@ __global__ void lars_apply_kernel(const float* __restrict__ p, float* __restrict
   const int off = seg_off[s], len = seg_len[s];
   float scale = gs, decay = 0.f;
   if (adapt[s]) {
-    const float wn = (float)sqrt(norms[2 * s]), gn = (float)sqrt(norms[2 * s + 1]);
+    double ww = 0.0, gg = 0.0;  // fixed block order (gridDim.x slots written by lars_norms_kernel)
+    const double* o = norms + 2 * (size_t)s * kLarsMaxBlocks;
+    for (int b = 0; b < (int)gridDim.x; ++b) { ww += o[2 * b]; gg += o[2 * b + 1]; }
+    const float wn = (float)sqrt(ww), gn = (float)sqrt(gg);
     const float trust = (wn > 0.f && gn > 0.f) ? eta * wn / (gn + wd * wn) : 1.f;
     scale = trust * gs;
     decay = trust * wd;
@@ -728,8 +734,9 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
-// sum of squares over a flat fp32 buffer (global-norm clipping), one fp64 atomic per block
-// (fp32 block partials add exactly in fp64: the norm does not depend on block order)
+// sum of squares over a flat fp32 buffer (global-norm clipping), one fp64 atomic per block. fp64
+// sums of fp32 block partials are exact (hence independent of block order) while the partials'
+// magnitudes span less than ~2^29; beyond that the last bits of the norm can depend on the order.
 __global__ void sumsq_kernel(const float* __restrict__ x, long long n, double* out) {
   float s = 0.f;
   for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) s += x[k] * x[k];
@@ -1047,9 +1054,7 @@ extern "C" int dbx_lars_scale(const float* p, float* g, const int* seg_off, cons
                               int nseg, int max_len, double* norms, float gs, float eta, float wd, hipStream_t st) {
   if (nseg <= 0) return 0;
   int bx = (int)((max_len + 255) / 256);
-  bx = bx < 1 ? 1 : (bx > 64 ? 64 : bx);
-  hipError_t e = hipMemsetAsync(norms, 0, sizeof(double) * 2 * nseg, st);
-  if (e != hipSuccess) return (int)e;
+  bx = bx < 1 ? 1 : (bx > kLarsMaxBlocks ? kLarsMaxBlocks : bx);
   hipLaunchKernelGGL(lars_norms_kernel, dim3(bx, nseg), dim3(256), 0, st, p, g, seg_off, seg_len, gs, norms);
   hipLaunchKernelGGL(lars_apply_kernel, dim3(bx, nseg), dim3(256), 0, st, p, g, seg_off, seg_len, adapt, norms, gs,
                      eta, wd);

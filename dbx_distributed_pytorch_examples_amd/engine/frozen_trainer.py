@@ -143,7 +143,9 @@ class FrozenFeatureTrainer:
                     return
                 torch.cuda.synchronize(self.dev)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                # thread-local whenever a process group (and its watchdog thread) exists, even at world 1
+                mode = "thread_local" if (dist.is_available() and dist.is_initialized()) else "global"
+                with torch.cuda.graph(g, capture_error_mode=mode):
                     self._head_step(self._backbone_eager().float(), self.lab)
                 torch.cuda.synchronize(self.dev)
                 self._sgraph = g

@@ -12,13 +12,19 @@ parameter's ``.grad`` as a view of the program's flat gradient buffer. The modul
 already ARE views of the program's flat fp32 master, so any torch optimizer steps them in place.
 
 * input: a float NCHW batch, already normalised (what torchvision-style transforms produce);
-  batches of another size than the compiled one run through the plain torch module on the same
-  parameters (correct, not accelerated);
+  batches of another size than the compiled one (a short final batch) run through the plain
+  torch module on the same parameters (correct, not accelerated); at world size > 1 their
+  gradients are all-reduced too, at the end of that backward (queued autograd callback), so the
+  replicas never diverge on a short batch;
 * gradients: a backward sets ``p.grad`` (or adds into a ``p.grad`` the caller owns); there is no
   accumulation across two backwards into the same view (call ``zero_grad`` between steps, the
   usual loop);
-* world size > 1: the flat gradient is all-reduced (averaged) in ONE collective at the end of
-  the backward; do not wrap the result in DDP as well (``frontends.accelerate`` knows this);
+* world size > 1: rank 0's parameters and BN buffers are broadcast at construction (DDP's
+  constructor semantics); the flat gradient is all-reduced (averaged) per
+  backward segment on a comm stream while the remaining segments' backward runs (the segment
+  boundaries NativeTrainer uses: head+layer4 | layer3 | layer2 | layer1 | stem), so most of the
+  all-reduce hides under the backward; do not wrap the result in DDP as well
+  (``frontends.accelerate`` knows this);
 * on the GPU the program's forward (train / eval) and backward are each captured as a HIP graph
   after two eager calls and replayed (the user loop is otherwise launch-bound at CIFAR sizes);
   the input / dlogits copies into the static buffers and the all-reduce stay outside the graphs.
@@ -72,6 +78,65 @@ class NativeResNet(nn.Module):
             gv = g.view(prm.shape[0], prm.shape[2], prm.shape[3], prm.shape[1]).permute(0, 3, 1, 2) \
                 if prm.dim() == 4 else g.view(prm.shape)
             self._grad_views.append((prm, gv))
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self._comm = None
+        self._fallback_active = False
+        self._sync_queued = False
+        if self.world > 1:
+            self._init_distributed()
+
+    # ------------------------------------------------------------------------------
+    def _init_distributed(self):
+        """DDP-constructor semantics (rank 0's weights and BN buffers everywhere), per-segment
+        gradient ranges for the overlapped all-reduce, and the short-batch fallback's gradient sync."""
+        from ..parallel.dist import host_sync_for_gloo
+        p, pg = self.prog, self.pg
+        src = 0 if pg is None else dist.get_global_rank(pg, 0)
+        with torch.no_grad():
+            host_sync_for_gloo(p.master, pg)
+            dist.broadcast(p.master, src, group=pg)
+            for bn in p.bns:
+                dist.broadcast(bn.mod.running_mean, src, group=pg)
+                dist.broadcast(bn.mod.running_var, src, group=pg)
+        self._seg_ranges = []
+        for rs in p.segment_param_ranges():
+            self._seg_ranges.append((min(r[1] for r in rs), max(r[1] + (r[2] + 15) // 16 * 16 for r in rs))
+                                    if rs else None)
+        if p.dev.type == "cuda":
+            self._comm = torch.cuda.Stream(device=p.dev, priority=-1)
+            # next to the comm stream the wgrad side stream costs more than it overlaps
+            # (NativeTrainer, profiles/r2s2_multirank/): weight gradients run on the main stream
+            p.overlap_wgrad = False
+        for prm in self.model.parameters():
+            if prm.requires_grad:
+                prm.register_post_accumulate_grad_hook(self._fallback_hook)
+
+    def _allreduce_range(self, lo: int, hi: int):
+        from ..parallel.dist import host_sync_for_gloo
+        g = self.prog.grad[lo:hi]
+        host_sync_for_gloo(g, self.pg)
+        dist.all_reduce(g, group=self.pg)
+
+    def _fallback_hook(self, prm):
+        # the torch-module path (batch of another size) at world > 1: all-reduce its gradients once
+        # the whole backward has accumulated them (what DDP would have done)
+        if self._fallback_active and not self._sync_queued:
+            self._sync_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._fallback_allreduce)
+
+    def _fallback_allreduce(self):
+        from ..parallel.dist import host_sync_for_gloo
+        self._sync_queued = False
+        self._fallback_active = False
+        grads = [prm.grad for prm in self.model.parameters() if prm.requires_grad and prm.grad is not None]
+        if not grads:
+            return
+        flat = torch._utils._flatten_dense_tensors([g.contiguous() for g in grads])
+        host_sync_for_gloo(flat, self.pg)
+        dist.all_reduce(flat, group=self.pg)
+        flat.div_(self.world)
+        for g, r in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+            g.copy_(r)
 
     @property
     def module(self) -> nn.Module:
@@ -106,7 +171,10 @@ class NativeResNet(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         p = self.prog
         if x.dim() != 4 or x.shape[0] != p.N or tuple(x.shape[2:]) != (p.H, p.W) or x.shape[1] != p.in_ch:
-            return self.model(x)  # another batch size / resolution: the torch module on the same parameters
+            # another batch size / resolution: the torch module on the same parameters (gradients
+            # all-reduced after its backward at world > 1, see _fallback_hook)
+            self._fallback_active = self.world > 1 and torch.is_grad_enabled() and self.training
+            return self.model(x)
         if not (torch.is_grad_enabled() and self.training):
             with torch.no_grad():
                 return self._native_forward(x)
@@ -150,13 +218,26 @@ class NativeResNet(nn.Module):
     def _native_backward(self, dlogits: torch.Tensor) -> None:
         p = self.prog
         p.dlogits.copy_(dlogits)
-        self._run("bwd", p.backward)
-        world = dist.get_world_size(self.pg) if (dist.is_available() and dist.is_initialized()) else 1
-        if world > 1:
-            from ..parallel.dist import host_sync_for_gloo
-            host_sync_for_gloo(p.grad, self.pg)
-            dist.all_reduce(p.grad, group=self.pg)
-            p.grad.div_(world)
+        if self.world == 1:
+            self._run("bwd", p.backward)
+        else:
+            # one graph per backward segment; each segment's gradient range is all-reduced on the
+            # comm stream while the next segment's backward runs (the reference's DDP overlap, M3)
+            cur = torch.cuda.current_stream(p.dev) if self._comm is not None else None
+            for k, (_, fn) in enumerate(p.backward_segments()):
+                self._run(f"bwd{k}", fn)
+                rg = self._seg_ranges[k]
+                if rg is None:
+                    continue
+                if cur is None:
+                    self._allreduce_range(*rg)
+                    continue
+                self._comm.wait_stream(cur)
+                with torch.cuda.stream(self._comm):
+                    self._allreduce_range(*rg)
+            if cur is not None:
+                cur.wait_stream(self._comm)
+            p.grad.div_(self.world)
         for prm, gv in self._grad_views:
             if not prm.requires_grad:
                 continue

@@ -183,7 +183,7 @@ class NativeTrainer:
         bn_names = {f"{bn.name}." for bn in self.prog.bns}
         adapt = torch.tensor([int(r[0].endswith(".weight") and not any(r[0].startswith(b) for b in bn_names))
                               for r in rs], dtype=torch.int32, device=dev)
-        return off, ln, adapt, torch.zeros(2 * len(rs), device=dev, dtype=torch.float64), max(r[2] for r in rs)
+        return off, ln, adapt, torch.zeros(K.LARS_MAX_BLOCKS * 2 * len(rs), device=dev, dtype=torch.float64), max(r[2] for r in rs)
 
     def _optimizer_phase(self):
         p, o = self.prog, self.opt

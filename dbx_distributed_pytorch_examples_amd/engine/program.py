@@ -392,9 +392,10 @@ class ResNetProgram:
         # the fused conv3 backward runs on the main stream while side-stream weight gradients use
         # self.ws: its per-workgroup slabs get their own workspace (<= 1024 slabs + 64 partials)
         fused = [b.convs[-1] for i, b in enumerate(self.blocks) if self._fuse3(b, i == len(self.blocks) - 1)]
-        # (slab count = resident workgroups <= 2 per CU; the CPU reference path uses no workspace)
-        self.ws_dw = (torch.empty(((512 + 64) * max(c.OC * c.IC for c in fused) if dev.type == "cuda" else 16),
-                                  device=dev, dtype=torch.float32) if fused else None)
+        # (slab count = resident workgroups, K.dwfused_grid; the CPU reference path uses no workspace)
+        self.ws_dw = (torch.empty((max((K.dwfused_grid(c.IC, c.OC) + 64) * c.OC * c.IC for c in fused)
+                                   if dev.type == "cuda" else 16), device=dev, dtype=torch.float32)
+                      if fused else None)
         fh, fw = self.feat_hw
         self.dfeat = self.blocks[-1].out  # placeholder name; real grad buffer below
         self.dlast = E(N, fh, fw, self.feat_c)

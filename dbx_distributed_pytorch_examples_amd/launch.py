@@ -22,6 +22,7 @@ run a function, hand rank 0's result back". :class:`Launcher` does exactly that,
 Safety rule of this machine pool: a process that has initialised the GPU must never exec
 another program, so the launcher refuses to spawn from a parent that has touched HIP.
 CLI (torchrun-like): ``python -m dbx_distributed_pytorch_examples_amd.launch --nproc-per-node 8 train.py ...``
+(or ``... --nproc-per-node 8 -m dbx_distributed_pytorch_examples_amd.train.cli ...``)
 """
 from __future__ import annotations
 
@@ -256,34 +257,36 @@ class DeepspeedTorchDistributor(Launcher):
 # ----------------------------------------------------------------------------------------
 # CLI: torchrun-like script launcher (subprocesses; the parent never touches the GPU)
 # ----------------------------------------------------------------------------------------
-def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(description="dbx launcher (one process per GPU)")
-    ap.add_argument("--nproc-per-node", "--nproc_per_node", type=int, default=1)
-    ap.add_argument("--nnodes", type=int, default=1)
-    ap.add_argument("--node-rank", type=int, default=0)
-    ap.add_argument("--master-addr", default="127.0.0.1")
-    ap.add_argument("--master-port", type=int, default=0)
-    ap.add_argument("--max-restarts", type=int, default=0)
-    ap.add_argument("--heartbeat-timeout", type=float, default=0.0)
-    ap.add_argument("script")
-    ap.add_argument("script_args", nargs=argparse.REMAINDER)
-    a = ap.parse_args(argv)
-    L = Launcher(a.nproc_per_node, a.nnodes, a.node_rank, a.master_addr, a.master_port or None,
-                 max_restarts=a.max_restarts, heartbeat_timeout=a.heartbeat_timeout or None)
-    for attempt in range(a.max_restarts + 1):
-        port = a.master_port or _free_port()
+def run_subprocess_ranks(nproc: int, cmd: List[str], nnodes: int = 1, node_rank: int = 0,
+                         master_addr: str = "127.0.0.1", master_port: Optional[int] = None,
+                         max_restarts: int = 0, heartbeat_timeout: Optional[float] = None,
+                         env: Optional[Dict[str, str]] = None) -> int:
+    """Start ``cmd`` (an argv list, e.g. ``[sys.executable, "bench.py", ...]``) once per local rank
+    with the torchrun environment set, watch the ranks, and return 0 when every rank exits 0.
+
+    A rank that fails ends the whole attempt (the others are terminated); ``max_restarts`` re-runs
+    all ranks. Used by the CLI below and by ``bench.py --gpus N`` when it is not already under a
+    launcher. The caller must not have initialised the GPU (children are fork+exec'd)."""
+    if _gpu_touched():
+        raise LaunchError("refusing to spawn ranks from a process that has already initialised the GPU")
+    L = Launcher(nproc, nnodes, node_rank, master_addr, master_port,
+                 max_restarts=max_restarts, heartbeat_timeout=heartbeat_timeout, env=env)
+    code = 1
+    for attempt in range(max_restarts + 1):
+        port = master_port or _free_port()
         hb_dir = tempfile.mkdtemp(prefix="dbx_hb_")
         procs = []
-        for lr in range(a.nproc_per_node):
-            env = dict(os.environ)
-            env.update(L._env(lr, port, hb_dir, attempt))
-            procs.append(subprocess.Popen([sys.executable, a.script] + a.script_args, env=env))
+        for lr in range(nproc):
+            e = dict(os.environ)
+            e.update(L._env(lr, port, hb_dir, attempt))
+            procs.append(subprocess.Popen(list(cmd), env=e))
         failed = None
         while True:
             codes = [p.poll() for p in procs]
             bad = [i for i, c in enumerate(codes) if c not in (None, 0)]
             if bad:
                 failed = f"rank(s) {bad} exited with {[codes[i] for i in bad]}"
+                code = next(c for c in codes if c not in (None, 0))
                 break
             if all(c == 0 for c in codes):
                 break
@@ -291,6 +294,7 @@ def main(argv=None) -> int:
                 stale = _stale_ranks(hb_dir, len(procs), L.hb_timeout)
                 if stale:
                     failed = f"watchdog: rank(s) {stale} made no progress for {L.hb_timeout}s"
+                    code = 124
                     break
             time.sleep(0.1)
         if failed:
@@ -302,12 +306,34 @@ def main(argv=None) -> int:
                     p.wait(10)
                 except subprocess.TimeoutExpired:
                     p.kill()
+                    p.wait()
             shutil.rmtree(hb_dir, ignore_errors=True)
-            print(f"[launch] attempt {attempt + 1} failed: {failed}", file=sys.stderr)
+            print(f"[launch] attempt {attempt + 1}/{max_restarts + 1} failed: {failed}", file=sys.stderr)
             continue
         shutil.rmtree(hb_dir, ignore_errors=True)
         return 0
-    return 1
+    return code if code else 1
+
+
+def main(argv=None) -> int:
+    """``python -m dbx_distributed_pytorch_examples_amd.launch --nproc-per-node 8 train.py args...``
+    or ``... --nproc-per-node 8 -m package.module args...`` (like torchrun / python -m)."""
+    ap = argparse.ArgumentParser(description="dbx launcher (one process per GPU)")
+    ap.add_argument("--nproc-per-node", "--nproc_per_node", type=int, default=1)
+    ap.add_argument("--nnodes", type=int, default=1)
+    ap.add_argument("--node-rank", type=int, default=0)
+    ap.add_argument("--master-addr", default="127.0.0.1")
+    ap.add_argument("--master-port", type=int, default=0)
+    ap.add_argument("--max-restarts", type=int, default=0)
+    ap.add_argument("--heartbeat-timeout", type=float, default=0.0)
+    ap.add_argument("-m", "--module", action="store_true",
+                    help="treat the target as a module name and run it as `python -m <module>`")
+    ap.add_argument("script", help="script path (or module name with -m)")
+    ap.add_argument("script_args", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    cmd = [sys.executable] + (["-m", a.script] if a.module else [a.script]) + a.script_args
+    return run_subprocess_ranks(a.nproc_per_node, cmd, a.nnodes, a.node_rank, a.master_addr,
+                                a.master_port or None, a.max_restarts, a.heartbeat_timeout or None)
 
 
 if __name__ == "__main__":

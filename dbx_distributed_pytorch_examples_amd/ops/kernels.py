@@ -426,10 +426,10 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
             and patch3_supported(IC, OC, R, S, stride, pad, IH, IW) and IH % 4 == 0
             and (tile == "patch" or _use_patch3(None, "wgrad"))):
         # 3x3 patch kernel (csrc/conv_patch3.hip): one fp32 slab per persistent workgroup
-        if 320 * OC * R * S * IC > ws.numel():  # 256 slabs + the two-level reduction's partials
+        if (num_cus() + 64) * OC * R * S * IC > ws.numel():  # one slab per CU + the reduction's partials
             raise ValueError("wgrad workspace too small for the patch kernel")
-        nsl = C().wgrad_patch3(dy.data_ptr(), x.data_ptr(), ws.data_ptr(), N, IH, IW, IC, OH, OW, OC, R, S, stride,
-                               pad, stream_ptr())
+        nsl = C().wgrad_patch3(dy.data_ptr(), x.data_ptr(), ws.data_ptr(), ws.numel(), N, IH, IW, IC, OH, OW, OC, R,
+                               S, stride, pad, stream_ptr())
         C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsl, float(scale), int(accumulate), stream_ptr())
         return dw
     if isinstance(tile, str):
@@ -478,13 +478,34 @@ def dwfused_supported(C: int, K: int, M: int) -> bool:
     return (C, K) in ((64, 256), (128, 512)) and M % 64 == 0 and 2 * M * K < 0xFFFFFF00
 
 
+def num_cus() -> int:
+    """Compute units of the current device (256 on MI355X); 256 when no GPU is visible."""
+    global _NUM_CUS
+    if _NUM_CUS is None:
+        try:
+            _NUM_CUS = int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count) \
+                if torch.cuda.is_available() else 256
+        except Exception:
+            _NUM_CUS = 256
+    return _NUM_CUS
+
+
+_NUM_CUS = None
+
+
+def dwfused_grid(C: int, K: int) -> int:
+    """Resident workgroups of the fused conv3 backward (csrc/conv_dwfused.hip launches
+    occupancy x CUs): 2 per CU for the 64 -> 256 variant, 1 per CU for 128 -> 512."""
+    return (2 if (C, K) == (64, 256) else 1) * num_cus()
+
+
 def dwfused_preferred(C: int, K: int, M: int) -> bool:
     """Schedule policy: the fused conv3 backward only when every resident workgroup walks >=
     DBX_FUSE_DW_MIN_TILES (default 8) tiles -- with fewer, the per-workgroup weight load and slab write
     and the lost wgrad side-stream overlap outweigh the saved traffic (TinyImageNet b512 fused at 2-4
     tiles per workgroup: 86.5k vs 87.2k img/s, profiles/r2s4_dwfused/)."""
     import os
-    grid = 512 if (C, K) == (64, 256) else 256  # resident workgroups: 2 / 1 per CU
+    grid = dwfused_grid(C, K)
     return dwfused_supported(C, K, M) and M >= int(os.environ.get("DBX_FUSE_DW_MIN_TILES", "8")) * grid * 64
 
 
@@ -745,18 +766,22 @@ def sgd_step(p, g, v, p16=None, *, lr, momentum, dampening=0.0, weight_decay=0.0
             float(weight_decay), int(nesterov), int(first), _p(grad_scale_ptr), float(grad_scale), stream_ptr())
 
 
+LARS_MAX_BLOCKS = 64  # csrc/nn_ops.hip kLarsMaxBlocks
+
+
 @_dispatch
 def lars_scale(p, g, seg_off, seg_len, adapt, norms, *, grad_scale, eta, weight_decay, max_len):
     """LARS pre-scaling of the flat gradient in place (then ``sgd_step`` with wd=0): per segment
     trust = eta*|w|/(|gs*g| + wd*|w|); adapted segments get g = trust*(gs*g + wd*w), the others gs*g.
-    ``seg_off`` / ``seg_len`` / ``adapt``: int32 device tensors [nseg]; ``norms``: fp64 [2*nseg] scratch."""
+    ``seg_off`` / ``seg_len`` / ``adapt``: int32 device tensors [nseg]; ``norms``: fp64 [nseg*64*2] scratch
+    (one partial pair per segment and block, summed in fixed block order: bit-reproducible)."""
     n = p.numel()
     _chk(p, torch.float32, "p")
     _chk(g, torch.float32, "g", n)
     nseg = seg_off.numel()
     for t, nm in ((seg_off, "seg_off"), (seg_len, "seg_len"), (adapt, "adapt")):
         _chk(t, torch.int32, nm, nseg)
-    _chk(norms, torch.float64, "norms", 2 * nseg)
+    _chk(norms, torch.float64, "norms", LARS_MAX_BLOCKS * 2 * nseg)
     C().lars_scale(p.data_ptr(), g.data_ptr(), seg_off.data_ptr(), seg_len.data_ptr(), adapt.data_ptr(), nseg,
                    int(max_len), norms.data_ptr(), float(grad_scale), float(eta), float(weight_decay), stream_ptr())
 

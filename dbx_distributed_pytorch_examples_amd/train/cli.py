@@ -1,7 +1,7 @@
 """Command-line training: ``python -m dbx_distributed_pytorch_examples_amd.train.cli CONFIG [k=v ...]``.
 
 One process per GPU: launch with ``python -m dbx_distributed_pytorch_examples_amd.launch
---nproc-per-node 8 -m ...`` or ``torchrun`` (env:// rendezvous, RCCL). ``--deepspeed FILE`` maps a
+--nproc-per-node 8 -m dbx_distributed_pytorch_examples_amd.train.cli CONFIG`` or ``torchrun`` (env:// rendezvous, RCCL). ``--deepspeed FILE`` maps a
 DeepSpeed JSON/YAML (the reference's `02_deepspeed/deepspeed_config.py` schema) onto the config.
 Prints one JSON summary line on rank 0.
 """

@@ -1,0 +1,49 @@
+"""bench.py contract on CPU: self-launched ranks (gloo), world/--gpus mismatch is an error, the
+JSON line carries the world size the process group formed and per-preset metric labels."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.timeout(600)
+
+
+def _run(args, env_extra=None, timeout=500):
+    env = dict(os.environ)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd="/tmp", env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_self_launch_two_ranks_gloo_cpu():
+    r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "0"],
+             {"DBX_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["world_size_seen"] == 2 and d["config"]["backend"] == "gloo"
+    assert d["config"]["global_batch"] == 8 and d["config"]["per_gpu_batch"] == 4  # explicit --batch wins
+    assert "ResNet-18 CIFAR-10" in d["metric"] and "CIFAR-10" in d["config"]["model"]
+    assert d["vs_baseline"] is None  # not the preset's batch: no comparable baseline
+
+
+def test_world_mismatch_is_an_error():
+    # under a launcher environment that says world 1, --gpus 2 must not report a number
+    r = _run(["--gpus", "2", "--steps", "1"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 3 and "refusing" in r.stderr and not r.stdout.strip()
+
+
+def test_no_gpus_visible_fails_before_spawning():
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("two GPUs visible: --gpus 2 would run")
+    r = _run(["--gpus", "2", "--steps", "1"], {"DBX_DIST_BACKEND": ""})
+    assert r.returncode == 3 and "GPU(s) visible" in r.stderr

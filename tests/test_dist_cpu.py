@@ -331,3 +331,55 @@ def _accel_native():
 def test_accelerate_native_module_two_ranks():
     is_native, grads_equal, params_equal, gnorm = Launcher(2, use_gpu=False).run(_accel_native)
     assert is_native and grads_equal and params_equal and gnorm > 0  # averaged gradients, replicas in sync
+
+
+def _native_module_sync():
+    """engine.native_module at world 2 (gloo, CPU reference ops): rank 0's weights are broadcast at
+    construction, the overlapped per-segment all-reduce gives exactly the mean of the per-rank
+    single-process gradients, and a short final batch (torch-module fallback) still averages the
+    gradients, so the replicas stay identical."""
+    import torch.distributed as tdist
+    from dbx_distributed_pytorch_examples_amd.engine.native_module import native_module
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    info = ddist.init_distributed(device="cpu")
+    rank = info.rank
+    torch.manual_seed(100 + rank)  # different init per rank: the constructor broadcast must fix it
+    nm = native_module(build_model("resnet18", num_classes=10), 4, (32, 32), torch.device("cpu")).train()
+
+    def flat(ts):
+        return torch.cat([t.detach().reshape(-1) for t in ts])
+
+    def gather(t):
+        out = [torch.empty_like(t) for _ in range(2)]
+        tdist.all_gather(out, t)
+        return out
+
+    par = gather(flat(nm.parameters()))
+    init_same = torch.equal(par[0], par[1])
+    singles = [tdist.new_group([r]) for r in range(2)]
+    ref = build_model("resnet18", num_classes=10)
+    ref.load_state_dict(nm.state_dict())
+    nm1 = native_module(ref, 4, (32, 32), torch.device("cpu"), process_group=singles[rank]).train()
+    g = torch.Generator().manual_seed(10 + rank)
+    x, y = torch.randn(4, 3, 32, 32, generator=g), torch.randint(0, 10, (4,), generator=g)
+    nn.functional.cross_entropy(nm1(x), y).backward()
+    gl = gather(flat(p.grad for p in nm1.parameters()))
+    expect = (gl[0] + gl[1]) / 2
+    nn.functional.cross_entropy(nm(x), y).backward()
+    got = flat(p.grad for p in nm.parameters())
+    grad_is_mean = torch.equal(got, expect)
+    for p in nm.parameters():
+        p.grad = None
+    nn.functional.cross_entropy(nm(x[:3]), y[:3]).backward()  # short batch -> torch fallback path
+    gs = gather(flat(p.grad for p in nm.parameters()))
+    short_synced = torch.equal(gs[0], gs[1]) and float(gs[0].norm()) > 0
+    ddist.destroy()
+    return init_same, grad_is_mean, short_synced
+
+
+def test_native_module_broadcast_overlap_and_short_batch_two_ranks():
+    init_same, grad_is_mean, short_synced = Launcher(2, use_gpu=False).run(_native_module_sync)
+    assert init_same, "rank 0's parameters were not broadcast at construction"
+    assert grad_is_mean, "overlapped per-segment all-reduce != mean of per-rank gradients"
+    assert short_synced, "short-batch fallback left the replicas' gradients different"

@@ -86,7 +86,7 @@ def test_native_lars_step_matches_autograd_lars_cpu(clip):
 def test_lars_kernel_matches_reference_gpu():
     p, g, off, ln, ad, mx = _segments(SHAPES, dev="cuda")
     pr, gr = p.cpu(), g.cpu()
-    K.lars_scale(p, g, off, ln, ad, torch.zeros(2 * len(SHAPES), device="cuda", dtype=torch.float64), grad_scale=0.125, eta=0.001,
+    K.lars_scale(p, g, off, ln, ad, torch.zeros(K.LARS_MAX_BLOCKS * 2 * len(SHAPES), device="cuda", dtype=torch.float64), grad_scale=0.125, eta=0.001,
                  weight_decay=5e-5, max_len=mx)
     R.lars_scale(pr, gr, off.cpu(), ln.cpu(), ad.cpu(), torch.zeros(2 * len(SHAPES)), grad_scale=0.125, eta=0.001,
                  weight_decay=5e-5, max_len=mx)
@@ -128,7 +128,7 @@ def test_lars_scale_bit_reproducible():
     outs = []
     for _ in range(3):
         g = g0.clone()
-        norms = torch.zeros(6, device="cuda", dtype=torch.float64)
+        norms = torch.zeros(K.LARS_MAX_BLOCKS * 6, device="cuda", dtype=torch.float64)
         K.lars_scale(p0, g, off, ln, ad, norms, grad_scale=0.25, eta=1e-3, weight_decay=1e-4, max_len=max(n))
         outs.append((g, norms))
     for g, nm in outs[1:]:

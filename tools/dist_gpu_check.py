@@ -1,15 +1,21 @@
 #!/usr/bin/env python3
-"""Multi-rank native training on GPU (world 2). On a one-GPU box both ranks share cuda:0 and talk
-over gloo (DBX_DIST_BACKEND=gloo); on a multi-GPU node the same script runs on RCCL. Checks:
-replicas stay bit-identical across ranks, the per-segment graph-captured path matches the eager
-path bit for bit, ZeRO-1 matches plain data parallel bit for bit (every reduction in the step is
-order-independent: fp64 statistics atomics, fixed-order split-K and shard sums).
+"""Multi-rank native training on GPU. On a one-GPU box the ranks share cuda:0 and talk over gloo
+(DBX_DIST_BACKEND=gloo); on a multi-GPU node the same script runs on RCCL, one GPU per rank.
+
+Checks (all on the segmented-graph + comm-stream path that world > 1 takes):
+  1. the data-parallel gradient equals the sum of every rank's single-process gradient of its own
+     batch (computed by a world-1 trainer on a one-rank subgroup, gathered and summed in rank
+     order): bit-equal at world 2 (a 2-term fp32 sum is order-free), <= 1e-6 relative above;
+  2. replicas stay bit-identical across ranks; the per-segment graph-captured path matches the
+     eager path bit for bit;
+  3. ZeRO-1 (reduce-scatter + sharded update + bf16 all-gather) matches plain data parallel.
   python -m dbx_distributed_pytorch_examples_amd.launch --nproc-per-node 2 tools/dist_gpu_check.py
 """
 import os
 import sys
 
 import torch
+import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig  # noqa: E402
@@ -17,35 +23,79 @@ from dbx_distributed_pytorch_examples_amd.models import build_model  # noqa: E40
 from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist  # noqa: E402
 from dbx_distributed_pytorch_examples_amd.utils import debug  # noqa: E402
 
+B = 16
 
-def run(use_graphs, zero=0, steps=4, bucket_mb=1.0):
+
+def batches(steps):
+    g = torch.Generator().manual_seed(100 + info.rank)
+    out = []
+    for _ in range(steps):
+        img = torch.randint(0, 256, (B, 32, 32, 3), dtype=torch.uint8, generator=g)
+        lab = torch.randint(0, 10, (B,), generator=g)
+        out.append((img.to(info.device), lab.to(info.device)))
+    return out
+
+
+def run(use_graphs, zero=0, steps=4, bucket_mb=1.0, pg=None, optim="sgd"):
     torch.manual_seed(0)
     m = build_model("resnet18", num_classes=10)
-    tr = NativeTrainer(m, 16, (32, 32), info.device, optim=OptimConfig(lr=0.05), use_graphs=use_graphs,
-                       bucket_cap_mb=bucket_mb, zero_stage=zero)
-    g = torch.Generator().manual_seed(100 + info.rank)
-    for _ in range(steps):
-        img = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, generator=g)
-        lab = torch.randint(0, 10, (16,), generator=g)
-        tr.step(img.to(info.device), lab.to(info.device))
+    opt = OptimConfig(lr=0.05) if optim == "sgd" else OptimConfig(name="adamw", lr=1e-3, weight_decay=0.01)
+    tr = NativeTrainer(m, B, (32, 32), info.device, optim=opt, use_graphs=use_graphs,
+                       bucket_cap_mb=bucket_mb, zero_stage=zero, process_group=pg)
+    for img, lab in batches(steps):
+        tr.step(img, lab)
     torch.cuda.synchronize()
-    loss, corr = tr.read_metrics()
-    return tr.prog.master.detach().clone(), loss
+    loss, _ = tr.read_metrics()
+    return tr, loss
 
 
 info = ddist.init_distributed()
-assert info.world_size == 2 or os.environ.get("DBX_FORCE_PG") == "1", info
-w_graph, loss = run(True)
+W = info.world_size
+assert W >= 2, info
+exact = W == 2
+
+# 1. DP gradient == sum of per-rank single-process gradients (one step, eager)
+singles = [dist.new_group([r]) for r in range(W)]
+tr_local, _ = run(False, steps=1, pg=singles[info.rank])
+assert tr_local.world == 1
+g_local = tr_local.prog.grad.detach().clone()
+del tr_local
+gathered = [torch.empty_like(g_local) for _ in range(W)]
+dist.all_gather(gathered, g_local)
+g_sum = gathered[0].clone()
+for t in gathered[1:]:
+    g_sum += t
+tr_dp, _ = run(False, steps=1)
+g_dp = tr_dp.prog.grad.detach().clone()
+del tr_dp
+relg = ((g_dp - g_sum).norm() / g_sum.norm()).item()
+assert (relg == 0.0) if exact else (relg < 1e-6), f"DP gradient != sum of per-rank gradients: {relg}"
+
+# 2. graphs vs eager, replicas in sync
+tr_g, loss = run(True)
+w_graph = tr_g.prog.master.detach().clone()
+del tr_g
 debug.assert_replicas_in_sync([w_graph], what="master weights (graphs)")
-w_eager, _ = run(False)
+tr_e, _ = run(False)
+w_eager = tr_e.prog.master.detach().clone()
+del tr_e
 debug.assert_replicas_in_sync([w_eager], what="master weights (eager)")
 rel = ((w_graph - w_eager).norm() / w_eager.norm()).item()
 assert rel == 0.0, f"graph vs eager mismatch {rel} (training is bit-reproducible: fp64 statistics atomics)"
-w_zero, _ = run(True, zero=1)
-debug.assert_replicas_in_sync([w_zero], what="master weights (ZeRO-1)")
-relz = ((w_zero - w_eager).norm() / w_eager.norm()).item()
-assert relz == 0.0, f"ZeRO-1 vs DP mismatch {relz}"
+
+# 3. ZeRO-1 == DP (SGD and AdamW)
+relz = {}
+for optim in ("sgd", "adamw"):
+    tr_z, _ = run(True, zero=1, optim=optim)
+    w_zero = tr_z.prog.master.detach().clone()
+    del tr_z
+    debug.assert_replicas_in_sync([w_zero], what=f"master weights (ZeRO-1 {optim})")
+    tr_d, _ = run(True, zero=0, optim=optim)
+    w_dp = tr_d.prog.master.detach().clone()
+    del tr_d
+    relz[optim] = ((w_zero - w_dp).norm() / w_dp.norm()).item()
+    assert (relz[optim] == 0.0) if exact else (relz[optim] < 1e-6), f"ZeRO-1 vs DP mismatch ({optim}) {relz[optim]}"
 if info.rank == 0:
-    print(f"dist_gpu_check OK: backend={info.backend} loss={loss:.3f} graph-vs-eager={rel:.2e} zero1-vs-dp={relz:.2e}",
-          flush=True)
+    print(f"dist_gpu_check OK: world={W} backend={info.backend} loss={loss:.3f} grad-vs-sum={relg:.2e} "
+          f"graph-vs-eager={rel:.2e} zero1-vs-dp sgd={relz['sgd']:.2e} adamw={relz['adamw']:.2e}", flush=True)
 ddist.destroy()
