@@ -55,6 +55,7 @@ int dbx_clip_factor(const double*, float, float*, hipStream_t);
 int dbx_normalize_u8(const unsigned char*, bf16*, const unsigned char*, int, int, int, int, float, float, float, float,
                      float, float, hipStream_t);
 int dbx_weight_prep(const float*, bf16*, const void*, int, hipStream_t);
+int dbx_weight_prep16(const bf16*, bf16*, const void*, int, hipStream_t);
 int dbx_augment_u8(const unsigned char*, bf16*, const float*, const unsigned char*, int, int, int, int, int, int, float,
                    float, float, float, float, float, hipStream_t);
 int dbx_cast_f32_bf16(const float*, bf16*, long long, hipStream_t);
@@ -273,6 +274,10 @@ PYBIND11_MODULE(_C, m) {
     check(dbx_augment_u8(P<const unsigned char*>(in), P<bf16*>(out), P<const float*>(boxes),
                          P<const unsigned char*>(flip), N, Hin, Win, Cin, Ho, Wo, m0, m1, m2, s0, s1, s2, S(st)),
           "augment_u8");
+  });
+  m.def("weight_prep16", [](uintptr_t src, uintptr_t wbuf, uintptr_t desc, int nlayers, uintptr_t st) {
+    check(dbx_weight_prep16(P<const bf16*>(src), P<bf16*>(wbuf), P<const void*>(desc), nlayers, S(st)),
+          "weight_prep16");
   });
   m.def("weight_prep", [](uintptr_t master, uintptr_t wbuf, uintptr_t desc, int nlayers, uintptr_t st) {
     check(dbx_weight_prep(P<const float*>(master), P<bf16*>(wbuf), P<const void*>(desc), nlayers, S(st)),

@@ -846,19 +846,23 @@ struct WDesc { long long src, fwd, tr; int K, RS, C, pad; };
 // blockIdx.y = layer. Layers with a dgrad copy (K, C multiples of 64) are processed in 64x64
 // (k, c) tiles per tap through LDS so both the KRSC and the transposed CRSK stores are
 // coalesced; the others (fc) are a plain vectorised cast.
-__global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restrict__ master, bf16* __restrict__ wbuf,
+// 4 consecutive source elements (fp32 master or, under ZeRO, the all-gathered bf16 copy) as bf16
+__device__ __forceinline__ bf16x4 load4_bf16(const float* p) {
+  const float4 v = *reinterpret_cast<const float4*>(p);
+  return bf16x4{(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+}
+__device__ __forceinline__ bf16x4 load4_bf16(const bf16* p) { return *reinterpret_cast<const bf16x4*>(p); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void weight_prep_kernel(const T* __restrict__ master, bf16* __restrict__ wbuf,
                                                           const WDesc* __restrict__ desc, int nlayers) {
   const WDesc d = desc[blockIdx.y];
   const int tid = threadIdx.x;
   if (d.tr < 0) {
     const long long n = (long long)d.K * d.RS * d.C;
     const long long n4 = n / 4;
-    const float4* m4 = reinterpret_cast<const float4*>(master + d.src);
-    for (long long i = (long long)blockIdx.x * 256 + tid; i < n4; i += (long long)gridDim.x * 256) {
-      const float4 v = m4[i];
-      const bf16x4 b = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
-      *reinterpret_cast<bf16x4*>(wbuf + d.fwd + 4 * i) = b;
-    }
+    for (long long i = (long long)blockIdx.x * 256 + tid; i < n4; i += (long long)gridDim.x * 256)
+      *reinterpret_cast<bf16x4*>(wbuf + d.fwd + 4 * i) = load4_bf16(master + d.src + 4 * i);
     for (long long i = 4 * n4 + (long long)blockIdx.x * 256 + tid; i < n; i += (long long)gridDim.x * 256)
       wbuf[d.fwd + i] = (bf16)master[d.src + i];
     return;
@@ -874,8 +878,7 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
     for (int p = 0; p < 4; ++p) {
       const int kr = p * 16 + (tid >> 4), cq = (tid & 15) * 4;
       const long long e = (long long)(k0 + kr) * rs + tap * d.C + c0 + cq;
-      const float4 v = *reinterpret_cast<const float4*>(master + d.src + e);
-      const bf16x4 b = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+      const bf16x4 b = load4_bf16(master + d.src + e);
       *reinterpret_cast<bf16x4*>(wbuf + d.fwd + e) = b;
       tile[kr][cq] = b[0]; tile[kr][cq + 1] = b[1]; tile[kr][cq + 2] = b[2]; tile[kr][cq + 3] = b[3];
     }
@@ -1082,7 +1085,13 @@ extern "C" int dbx_augment_u8(const unsigned char* in, bf16* out, const float* b
   RET_LAST;
 }
 extern "C" int dbx_weight_prep(const float* master, bf16* wbuf, const void* desc_dev, int nlayers, hipStream_t st) {
-  hipLaunchKernelGGL(weight_prep_kernel, dim3(512, nlayers), dim3(256), 0, st, master, wbuf, (const WDesc*)desc_dev, nlayers);
+  hipLaunchKernelGGL(weight_prep_kernel<float>, dim3(512, nlayers), dim3(256), 0, st, master, wbuf,
+                     (const WDesc*)desc_dev, nlayers);
+  RET_LAST;
+}
+extern "C" int dbx_weight_prep16(const bf16* src, bf16* wbuf, const void* desc_dev, int nlayers, hipStream_t st) {
+  hipLaunchKernelGGL(weight_prep_kernel<bf16>, dim3(512, nlayers), dim3(256), 0, st, src, wbuf,
+                     (const WDesc*)desc_dev, nlayers);
   RET_LAST;
 }
 extern "C" int dbx_cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t st) {

@@ -55,12 +55,17 @@ class NativeTrainer:
                  zero_stage: int = 0):
         self.dev = device
         optim = optim or OptimConfig()
-        self.prog = ResNetProgram(model, batch, image_hw, device, src_hw=src_hw, mean=mean, std=std)
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        if zero_stage and optim.name == "lars":
+            raise ValueError("LARS runs on the full flat buffer; use zero_stage=0")
+        # ZeRO: segment groups aligned to 16 x world elements (equal per-rank parts) and a flat bf16
+        # parameter copy (the all-gather target the weight preparation reads)
+        self.prog = ResNetProgram(model, batch, image_hw, device, src_hw=src_hw, mean=mean, std=std,
+                                  param_align=16 * self.world if zero_stage else 16, param16=bool(zero_stage))
         self.prog.build_backward()
         self.opt = optim
         self.smoothing = label_smoothing
-        self.pg = process_group
-        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         n = self.prog.n_params
         self.mom = torch.zeros(n, device=device)
         self.mom2 = torch.zeros(n, device=device) if optim.name in ("adam", "adamw") else None
@@ -90,41 +95,44 @@ class NativeTrainer:
             # (profiles/r2s2_multirank/). Weight gradients then run in order on the main stream.
             self.prog.overlap_wgrad = False
         self.flip = None
+        self.seg_ranges = self._segment_ranges()
         self.zero = None
         if zero_stage:
-            from ..parallel.zero import ZeroShardedOptimizer
-            self.zero = ZeroShardedOptimizer(self.prog.master, self.prog.grad, optim, stage=zero_stage,
-                                             process_group=process_group)
+            from ..parallel.zero import SegmentedZero
+            self.zero = SegmentedZero(self.prog, optim, self.seg_ranges, self.prog.bn_param_blocks(),
+                                      stage=zero_stage, process_group=process_group)
             self.mom = self.zero.m  # shard-sized optimizer state only
             self.mom2 = self.zero.v
-        self.lars = None
-        if optim.name == "lars":
-            if zero_stage:
-                raise ValueError("LARS runs on the full flat buffer; use zero_stage=0")
-            self.lars = self._lars_segments()
+        self.lars = self._lars_segments() if optim.name == "lars" else None
         self._build_phases()
         # broadcast initial parameters from rank 0 (DDP constructor semantics, M2)
         if self.world > 1:
-            dist.broadcast(self.prog.master, 0, group=process_group)
+            src = 0 if process_group is None else dist.get_global_rank(process_group, 0)
+            host_sync_for_gloo(self.prog.master, process_group)
+            dist.broadcast(self.prog.master, src, group=process_group)
             for bn in self.prog.bns:
-                dist.broadcast(bn.mod.running_mean, 0, group=process_group)
-                dist.broadcast(bn.mod.running_var, 0, group=process_group)
-        self._ar_bufs = {}
+                dist.broadcast(bn.mod.running_mean, src, group=process_group)
+                dist.broadcast(bn.mod.running_var, src, group=process_group)
+        if self.zero is not None:
+            self.zero.refresh_param16()
 
     # ----------------------------------------------------------------------------------
+    def _segment_ranges(self):
+        """Contiguous [lo, hi) of every backward segment's gradients (None: no parameters)."""
+        out = []
+        for rs in self.prog.segment_param_ranges():
+            if not rs:
+                out.append(None)
+                continue
+            out.append((min(r[1] for r in rs), max(r[1] + (r[2] + 15) // 16 * 16 for r in rs)))
+        return out
+
     def _build_phases(self):
+        """Phases = (name, fn, post): ``fn`` is graph-captured (no collectives); ``post`` is what the
+        multi-rank path issues on the comm stream after the phase -- a gradient range (all-reduce,
+        or ZeRO reduce-scatter) or a callable (ZeRO norm all-reduce / parameter all-gather)."""
         p = self.prog
         segs = p._segments
-        ranges = p.segment_param_ranges()
-        # contiguous [lo, hi) of every backward segment's gradients
-        self.seg_ranges = []
-        for rs in ranges:
-            if not rs:
-                self.seg_ranges.append(None)
-                continue
-            lo = min(r[1] for r in rs)
-            hi = max(r[1] + (r[2] + 15) // 16 * 16 for r in rs)
-            self.seg_ranges.append((lo, hi))
 
         def fwd_phase():
             p.prepare_weights()
@@ -140,7 +148,12 @@ class NativeTrainer:
             phases.append((name, fn, rg))
         if self.segmented:
             phases = self._merge_phases(phases)
-        phases.append(("optimizer", self._optimizer_phase, None))
+        z = self.zero
+        # ZeRO + clipping with collectives: the shard's sum of squares is all-reduced between phases
+        self._zero_norm_separate = z is not None and bool(self.opt.grad_clip) and self.segmented
+        if self._zero_norm_separate:
+            phases.append(("opt_norm", z.norm_phase, z.allreduce_norm))
+        phases.append(("optimizer", self._optimizer_phase, z.gather if z is not None else None))
         self.phases = phases
 
     def _merge_phases(self, phases):
@@ -152,7 +165,7 @@ class NativeTrainer:
         14.45k / 14.43k (profiles/r2s2_multirank/step_layout_ab.txt) -- boundaries are not what
         the segmented path cost: the wgrad side stream next to the comm streams was (now off in
         this mode, see __init__). The finer split (more overlap, smallest exposed tail) stays.
-        Groups merge only when their gradient ranges are adjacent."""
+        Groups merge only when their gradient ranges are disjoint and in order."""
         spec = os.environ.get("DBX_SEG_GROUPS", "")
         if not spec:
             return phases
@@ -165,7 +178,8 @@ class NativeTrainer:
             grp = phases[pos:pos + sz]
             pos += sz
             rgs = sorted(rg for _, _, rg in grp if rg is not None)
-            if any(a[1] != b[0] for a, b in zip(rgs, rgs[1:])):
+            # consecutive phases own consecutive parameter groups (at most alignment padding between)
+            if any(a[1] > b[0] for a, b in zip(rgs, rgs[1:])):
                 return phases  # non-adjacent gradient ranges: keep one segment per phase
             fns = [fn for _, fn, _ in grp]
             merged.append(("+".join(nm for nm, _, _ in grp),
@@ -188,12 +202,13 @@ class NativeTrainer:
     def _optimizer_phase(self):
         p, o = self.prog, self.opt
         if self.zero is not None:
-            # ZeRO-1/2: update this rank's shard of the flat master with its shard of the
-            # optimizer state, then all-gather the master (collective: runs eagerly, not captured
-            # at world > 1). lr / bias corrections come from the device-side hyper tensor so a
-            # captured world-1 step follows set_lr() and the step count on every replay.
-            self.zero.step(grads_already_reduced=(self.zero.stage == 1 or self.world == 1), lr=o.lr,
-                           hyper=self.hyper)
+            # ZeRO-1/2: update this rank's shard of the fp32 master with its shard of the optimizer
+            # state (the reduce-scatter and the all-gather run around this phase, not inside it:
+            # the phase is captured at every world size). lr / bias corrections come from the
+            # device-side hyper tensor so a replayed step follows set_lr() and the step count.
+            if o.grad_clip and not self._zero_norm_separate:
+                self.zero.norm_phase()
+            self.zero.update(hyper=self.hyper)
             return
         gsp = None
         if o.grad_clip and o.grad_clip > 0:
@@ -222,9 +237,17 @@ class NativeTrainer:
                         grad_scale_ptr=gsp, grad_scale=gscale, hyper=self.hyper)
 
     # ----------------------------------------------------------------------------------
+    def _post(self, post):
+        if post is None:
+            return
+        if callable(post):
+            post()
+        elif self.zero is not None:
+            self.zero.reduce_range(*post)
+        else:
+            self._allreduce_range(*post)
+
     def _allreduce_range(self, lo: int, hi: int):
-        if self.zero is not None and self.zero.stage >= 2:
-            return  # ZeRO-2: gradients are reduce-scattered by the optimizer phase instead
         g = self.prog.grad
         host_sync_for_gloo(g, self.pg)
         pos = lo
@@ -253,30 +276,34 @@ class NativeTrainer:
     def set_lr(self, lr: float):
         self.opt.lr = float(lr)
 
+    def _waits_comm(self, i: int, name: str) -> bool:
+        # the optimizer phases consume the reduced gradients / norm; the first phase of a step
+        # consumes the previous step's all-gathered parameters
+        return self.segmented and (i == 0 or name in ("optimizer", "opt_norm"))
+
     def _run_phases_eager(self):
-        if self.dev.type != "cuda":  # CPU (reference ops; gloo all-reduce, synchronous)
-            for name, fn, rg in self.phases:
+        if self.dev.type != "cuda":  # CPU (reference ops; gloo collectives, synchronous)
+            for name, fn, post in self.phases:
                 fn()
-                if rg is not None and self.segmented:
-                    self._allreduce_range(*rg)
+                if self.segmented:
+                    self._post(post)
             return
         cur = torch.cuda.current_stream(self.dev)
-        for name, fn, rg in self.phases:
-            if name == "optimizer" and self.segmented:
+        for i, (name, fn, post) in enumerate(self.phases):
+            if self._waits_comm(i, name):
                 cur.wait_stream(self.comm_stream)
             if self.phase_timer is not None:
                 with self.phase_timer.phase(name):
                     fn()
             else:
                 fn()
-            if rg is not None and self.segmented:
+            if post is not None and self.segmented:
                 self.comm_stream.wait_stream(cur)
                 with torch.cuda.stream(self.comm_stream):
-                    self._allreduce_range(*rg)
+                    self._post(post)
 
     def _graph_phases(self):
-        # the ZeRO optimizer phase issues collectives: keep it out of the captured graphs
-        return [ph for ph in self.phases if not (ph[0] == "optimizer" and self.zero is not None and self.world > 1)]
+        return self.phases
 
     def _capture(self):
         """Capture each phase (or the whole step when not segmented) into HIP graphs."""
@@ -310,17 +337,14 @@ class NativeTrainer:
         if not self.segmented:
             self.graphs[0].replay()
             return
-        for (name, _, rg), g in zip(self._graph_phases(), self.graphs):
-            if name == "optimizer":
+        for i, ((name, _, post), g) in enumerate(zip(self._graph_phases(), self.graphs)):
+            if self._waits_comm(i, name):
                 cur.wait_stream(self.comm_stream)
             g.replay()
-            if rg is not None:
+            if post is not None:
                 self.comm_stream.wait_stream(cur)
                 with torch.cuda.stream(self.comm_stream):
-                    self._allreduce_range(*rg)
-        if len(self.graphs) < len(self.phases):  # eager ZeRO optimizer phase
-            cur.wait_stream(self.comm_stream)
-            self._optimizer_phase()
+                    self._post(post)
 
     # ----------------------------------------------------------------------------------
     def step(self, images_u8: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
@@ -370,6 +394,8 @@ class NativeTrainer:
         A short final batch is padded (padding rows get label -> excluded by the caller)."""
         p = self.prog
         p.training = False
+        if self.comm_stream is not None:  # the last step's parameter all-gather (ZeRO)
+            torch.cuda.current_stream(self.dev).wait_stream(self.comm_stream)
         n = images_u8.shape[0]
         p.img_u8[:n].copy_(images_u8)
         p.labels[:n].copy_(labels)
@@ -381,6 +407,21 @@ class NativeTrainer:
         out = p.forward(smoothing=0.0, compute_grad=False, metrics=False)
         p.training = True
         return out[:n]
+
+    def sync_master(self) -> None:
+        """Make the module's fp32 parameters (views of the flat master) complete on every rank:
+        under ZeRO each rank only updates its shard (collective; call on all ranks before a
+        checkpoint / state_dict)."""
+        if self.zero is not None:
+            if self.dev.type == "cuda" and self.comm_stream is not None:
+                torch.cuda.current_stream(self.dev).wait_stream(self.comm_stream)
+            self.zero.gather_master()
+
+    def params_changed(self) -> None:
+        """Call after writing the parameters from outside (checkpoint load): ZeRO re-derives its
+        bf16 parameter copy from the (full) fp32 master."""
+        if self.zero is not None:
+            self.zero.refresh_param16()
 
     def read_metrics(self, reset: bool = True) -> Tuple[float, float]:
         m = self.prog.metrics[:2].tolist()

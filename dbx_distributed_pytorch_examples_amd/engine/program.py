@@ -122,9 +122,14 @@ class ResNetProgram:
     """Compile a ResNet nn.Module into a fixed-shape NHWC program for (batch, H, W)."""
 
     def __init__(self, model: nn.Module, batch: int, image_hw: Tuple[int, int], device: torch.device,
-                 src_hw: Optional[Tuple[int, int]] = None, mean=None, std=None):
+                 src_hw: Optional[Tuple[int, int]] = None, mean=None, std=None, param_align: int = 16,
+                 param16: bool = False):
         """``image_hw``: network input size; ``src_hw``: size of the uint8 images handed in
-        (crop/resize to image_hw happens on the GPU, ``augment_u8``); default = image_hw."""
+        (crop/resize to image_hw happens on the GPU, ``augment_u8``); default = image_hw.
+        ``param_align``: every backward segment's parameter group starts on a multiple of this many
+        elements (ZeRO: 16 x world, so a segment splits into equal per-rank parts); ``param16``:
+        keep a flat bf16 copy of the parameters (``self.param16``, ZeRO's all-gather target) and
+        derive the compute weights from it instead of from the fp32 master."""
         if not supports(model):
             raise TypeError(f"ResNetProgram does not support {type(model).__name__}")
         self.model = model
@@ -167,6 +172,8 @@ class ResNetProgram:
         self.fuse_stem_bwd = os.environ.get("DBX_FUSE_STEM_BWD", "0") == "1"
         self._wstream = None
         self._side_pending = False
+        self.param_align = max(16, int(param_align))
+        self._want_param16 = param16
         self._build_layers()
         self._alloc_params()
         self._alloc_activations()
@@ -255,12 +262,26 @@ class ResNetProgram:
         entries.append(("fc_w", self.fc, "weight", self.fc.weight.numel()))
         entries.append(("fc_b", self.fc, "bias", self.fc.bias.numel()))
         assert len(entries) == len(self.convs) + 2 * len(self.bns) + 2, "parameter grouping lost a tensor"
-        # 16-element alignment of every tensor (vectorised kernels, 64-B bucket edges)
+        # 16-element alignment of every tensor (vectorised kernels, 64-B bucket edges); every
+        # backward segment's group (stem | layer1..4 | fc) starts on a multiple of param_align
+        A = self.param_align
+        group_of = []  # group index per entry (fc: its own group: the "head" backward segment)
+        for gi, pre in enumerate(groups):
+            for cv in self.convs:
+                if cv.name.startswith(pre) or (cv.stem and "conv1." in pre):
+                    group_of.append(gi)
+            for bn in self.bns:
+                if bn.name.startswith(pre) or (bn is self.stem_bn and "bn1." in pre):
+                    group_of += [gi, gi]
+        group_of += [len(groups), len(groups)]
         total = 0
         offs = []
-        for e in entries:
+        for i, e in enumerate(entries):
+            if i > 0 and group_of[i] != group_of[i - 1]:
+                total = (total + A - 1) // A * A
             offs.append(total)
             total += (e[3] + 15) // 16 * 16
+        total = (total + A - 1) // A * A
         self.n_params = total
         self.master = torch.zeros(total, device=dev, dtype=torch.float32)
         self.grad = torch.zeros(total, device=dev, dtype=torch.float32)
@@ -309,6 +330,7 @@ class ResNetProgram:
                     else:
                         self.fc_b_off, self.fc_b_grad = off, self.grad[off:off + n]
                     self.param_ranges.append((f"fc.{attr}", off, n))
+        self.param16 = torch.zeros(total, device=dev, dtype=torch.bfloat16) if self._want_param16 else None
         self.nbt = torch.tensor(nbt_vals, dtype=torch.int64, device=dev)
         for i, mod in enumerate(nbt_mods):
             mod.num_batches_tracked.data = self.nbt[i]
@@ -436,12 +458,25 @@ class ResNetProgram:
     # ----------------------------------------------------------------------------------
     def prepare_weights(self):
         """fp32 master -> bf16 compute copies (KRSC fwd, CRSK dgrad, fc, stem 8x8x4)."""
-        K.weight_prep(self.master, self.w16buf, self.wdesc, self.n_wdesc)
+        src = self.master if self.param16 is None else self.param16  # ZeRO: the all-gathered bf16 copy
+        K.weight_prep(src, self.w16buf, self.wdesc, self.n_wdesc)
         st = self.stem
-        w = self.master[st.off:st.off + st.numel].view(st.OC, st.R, st.S, st.IC)
+        w = src[st.off:st.off + st.numel].view(st.OC, st.R, st.S, st.IC)
         stem16 = st.w16.view(st.OC, 8, 8, 4)
         stem16[:, :st.R, :st.S, :st.IC].copy_(w)
-        self.fc_b16.copy_(self.fc.bias.detach())
+        self.fc_b16.copy_(src[self.fc_b_off:self.fc_b_off + self.num_classes])
+
+    def bn_param_blocks(self) -> List[Tuple[int, int]]:
+        """Contiguous [lo, hi) blocks of the flat buffer holding BatchNorm affine parameters (read in
+        fp32 by the BN kernels), merged where adjacent."""
+        rs = sorted((o, o + (bn.C + 15) // 16 * 16) for bn in self.bns for o in (bn.off_w, bn.off_b))
+        out: List[Tuple[int, int]] = []
+        for lo, hi in rs:
+            if out and out[-1][1] == lo:
+                out[-1] = (out[-1][0], hi)
+            else:
+                out.append((lo, hi))
+        return out
 
     def load_input_u8(self, flip: Optional[torch.Tensor] = None):
         """uint8 images (+ per-sample crop boxes / flips in self.boxes / self.flip) -> bf16 NHWC4."""

@@ -811,6 +811,21 @@ def global_norm_clip_factor(g, max_norm, work):
 
 
 @_dispatch
+def sumsq_accum(g, work):
+    """work[0:2] (viewed as one fp64) += sum of squares of the fp32 tensor ``g`` (no zeroing)."""
+    _chk(g, torch.float32, "g")
+    _chk(work, torch.float32, "work")
+    C().sumsq(g.data_ptr(), g.numel(), work.data_ptr(), stream_ptr())
+
+
+@_dispatch
+def clip_factor(work, max_norm):
+    """work[2:4] = (min(1, max_norm / (norm + 1e-6)), norm) from the fp64 sum of squares in work[0:2]."""
+    C().clip_factor(work.data_ptr(), float(max_norm), work[2:].data_ptr(), stream_ptr())
+    return work[2:3]
+
+
+@_dispatch
 def normalize_u8(img, out, mean, std, flip=None):
     N, H, W, Cin = img.shape
     _chk(img, torch.uint8, "img")
@@ -839,7 +854,12 @@ def augment_u8(img, out, boxes, mean, std, flip=None):
 
 @_dispatch
 def weight_prep(master, wbuf, desc_dev, nlayers):
-    C().weight_prep(master.data_ptr(), wbuf.data_ptr(), desc_dev.data_ptr(), nlayers, stream_ptr())
+    """bf16 forward (KRSC) and dgrad (CRSK) weight copies from the flat fp32 master -- or from a
+    flat bf16 parameter copy of the same layout (ZeRO: the all-gathered ``param16``)."""
+    if master.dtype == torch.bfloat16:
+        C().weight_prep16(master.data_ptr(), wbuf.data_ptr(), desc_dev.data_ptr(), nlayers, stream_ptr())
+    else:
+        C().weight_prep(master.data_ptr(), wbuf.data_ptr(), desc_dev.data_ptr(), nlayers, stream_ptr())
 
 
 @_dispatch

@@ -399,6 +399,18 @@ def global_norm_clip_factor(g, max_norm, work):
     return work[2:3]
 
 
+def sumsq_accum(g, work):
+    w = work[0:2].view(torch.float64)
+    w += (g.double() ** 2).sum()
+
+
+def clip_factor(work, max_norm):
+    nrm = torch.sqrt(work[0:2].view(torch.float64)[0]).float()
+    work[2] = torch.clamp(max_norm / (nrm + 1e-6), max=1.0)
+    work[3] = nrm
+    return work[2:3]
+
+
 def normalize_u8(img, out, mean, std, flip=None):
     N, H, W, Cin = img.shape
     f = img.float() / 255.0
@@ -447,7 +459,7 @@ def weight_prep(master, wbuf, desc_dev, nlayers):
         src, fwd, tr = (int(x) for x in row[:6].view(torch.int64))
         k, rs, c = int(row[6]), int(row[7]), int(row[8])
         n = k * rs * c
-        w = master[src:src + n]
+        w = master[src:src + n].float()
         if fwd >= 0:
             wbuf[fwd:fwd + n].copy_(w.bfloat16())
         if tr >= 0:

@@ -1,24 +1,33 @@
-"""ZeRO-1 / ZeRO-2 sharded optimizer over flat fp32 buffers.
+"""ZeRO-1 / ZeRO-2 sharded optimizers over flat fp32 buffers.
 
 The reference ships DeepSpeed ZeRO configs (`/root/reference/02_deepspeed/deepspeed_config.py:53-105`:
 stage 1 with ``overlap_comm``, ``contiguous_gradients``, ``reduce_scatter`` and 5e8 buckets; stage
 2; stage 3; stage 3 + CPU offload) but never passes them to DeepSpeed. Here
-they are real:
+they are real, with DeepSpeed's communication pattern:
 
-* **stage 1** — gradients all-reduced as in DDP (bucketed, overlapped), then each rank updates
-  only ITS contiguous 1/world shard of the flat master with its shard of the optimizer state
-  (momentum / Adam moments), then the shards are all-gathered back into the full master;
-* **stage 2** — gradients are reduce-scattered instead (each rank only ever holds the summed
-  gradient of its own shard), then the same shard update + all-gather.
+* :class:`SegmentedZero` (the native ResNet program, ``NativeTrainer(zero_stage=1|2)``):
+  - each backward segment's gradient range (head | layer4 | layer3 | layer2 | layer1 | stem,
+    padded so it splits into ``world`` equal parts) is **reduce-scattered** on the comm stream
+    as soon as that segment's backward graph has run, overlapped with the remaining backward
+    (``overlap_comm`` + ``reduce_scatter``); rank r receives the summed gradient of part r of
+    every segment -- its shard;
+  - the fused AdamW / SGD kernel updates only the shard of the fp32 master with the
+    shard-sized optimizer state, and writes the updated shard as **bf16** into a staging buffer;
+  - one **bf16 all-gather** per segment rebuilds the full bf16 parameter copy (``prog.param16``)
+    the next forward's weight preparation reads; the fp32 BatchNorm affine parameters (consumed
+    in fp32 by the BN kernels) are exchanged exactly in fp32 (~0.2 % of the parameters).
 
-Both are bit-compatible with plain data parallel + the same optimizer (tests/test_dist_cpu.py).
-Stage 3 (parameter sharding) and CPU offload live in ``parallel/fsdp.py`` (the training engine
-routes ``zero.stage=3`` / ``offload_*`` there). This flat-buffer optimizer serves the native ResNet
-program, whose captured HIP graph needs resident full parameters: asked for stage 3 directly it
-runs stage 2 with a warning (ResNet-50's 102 MB of fp32 params fit 288 GB of HBM ~2800 times).
+  Per step each rank sends (w-1)/w x (4 + 2) bytes per parameter (fp32 reduce-scatter + bf16
+  all-gather) instead of 2 (w-1)/w x 4 for a data-parallel all-reduce followed by an fp32
+  parameter all-gather. No collective is captured: the update runs inside the step's HIP graph
+  at any world size, the collectives are issued between graph replays. Stages 1 and 2 have the
+  same traffic here (the program's flat gradient buffer is resident either way; ResNet-50's
+  102 MB of fp32 gradients are nothing against 288 GB of HBM).
+* :class:`ZeroShardedOptimizer` (generic flat buffers, the autograd engine): stage 1 slices the
+  already all-reduced gradient, stage 2 reduce-scatters it; same shard update + all-gather.
 
-The shard update runs the fused HIP optimizer kernels (ops.kernels.sgd_step / adam_step) on GPU
-and their PyTorch references on CPU.
+Both are bit-compatible with plain data parallel + the same optimizer (tests/test_dist_cpu.py,
+tools/dist_gpu_check.py). Stage 3 (parameter sharding) and CPU offload live in ``parallel/fsdp.py``.
 """
 from __future__ import annotations
 
@@ -77,6 +86,8 @@ class ZeroShardedOptimizer:
         self._gshard = torch.zeros(per, device=dev)
         self._pshard = torch.zeros(per, device=dev)
         self._clip = torch.zeros(4, device=dev)
+        # padded full-length staging (reduce-scatter input / all-gather output): allocated once
+        self._full = torch.zeros(self.padded, device=dev) if (self.world > 1 and self.padded != n) else None
 
     def shard_of(self, t: torch.Tensor) -> torch.Tensor:
         return t[self.lo:self.hi]
@@ -84,9 +95,8 @@ class ZeroShardedOptimizer:
     def _padded_view(self, t: torch.Tensor) -> torch.Tensor:
         if t.numel() == self.padded:
             return t
-        out = torch.zeros(self.padded, device=t.device, dtype=t.dtype)
-        out[:t.numel()].copy_(t)
-        return out
+        self._full[:t.numel()].copy_(t)  # the pad tail stays zero
+        return self._full
 
     @torch.no_grad()
     def step(self, grads_already_reduced: bool = True, lr: Optional[float] = None,
@@ -138,10 +148,11 @@ class ZeroShardedOptimizer:
         if self.world == 1:
             self.master[self.lo:self.hi].copy_(p[:n_own])
             return
-        full = torch.empty(self.padded, device=p.device, dtype=p.dtype)
+        full = self.master if self._full is None else self._full
         host_sync_for_gloo(p, self.pg)
         dist.all_gather_into_tensor(full, p, group=self.pg)
-        self.master.copy_(full[:self.master.numel()])
+        if full is not self.master:
+            self.master.copy_(full[:self.master.numel()])
 
     def state_dict(self):
         return {"stage": self.stage, "step": self.step_count, "rank": self.rank, "world": self.world,
@@ -150,6 +161,184 @@ class ZeroShardedOptimizer:
     def load_state_dict(self, sd):
         if sd["world"] != self.world:
             raise ValueError("ZeRO optimizer state was saved with a different world size")
+        self.step_count = sd["step"]
+        self.m.copy_(sd["m"])
+        if self.v is not None and sd["v"] is not None:
+            self.v.copy_(sd["v"])
+
+
+# ================================================================================================
+# ZeRO for the native ResNet program: per-segment reduce-scatter, sharded update, bf16 all-gather
+# ================================================================================================
+def _reduce_scatter_sum(out: torch.Tensor, inp: torch.Tensor, rank: int, pg) -> None:
+    """out = (sum over ranks of inp)[rank part]; gloo has no reduce-scatter: all-reduce + slice."""
+    host_sync_for_gloo(inp, pg)
+    if dist.get_backend(pg) == "gloo":
+        dist.all_reduce(inp, group=pg)
+        out.copy_(inp[rank * out.numel():(rank + 1) * out.numel()])
+    else:
+        dist.reduce_scatter_tensor(out, inp, group=pg)
+
+
+class SegmentedZero:
+    """ZeRO-1/2 over a ResNetProgram's flat buffers (see the module docstring).
+
+    ``seg_ranges``: the [lo, hi) gradient range of every backward segment; each must start on a
+    multiple of ``align = 16 * world`` (``ResNetProgram(param_align=...)`` pads the flat layout
+    so) and is extended to the next such multiple. ``bn_ranges``: [lo, hi) blocks of fp32
+    parameters that must stay exact (the BatchNorm affines)."""
+
+    def __init__(self, prog, optim, seg_ranges, bn_ranges, stage: int = 1, process_group=None):
+        if optim.name not in ("sgd", "adam", "adamw"):
+            raise ValueError(f"sharded optimizer supports sgd / adam / adamw, not {optim.name!r}")
+        if stage == 3:
+            warnings.warn("native program: ZeRO stage 3 runs as stage 2 (the captured graph needs resident "
+                          "parameters; parameter sharding is parallel.fsdp.ShardedDataParallel)")
+            stage = 2
+        self.stage = stage
+        self.prog, self.o, self.pg = prog, optim, process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        W, r = self.world, self.rank
+        align = 16 * W
+        dev = prog.master.device
+        self.parts = []  # (lo, hi, per, own_lo, shard_off)
+        off = 0
+        for rg in seg_ranges:
+            if rg is None:
+                continue
+            lo, hi = rg
+            hi = (hi + align - 1) // align * align
+            if lo % align or hi > prog.master.numel():
+                raise ValueError(f"segment range {rg} not aligned to {align} (build the program with param_align)")
+            per = (hi - lo) // W
+            self.parts.append((lo, hi, per, lo + r * per, off))
+            off += per
+        self.parts.sort()
+        for a, b in zip(self.parts, self.parts[1:]):
+            if a[1] > b[0]:
+                raise ValueError("overlapping segment ranges")
+        self.shard_n = off
+        self.m = torch.zeros(off, device=dev)
+        self.v = torch.zeros(off, device=dev) if optim.name in ("adam", "adamw") else None
+        self.gsh = torch.zeros(off, device=dev) if W > 1 else None          # reduce-scatter output
+        self.p16sh = torch.zeros(off, device=dev, dtype=torch.bfloat16) if W > 1 else None  # all-gather input
+        self.param16 = prog.param16
+        self.work = torch.zeros(4, device=dev)  # [0:2] fp64 sum of squares, [2] clip factor, [3] norm
+        self.step_count = 0
+        # exact fp32 exchange of the BN affine blocks: this rank's pieces summed with zeros elsewhere
+        self.bn_ranges = [tuple(b) for b in bn_ranges]
+        nbn = sum(hi - lo for lo, hi in self.bn_ranges)
+        self.bnbuf = torch.zeros(max(1, nbn), device=dev) if W > 1 else None
+        self._bn_own = []  # (buf_off, master_lo, length) of the owned pieces
+        bo = 0
+        for lo, hi in self.bn_ranges:
+            for (_, _, per, own, _) in self.parts:
+                a, b = max(lo, own), min(hi, own + per)
+                if a < b:
+                    self._bn_own.append((bo + a - lo, a, b - a))
+            bo += hi - lo
+        self.bytes_per_step = int(sum((hi - lo) * (W - 1) / W * (4 + 2) for (lo, hi, *_ ) in self.parts) + 8 * nbn) \
+            if W > 1 else 0
+
+    # ---- helpers ------------------------------------------------------------------------
+    def _gpart(self, part):
+        lo, hi, per, own, so = part
+        return self.prog.grad[own:own + per] if self.world == 1 else self.gsh[so:so + per]
+
+    def refresh_param16(self) -> None:
+        """bf16 copy of the FULL fp32 master (every rank holds it: after the constructor broadcast
+        or a checkpoint load)."""
+        from ..ops import kernels as K
+        K.cast_f32_bf16(self.prog.master, self.param16)
+
+    # ---- collectives (issued between graph replays, on the comm stream) -------------------
+    def reduce_range(self, lo: int, hi: int) -> None:
+        """Reduce-scatter every part inside the backward range [lo, hi)."""
+        if self.world == 1:
+            return
+        for part in self.parts:
+            plo, phi, per, own, so = part
+            if lo <= plo < hi:
+                _reduce_scatter_sum(self.gsh[so:so + per], self.prog.grad[plo:phi], self.rank, self.pg)
+
+    def allreduce_norm(self) -> None:
+        if self.world > 1:
+            s = self.work[0:2].view(torch.float64)
+            host_sync_for_gloo(s, self.pg)
+            dist.all_reduce(s, group=self.pg)
+
+    def gather(self) -> None:
+        """bf16 all-gather of the updated shards into param16; exact fp32 exchange of the BN blocks."""
+        if self.world == 1:
+            return
+        host_sync_for_gloo(self.p16sh, self.pg)
+        for (lo, hi, per, own, so) in self.parts:
+            dist.all_gather_into_tensor(self.param16[lo:hi], self.p16sh[so:so + per], group=self.pg)
+        if self.bn_ranges:  # every rank joins, owner of a BN piece or not
+            self.bnbuf.zero_()
+            for bo, ml, n in self._bn_own:
+                self.bnbuf[bo:bo + n].copy_(self.prog.master[ml:ml + n])
+            host_sync_for_gloo(self.bnbuf, self.pg)
+            dist.all_reduce(self.bnbuf, group=self.pg)
+            bo = 0
+            for lo, hi in self.bn_ranges:
+                self.prog.master[lo:hi].copy_(self.bnbuf[bo:bo + hi - lo])
+                bo += hi - lo
+
+    @torch.no_grad()
+    def gather_master(self) -> None:
+        """Full fp32 master on every rank (collective; before checkpoints / state_dict)."""
+        if self.world == 1:
+            return
+        m = self.prog.master
+        host_sync_for_gloo(m, self.pg)
+        for (lo, hi, per, own, so) in self.parts:
+            buf = torch.empty(hi - lo, device=m.device)
+            dist.all_gather_into_tensor(buf, m[own:own + per].contiguous(), group=self.pg)
+            m[lo:hi].copy_(buf)
+
+    # ---- graph-capturable compute -------------------------------------------------------------
+    def norm_phase(self) -> None:
+        """Local sum of squares of this rank's gradient shard (global-norm clipping)."""
+        from ..ops import kernels as K
+        self.work.zero_()
+        for part in self.parts:
+            K.sumsq_accum(self._gpart(part), self.work)
+
+    def update(self, hyper=None, lr=None) -> None:
+        """Shard update (fused kernels), writing the bf16 shard for the all-gather (world 1: the
+        full bf16 copy directly). Clipping: ``norm_phase`` (+ ``allreduce_norm``) ran before."""
+        from ..ops import kernels as K
+        o, W = self.o, self.world
+        gs = 1.0 / W
+        gsp = None
+        if getattr(o, "grad_clip", 0.0):
+            gsp = K.clip_factor(self.work, o.grad_clip * W)  # gradients are sums over ranks
+        lr = o.lr if lr is None else lr
+        for part in self.parts:
+            lo, hi, per, own, so = part
+            p = self.prog.master[own:own + per]
+            g = self._gpart(part)
+            p16 = self.param16[own:own + per] if W == 1 else self.p16sh[so:so + per]
+            m = self.m[so:so + per]
+            if o.name == "sgd":
+                K.sgd_step(p, g, m, p16, lr=lr, momentum=o.momentum, dampening=getattr(o, "dampening", 0.0),
+                           weight_decay=o.weight_decay, nesterov=o.nesterov, first=False, grad_scale_ptr=gsp,
+                           grad_scale=gs, hyper=hyper)
+            else:
+                K.adam_step(p, g, m, self.v[so:so + per], p16, lr=lr, beta1=o.betas[0], beta2=o.betas[1], eps=o.eps,
+                            weight_decay=o.weight_decay, decoupled=(o.name == "adamw"), step=max(1, self.step_count),
+                            grad_scale_ptr=gsp, grad_scale=gs, hyper=hyper)
+
+    def state_dict(self):
+        return {"stage": self.stage, "step": self.step_count, "rank": self.rank, "world": self.world,
+                "layout": [p[:3] for p in self.parts],
+                "m": self.m.cpu(), "v": None if self.v is None else self.v.cpu()}
+
+    def load_state_dict(self, sd):
+        if sd["world"] != self.world or [tuple(x) for x in sd.get("layout", [])] != [p[:3] for p in self.parts]:
+            raise ValueError("ZeRO optimizer state was saved with a different world size / shard layout")
         self.step_count = sd["step"]
         self.m.copy_(sd["m"])
         if self.v is not None and sd["v"] is not None:

@@ -319,6 +319,7 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
         if path:
             st = torch.load(path, map_location="cpu", weights_only=True)
             model.load_state_dict(st["model"])
+            _params_changed(runner)
             _restore_trainer_state(runner, st.get("trainer"))
             start_epoch, step = int(st.get("epoch", 0)), int(st.get("step", 0))
             _restore_shard_state(runner, cfg.checkpoint_dir, start_epoch)
@@ -327,6 +328,7 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
     elif cfg.resume and cfg.resume != "latest":
         st = torch.load(cfg.resume, map_location="cpu", weights_only=True)
         model.load_state_dict(st["model"])
+        _params_changed(runner)
     # --- mlflow ------------------------------------------------------------------------------
     is_main = ddist.get_rank() == 0
     if is_main and log_mlflow:
@@ -375,6 +377,7 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
         for cb in callbacks or []:
             cb(epoch + 1, rec, runner)
         if cfg.checkpoint_dir and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
+            _sync_master(runner)  # every rank (collective): ZeRO shards -> full fp32 parameters
             _save_shard_state(runner, cfg.checkpoint_dir, epoch + 1)  # every rank: its ZeRO shard
         if cfg.checkpoint_dir and is_main and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
             ckpt.save_checkpoint(cfg.checkpoint_dir, runner.model, None, epoch + 1, step=step,
@@ -396,6 +399,7 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
     if torch.cuda.is_available() and dev.type == "cuda":
         torch.cuda.synchronize()
     el = time.perf_counter() - t_start
+    _sync_master(runner)  # the returned / logged model holds the full parameters on every rank
     res.steps = step
     res.images_per_sec = imgs / el if el > 0 else 0.0
     res.model = runner.model
@@ -405,6 +409,18 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
         mlflow.log_dict({"history": res.history}, "training_history.json")
         mlflow.end_run()
     return res
+
+
+def _sync_master(runner) -> None:
+    f = getattr(runner.tr, "sync_master", None)
+    if f is not None:
+        f()
+
+
+def _params_changed(runner) -> None:
+    f = getattr(runner.tr, "params_changed", None)
+    if f is not None:
+        f()
 
 
 def _trainer_state(runner) -> Dict[str, Any]:

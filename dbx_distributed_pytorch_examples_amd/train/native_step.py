@@ -32,7 +32,11 @@ def build_native_step(args, info):
     def step():
         tr.step()
 
-    return step, {"memory_format": "nhwc", "graphs": use_graphs,
+    extra = {}
+    if tr.zero is not None:
+        extra["zero"] = (f"ZeRO-{tr.zero.stage}: per-segment fp32 reduce-scatter (overlapped with backward), sharded "
+                         f"{opt.name} update, bf16 all-gather; {tr.zero.bytes_per_step / 2**20:.1f} MiB sent/rank/step")
+    return step, {**extra, "memory_format": "nhwc", "graphs": use_graphs,
                   "ddp": (f"flat-bucket {'RCCL' if info.backend == 'nccl' else info.backend} all-reduce, "
                           f"{tr.bucket_cap * 4 >> 20} MiB chunks, "
                           f"{str(ar_dtype).split('.')[-1]}, overlapped per backward segment") if tr.world > 1 else "none",

@@ -383,3 +383,42 @@ def test_native_module_broadcast_overlap_and_short_batch_two_ranks():
     assert init_same, "rank 0's parameters were not broadcast at construction"
     assert grad_is_mean, "overlapped per-segment all-reduce != mean of per-rank gradients"
     assert short_synced, "short-batch fallback left the replicas' gradients different"
+
+
+def _native_zero_vs_dp(optim, clip):
+    """NativeTrainer ZeRO-1 (per-segment reduce-scatter, sharded update, bf16 all-gather + exact fp32 BN
+    exchange) against plain data parallel: the full fp32 parameters after 3 steps must be identical."""
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
+    info = ddist.init_distributed(device="cpu")
+    out, nbytes, shard = {}, 0, 0
+    for z in (0, 1):
+        torch.manual_seed(0)
+        m = build_model("resnet18", num_classes=10)
+        o = OptimConfig(lr=0.05, grad_clip=clip) if optim == "sgd" else \
+            OptimConfig(name="adamw", lr=1e-3, weight_decay=0.01, grad_clip=clip)
+        tr = NativeTrainer(m, 4, (32, 32), torch.device("cpu"), optim=o, zero_stage=z)
+        g = torch.Generator().manual_seed(7 + info.rank)
+        for _ in range(3):
+            tr.step(torch.randint(0, 256, (4, 32, 32, 3), dtype=torch.uint8, generator=g),
+                    torch.randint(0, 10, (4,), generator=g))
+        tr.sync_master()
+        out[z] = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+        if z:
+            nbytes, shard = tr.zero.bytes_per_step, tr.zero.m.numel()
+    ddist.destroy()
+    rel = ((out[0] - out[1]).norm() / out[0].norm()).item()
+    return torch.equal(out[0], out[1]), rel, nbytes, shard, out[0].numel()
+
+
+@pytest.mark.parametrize("world,optim,clip", [(2, "sgd", 0.0), (2, "adamw", 0.3), (4, "adamw", 0.0)])
+def test_native_zero1_matches_dp(world, optim, clip):
+    equal, rel, nbytes, shard, n = Launcher(world, use_gpu=False).run(_native_zero_vs_dp, optim, clip)
+    if world == 2:  # a two-term fp32 sum does not depend on the collective's reduction order
+        assert equal, f"ZeRO-1 parameters differ from data parallel (rel {rel})"
+    else:  # reduce-scatter vs all-reduce may sum the 4 ranks in another order: last-bit differences
+        assert rel < 1e-6, rel
+    assert shard <= n // world + 16 * world * 6  # optimizer state is sharded
+    # reduce-scatter fp32 + all-gather bf16: ~ (w-1)/w * 6 bytes per parameter (DDP all-reduce alone: 8)
+    assert nbytes < (world - 1) / world * 6.2 * n
