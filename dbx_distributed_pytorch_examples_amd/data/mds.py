@@ -18,8 +18,10 @@ Compression (``compression='gz' | 'gz:<level>' | 'bz2' | 'zstd[:<level>]'``): as
 a compressed shard is stored as ``zip_data`` (``shard.00000.mds.gz`` ...) next to the uncompressed
 ``raw_data`` description; the reader decompresses it once into its ``local`` directory and then
 memory-maps the raw shard (the C++ assembler always reads raw shards). ``gz`` / ``bz2`` use the
-standard library; ``zstd`` needs the ``zstandard`` module, absent here: the writer then falls back to
-uncompressed shards with a warning and the reader raises a clear error for zstd shards it cannot open.
+standard library; ``zstd`` (the reference's choice, `03a…:195`) goes through the system ``libzstd.so.1``
+loaded with ctypes (``ZSTD_compress`` / ``ZSTD_decompress``, GIL released during the call) or the
+``zstandard`` module when that is installed; only when neither exists does the writer fall back to
+uncompressed shards (with a warning) and the reader raise a clear error for the zstd shards.
 Raw ``pil`` pixels are what the native loader wants anyway (no image decode at all). Parity with
 mosaicml-streaming's own reader is "unpinned" (not installed); tests pin the format round-trip
 (tests/test_data.py).
@@ -127,6 +129,65 @@ def _fixed_size(enc: str) -> Optional[int]:
 # ---------------------------------------------------------------------------------------
 # compression codecs (mosaicml-streaming names: "gz", "gz:6", "bz2", "zstd", "zstd:7")
 # ---------------------------------------------------------------------------------------
+class _LibZstd:
+    """The zstd frame format through the system library (ctypes; no headers / package needed)."""
+    _UNKNOWN, _ERROR = (1 << 64) - 1, (1 << 64) - 2  # ZSTD_CONTENTSIZE_UNKNOWN / _ERROR
+
+    def __init__(self, lib):
+        import ctypes as C
+        self.C, self.lib = C, lib
+        sz, vp, cp = C.c_size_t, C.c_void_p, C.c_char_p
+        lib.ZSTD_compressBound.restype, lib.ZSTD_compressBound.argtypes = sz, [sz]
+        lib.ZSTD_compress.restype, lib.ZSTD_compress.argtypes = sz, [vp, sz, vp, sz, C.c_int]
+        lib.ZSTD_decompress.restype, lib.ZSTD_decompress.argtypes = sz, [vp, sz, vp, sz]
+        lib.ZSTD_getFrameContentSize.restype, lib.ZSTD_getFrameContentSize.argtypes = C.c_ulonglong, [vp, sz]
+        lib.ZSTD_isError.restype, lib.ZSTD_isError.argtypes = C.c_uint, [sz]
+        lib.ZSTD_getErrorName.restype, lib.ZSTD_getErrorName.argtypes = cp, [sz]
+
+    def _check(self, r: int, what: str) -> int:
+        if self.lib.ZSTD_isError(r):
+            raise RuntimeError(f"zstd {what}: {self.lib.ZSTD_getErrorName(r).decode()}")
+        return r
+
+    def compress(self, data: bytes, level: int = 3) -> bytes:
+        cap = self.lib.ZSTD_compressBound(len(data))
+        out = self.C.create_string_buffer(cap)
+        n = self._check(self.lib.ZSTD_compress(out, cap, data, len(data), int(level)), "compress")
+        return out.raw[:n]
+
+    def decompress(self, data: bytes, size: Optional[int] = None) -> bytes:
+        fs = self.lib.ZSTD_getFrameContentSize(data, len(data))
+        if fs == self._ERROR:
+            raise RuntimeError("zstd decompress: not a zstd frame")
+        if fs == self._UNKNOWN:
+            if size is None:
+                raise RuntimeError("zstd decompress: frame without a content size and no size hint")
+            fs = size
+        out = self.C.create_string_buffer(max(1, fs))
+        n = self._check(self.lib.ZSTD_decompress(out, fs, data, len(data)), "decompress")
+        return out.raw[:n]
+
+
+_ZSTD: Any = False
+
+
+def _libzstd() -> Optional[_LibZstd]:
+    global _ZSTD
+    if _ZSTD is False:
+        _ZSTD = None
+        import ctypes
+        import ctypes.util
+        for name in ("libzstd.so.1", ctypes.util.find_library("zstd") or ""):
+            if not name:
+                continue
+            try:
+                _ZSTD = _LibZstd(ctypes.CDLL(name))
+                break
+            except (OSError, AttributeError):
+                continue
+    return _ZSTD
+
+
 def _codec(spec: str, decoder: bool = False):
     """-> (compress fn, file extension), or (extension, decompress fn) with ``decoder=True``."""
     algo, _, lvl = spec.partition(":")
@@ -140,12 +201,17 @@ def _codec(spec: str, decoder: bool = False):
         return ("bz2", bz2.decompress) if decoder else \
             ((lambda b: bz2.compress(b, 9 if level is None else level)), "bz2")
     if algo == "zstd":
+        z = _libzstd()
+        if z is not None:
+            if decoder:
+                return "zstd", z.decompress
+            return (lambda b: z.compress(b, 3 if level is None else level)), "zstd"
         try:
             import zstandard
         except ImportError:
-            raise RuntimeError(f"MDS compression {spec!r} needs the zstandard module (not installed)") from None
+            raise RuntimeError(f"MDS compression {spec!r} needs libzstd.so.1 or the zstandard module") from None
         if decoder:
-            return "zstd", (lambda b: zstandard.ZstdDecompressor().decompress(b))
+            return "zstd", (lambda b, size=None: zstandard.ZstdDecompressor().decompress(b, max_output_size=size or 0))
         return (lambda b: zstandard.ZstdCompressor(level=3 if level is None else level).compress(b)), "zstd"
     raise RuntimeError(f"unsupported MDS compression {spec!r} (gz, bz2, zstd)")
 
@@ -295,9 +361,9 @@ class StreamingDataset(IterableDataset):
             raw_path = os.path.join(self.local, sh["raw_data"]["basename"])
             if sh.get("compression") and not (os.path.exists(raw_path)
                                               and os.path.getsize(raw_path) == sh["raw_data"]["bytes"]):
-                _, dec = _codec(sh["compression"], decoder=True)
+                ext, dec = _codec(sh["compression"], decoder=True)
                 with open(os.path.join(self.local, sh["zip_data"]["basename"]), "rb") as f:
-                    data = dec(f.read())
+                    data = dec(f.read(), sh["raw_data"]["bytes"]) if ext == "zstd" else dec(f.read())
                 if len(data) != sh["raw_data"]["bytes"]:
                     raise ValueError(f"{sh['zip_data']['basename']}: decompressed {len(data)} bytes, "
                                      f"index says {sh['raw_data']['bytes']}")

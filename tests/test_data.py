@@ -31,7 +31,7 @@ def test_mds_roundtrip_and_shards():
         assert it["label"] == ds[i][1]
 
 
-@pytest.mark.parametrize("comp", ["gz", "gz:1", "bz2"])
+@pytest.mark.parametrize("comp", ["gz", "gz:1", "bz2", "zstd", "zstd:7"])
 def test_mds_compressed_shards(comp):
     """compressed shards (zip_data next to raw_data, as mosaicml-streaming writes them) are
     decompressed once into the reader's local directory; remote keeps only the compressed files"""
@@ -56,7 +56,24 @@ def test_mds_compressed_shards(comp):
     assert np.array_equal(np.asarray(sd2[5]["image"]), ds[5][0])
 
 
-def test_mds_zstd_without_module_falls_back():
+def test_mds_zstd_frames_roundtrip():
+    """zstd through the system libzstd (ctypes): standard frames with the content size, and a
+    frame without one decoded with the index's raw size as the hint."""
+    from dbx_distributed_pytorch_examples_amd.data import mds
+    z = mds._libzstd()
+    if z is None:
+        pytest.skip("no libzstd.so.1 on this host")
+    data = bytes(range(256)) * 999 + b"tail"
+    c = z.compress(data, 5)
+    assert c[:4] == b"\x28\xb5\x2f\xfd" and len(c) < len(data) // 10  # zstd magic, compressed
+    assert z.decompress(c) == data
+    with pytest.raises(RuntimeError, match="not a zstd frame"):
+        z.decompress(b"garbage!")
+
+
+def test_mds_zstd_without_any_codec_falls_back(monkeypatch):
+    from dbx_distributed_pytorch_examples_amd.data import mds
+    monkeypatch.setattr(mds, "_ZSTD", None)  # as if libzstd were missing
     try:
         import zstandard  # noqa: F401
         pytest.skip("zstandard installed: the fallback path is not taken")

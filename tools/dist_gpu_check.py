@@ -44,6 +44,7 @@ def run(use_graphs, zero=0, steps=4, bucket_mb=1.0, pg=None, optim="sgd"):
                        bucket_cap_mb=bucket_mb, zero_stage=zero, process_group=pg)
     for img, lab in batches(steps):
         tr.step(img, lab)
+    tr.sync_master()  # ZeRO: every rank updated only its shard of the fp32 master
     torch.cuda.synchronize()
     loss, _ = tr.read_metrics()
     return tr, loss
