@@ -78,6 +78,11 @@ def parse_args(argv=None):
     p.add_argument("--zero", type=int, default=0, choices=[0, 1, 2], help="native impl: ZeRO stage")
     p.add_argument("--preset", default="", choices=[""] + sorted(PRESETS),
                    help="one of BASELINE.json's other configs (sets model/size/classes/batch/optim)")
+    p.add_argument("--data", default="synthetic", choices=["synthetic", "mds"],
+                   help="mds: every step's batch comes from zstd MDS shards written first (the 03a path): "
+                        "C++ shard reader -> pinned staging ring -> async H2D -> GPU augment -> native step")
+    p.add_argument("--mds-samples", type=int, default=0, help="samples per rank written for --data mds "
+                   "(default: enough for warmup + steps, at least 8 batches)")
     p.add_argument("--json-out", default=None)
     a = p.parse_args(argv)
     given = {t.split("=", 1)[0] for t in (sys.argv[1:] if argv is None else argv) if t.startswith("--")}
@@ -165,8 +170,10 @@ def main(argv=None) -> int:
         "scaling": "weak",
         "vs_baseline": (round(value / (base * n), 4) if base else None),
         "dtype": "bf16",
-        "data": f"synthetic (uint8 NHWC {args.image_size}x{args.image_size} images + random labels, on-device; "
-                "random-init weights)",
+        "data": (f"synthetic (uint8 NHWC {args.image_size}x{args.image_size} images + random labels, on-device; "
+                 "random-init weights)") if args.data == "synthetic" else (
+            f"synthetic images of the config's shape streamed from zstd MDS shards ({meta.get('mds', '')}); "
+            "random-init weights"),
         "config": {
             "model": f"{args.model} {dname} {args.image_size}x{args.image_size} {args.num_classes} classes"
                      + (" large-batch (global 8192 at 8 GPUs)" if headline and args.batch == 1024 else ""),

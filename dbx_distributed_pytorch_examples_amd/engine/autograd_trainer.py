@@ -103,7 +103,11 @@ class AutogradTrainer:
                                            offload_param=offload_param)
             zero_stage = 0
         else:
-            self.ddp = DistributedDataParallel(self.model, bucket_cap_mb=bucket_cap_mb, allreduce_dtype=allreduce_dtype)
+            from .native_module import NativeResNet
+            # a native_module inside averages its own gradients (overlapped, per backward segment)
+            own_sync = any(isinstance(m, NativeResNet) for m in self.model.modules())
+            self.ddp = DistributedDataParallel(self.model, bucket_cap_mb=bucket_cap_mb, allreduce_dtype=allreduce_dtype,
+                                               gradient_sync=not own_sync)
         self.world = self.ddp.world
         self.o = optim
         self.smoothing = label_smoothing

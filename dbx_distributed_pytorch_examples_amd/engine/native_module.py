@@ -12,7 +12,9 @@ parameter's ``.grad`` as a view of the program's flat gradient buffer. The modul
 already ARE views of the program's flat fp32 master, so any torch optimizer steps them in place.
 
 * input: a float NCHW batch, already normalised (what torchvision-style transforms produce);
-  batches of another size than the compiled one (a short final batch) run through the plain
+  the program is compiled for a given batch x image size, or lazily for the first training
+  batch (``Accelerator.prepare`` / ``ray.prepare_model`` wrap supported ResNets that way by
+  default); batches of another size (a short final batch) run through the plain
   torch module on the same parameters (correct, not accelerated); at world size > 1 their
   gradients are all-reduced too, at the end of that backward (queued autograd callback), so the
   replicas never diverge on a short batch;
@@ -55,58 +57,68 @@ class _NativeFn(torch.autograd.Function):
 
 
 class NativeResNet(nn.Module):
-    def __init__(self, model: nn.Module, batch: int, image_hw: Tuple[int, int], device: torch.device,
-                 process_group=None):
+    def __init__(self, model: nn.Module, batch: Optional[int], image_hw: Optional[Tuple[int, int]],
+                 device: torch.device, process_group=None):
+        """``batch`` / ``image_hw`` None: compile lazily, for the shape of the first training batch
+        (``ray.prepare_model`` / ``Accelerator.prepare`` see no loader shape). The Parameter objects
+        of ``model`` stay the same (re-pointed at the flat master), so an optimizer created before
+        or after wrapping steps the live weights either way."""
         super().__init__()
         if not supports(model):
             raise TypeError(f"native_module: {type(model).__name__} is not a supported ResNet")
-        self.model = model
-        self.prog = ResNetProgram(model, batch, image_hw, device)
-        self.prog.build_backward()
+        self.model = model.to(device)
+        self.dev = device
         self.pg = process_group
+        self.prog = None
         self.use_graphs = device.type == "cuda" and os.environ.get("DBX_NATIVE_MODULE_GRAPHS", "1") != "0"
-        self._graphs = {}  # "fwd_train" / "fwd_eval" / "bwd" -> CUDAGraph
+        self._graphs = {}  # "fwd_train" / "fwd_eval" / "bwd*" -> CUDAGraph
         self._calls = {}
         # autograd needs one leaf that requires grad to route the loss back into _NativeFn
         self._anchor = nn.Parameter(torch.zeros((), device=device), requires_grad=True)
-        p = self.prog
         self._grad_views = []
-        for prm in model.parameters():
-            off = (prm.data_ptr() - p.master.data_ptr()) // 4
-            n = prm.numel()
-            g = p.grad[off:off + n]
-            gv = g.view(prm.shape[0], prm.shape[2], prm.shape[3], prm.shape[1]).permute(0, 3, 1, 2) \
-                if prm.dim() == 4 else g.view(prm.shape)
-            self._grad_views.append((prm, gv))
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self._comm = None
         self._fallback_active = False
         self._sync_queued = False
         if self.world > 1:
             self._init_distributed()
+        if batch:
+            self._build(int(batch), tuple(image_hw))
+
+    def _build(self, batch: int, image_hw: Tuple[int, int]) -> None:
+        """Compile the program (parameters / BN buffers move into its flat buffers, same objects)."""
+        self.prog = p = ResNetProgram(self.model, batch, image_hw, self.dev)
+        p.build_backward()
+        self._grad_views = []
+        for prm in self.model.parameters():
+            off = (prm.data_ptr() - p.master.data_ptr()) // 4
+            n = prm.numel()
+            g = p.grad[off:off + n]
+            gv = g.view(prm.shape[0], prm.shape[2], prm.shape[3], prm.shape[1]).permute(0, 3, 1, 2) \
+                if prm.dim() == 4 else g.view(prm.shape)
+            self._grad_views.append((prm, gv))
+        if self.world > 1:
+            self._seg_ranges = []
+            for rs in p.segment_param_ranges():
+                self._seg_ranges.append((min(r[1] for r in rs), max(r[1] + (r[2] + 15) // 16 * 16 for r in rs))
+                                        if rs else None)
+            if p.dev.type == "cuda":
+                self._comm = torch.cuda.Stream(device=p.dev, priority=-1)
+                # next to the comm stream the wgrad side stream costs more than it overlaps
+                # (NativeTrainer, profiles/r2s2_multirank/): weight gradients run on the main stream
+                p.overlap_wgrad = False
 
     # ------------------------------------------------------------------------------
     def _init_distributed(self):
-        """DDP-constructor semantics (rank 0's weights and BN buffers everywhere), per-segment
-        gradient ranges for the overlapped all-reduce, and the short-batch fallback's gradient sync."""
+        """DDP-constructor semantics (rank 0's weights and BN buffers everywhere) and the
+        short-batch fallback's gradient sync."""
         from ..parallel.dist import host_sync_for_gloo
-        p, pg = self.prog, self.pg
+        pg = self.pg
         src = 0 if pg is None else dist.get_global_rank(pg, 0)
         with torch.no_grad():
-            host_sync_for_gloo(p.master, pg)
-            dist.broadcast(p.master, src, group=pg)
-            for bn in p.bns:
-                dist.broadcast(bn.mod.running_mean, src, group=pg)
-                dist.broadcast(bn.mod.running_var, src, group=pg)
-        self._seg_ranges = []
-        for rs in p.segment_param_ranges():
-            self._seg_ranges.append((min(r[1] for r in rs), max(r[1] + (r[2] + 15) // 16 * 16 for r in rs))
-                                    if rs else None)
-        if p.dev.type == "cuda":
-            self._comm = torch.cuda.Stream(device=p.dev, priority=-1)
-            # next to the comm stream the wgrad side stream costs more than it overlaps
-            # (NativeTrainer, profiles/r2s2_multirank/): weight gradients run on the main stream
-            p.overlap_wgrad = False
+            for t in list(self.model.parameters()) + list(self.model.buffers()):
+                host_sync_for_gloo(t, pg)
+                dist.broadcast(t.data, src, group=pg)
         for prm in self.model.parameters():
             if prm.requires_grad:
                 prm.register_post_accumulate_grad_hook(self._fallback_hook)
@@ -169,8 +181,12 @@ class NativeResNet(nn.Module):
 
     # ------------------------------------------------------------------------------
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if (self.prog is None and x.dim() == 4 and x.is_cuda and self.training and torch.is_grad_enabled()
+                and x.shape[1] == self.model.conv1.in_channels):
+            self._build(x.shape[0], tuple(x.shape[2:]))  # lazy: the first training batch's shape
         p = self.prog
-        if x.dim() != 4 or x.shape[0] != p.N or tuple(x.shape[2:]) != (p.H, p.W) or x.shape[1] != p.in_ch:
+        if (p is None or x.dim() != 4 or x.shape[0] != p.N or tuple(x.shape[2:]) != (p.H, p.W)
+                or x.shape[1] != p.in_ch):
             # another batch size / resolution: the torch module on the same parameters (gradients
             # all-reduced after its backward at world > 1, see _fallback_hook)
             self._fallback_active = self.world > 1 and torch.is_grad_enabled() and self.training
@@ -247,10 +263,11 @@ class NativeResNet(nn.Module):
                 prm.grad.add_(gv)
 
 
-def native_module(model: nn.Module, batch: int, image_hw: Tuple[int, int] = (224, 224),
+def native_module(model: nn.Module, batch: Optional[int] = None, image_hw: Optional[Tuple[int, int]] = (224, 224),
                   device: Optional[torch.device] = None, process_group=None) -> NativeResNet:
     """Wrap a supported ResNet (torchvision-layout ResNet-18/34/50/..., the CIFAR-stem ResNet-18)
-    for a fixed ``batch`` x ``image_hw``; see the module docstring."""
+    for a fixed ``batch`` x ``image_hw`` (``batch=None``: for the first training batch's shape);
+    see the module docstring."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     return NativeResNet(model, batch, image_hw, device, process_group)

@@ -15,7 +15,8 @@ activation arena, because that is what lets the hot path be fused and graph-capt
   buckets become ready so RCCL all-reduces overlap the remaining backward.
 
 Parameters live in ONE flat fp32 master buffer (conv weights in KRSC order); the module's
-``nn.Parameter`` s are re-pointed at views of it (conv weights as channels_last views), so
+``nn.Parameter`` s are re-pointed at views of it (``.data`` swap: the Parameter objects, and any
+optimizer already holding them, stay valid; conv weights as channels_last views), so
 ``model.state_dict()`` / ``load_state_dict`` / checkpoint files keep torchvision layouts.
 
 Supported module trees: ``models.ResNet`` (BasicBlock / Bottleneck, any in_channels <= 4) and
@@ -36,6 +37,14 @@ from ..ops import kernels as K
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def _repoint(p: nn.Parameter, view: torch.Tensor) -> None:
+    """Make the EXISTING Parameter object a view of the flat master (``.data`` swap): optimizers and
+    hooks created on the module before compilation keep working on the live weights."""
+    p.data = view
+    if p.grad is not None and (p.grad.device != view.device or p.grad.shape != view.shape):
+        p.grad = None
 
 
 def supports(model: nn.Module) -> bool:
@@ -297,7 +306,7 @@ class ResNetProgram:
                     flat = self.master[off:off + n]
                     flat.copy_(src.permute(0, 2, 3, 1).reshape(-1))
                     view = flat.view(cv.OC, cv.R, cv.S, cv.IC).permute(0, 3, 1, 2)  # channels_last view
-                    cv.mod.weight = nn.Parameter(view, requires_grad=cv.mod.weight.requires_grad)
+                    _repoint(cv.mod.weight, view)
                     cv.grad = self.grad[off:off + n].view(cv.OC, cv.R * cv.S * cv.IC)
                     self.param_ranges.append((cv.name + ".weight", off, n))
                 elif kind in ("bn_w", "bn_b"):
@@ -306,7 +315,7 @@ class ResNetProgram:
                     p = getattr(mod, attr)
                     flat = self.master[off:off + n]
                     flat.copy_(p.detach().to(dev, torch.float32))
-                    setattr(mod, attr, nn.Parameter(flat, requires_grad=p.requires_grad))
+                    _repoint(p, flat)
                     if kind == "bn_w":
                         bn.off_w, bn.gamma, bn.dgamma = off, flat, self.grad[off:off + n]
                     else:
@@ -324,7 +333,7 @@ class ResNetProgram:
                     flat = self.master[off:off + n]
                     flat.copy_(p.detach().reshape(-1).to(dev, torch.float32))
                     view = flat.view(p.shape)
-                    setattr(self.fc, attr, nn.Parameter(view, requires_grad=p.requires_grad))
+                    _repoint(p, view)
                     if attr == "weight":
                         self.fc_w_off, self.fc_w_grad = off, self.grad[off:off + n].view(p.shape)
                     else:

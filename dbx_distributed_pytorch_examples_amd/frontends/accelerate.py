@@ -6,9 +6,15 @@ this rank's GPU (channels_last), wraps it in the flat-bucket DDP, re-shards the 
 all-reduces; ``gather`` / ``reduce`` are packed collectives; ``log`` forwards to the MLflow-compat
 tracker (``log_with="mlflow"``). bf16 autocast is enabled by ``mixed_precision="bf16"``.
 
-A model already wrapped by :func:`~dbx_distributed_pytorch_examples_amd.engine.native_module.native_module`
-(the notebook's loop on the native HIP kernels) is passed through unwrapped: its backward all-reduces its
-flat gradient in one collective itself.
+On a GPU, ``prepare`` puts a supported ResNet (the notebook's ``resnet50`` with a new ``fc``,
+`04_accelerate/01_cifar_accelerate.ipynb:475-503`) on the native HIP kernels by default:
+:func:`~dbx_distributed_pytorch_examples_amd.engine.native_module.native_module` compiles it for
+the first training batch's shape (``DBX_ACCELERATE_NATIVE=0`` or ``mixed_precision="no"`` keep the
+stock module). The Parameter objects do not change, so the optimizer the notebook built before
+``prepare`` keeps stepping the live weights; the module all-reduces its own gradient per backward
+segment, overlapped with the backward, so it is not wrapped in DDP. A model already wrapped by
+``native_module`` is passed through as is. Any other model runs under ``torch.autocast(bf16)`` with
+fp32 outputs when ``mixed_precision="bf16"`` (the default).
 """
 from __future__ import annotations
 
@@ -118,13 +124,18 @@ class Accelerator:
 
     def _prep_one(self, obj):
         if isinstance(obj, torch.nn.Module):
-            from ..engine.native_module import NativeResNet
+            import os
+            from ..engine.native_module import NativeResNet, native_module
+            from ..engine.program import supports
             if isinstance(obj, NativeResNet):
                 return obj  # on the device already; gradients all-reduced by its own backward
+            if (self.device.type == "cuda" and self.mixed_precision == "bf16" and supports(obj)
+                    and os.environ.get("DBX_ACCELERATE_NATIVE", "1") != "0"):
+                return native_module(obj, None, None, self.device)  # compiled for the first batch
             m = obj.to(self.device)
             if self.device.type == "cuda":
                 m = m.to(memory_format=torch.channels_last)
-            d = DistributedDataParallel(m)
+            d = DistributedDataParallel(m, autocast_dtype=torch.bfloat16 if self.mixed_precision == "bf16" else None)
             self._models.append(d)
             return d
         if isinstance(obj, torch.optim.Optimizer):

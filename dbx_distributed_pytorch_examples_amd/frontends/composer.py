@@ -7,10 +7,11 @@ Algorithms map onto the engine: label smoothing -> the CE target, CutMix -> the 
 The model follows Composer's ``forward(batch)`` / ``loss(outputs, batch)`` convention
 (``models.ComposerResNet50``); plain modules work too.
 
-On one GPU a ``ComposerResNet50`` trains on the native HIP program: its inner ResNet is wrapped by
-``engine.native_module`` for the train loader's batch size and image size (CutMix's soft targets and
-label smoothing stay torch ops on the logits; other batch sizes run the torch module on the same
-parameters). ``DBX_COMPOSER_NATIVE=0`` keeps the stock module (2.5x slower at the notebook's
+On GPUs a ``ComposerResNet50`` trains on the native HIP program at any world size: its inner ResNet
+is wrapped by ``engine.native_module`` for the train loader's batch size and image size (CutMix's
+soft targets and label smoothing stay torch ops on the logits; other batch sizes run the torch
+module on the same parameters); at world > 1 the wrapped program averages its own gradients per
+backward segment (overlapped with the backward), so the trainer's DDP only passes them through. ``DBX_COMPOSER_NATIVE=0`` keeps the stock module (2.5x slower at the notebook's
 b128 CIFAR shape, ``profiles/r2s5_native_module/``).
 """
 from __future__ import annotations
@@ -104,7 +105,7 @@ class Trainer:
         from ..engine.program import supports
         from ..models.wrappers import ComposerResNet50
         if (os.environ.get("DBX_COMPOSER_NATIVE", "1") == "0" or self.info.device.type != "cuda"
-                or ddist.get_world_size() > 1 or not isinstance(model, ComposerResNet50)):
+                or not isinstance(model, ComposerResNet50)):
             return model
         bs = getattr(dl, "batch_size", None)
         try:

@@ -107,16 +107,21 @@ def report(metrics: Dict[str, Any], checkpoint: Optional[Checkpoint] = None) -> 
         shutil.copytree(checkpoint.path, os.path.join(trial, f"checkpoint_{n:06d}"), dirs_exist_ok=True)
 
 
-def prepare_model(model: torch.nn.Module, native_batch: int = 0, native_hw=(32, 32), **ddp_kw) -> torch.nn.Module:
-    """``ray.train.torch.prepare_model``. ``native_batch`` > 0 (GPU, a supported ResNet): the worker's own loop
-    runs on the native HIP program (``engine.native_module``; gradients averaged by its backward), else the
-    model is moved to the device and wrapped in the flat-bucket DDP at world > 1."""
+def prepare_model(model: torch.nn.Module, native_batch: Optional[int] = None, native_hw=None,
+                  **ddp_kw) -> torch.nn.Module:
+    """``ray.train.torch.prepare_model`` (`05_ray/02_cifar_resnet_pytorch_ray.ipynb:280`). On a GPU a
+    supported ResNet runs the worker's own loop on the native HIP program by default
+    (``engine.native_module``, compiled for the first training batch's shape unless ``native_batch``
+    / ``native_hw`` fix it; its backward averages the gradients per segment, overlapped with the
+    backward; ``native_batch=0`` or ``DBX_RAY_NATIVE=0`` opt out). Otherwise the model is moved to
+    the device and wrapped in the flat-bucket DDP at world > 1."""
     info = ddist.init_distributed(device="cpu" if os.environ.get("DBX_FORCE_CPU") == "1" else None)
-    if native_batch and info.device.type == "cuda":
+    if (native_batch != 0 and info.device.type == "cuda" and os.environ.get("DBX_RAY_NATIVE", "1") != "0"):
         from ..engine.native_module import native_module
         from ..engine.program import supports
         if supports(model):
-            return native_module(model, native_batch, tuple(native_hw), info.device)
+            return native_module(model, native_batch or None, tuple(native_hw) if native_hw else None,
+                                 info.device)
     model = model.to(info.device)
     if info.device.type == "cuda":
         model = model.to(memory_format=torch.channels_last)

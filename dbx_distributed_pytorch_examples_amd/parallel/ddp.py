@@ -55,11 +55,19 @@ class FlatGradBuffer:
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 64.0,
                  broadcast_buffers: bool = False, allreduce_dtype: torch.dtype = torch.float32,
-                 find_unused_parameters: bool = False, gradient_predivide: bool = True):
+                 find_unused_parameters: bool = False, gradient_predivide: bool = True,
+                 autocast_dtype: Optional[torch.dtype] = None, gradient_sync: bool = True):
+        """``autocast_dtype``: run the wrapped forward under ``torch.autocast`` with that dtype and
+        return floating outputs as fp32 (HF Accelerate's ``mixed_precision`` + ``convert_to_fp32``);
+        ``gradient_sync=False``: a module that averages its own gradients (``engine.native_module``):
+        no broadcast, no bucket all-reduce -- only the flat-buffer / no_sync interface."""
         super().__init__()
         self.module = module
         self.pg = process_group
+        self.autocast_dtype = autocast_dtype
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        if not gradient_sync:
+            self.world = 1
         self.broadcast_buffers = broadcast_buffers
         self.allreduce_dtype = allreduce_dtype
         self.find_unused = find_unused_parameters
@@ -160,7 +168,12 @@ class DistributedDataParallel(nn.Module):
                 self.flat.zero_()
                 self.flat.attach()
         self._reset_round()
-        return self.module(*args, **kw)
+        if self.autocast_dtype is None:
+            return self.module(*args, **kw)
+        dev = next((t.device.type for t in args if isinstance(t, torch.Tensor)), "cpu")
+        with torch.autocast(dev, dtype=self.autocast_dtype, enabled=dev == "cuda"):
+            out = self.module(*args, **kw)
+        return _to_fp32(out)
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -185,6 +198,16 @@ class DistributedDataParallel(nn.Module):
     @property
     def grad_buffer(self) -> Optional[torch.Tensor]:
         return self.flat.buffer if self.flat is not None else None
+
+
+def _to_fp32(out):
+    if isinstance(out, torch.Tensor):
+        return out.float() if out.is_floating_point() else out
+    if isinstance(out, (list, tuple)):
+        return type(out)(_to_fp32(o) for o in out)
+    if isinstance(out, dict):
+        return {k: _to_fp32(v) for k, v in out.items()}
+    return out
 
 
 def unwrap(model: nn.Module) -> nn.Module:

@@ -23,16 +23,19 @@ def build_native_step(args, info):
     ar_dtype = torch.bfloat16 if os.environ.get("DBX_ALLREDUCE_BF16", "0") == "1" else torch.float32
     tr = NativeTrainer(model, args.batch, (args.image_size, args.image_size), dev, optim=opt,
                        use_graphs=use_graphs, allreduce_dtype=ar_dtype, zero_stage=getattr(args, "zero", 0))
-    g = torch.Generator(device="cpu").manual_seed(1000 + info.rank)
-    img = torch.randint(0, 256, (args.batch, args.image_size, args.image_size, 3), dtype=torch.uint8, generator=g)
-    lab = torch.randint(0, args.num_classes, (args.batch,), dtype=torch.int64, generator=g)
-    tr.prog.img_u8.copy_(img)
-    tr.prog.labels.copy_(lab)
-
-    def step():
-        tr.step()
-
     extra = {}
+    if getattr(args, "data", "synthetic") == "mds":
+        step, extra["mds"] = _mds_step(args, info, tr)
+    else:
+        g = torch.Generator(device="cpu").manual_seed(1000 + info.rank)
+        img = torch.randint(0, 256, (args.batch, args.image_size, args.image_size, 3), dtype=torch.uint8, generator=g)
+        lab = torch.randint(0, args.num_classes, (args.batch,), dtype=torch.int64, generator=g)
+        tr.prog.img_u8.copy_(img)
+        tr.prog.labels.copy_(lab)
+
+        def step():
+            tr.step()
+
     if tr.zero is not None:
         extra["zero"] = (f"ZeRO-{tr.zero.stage}: per-segment fp32 reduce-scatter (overlapped with backward), sharded "
                          f"{opt.name} update, bf16 all-gather; {tr.zero.bytes_per_step / 2**20:.1f} MiB sent/rank/step")
@@ -41,3 +44,73 @@ def build_native_step(args, info):
                           f"{tr.bucket_cap * 4 >> 20} MiB chunks, "
                           f"{str(ar_dtype).split('.')[-1]}, overlapped per backward segment") if tr.world > 1 else "none",
                   "kernels": "dbx HIP (conv implicit-GEMM MFMA + fused BN/ReLU/pool/CE/SGD)"}
+
+
+def _mds_step(args, info, tr):
+    """The 03a input path, timed with the step. Every rank writes ``--mds-samples`` synthetic
+    images of the config's shape as zstd MDS shards ('pil' + 'int' columns, the reference's
+    ``MDSWriter(..., compression='zstd')`` call, `03a_tiny_imagenet_torch_distributor_resnet_mds.py:179-223`)
+    into its part of one dataset; rank 0 merges the parts' indexes; then every step takes its batch
+    from ``NativeImageLoader`` over the shared ``StreamingDataset`` (deterministic rank partition):
+    C++ shard reader -> pinned staging ring -> async H2D on the copy stream -> GPU augment (random
+    crop + flip) inside the captured step."""
+    import atexit
+    import json
+    import os
+    import shutil
+    import tempfile
+    import time
+
+    import numpy as np
+    from PIL import Image
+
+    from ..data.loader import AugmentSpec, NativeImageLoader
+    from ..data.mds import MDSWriter, StreamingDataset
+    from ..parallel import dist as ddist
+    s, B = args.image_size, args.batch
+    n = args.mds_samples or max(8 * B, (args.steps + args.warmup + 2) * B)
+    root = ddist.broadcast_object(tempfile.mkdtemp(prefix="dbx_bench_mds_") if info.rank == 0 else None)
+    part = os.path.join(root, f"part{info.rank}")
+    rng = np.random.default_rng(100 + info.rank)
+    t0 = time.time()
+    with MDSWriter(part, {"image": "pil", "label": "int"}, compression="zstd", size_limit=1 << 26) as w:
+        for _ in range(n):
+            w.write({"image": Image.fromarray(rng.integers(0, 256, (s, s, 3), dtype=np.uint8)),
+                     "label": int(rng.integers(0, args.num_classes))})
+    t_write = time.time() - t0
+    ddist.barrier()
+    if info.rank == 0:
+        shards = []
+        for r in range(info.world_size):
+            with open(os.path.join(root, f"part{r}", "index.json")) as f:
+                for sh in json.load(f)["shards"]:
+                    for k in ("raw_data", "zip_data"):
+                        if sh.get(k):
+                            sh[k]["basename"] = f"part{r}/" + sh[k]["basename"]
+                    shards.append(sh)
+        with open(os.path.join(root, "index.json"), "w") as f:
+            json.dump({"version": 2, "shards": shards}, f)
+        StreamingDataset(local=root)  # decompress every shard once, before the other ranks open it
+        atexit.register(shutil.rmtree, root, True)
+    ddist.barrier()
+    ds = StreamingDataset(local=root, shuffle=True, batch_size=B)
+    aug = AugmentSpec(mode="random_crop", pad=4 if s == 32 else 0, hflip=True)
+    ld = NativeImageLoader(ds, B, (s, s), tr.dev, augment=aug, nthreads=8, prefetch=3)
+    state = {"it": iter(ld), "epoch": 0}
+
+    def next_batch():
+        try:
+            return next(state["it"])
+        except StopIteration:
+            state["epoch"] += 1
+            ld.set_epoch(state["epoch"])
+            state["it"] = iter(ld)
+            return next(state["it"])
+
+    def step():
+        img, lab, boxes, flips = next_batch()
+        tr.step(img, lab, boxes, flips)
+
+    desc = (f"{n} samples per rank in {len(ds.shards)} shards (written in {t_write:.1f} s), C++ reader "
+            f"{'on' if ld.native is not None else 'off'}, pinned ring + copy stream")
+    return step, desc

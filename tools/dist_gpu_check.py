@@ -45,9 +45,14 @@ def run(use_graphs, zero=0, steps=4, bucket_mb=1.0, pg=None, optim="sgd"):
     for img, lab in batches(steps):
         tr.step(img, lab)
     tr.sync_master()  # ZeRO: every rank updated only its shard of the fp32 master
-    torch.cuda.synchronize()
+    if info.device.type == "cuda":
+        torch.cuda.synchronize()
     loss, _ = tr.read_metrics()
     return tr, loss
+
+
+def params(tr):
+    return torch.cat([p.detach().reshape(-1) for p in tr.prog.model.parameters()]).clone()
 
 
 info = ddist.init_distributed()
@@ -88,11 +93,11 @@ assert rel == 0.0, f"graph vs eager mismatch {rel} (training is bit-reproducible
 relz = {}
 for optim in ("sgd", "adamw"):
     tr_z, _ = run(True, zero=1, optim=optim)
-    w_zero = tr_z.prog.master.detach().clone()
+    w_zero = params(tr_z)  # the ZeRO flat layout is padded differently: compare the module's tensors
     del tr_z
     debug.assert_replicas_in_sync([w_zero], what=f"master weights (ZeRO-1 {optim})")
     tr_d, _ = run(True, zero=0, optim=optim)
-    w_dp = tr_d.prog.master.detach().clone()
+    w_dp = params(tr_d)
     del tr_d
     relz[optim] = ((w_zero - w_dp).norm() / w_dp.norm()).item()
     assert (relz[optim] == 0.0) if exact else (relz[optim] < 1e-6), f"ZeRO-1 vs DP mismatch ({optim}) {relz[optim]}"
