@@ -93,4 +93,19 @@ struct StemBwdArgs {
   int M, nsplit, m_per_split;
   unsigned long long mag_hw, mag_w;          // ceil(2^40 / (H*W)), ceil(2^40 / W)
 };
+// classifier-head GEMM (head_ops.hip): C[M][N] = alpha * A(m,k) B(k,n) (+ bias) (+ C), dropout on A or B
+struct GemmArgs {
+  const bf16* A;
+  const bf16* B;
+  void* C;               // fp32 or bf16 [M][ldc]
+  const float* bias_f;   // [N] fp32 (nullable)
+  const bf16* bias_h;    // [N] bf16 (nullable)
+  int M, N, K, lda, ldb, ldc;
+  float alpha;
+  int accumulate;        // C += result
+  unsigned long long seed;
+  unsigned offset, thresh;  // dropout: keep if the Philox draw < thresh
+  float inv_keep;
+};
+
 }  // namespace dbx

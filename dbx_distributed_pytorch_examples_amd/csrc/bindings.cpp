@@ -43,7 +43,8 @@ int dbx_pool_bn_bwd(const bf16*, const unsigned char*, const bf16*, const float*
                     hipStream_t);
 int dbx_avgpool_fwd(const bf16*, bf16*, int, int, int, hipStream_t);
 int dbx_avgpool_bwd(const bf16*, bf16*, int, int, int, hipStream_t);
-int dbx_softmax_ce(const void*, int, const long long*, void*, float*, double*, int, int, float, float, hipStream_t);
+int dbx_softmax_ce(const void*, int, const long long*, void*, float*, double*, int, int, float, float,
+                   const long long*, const float*, hipStream_t);
 int dbx_sgd(float*, const float*, float*, bf16*, long long, const float*, float, float, float, float, int, int,
             const float*, float, hipStream_t);
 int dbx_adam(float*, const float*, float*, float*, bf16*, long long, const float*, float, float, float, float, float, int,
@@ -57,7 +58,10 @@ int dbx_normalize_u8(const unsigned char*, bf16*, const unsigned char*, int, int
 int dbx_weight_prep(const float*, bf16*, const void*, int, hipStream_t);
 int dbx_weight_prep16(const bf16*, bf16*, const void*, int, hipStream_t);
 int dbx_augment_u8(const unsigned char*, bf16*, const float*, const unsigned char*, int, int, int, int, int, int, float,
-                   float, float, float, float, float, hipStream_t);
+                   float, float, float, float, float, const int*, const int*, hipStream_t);
+int dbx_small_gemm(int, int, int, int, const dbx::GemmArgs*, hipStream_t);
+int dbx_colsum(const bf16*, float*, int, int, int, hipStream_t);
+int dbx_dropout(const bf16*, bf16*, long long, unsigned long long, unsigned, unsigned, float, hipStream_t);
 int dbx_cast_f32_bf16(const float*, bf16*, long long, hipStream_t);
 int dbx_cast_bf16_f32(const bf16*, float*, long long, float, int, hipStream_t);
 }
@@ -233,9 +237,11 @@ PYBIND11_MODULE(_C, m) {
     check(dbx_avgpool_bwd(P<const bf16*>(dout), P<bf16*>(dx), N, HW, C, S(st)), "avgpool_bwd");
   });
   m.def("softmax_ce", [](uintptr_t logits, int is_bf16, uintptr_t labels, uintptr_t dlogits, uintptr_t loss_out,
-                         uintptr_t stats, int B, int C, float smoothing, float gscale, uintptr_t st) {
+                         uintptr_t stats, int B, int C, float smoothing, float gscale, uintptr_t labels2, uintptr_t lam,
+                         uintptr_t st) {
     check(dbx_softmax_ce(P<const void*>(logits), is_bf16, P<const long long*>(labels), P<void*>(dlogits),
-                         P<float*>(loss_out), P<double*>(stats), B, C, smoothing, gscale, S(st)),
+                         P<float*>(loss_out), P<double*>(stats), B, C, smoothing, gscale,
+                         P<const long long*>(labels2), P<const float*>(lam), S(st)),
           "softmax_ce");
   });
   m.def("sgd", [](uintptr_t p, uintptr_t g, uintptr_t v, uintptr_t p16, long long n, uintptr_t hyper, float lr,
@@ -270,10 +276,27 @@ PYBIND11_MODULE(_C, m) {
           "normalize_u8");
   });
   m.def("augment_u8", [](uintptr_t in, uintptr_t out, uintptr_t boxes, uintptr_t flip, int N, int Hin, int Win, int Cin,
-                         int Ho, int Wo, float m0, float m1, float m2, float s0, float s1, float s2, uintptr_t st) {
+                         int Ho, int Wo, float m0, float m1, float m2, float s0, float s1, float s2, uintptr_t perm,
+                         uintptr_t mixbox, uintptr_t st) {
     check(dbx_augment_u8(P<const unsigned char*>(in), P<bf16*>(out), P<const float*>(boxes),
-                         P<const unsigned char*>(flip), N, Hin, Win, Cin, Ho, Wo, m0, m1, m2, s0, s1, s2, S(st)),
+                         P<const unsigned char*>(flip), N, Hin, Win, Cin, Ho, Wo, m0, m1, m2, s0, s1, s2,
+                         P<const int*>(perm), P<const int*>(mixbox), S(st)),
           "augment_u8");
+  });
+  m.def("small_gemm", [](int ta, int tb, int out_f32, int drop, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias_f,
+                         uintptr_t bias_h, int M, int N, int K, int lda, int ldb, int ldc, float alpha, int accumulate,
+                         unsigned long long seed, unsigned offset, unsigned thresh, float inv_keep, uintptr_t st) {
+    // classifier-head GEMM (head_ops.hip)
+    dbx::GemmArgs g{P<const bf16*>(A), P<const bf16*>(B), P<void*>(C), P<const float*>(bias_f), P<const bf16*>(bias_h),
+                    M, N, K, lda, ldb, ldc, alpha, accumulate, seed, offset, thresh, inv_keep};
+    check(dbx_small_gemm(ta, tb, out_f32, drop, &g, S(st)), "small_gemm");
+  });
+  m.def("colsum", [](uintptr_t X, uintptr_t out, int M, int N, int accumulate, uintptr_t st) {
+    check(dbx_colsum(P<const bf16*>(X), P<float*>(out), M, N, accumulate, S(st)), "colsum");
+  });
+  m.def("dropout", [](uintptr_t x, uintptr_t y, long long n, unsigned long long seed, unsigned offset, unsigned thresh,
+                      float inv_keep, uintptr_t st) {
+    check(dbx_dropout(P<const bf16*>(x), P<bf16*>(y), n, seed, offset, thresh, inv_keep, S(st)), "dropout");
   });
   m.def("weight_prep16", [](uintptr_t src, uintptr_t wbuf, uintptr_t desc, int nlayers, uintptr_t st) {
     check(dbx_weight_prep16(P<const bf16*>(src), P<bf16*>(wbuf), P<const void*>(desc), nlayers, S(st)),

@@ -542,7 +542,10 @@ __global__ void avgpool_bwd_kernel(const bf16* __restrict__ dout, bf16* __restri
 template <typename T>
 __global__ void softmax_ce_kernel(const T* __restrict__ logits, const long long* __restrict__ labels,
                                   T* __restrict__ dlogits, float* __restrict__ loss_out, double* stats,
-                                  int B, int C, float smoothing, float gscale) {
+                                  int B, int C, float smoothing, float gscale,
+                                  const long long* __restrict__ labels2, const float* __restrict__ lam_ptr) {
+  // labels2 / lam_ptr (CutMix): target = lam * onehot(label) + (1 - lam) * onehot(label2), then label
+  // smoothing on top (Composer applies LabelSmoothing to the mixed targets); accuracy vs label
   const int row = blockIdx.x;
   const T* x = logits + (size_t)row * C;
   const int tid = threadIdx.x;
@@ -586,8 +589,11 @@ __global__ void softmax_ce_kernel(const T* __restrict__ logits, const long long*
   const float lse = mx + __logf(se);
   const long long lab = labels[row];
   const float xl = (float)x[lab];
-  // loss = -(1-eps)*log p_lab - eps/C * sum_c log p_c
-  const float loss = (1.f - smoothing) * (lse - xl) + smoothing * (lse - sx / C);
+  const float lam = labels2 ? lam_ptr[0] : 1.f;
+  const long long lab2 = labels2 ? labels2[row] : lab;
+  const float xl2 = (float)x[lab2];
+  // loss = -(1-eps) * [lam log p_lab + (1-lam) log p_lab2] - eps/C * sum_c log p_c
+  const float loss = (1.f - smoothing) * (lam * (lse - xl) + (1.f - lam) * (lse - xl2)) + smoothing * (lse - sx / C);
   if (tid == 0) {
     if (loss_out) loss_out[row] = loss;
     if (stats) {
@@ -599,7 +605,7 @@ __global__ void softmax_ce_kernel(const T* __restrict__ logits, const long long*
     const float inv = gscale / B;
     for (int c = tid; c < C; c += 256) {
       const float p = __expf((float)x[c] - lse);
-      const float t = (c == lab ? (1.f - smoothing) : 0.f) + smoothing / C;
+      const float t = (1.f - smoothing) * ((c == lab ? lam : 0.f) + (c == lab2 ? 1.f - lam : 0.f)) + smoothing / C;
       dlogits[(size_t)row * C + c] = (T)((p - t) * inv);
     }
   }
@@ -785,23 +791,36 @@ __global__ void normalize_u8_kernel(const unsigned char* __restrict__ in, bf16* 
 // ----------------------------------------------------------------------------------------
 // One block per output row (n, oy): the box, flip and the two source rows are block-uniform, so
 // per pixel only the column interpolation is computed (32-bit index math throughout).
+// CutMix (Composer's CutMix(alpha=1), `03_composer/01_cifar_composer_resnet.ipynb:430`):
+// with perm / mixbox set, output pixels inside the batch-wide box [y0, y1) x [x0, x1) come from
+// sample perm[n] -- sampled with ITS crop box and flip, i.e. exactly the pixels of the augmented
+// image perm[n] at the same output position (Composer pastes after the per-sample transforms).
 __global__ __launch_bounds__(256) void augment_u8_kernel(const unsigned char* __restrict__ in, bf16* __restrict__ out,
                                                          const float* __restrict__ boxes,
                                                          const unsigned char* __restrict__ flip, int N, int Hin,
                                                          int Win, int Cin, int Ho, int Wo, float m0, float m1,
-                                                         float m2, float s0, float s1, float s2) {
+                                                         float m2, float s0, float s1, float s2,
+                                                         const int* __restrict__ perm, const int* __restrict__ mixbox) {
   constexpr int kRowMax = 4096;
   __shared__ __attribute__((aligned(16))) unsigned char srow[2][kRowMax];
+  const int my0 = mixbox ? mixbox[0] : 0, my1 = mixbox ? mixbox[1] : 0;
+  const int mx0 = mixbox ? mixbox[2] : 0, mx1 = mixbox ? mixbox[3] : 0;
+  const float i0 = 1.f / (255.f * s0), i1 = 1.f / (255.f * s1), i2 = 1.f / (255.f * s2);
   for (int row = blockIdx.x; row < N * Ho; row += gridDim.x) {  // row = n * Ho + oy
   const int n = row / Ho, oy = row - n * Ho;
-  const float by = boxes[4 * n], bx = boxes[4 * n + 1], bh = boxes[4 * n + 2], bw = boxes[4 * n + 3];
-  const bool fl = flip && flip[n];
+  const bool mixrow = perm && oy >= my0 && oy < my1 && mx0 < mx1;  // block-uniform
+  // pass 0: sample n outside the box (everywhere when not mixing); pass 1: sample perm[n] inside
+  for (int pass = 0; pass < (mixrow ? 2 : 1); ++pass) {
+  const int sn = pass ? perm[n] : n;
+  const int xlo = pass ? mx0 : 0, xhi = pass ? mx1 : Wo;
+  const float by = boxes[4 * sn], bx = boxes[4 * sn + 1], bh = boxes[4 * sn + 2], bw = boxes[4 * sn + 3];
+  const bool fl = flip && flip[sn];
   float sy = by + (oy + 0.5f) * bh / Ho - 0.5f;
   sy = fminf(fmaxf(sy, 0.f), (float)(Hin - 1));
   const int y0 = (int)sy, y1 = min(y0 + 1, Hin - 1);
   const float wy = sy - y0;
-  const unsigned char* g0 = in + ((size_t)n * Hin + y0) * Win * Cin;
-  const unsigned char* g1 = in + ((size_t)n * Hin + y1) * Win * Cin;
+  const unsigned char* g0 = in + ((size_t)sn * Hin + y0) * Win * Cin;
+  const unsigned char* g1 = in + ((size_t)sn * Hin + y1) * Win * Cin;
   // the two source rows are staged in LDS with 16-byte loads (the bilinear taps are byte gathers)
   const int rb = Win * Cin;
   const bool staged = rb <= kRowMax && (((size_t)g0 | (size_t)g1) & 15) == 0 && (rb & 15) == 0;  // block-uniform
@@ -813,9 +832,9 @@ __global__ __launch_bounds__(256) void augment_u8_kernel(const unsigned char* __
     __syncthreads();
   }
   const float sxs = bw / Wo;
-  const float i0 = 1.f / (255.f * s0), i1 = 1.f / (255.f * s1), i2 = 1.f / (255.f * s2);
   auto body = [&](const unsigned char* r0, const unsigned char* r1) __attribute__((always_inline)) {
-    for (int ox = threadIdx.x; ox < Wo; ox += blockDim.x) {
+    for (int ox = xlo + threadIdx.x; ox < xhi; ox += blockDim.x) {
+      if (mixrow && !pass && ox >= mx0 && ox < mx1) continue;  // pasted by pass 1
       const int oxx = fl ? (Wo - 1 - ox) : ox;
       float sx = bx + (oxx + 0.5f) * sxs - 0.5f;
       sx = fminf(fmaxf(sx, 0.f), (float)(Win - 1));
@@ -835,7 +854,8 @@ __global__ __launch_bounds__(256) void augment_u8_kernel(const unsigned char* __
   };
   if (staged) body(&srow[0][0], &srow[1][0]);  // LDS byte gathers (ds_read_u8)
   else body(g0, g1);
-  __syncthreads();  // srow reuse by the next row
+  __syncthreads();  // srow reuse by the next pass / row
+  }
   }
 }
 
@@ -1030,13 +1050,14 @@ extern "C" int dbx_avgpool_bwd(const bf16* dout, bf16* dx, int N, int HW, int C,
   RET_LAST;
 }
 extern "C" int dbx_softmax_ce(const void* logits, int is_bf16, const long long* labels, void* dlogits, float* loss_out,
-                              double* stats, int B, int C, float smoothing, float gscale, hipStream_t st) {
+                              double* stats, int B, int C, float smoothing, float gscale, const long long* labels2,
+                              const float* lam, hipStream_t st) {
   if (is_bf16)
     hipLaunchKernelGGL(softmax_ce_kernel<bf16>, dim3(B), dim3(256), 0, st, (const bf16*)logits, labels, (bf16*)dlogits,
-                       loss_out, stats, B, C, smoothing, gscale);
+                       loss_out, stats, B, C, smoothing, gscale, labels2, lam);
   else
     hipLaunchKernelGGL(softmax_ce_kernel<float>, dim3(B), dim3(256), 0, st, (const float*)logits, labels,
-                       (float*)dlogits, loss_out, stats, B, C, smoothing, gscale);
+                       (float*)dlogits, loss_out, stats, B, C, smoothing, gscale, labels2, lam);
   RET_LAST;
 }
 extern "C" int dbx_sgd(float* p, const float* g, float* v, bf16* p16, long long n, const float* hyper, float lr,
@@ -1079,9 +1100,9 @@ extern "C" int dbx_normalize_u8(const unsigned char* in, bf16* out, const unsign
 }
 extern "C" int dbx_augment_u8(const unsigned char* in, bf16* out, const float* boxes, const unsigned char* flip, int N,
                               int Hin, int Win, int Cin, int Ho, int Wo, float m0, float m1, float m2, float s0, float s1,
-                              float s2, hipStream_t st) {
+                              float s2, const int* perm, const int* mixbox, hipStream_t st) {
   hipLaunchKernelGGL(augment_u8_kernel, dim3(N * Ho < 4096 ? N * Ho : 4096), dim3(Wo >= 256 ? 256 : ((Wo + 63) / 64) * 64), 0, st, in, out, boxes, flip, N,
-                     Hin, Win, Cin, Ho, Wo, m0, m1, m2, s0, s1, s2);
+                     Hin, Win, Cin, Ho, Wo, m0, m1, m2, s0, s1, s2, perm, mixbox);
   RET_LAST;
 }
 extern "C" int dbx_weight_prep(const float* master, bf16* wbuf, const void* desc_dev, int nlayers, hipStream_t st) {

@@ -52,7 +52,7 @@ class NativeTrainer:
                  optim: Optional[OptimConfig] = None, label_smoothing: float = 0.0, use_graphs: bool = True,
                  bucket_cap_mb: float = 64.0, allreduce_dtype: torch.dtype = torch.float32,
                  process_group=None, src_hw: Optional[Tuple[int, int]] = None, mean=None, std=None,
-                 zero_stage: int = 0):
+                 zero_stage: int = 0, cutmix_alpha: float = 0.0, seed: int = 0):
         self.dev = device
         optim = optim or OptimConfig()
         self.pg = process_group
@@ -66,6 +66,14 @@ class NativeTrainer:
         self.prog.build_backward()
         self.opt = optim
         self.smoothing = label_smoothing
+        # CutMix (Composer's CutMix(alpha), `03_composer/01_cifar_composer_resnet.ipynb:430`): per step a
+        # batch permutation and one box are sampled here (host, tiny) and applied on the device by the
+        # augment kernel (paste) and the CE kernel (mixed soft targets) inside the captured step
+        self.cutmix_alpha = float(cutmix_alpha)
+        self._rng = __import__("numpy").random.default_rng(seed + 7919 * (dist.get_rank(process_group)
+                                                                          if self.world > 1 else 0))
+        if self.cutmix_alpha > 0:
+            self.prog.enable_cutmix()
         n = self.prog.n_params
         self.mom = torch.zeros(n, device=device)
         self.mom2 = torch.zeros(n, device=device) if optim.name in ("adam", "adamw") else None
@@ -262,6 +270,28 @@ class NativeTrainer:
                 chunk.copy_(buf)
             pos = end
 
+    def _sample_cutmix(self):
+        """lam ~ Beta(a, a); box of area (1 - lam) at a uniform centre, clipped; lam re-derived from
+        the clipped area (Composer's CutMix); one permutation of the batch."""
+        p, r = self.prog, self._rng
+        H, W = p.H, p.W
+        lam = float(r.beta(self.cutmix_alpha, self.cutmix_alpha))
+        cut = (1.0 - lam) ** 0.5
+        ch, cw = int(H * cut), int(W * cut)
+        cy, cx = int(r.integers(0, H)), int(r.integers(0, W))
+        y0, y1 = min(max(cy - ch // 2, 0), H), min(max(cy + ch // 2, 0), H)
+        x0, x1 = min(max(cx - cw // 2, 0), W), min(max(cx + cw // 2, 0), W)
+        lam = 1.0 - (y1 - y0) * (x1 - x0) / float(H * W)
+        perm = torch.from_numpy(r.permutation(p.N).astype("int32"))
+        box = torch.tensor([y0, y1, x0, x1], dtype=torch.int32)
+        lamt = torch.tensor([lam], dtype=torch.float32)
+        if self.dev.type == "cuda":
+            perm, box, lamt = perm.pin_memory(), box.pin_memory(), lamt.pin_memory()
+        self._mix_host = (perm, box, lamt)  # keep the pinned sources alive until the copies ran
+        p.mix_perm.copy_(perm, non_blocking=True)
+        p.mix_box.copy_(box, non_blocking=True)
+        p.mix_lam.copy_(lamt, non_blocking=True)
+
     def _set_hyper(self):
         o = self.opt
         self.step_count += 1
@@ -362,6 +392,8 @@ class NativeTrainer:
             p.boxes.copy_(boxes, non_blocking=True)
         if flips is not None:
             p.flip.copy_(flips, non_blocking=True)
+        if self.cutmix_alpha > 0:
+            self._sample_cutmix()
         self._set_hyper()
         self._step_inner()
         if self.zero is not None:

@@ -461,6 +461,18 @@ class ResNetProgram:
             bn.coeff = self.bn_arena[o:o + 3 * bn.C]; o += 3 * bn.C
         self.mean_t = torch.tensor(IMAGENET_MEAN)
         self.std_t = torch.tensor(IMAGENET_STD)
+        # CutMix state (enable_cutmix): sampled on the host per step, consumed on the device by the
+        # augment kernel (box paste) and the CE kernel (mixed soft targets)
+        self.cutmix = False
+        self.mix_perm = self.mix_box = self.mix_lam = self.labels2 = None
+
+    def enable_cutmix(self) -> None:
+        dev = self.dev
+        self.cutmix = True
+        self.mix_perm = torch.arange(self.N, device=dev, dtype=torch.int32)
+        self.mix_box = torch.zeros(4, device=dev, dtype=torch.int32)  # y0, y1, x0, x1 (empty: no mixing)
+        self.mix_lam = torch.ones(1, device=dev, dtype=torch.float32)
+        self.labels2 = torch.zeros(self.N, device=dev, dtype=torch.int64)
 
     # ----------------------------------------------------------------------------------
     # per-step pieces
@@ -493,7 +505,11 @@ class ResNetProgram:
         std = self.norm_std or (IMAGENET_STD if self.in_ch == 3 else (0.5, 0.5, 0.5))
         if self.norm_mean and len(mean) == 1:
             mean, std = mean * 3, std * 3
-        K.augment_u8(self.img_u8, self.x4, self.boxes, mean, std, self.flip if flip is None else flip)
+        mix = self.cutmix and self.training
+        K.augment_u8(self.img_u8, self.x4, self.boxes, mean, std, self.flip if flip is None else flip,
+                     perm=self.mix_perm if mix else None, mixbox=self.mix_box if mix else None)
+        if mix:  # the pasted samples' labels (device gather, inside the captured step)
+            torch.index_select(self.labels, 0, self.mix_perm.long(), out=self.labels2)
 
     def _bn_fwd(self, bn: BNL, count: int):
         mod = bn.mod
@@ -559,9 +575,12 @@ class ResNetProgram:
         K.avgpool_fwd(x, self.pooled)
         if features_only:
             return self.pooled
-        torch.addmm(self.fc_b16, self.pooled, self.fc_w16.t(), out=self.logits)
+        F, Cn = self.feat_c, self.num_classes
+        K.small_gemm(self.pooled, self.fc_w16, self.logits, M=N, N=Cn, K=F, bias=self.fc_b16)
+        mix = self.cutmix and self.training
         K.softmax_ce(self.logits, self.labels, self.dlogits if compute_grad else None, None,
-                     self.metrics if metrics else None, smoothing=smoothing, grad_scale=grad_scale)
+                     self.metrics if metrics else None, smoothing=smoothing, grad_scale=grad_scale,
+                     labels2=self.labels2 if mix else None, lam=self.mix_lam if mix else None)
         return self.logits
 
     def backward_segments(self):
@@ -615,10 +634,12 @@ class ResNetProgram:
             self._side_pending = False
 
     def _bwd_head(self):
-        # fc: dW = dlogits^T @ pooled (fp32 accumulate), db = sum dlogits, dpooled = dlogits @ W
-        torch.mm(self.dlogits.t().float(), self.pooled.float(), out=self.fc_w_grad)
-        torch.sum(self.dlogits.float(), 0, out=self.fc_b_grad)
-        torch.mm(self.dlogits, self.fc_w16, out=self.dpooled)
+        # fc on MFMA (csrc/head_ops.hip): dW = dlogits^T pooled (fp32, straight into the flat gradient),
+        # db = column sums of dlogits, dpooled = dlogits W
+        N, F, Cn = self.N, self.feat_c, self.num_classes
+        K.small_gemm(self.dlogits, self.pooled, self.fc_w_grad, ta=True, tb=True, M=Cn, N=F, K=N)
+        K.colsum(self.dlogits, self.fc_b_grad)
+        K.small_gemm(self.dlogits, self.fc_w16, self.dpooled, ta=False, tb=True, M=N, N=F, K=Cn)
         K.avgpool_bwd(self.dpooled, self.dlast)
 
     def _bn_bwd(self, bn: BNL, dout, y, dy, count, mask_mode, mref=None, gout=None):

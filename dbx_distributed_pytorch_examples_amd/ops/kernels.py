@@ -739,7 +739,11 @@ def avgpool_bwd(dout, dx):
 
 
 @_dispatch
-def softmax_ce(logits, labels, dlogits=None, loss_out=None, stats=None, smoothing=0.0, grad_scale=1.0):
+def softmax_ce(logits, labels, dlogits=None, loss_out=None, stats=None, smoothing=0.0, grad_scale=1.0,
+               labels2=None, lam=None):
+    """Fused softmax cross-entropy (+ label smoothing) with dlogits, per-row loss, device-side
+    loss-sum / correct counters. ``labels2`` [B] int64 + ``lam`` fp32[1] device (CutMix): the target
+    is lam * onehot(labels) + (1 - lam) * onehot(labels2), smoothed on top."""
     B, Cc = logits.shape
     if logits.dtype not in (torch.float32, torch.bfloat16) or not logits.is_contiguous():
         raise TypeError("logits must be contiguous fp32/bf16")
@@ -748,8 +752,71 @@ def softmax_ce(logits, labels, dlogits=None, loss_out=None, stats=None, smoothin
         _chk(dlogits, logits.dtype, "dlogits", B * Cc)
     if stats is not None:
         _chk(stats, torch.float64, "stats", 2)
+    if (labels2 is None) != (lam is None):
+        raise ValueError("labels2 and lam come together")
+    if labels2 is not None:
+        _chk(labels2, torch.int64, "labels2", B)
+        _chk(lam, torch.float32, "lam", 1)
     C().softmax_ce(logits.data_ptr(), int(logits.dtype == torch.bfloat16), labels.data_ptr(), _p(dlogits),
-                   _p(loss_out), _p(stats), B, Cc, float(smoothing), float(grad_scale), stream_ptr())
+                   _p(loss_out), _p(stats), B, Cc, float(smoothing), float(grad_scale), _p(labels2), _p(lam),
+                   stream_ptr())
+
+
+def dropout_threshold(p_drop: float) -> Tuple[int, float]:
+    """(thresh, 1/keep) for a Philox draw u32 < thresh keeping an element with prob 1 - p_drop."""
+    keep = 1.0 - float(p_drop)
+    if not 0.0 < keep <= 1.0:
+        raise ValueError("dropout probability must be in [0, 1)")
+    return min(0xFFFFFFFF, int(round(keep * 4294967296.0))), 1.0 / keep
+
+
+@_dispatch
+def small_gemm(A, B, out, *, ta=False, tb=False, M, N, K, alpha=1.0, bias=None, accumulate=False,
+               dropout=None):
+    """out[M, N] (fp32 / bf16) = alpha * A(m, k) B(k, n) (+ bias[n]) (+ out) on MFMA (csrc/head_ops.hip).
+    A: ``ta`` False -> [M, K], True -> [K, M]; B: ``tb`` False -> [N, K], True -> [K, N] (bf16, contiguous).
+    ``dropout``: (operand "A" | "B", p, seed, offset) -- Philox mask on that operand's elements."""
+    _chk(A, torch.bfloat16, "A", M * K)
+    _chk(B, torch.bfloat16, "B", N * K)
+    if out.dtype not in (torch.float32, torch.bfloat16) or out.numel() != M * N or not out.is_contiguous():
+        raise ValueError("out must be a contiguous fp32/bf16 [M, N]")
+    bf = bh = None
+    if bias is not None:
+        if bias.numel() != N:
+            raise ValueError("bias must have N elements")
+        bf, bh = (bias, None) if bias.dtype == torch.float32 else (None, bias)
+    drop, seed, off, thr, inv = 0, 0, 0, 0, 1.0
+    if dropout is not None:
+        which, pd, seed, off = dropout
+        drop = 1 if which == "A" else 2
+        thr, inv = dropout_threshold(pd)
+    lda = M if ta else K
+    ldb = N if tb else K
+    C().small_gemm(int(ta), int(tb), int(out.dtype == torch.float32), drop, A.data_ptr(), B.data_ptr(), out.data_ptr(),
+                   _p(bf), _p(bh), M, N, K, lda, ldb, N, float(alpha), int(accumulate), int(seed) & ((1 << 64) - 1),
+                   int(off) & 0xFFFFFFFF, thr, float(inv), stream_ptr())
+    return out
+
+
+@_dispatch
+def colsum(x, out, accumulate=False):
+    """out[n] (+)= sum_m x[m, n] (bf16 -> fp32, fixed order): the fc bias gradient."""
+    M, N = x.shape
+    _chk(x, torch.bfloat16, "x")
+    _chk(out, torch.float32, "out", N)
+    C().colsum(x.data_ptr(), out.data_ptr(), M, N, int(accumulate), stream_ptr())
+    return out
+
+
+@_dispatch
+def dropout(x, y, p, seed, offset):
+    """y = x * Philox mask (keep 1-p, scale 1/(1-p)); the same (seed, offset) regenerate the mask."""
+    _chk(x, torch.bfloat16, "x")
+    _chk(y, torch.bfloat16, "y", x.numel())
+    thr, inv = dropout_threshold(p)
+    C().dropout(x.data_ptr(), y.data_ptr(), x.numel(), int(seed) & ((1 << 64) - 1), int(offset) & 0xFFFFFFFF, thr,
+                float(inv), stream_ptr())
+    return y
 
 
 @_dispatch
@@ -837,9 +904,11 @@ def normalize_u8(img, out, mean, std, flip=None):
 
 
 @_dispatch
-def augment_u8(img, out, boxes, mean, std, flip=None):
+def augment_u8(img, out, boxes, mean, std, flip=None, perm=None, mixbox=None):
     """uint8 NHWC -> bf16 NHWC4: per-sample crop box [N,4] (y0, x0, h, w; fp32) bilinear-resized to
-    out's H x W, optional flip [N] uint8, normalised."""
+    out's H x W, optional flip [N] uint8, normalised. CutMix: ``perm`` [N] int32 + ``mixbox`` int32
+    [y0, y1, x0, x1] (output coordinates; empty box = no mixing) paste sample perm[n]'s augmented
+    pixels into the box."""
     N, Hin, Win, Cin = img.shape
     _, Ho, Wo, C4 = out.shape
     _chk(img, torch.uint8, "img")
@@ -847,9 +916,14 @@ def augment_u8(img, out, boxes, mean, std, flip=None):
     _chk(boxes, torch.float32, "boxes", N * 4)
     if flip is not None:
         _chk(flip, torch.uint8, "flip", N)
+    if (perm is None) != (mixbox is None):
+        raise ValueError("perm and mixbox come together")
+    if perm is not None:
+        _chk(perm, torch.int32, "perm", N)
+        _chk(mixbox, torch.int32, "mixbox", 4)
     C().augment_u8(img.data_ptr(), out.data_ptr(), boxes.data_ptr(), _p(flip), N, Hin, Win, Cin, Ho, Wo,
                    float(mean[0]), float(mean[1]), float(mean[2]), float(std[0]), float(std[1]), float(std[2]),
-                   stream_ptr())
+                   _p(perm), _p(mixbox), stream_ptr())
 
 
 @_dispatch

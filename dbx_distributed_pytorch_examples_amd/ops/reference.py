@@ -336,12 +336,15 @@ def avgpool_bwd(dout, dx):
     dx.copy_((dout.float() / (H * W))[:, None, None, :].expand(N, H, W, C).bfloat16())
 
 
-def softmax_ce(logits, labels, dlogits=None, loss_out=None, stats=None, smoothing=0.0, grad_scale=1.0):
+def softmax_ce(logits, labels, dlogits=None, loss_out=None, stats=None, smoothing=0.0, grad_scale=1.0,
+               labels2=None, lam=None):
     B, C = logits.shape
     lf = logits.float()
     lse = torch.logsumexp(lf, 1)
     xl = lf.gather(1, labels[:, None]).squeeze(1)
-    loss = (1 - smoothing) * (lse - xl) + smoothing * (lse - lf.mean(1))
+    lm = float(lam.reshape(-1)[0]) if labels2 is not None else 1.0
+    xl2 = lf.gather(1, labels2[:, None]).squeeze(1) if labels2 is not None else xl
+    loss = (1 - smoothing) * (lm * (lse - xl) + (1 - lm) * (lse - xl2)) + smoothing * (lse - lf.mean(1))
     if loss_out is not None:
         loss_out.copy_(loss)
     if stats is not None:
@@ -350,7 +353,9 @@ def softmax_ce(logits, labels, dlogits=None, loss_out=None, stats=None, smoothin
     if dlogits is not None:
         p = torch.softmax(lf, 1)
         t = torch.full_like(p, smoothing / C)
-        t.scatter_add_(1, labels[:, None], torch.full((B, 1), 1 - smoothing, device=p.device))
+        t.scatter_add_(1, labels[:, None], torch.full((B, 1), (1 - smoothing) * lm, device=p.device))
+        if labels2 is not None:
+            t.scatter_add_(1, labels2[:, None], torch.full((B, 1), (1 - smoothing) * (1 - lm), device=p.device))
         dlogits.copy_(((p - t) * grad_scale / B).to(dlogits.dtype))
 
 
@@ -426,7 +431,14 @@ def normalize_u8(img, out, mean, std, flip=None):
     out.copy_(o.bfloat16())
 
 
-def augment_u8(img, out, boxes, mean, std, flip=None):
+def augment_u8(img, out, boxes, mean, std, flip=None, perm=None, mixbox=None):
+    if perm is not None:  # CutMix: the augmented batch, then the box pasted from sample perm[n]
+        augment_u8(img, out, boxes, mean, std, flip)
+        y0, y1, x0, x1 = (int(v) for v in mixbox.tolist())
+        if y0 < y1 and x0 < x1:
+            src = out.clone()
+            out[:, y0:y1, x0:x1] = src[perm.long()][:, y0:y1, x0:x1]
+        return
     N, Hin, Win, Cin = img.shape
     _, Ho, Wo, _ = out.shape
     dev = img.device
@@ -479,3 +491,71 @@ def lars_scale(p, g, seg_off, seg_len, adapt, norms, *, grad_scale, eta, weight_
         if a:
             trust = float(eta * wn / (gn + weight_decay * wn)) if (wn > 0 and gn > 0) else 1.0
             d.add_(w, alpha=weight_decay).mul_(trust)
+
+
+# ---- classifier head (csrc/head_ops.hip) ------------------------------------------------------------
+def philox_u32(idx, seed: int, offset: int):
+    """Philox-4x32-10 word ``idx % 4`` of counter (idx / 4 lo, idx / 4 hi, offset, 0), key seed --
+    bit-identical to head_ops.hip (numpy uint64 arithmetic)."""
+    import numpy as np
+    idx = np.asarray(idx, dtype=np.uint64)
+    M32 = np.uint64(0xFFFFFFFF)
+    c0 = (idx >> np.uint64(2)) & M32
+    c1 = (idx >> np.uint64(34)) & M32
+    c2 = np.full_like(idx, np.uint64(offset & 0xFFFFFFFF))
+    c3 = np.zeros_like(idx)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        n0 = (p1 >> np.uint64(32)) ^ c1 ^ np.uint64(k0)
+        n1 = p1 & M32
+        n2 = (p0 >> np.uint64(32)) ^ c3 ^ np.uint64(k1)
+        n3 = p0 & M32
+        c0, c1, c2, c3 = n0, n1, n2, n3
+        k0 = (k0 + 0x9E3779B9) & 0xFFFFFFFF
+        k1 = (k1 + 0xBB67AE85) & 0xFFFFFFFF
+    w = idx & np.uint64(3)
+    return np.where(w == 0, c0, np.where(w == 1, c1, np.where(w == 2, c2, c3)))
+
+
+def dropout_mask(numel: int, p: float, seed: int, offset: int, device=None) -> torch.Tensor:
+    import numpy as np
+    keep = 1.0 - p
+    thr = min(0xFFFFFFFF, int(round(keep * 4294967296.0)))
+    u = philox_u32(np.arange(numel, dtype=np.uint64), seed, offset)
+    return torch.from_numpy((u < np.uint64(thr)).astype(np.float32) / keep).to(device)
+
+
+def small_gemm(A, B, out, *, ta=False, tb=False, M, N, K, alpha=1.0, bias=None, accumulate=False, dropout=None):
+    a = A.float().reshape(K, M).t() if ta else A.float().reshape(M, K)
+    b = B.float().reshape(K, N) if tb else B.float().reshape(N, K).t()
+    if dropout is not None:
+        which, pd, seed, off = dropout
+        src = A if which == "A" else B
+        mk = dropout_mask(src.numel(), pd, int(seed), int(off), src.device).reshape(src.shape)
+        if which == "A":
+            a = (A.float() * mk).bfloat16().float().reshape(K, M).t() if ta else \
+                (A.float() * mk).bfloat16().float().reshape(M, K)
+        else:
+            b = (B.float() * mk).bfloat16().float().reshape(K, N) if tb else \
+                (B.float() * mk).bfloat16().float().reshape(N, K).t()
+    r = alpha * (a @ b)
+    if bias is not None:
+        r = r + bias.float().reshape(1, N)
+    o = out.reshape(M, N)
+    if accumulate:
+        r = r + o.float()
+    o.copy_(r.to(out.dtype))
+    return out
+
+
+def colsum(x, out, accumulate=False):
+    s = x.float().sum(0)
+    out.copy_(out + s if accumulate else s)
+    return out
+
+
+def dropout(x, y, p, seed, offset):
+    y.copy_((x.float() * dropout_mask(x.numel(), p, int(seed), int(offset), x.device).reshape(x.shape)).to(y.dtype))
+    return y

@@ -136,7 +136,8 @@ class _Native:
                                                       trust_coefficient=o.trust_coefficient),
                                     label_smoothing=cfg.data.label_smoothing, use_graphs=cfg.graphs,
                                     bucket_cap_mb=cfg.bucket_cap_mb, allreduce_dtype=ar,
-                                    src_hw=(h, w), mean=mean, std=std, zero_stage=cfg.zero.stage)
+                                    src_hw=(h, w), mean=mean, std=std, zero_stage=cfg.zero.stage,
+                                    cutmix_alpha=cfg.data.cutmix_alpha, seed=cfg.seed)
         if not cfg.data.augment:
             aug = AugmentSpec()
         elif (h, w) == (s, s) and s <= 64:
@@ -262,7 +263,7 @@ def _pick_engine(cfg: TrainConfig, model, ds, dev) -> str:
         not any(p.requires_grad for p in model.resnet.parameters() if p is not None and
                 not any(p is q for q in model.resnet.fc.parameters()))
     if dev.type == "cuda" and (supports(model) or frozen) and _uint8_source(ds) and cfg.grad_accum == 1 \
-            and cfg.data.cutmix_alpha == 0:
+            and (cfg.data.cutmix_alpha == 0 or not frozen):  # CutMix: native box paste + soft-target CE
         return "native"
     return "autograd"
 
