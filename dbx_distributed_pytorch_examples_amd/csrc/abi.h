@@ -106,6 +106,7 @@ struct GemmArgs {
   unsigned long long seed;
   unsigned offset, thresh;  // dropout: keep if the Philox draw < thresh
   float inv_keep;
+  const unsigned* offset_dev;  // nullable: the Philox offset read from device memory (graph replays)
 };
 
 }  // namespace dbx

@@ -61,7 +61,8 @@ int dbx_augment_u8(const unsigned char*, bf16*, const float*, const unsigned cha
                    float, float, float, float, float, const int*, const int*, hipStream_t);
 int dbx_small_gemm(int, int, int, int, const dbx::GemmArgs*, hipStream_t);
 int dbx_colsum(const bf16*, float*, int, int, int, hipStream_t);
-int dbx_dropout(const bf16*, bf16*, long long, unsigned long long, unsigned, unsigned, float, hipStream_t);
+int dbx_dropout(const bf16*, bf16*, long long, unsigned long long, unsigned, unsigned, float, const unsigned*,
+                hipStream_t);
 int dbx_cast_f32_bf16(const float*, bf16*, long long, hipStream_t);
 int dbx_cast_bf16_f32(const bf16*, float*, long long, float, int, hipStream_t);
 }
@@ -285,18 +286,21 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("small_gemm", [](int ta, int tb, int out_f32, int drop, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias_f,
                          uintptr_t bias_h, int M, int N, int K, int lda, int ldb, int ldc, float alpha, int accumulate,
-                         unsigned long long seed, unsigned offset, unsigned thresh, float inv_keep, uintptr_t st) {
+                         unsigned long long seed, unsigned offset, unsigned thresh, float inv_keep, uintptr_t offset_dev,
+                         uintptr_t st) {
     // classifier-head GEMM (head_ops.hip)
     dbx::GemmArgs g{P<const bf16*>(A), P<const bf16*>(B), P<void*>(C), P<const float*>(bias_f), P<const bf16*>(bias_h),
-                    M, N, K, lda, ldb, ldc, alpha, accumulate, seed, offset, thresh, inv_keep};
+                    M, N, K, lda, ldb, ldc, alpha, accumulate, seed, offset, thresh, inv_keep,
+                    P<const unsigned*>(offset_dev)};
     check(dbx_small_gemm(ta, tb, out_f32, drop, &g, S(st)), "small_gemm");
   });
   m.def("colsum", [](uintptr_t X, uintptr_t out, int M, int N, int accumulate, uintptr_t st) {
     check(dbx_colsum(P<const bf16*>(X), P<float*>(out), M, N, accumulate, S(st)), "colsum");
   });
   m.def("dropout", [](uintptr_t x, uintptr_t y, long long n, unsigned long long seed, unsigned offset, unsigned thresh,
-                      float inv_keep, uintptr_t st) {
-    check(dbx_dropout(P<const bf16*>(x), P<bf16*>(y), n, seed, offset, thresh, inv_keep, S(st)), "dropout");
+                      float inv_keep, uintptr_t offset_dev, uintptr_t st) {
+    check(dbx_dropout(P<const bf16*>(x), P<bf16*>(y), n, seed, offset, thresh, inv_keep, P<const unsigned*>(offset_dev),
+                      S(st)), "dropout");
   });
   m.def("weight_prep16", [](uintptr_t src, uintptr_t wbuf, uintptr_t desc, int nlayers, uintptr_t st) {
     check(dbx_weight_prep16(P<const bf16*>(src), P<bf16*>(wbuf), P<const void*>(desc), nlayers, S(st)),

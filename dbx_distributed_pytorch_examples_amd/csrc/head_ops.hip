@@ -52,6 +52,7 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
   __shared__ __attribute__((aligned(16))) bf16 sB[BN * BK];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const unsigned doff = (DROP && g.offset_dev) ? *g.offset_dev : g.offset;  // step counter (device)
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
       for (int j = 0; j < 8; ++j) {
         const int k = kk + j;
         const unsigned long long e = T == 0 ? (unsigned long long)r * ld + k : (unsigned long long)k * ld + r;
-        v[j] = (bf16)((float)v[j] * drop_scale(e, g.seed, g.offset, g.thresh, g.inv_keep));
+        v[j] = (bf16)((float)v[j] * drop_scale(e, g.seed, doff, g.thresh, g.inv_keep));
       }
     }
     *reinterpret_cast<bf16x8*>(img + srow * BK + swz(srow, sch) * 8) = v;
@@ -147,7 +148,8 @@ __global__ void colsum_kernel(const bf16* __restrict__ X, float* __restrict__ ou
 
 // y = x * dropout-mask (the forward's h, for frozen-head training that keeps it; deterministic)
 __global__ void dropout_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long long n, unsigned long long seed,
-                               unsigned offset, unsigned thresh, float inv_keep) {
+                               unsigned offset, unsigned thresh, float inv_keep, const unsigned* offset_dev) {
+  if (offset_dev) offset = *offset_dev;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     y[i] = (bf16)((float)x[i] * drop_scale((unsigned long long)i, seed, offset, thresh, inv_keep));
 }
@@ -188,9 +190,10 @@ extern "C" int dbx_colsum(const bf16* X, float* out, int M, int N, int accumulat
 }
 
 extern "C" int dbx_dropout(const bf16* x, bf16* y, long long n, unsigned long long seed, unsigned offset,
-                           unsigned thresh, float inv_keep, hipStream_t st) {
+                           unsigned thresh, float inv_keep, const unsigned* offset_dev, hipStream_t st) {
   long long blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(dropout_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, n, seed, offset, thresh, inv_keep);
+  hipLaunchKernelGGL(dropout_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, n, seed, offset, thresh, inv_keep,
+                     offset_dev);
   return (int)hipGetLastError();
 }

@@ -775,7 +775,8 @@ def small_gemm(A, B, out, *, ta=False, tb=False, M, N, K, alpha=1.0, bias=None, 
                dropout=None):
     """out[M, N] (fp32 / bf16) = alpha * A(m, k) B(k, n) (+ bias[n]) (+ out) on MFMA (csrc/head_ops.hip).
     A: ``ta`` False -> [M, K], True -> [K, M]; B: ``tb`` False -> [N, K], True -> [K, N] (bf16, contiguous).
-    ``dropout``: (operand "A" | "B", p, seed, offset) -- Philox mask on that operand's elements."""
+    ``dropout``: (operand "A" | "B", p, seed, offset) -- Philox mask on that operand's elements; ``offset``
+    an int or an int32[1] device tensor (read by the kernel: a replayed graph draws a new mask each step)."""
     _chk(A, torch.bfloat16, "A", M * K)
     _chk(B, torch.bfloat16, "B", N * K)
     if out.dtype not in (torch.float32, torch.bfloat16) or out.numel() != M * N or not out.is_contiguous():
@@ -785,16 +786,19 @@ def small_gemm(A, B, out, *, ta=False, tb=False, M, N, K, alpha=1.0, bias=None, 
         if bias.numel() != N:
             raise ValueError("bias must have N elements")
         bf, bh = (bias, None) if bias.dtype == torch.float32 else (None, bias)
-    drop, seed, off, thr, inv = 0, 0, 0, 0, 1.0
+    drop, seed, off, thr, inv, offd = 0, 0, 0, 0, 1.0, None
     if dropout is not None:
         which, pd, seed, off = dropout
         drop = 1 if which == "A" else 2
         thr, inv = dropout_threshold(pd)
+        if isinstance(off, torch.Tensor):
+            _chk(off, torch.int32, "dropout offset", 1)
+            off, offd = 0, off
     lda = M if ta else K
     ldb = N if tb else K
     C().small_gemm(int(ta), int(tb), int(out.dtype == torch.float32), drop, A.data_ptr(), B.data_ptr(), out.data_ptr(),
                    _p(bf), _p(bh), M, N, K, lda, ldb, N, float(alpha), int(accumulate), int(seed) & ((1 << 64) - 1),
-                   int(off) & 0xFFFFFFFF, thr, float(inv), stream_ptr())
+                   int(off) & 0xFFFFFFFF, thr, float(inv), _p(offd), stream_ptr())
     return out
 
 
@@ -814,8 +818,12 @@ def dropout(x, y, p, seed, offset):
     _chk(x, torch.bfloat16, "x")
     _chk(y, torch.bfloat16, "y", x.numel())
     thr, inv = dropout_threshold(p)
+    offd = None
+    if isinstance(offset, torch.Tensor):
+        _chk(offset, torch.int32, "offset", 1)
+        offset, offd = 0, offset
     C().dropout(x.data_ptr(), y.data_ptr(), x.numel(), int(seed) & ((1 << 64) - 1), int(offset) & 0xFFFFFFFF, thr,
-                float(inv), stream_ptr())
+                float(inv), _p(offd), stream_ptr())
     return y
 
 

@@ -533,7 +533,8 @@ def small_gemm(A, B, out, *, ta=False, tb=False, M, N, K, alpha=1.0, bias=None, 
     if dropout is not None:
         which, pd, seed, off = dropout
         src = A if which == "A" else B
-        mk = dropout_mask(src.numel(), pd, int(seed), int(off), src.device).reshape(src.shape)
+        off = int(off.reshape(-1)[0]) if isinstance(off, torch.Tensor) else int(off)
+        mk = dropout_mask(src.numel(), pd, int(seed), off, src.device).reshape(src.shape)
         if which == "A":
             a = (A.float() * mk).bfloat16().float().reshape(K, M).t() if ta else \
                 (A.float() * mk).bfloat16().float().reshape(M, K)
@@ -557,5 +558,6 @@ def colsum(x, out, accumulate=False):
 
 
 def dropout(x, y, p, seed, offset):
+    offset = int(offset.reshape(-1)[0]) if isinstance(offset, torch.Tensor) else int(offset)
     y.copy_((x.float() * dropout_mask(x.numel(), p, int(seed), int(offset), x.device).reshape(x.shape)).to(y.dtype))
     return y
