@@ -458,9 +458,15 @@ static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, int dma, hipSt
 }
 
 
+extern "C" int dbx_conv_fast(int mode, int bn, const IGemmArgs* args, int stats, int accum, int epi, hipStream_t st);
+
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
                               int accum, int epi, hipStream_t st, int dma) {
   const IGemmArgs& a = *args;
+  if (dma == 4) {  // eight-wave 256-row kernel (conv_fast.hip): plain operands, stride-1 data gradients
+    if (bm != 256 || pro || mode == STEM || (mode == DGRAD && (a.osub != 1 || a.add_sub > 1))) return -65;
+    return dbx_conv_fast(mode, bn, args, stats, accum, epi, st);
+  }
   if (mode == FWD_PATCH || mode == DGRAD_PATCH) {  // 3x3 weights-stationary patch kernel (conv_patch3.hip)
     if (pro && !a.relu_in) return -7;
     return dbx_conv_patch3(mode == FWD_PATCH ? FWD : DGRAD, args, pro, stats, epi, st, dma);  // dma: 1 = streamed
