@@ -196,7 +196,7 @@ extern "C" int dbx_conv_fast(int mode, int bn, const IGemmArgs* args, int stats,
                              : launch_fast<BN_, DGRAD, false, false, 0>(a, st);               \
   if (epi == 1) return accum ? launch_fast<BN_, DGRAD, false, true, 1>(a, st)                  \
                              : launch_fast<BN_, DGRAD, false, false, 1>(a, st);
-    if (bn == 256) {  // the MASK_Y epilogue next to 128 accumulators per lane spills: 128-wide tiles
+    if (bn == 256) {  // the MASK_Y epilogue next to 128 accumulators per lane spills (~95 VGPRs): 128-wide
       DBX_FAST_DG(256)
       return -66;
     }

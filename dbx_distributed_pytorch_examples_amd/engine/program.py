@@ -179,6 +179,10 @@ class ResNetProgram:
         # streaming pool/BN pass + the stem wgrad (the 4-window argmax routing per element is VALU work
         # that the two-workgroups-per-CU MFMA kernel cannot hide; profiles/r2s4_stem/)
         self.fuse_stem_bwd = os.environ.get("DBX_FUSE_STEM_BWD", "0") == "1"
+        # 3x3 convs whose plain-operand shape has an eight-wave kernel entry (ops/tune_table.json "fwd0",
+        # csrc/conv_fast.hip): the forward materialises the input BN output relu(bn(y)) once (the
+        # block's acts buffer, which backward needs anyway) and runs the conv without a prologue
+        self.fast_mat = os.environ.get("DBX_FAST_MAT", "1") == "1"
         self._wstream = None
         self._side_pending = False
         self.param_align = max(16, int(param_align))
@@ -401,6 +405,8 @@ class ResNetProgram:
             # dgrad epilogue that computes them for the ReLU mask anyway: the weight gradient then
             # reads them instead of re-applying BN+ReLU to every staged tile
             b.acts = [E(N, cv.OH, cv.OW, cv.OC) if self.act_writeback else None for cv in b.convs[:-1]]
+            # acts[j] computed in the forward (eight-wave consumer conv j+1): see self.fast_mat
+            b.mat = [self._materialize(b.convs[j + 1]) and b.acts[j] is not None for j in range(len(b.convs) - 1)]
             h, w, c = b.in_shape
             b.dx = E(N, h, w, c)
             if b.ds_conv is not None:
@@ -547,6 +553,10 @@ class ResNetProgram:
                                in_shift=pb.bns[-1].shift, relu_in=True, tail_res=res, tail_res_scale=rsc,
                                tail_res_shift=rsh, tail_out=pb.out, tail_bits=pb.obits if tr else None)
                     pending = None
+                elif i > 0 and b.mat[i - 1]:  # materialised BN output -> plain-operand (eight-wave) conv
+                    K.bn_apply(b.ys[i - 1], prev_bn.scale, prev_bn.shift, b.acts[i - 1], relu=True)
+                    K.conv_fwd(b.acts[i - 1], cv.w16, b.ys[i], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
+                               stats=b.bns[i].stats if tr else None)
                 else:
                     src = x if i == 0 else b.ys[i - 1]
                     K.conv_fwd(src, cv.w16, b.ys[i], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
@@ -718,9 +728,11 @@ class ResNetProgram:
                 self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                             in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
             if kw is not None:
+                # (the forward materialised acts[j-1] already when b.mat[j-1]: no write-back)
                 K.conv_dgrad(src, cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                              epilogue=K.BNBwdEpilogue(K.MASK_Y, b.ys[j - 1], pbn.mean, pbn.invstd, pbn.bstats,
-                                                      scale=pbn.scale, shift=pbn.shift, act_out=act), **kw)
+                                                      scale=pbn.scale, shift=pbn.shift,
+                                                      act_out=None if b.mat[j - 1] else act), **kw)
             if act is not None:
                 self._wgrad(b.dys[j], act, cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad)
             elif kw and not pre:
@@ -764,6 +776,13 @@ class ResNetProgram:
                      addsrc=addsrc, add_sub=sub, epilogue=epi, **kw0)
         if kw0:
             self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
+
+    def _materialize(self, cv: ConvL) -> bool:
+        """Does conv ``cv`` (a block-internal 3x3) take a materialised BN output on the eight-wave kernel?"""
+        if not (self.fast_mat and self.dev.type == "cuda" and cv.R == 3 and cv.stride == 1):
+            return False
+        t = K.pick_tile(self.N * cv.OH * cv.OW, cv.OC, "fwd0", cv.IC, cv.R, cv.stride)
+        return len(t) > 2 and t[2] in (4, 5)
 
     def _fuse3(self, b: BlockL, last: bool) -> bool:
         """Run block b's conv3 backward through K.conv_dwfused (the 64 -> 256 conv3 of the 56x56

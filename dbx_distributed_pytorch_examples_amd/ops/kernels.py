@@ -105,8 +105,12 @@ def pick_tile(M: int, OC: int, mode: str = "fwd", K_in: int = 0, R: int = 0, str
     heuristic: biggest tile that still puts >= ~2 workgroups on each of the 256 CUs."""
     if use_table:
         t = _tune_table().get(tune_key(mode, M, OC, K_in, R, stride))
-        if t is None and (mode == "fwdt" or mode.endswith("b")):  # prologue variants: the plain winner
-            t = _tune_table().get(tune_key("fwd" if mode == "fwdt" else mode[:-1], M, OC, K_in, R, stride))
+        if t is None and (mode in ("fwdt", "fwd0") or mode.endswith("b")):  # variants: the base entry
+            t = _tune_table().get(tune_key("fwd" if mode in ("fwdt", "fwd0") else mode[:-1], M, OC, K_in, R, stride))
+            if t is not None and len(t) > 2 and t[2] in (4, 5) and mode != "fwd0":
+                t = None  # an eight-wave (plain operand) entry does not serve the prologue variants
+        if t is not None and len(t) > 2 and t[2] in (4, 5) and not _fast_enabled():
+            t = None  # DBX_FAST=0: no eight-wave kernel (A/B runs)
         if t is not None and OC % t[1] == 0:
             return t  # (bm, bn) or (bm, bn, dma): a measured operand path (tools/tune_conv.py)
     if OC % 128 == 0 and ((M + 127) // 128) * (OC // 128) >= 512:
@@ -117,6 +121,16 @@ def pick_tile(M: int, OC: int, mode: str = "fwd", K_in: int = 0, R: int = 0, str
 
 
 _DMA_ENV = None
+_FAST_ENV = None
+
+
+def _fast_enabled() -> bool:
+    """DBX_FAST (default 1): use the eight-wave kernel entries of the tune table (csrc/conv_fast.hip)."""
+    global _FAST_ENV
+    if _FAST_ENV is None:
+        import os
+        _FAST_ENV = os.environ.get("DBX_FAST", "1") != "0"
+    return _FAST_ENV
 
 
 def _tile_dma(t) -> Tuple[int, int, int]:
@@ -166,7 +180,7 @@ def _use_patch3(tile, mode: str) -> int:
 @_dispatch
 def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None,
              relu_in=True, tile=None, tail_res=None, tail_res_scale=None, tail_res_shift=None, tail_out=None,
-             tail_bits=None):
+             tail_bits=None, _split=True):
     """Y = conv(act(X), W); act = relu(X*in_scale + in_shift) with a BN prologue. "Tail" mode
     (``tail_res`` given; 1x1 stride-1 convs): act = relu(X*in_scale + in_shift + r), r = tail_res or
     tail_res*tail_res_scale + tail_res_shift -- the previous residual block's output computed on the
@@ -203,13 +217,44 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     else:
         if isinstance(tile, str):
             raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 conv at width 56")
-        bm, bn, dma = _tile_dma(tile or pick_tile(N * OH * OW, OC, "fwd" if tail_res is None else "fwdt", IC, R,
-                                                  stride))
+        plain = in_scale is None and tail_res is None
+        bm, bn, dma = _tile_dma(tile or pick_tile(N * OH * OW, OC, "fwd0" if plain else
+                                                  ("fwd" if tail_res is None else "fwdt"), IC, R, stride))
+    if dma in (4, 5) and (in_scale is not None or tail_res is not None):
+        if tile is not None:
+            raise ValueError("the eight-wave kernel (tile dma 4 / 5) takes plain operands (no BN prologue / tail)")
+        bm, bn, dma = _tile_dma(pick_tile(N * OH * OW, OC, use_table=False))
+    if dma == 5:  # eight-wave kernel over the whole batch (no split)
+        dma = 4
+    elif dma == 4 and _split:
+        n1 = fast_split(N, OH * OW, OC, bn)
+        kw = dict(R=R, S=S, stride=stride, pad=pad, stats=stats, _split=False)
+        if n1 > 0:
+            conv_fwd(x[:n1], w16, out[:n1], tile=(256, bn, 4), **kw)
+        if n1 < N:  # the leftover images on small four-wave tiles (they fill the chip)
+            conv_fwd(x[n1:], w16, out[n1:], tile=pick_tile((N - n1) * OH * OW, OC, use_table=False), **kw)
+        return out
     C().conv_igemm(mode, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
                    R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
                    _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma)
     return out
+
+
+def fast_split(N: int, per_img: int, OC: int, bn: int) -> int:
+    """Images handled by the eight-wave kernel (csrc/conv_fast.hip: one 256 x bn tile per CU, one
+    workgroup per CU) when the rest of the batch goes to the four-wave kernel: the fast launch covers
+    only FULL rounds of num_cus() tiles (a partial last round would leave most CUs idle for a whole
+    tile time: 784 tiles on 256 CUs = 3.06 rounds = 4 tile times); the leftover images run as
+    small tiles that fill the chip. Returns N (no split), 0 (no full round: don't use the fast kernel)
+    or the split point."""
+    P = num_cus()
+    ntn = OC // bn
+    ntile = -(-N * per_img // 256) * ntn
+    if ntile % P == 0:
+        return N
+    full_m = (ntile // P) * P // ntn * 256
+    return min(N, full_m // per_img)
 
 
 def tail_supported(IC: int, R: int, S: int, stride: int, pad: int) -> bool:
@@ -253,6 +298,14 @@ class BNBwdEpilogue:
         self.mbits, self.scale, self.shift = mbits, scale, shift
         self.ybn2, self.mean2, self.inv2, self.stats2 = ybn2, mean2, inv2, stats2
 
+    def batch_slice(self, n0: int, n1: int, N: int) -> "BNBwdEpilogue":
+        """The same epilogue over images [n0, n1) of an N-image batch (per-pixel tensors sliced)."""
+        def sl(t):
+            return None if t is None else t.view(N, -1)[n0:n1]
+        return BNBwdEpilogue(self.mode, sl(self.ybn), self.mean1, self.inv1, self.stats1, mbits=sl(self.mbits),
+                             scale=self.scale, shift=self.shift, ybn2=sl(self.ybn2), mean2=self.mean2, inv2=self.inv2,
+                             stats2=self.stats2, act_out=sl(self.act_out))
+
     def args(self):
         return (self.mode, _p(self.mbits), _p(self.ybn), _p(self.ybn2), _p(self.scale), _p(self.shift),
                 _p(self.mean1), _p(self.inv1), _p(self.mean2), _p(self.inv2), _p(self.stats1), _p(self.stats2))
@@ -260,7 +313,7 @@ class BNBwdEpilogue:
 
 @_dispatch
 def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, addsrc=None, add_sub=1,
-               epilogue: "BNBwdEpilogue" = None, bwd_y=None, bwd_coeff=None, dy_out=None):
+               epilogue: "BNBwdEpilogue" = None, bwd_y=None, bwd_coeff=None, dy_out=None, _split=True):
     """dX = conv_transpose(dY, W): dy [N,P,Q,K], wt16 [C, R*S*K] (CRSK), dx [N,H,W,C].
 
     Stride > 1 runs one dense launch per output phase (``dgrad_phases``): no MFMA work on the
@@ -322,6 +375,25 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         return dx
     if isinstance(tile, str):
         raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 dgrad at width 56 (no addend / fold)")
+    t_sel = tile
+    if t_sel is None:
+        t_sel = pick_tile(N * H * W, Cc, f"dgrad{epilogue.mode if epilogue else 0}" + ("b" if bwd_y is not None else ""),
+                          K, R, stride)
+    if t_sel is not None and _tile_dma(t_sel)[2] in (4, 5) and (bwd_y is not None or stride != 1 or add_sub != 1):
+        if tile is not None:
+            raise ValueError("the eight-wave kernel (tile dma 4 / 5) runs stride-1 dgrads without fold / subsampled addend")
+        tile = t_sel = pick_tile(N * H * W, Cc, use_table=False)  # not eligible: the four-wave kernel
+    if t_sel is not None and _tile_dma(t_sel)[2] == 5:
+        tile = (256, _tile_dma(t_sel)[1], 4)  # eight-wave kernel over the whole batch (no split)
+    elif t_sel is not None and _tile_dma(t_sel)[2] == 4 and _split:
+        bn = _tile_dma(t_sel)[1]
+        n1 = fast_split(N, H * W, Cc, bn)
+        for (a0, a1, t) in ((0, n1, (256, bn, 4)), (n1, N, pick_tile((N - n1) * H * W, Cc, use_table=False))):
+            if a1 > a0:
+                conv_dgrad(dy[a0:a1], wt16, dx[a0:a1], R=R, S=S, stride=stride, pad=pad, accumulate=accumulate,
+                           tile=t, addsrc=None if addsrc is None else addsrc[a0:a1], add_sub=add_sub,
+                           epilogue=None if epilogue is None else epilogue.batch_slice(a0, a1, N), _split=False)
+        return dx
     phases = dgrad_phases(H, W, R, S, stride, pad)
     if not accumulate and any(ph[5] == 0 or ph[7] == 0 for ph in phases):
         if epilogue is not None:
