@@ -60,6 +60,10 @@ int dbx_weight_prep16(const bf16*, bf16*, const void*, int, hipStream_t);
 int dbx_augment_u8(const unsigned char*, bf16*, const float*, const unsigned char*, int, int, int, int, int, int, float,
                    float, float, float, float, float, const int*, const int*, hipStream_t);
 int dbx_small_gemm(int, int, int, int, const dbx::GemmArgs*, hipStream_t);
+long long dbx_mnist_saved_bytes();
+int dbx_mnist_fwd(const float*, const float*, void*, float*, int, unsigned long long, unsigned, int, hipStream_t);
+int dbx_mnist_bwd(const float*, const float*, const void*, const float*, float*, float*, int, unsigned long long,
+                  unsigned, hipStream_t);
 int dbx_colsum(const bf16*, float*, int, int, int, hipStream_t);
 int dbx_dropout(const bf16*, bf16*, long long, unsigned long long, unsigned, unsigned, float, const unsigned*,
                 hipStream_t);
@@ -293,6 +297,18 @@ PYBIND11_MODULE(_C, m) {
                     M, N, K, lda, ldb, ldc, alpha, accumulate, seed, offset, thresh, inv_keep,
                     P<const unsigned*>(offset_dev)};
     check(dbx_small_gemm(ta, tb, out_f32, drop, &g, S(st)), "small_gemm");
+  });
+  m.def("mnist_saved_bytes", []() { return dbx_mnist_saved_bytes(); });
+  m.def("mnist_fwd", [](uintptr_t x, uintptr_t params, uintptr_t saved, uintptr_t logp, int N, unsigned long long seed,
+                        unsigned offset, int train, uintptr_t st) {
+    // fused MNIST Net forward, one workgroup per image (mnist_ops.hip)
+    check(dbx_mnist_fwd(P<const float*>(x), P<const float*>(params), P<void*>(saved), P<float*>(logp), N, seed, offset,
+                        train, S(st)), "mnist_fwd");
+  });
+  m.def("mnist_bwd", [](uintptr_t x, uintptr_t params, uintptr_t saved, uintptr_t dlogp, uintptr_t gws, uintptr_t grad,
+                        int N, unsigned long long seed, unsigned offset, uintptr_t st) {
+    check(dbx_mnist_bwd(P<const float*>(x), P<const float*>(params), P<const void*>(saved), P<const float*>(dlogp),
+                        P<float*>(gws), P<float*>(grad), N, seed, offset, S(st)), "mnist_bwd");
   });
   m.def("colsum", [](uintptr_t X, uintptr_t out, int M, int N, int accumulate, uintptr_t st) {
     check(dbx_colsum(P<const bf16*>(X), P<float*>(out), M, N, accumulate, S(st)), "colsum");

@@ -5,6 +5,7 @@ Reference functions, same names / signatures, real data parallelism:
 * MNIST: ``train_one_epoch``, ``train(log_dir)``, ``test(log_dir)`` (`01_basic_torch_distributor.py:93-181`)
   and ``main_fn(directory)`` (`:248-328`: process group, ShardSampler, DDP, rank-0 checkpoint /
   log / eval) — run with ``TorchDistributor(num_processes=N, local_mode=True).run(main_fn, dir)``;
+  on a GPU the ``Net`` trains on the fused HIP kernels (``engine.native_mnist``);
 * ResNet: ``train_func(*, train_dataset, test_dataset, batch_size=32, epochs=5, mlflow_run_id=None)``
   (`02_cifar_torch_distributor_resnet.py:165-304`, `03_tiny_imagenet…:149-288`). The reference's
   version never forms a process group (each rank trains an independent replica, SURVEY.md §0);
@@ -70,13 +71,14 @@ def _mnist(train: bool, dataset=None):
 def train(log_dir: str, dataset=None, epochs: int = num_epochs, device: Optional[str] = None):
     """Single-process MNIST training (`01_basic…:134-153`); checkpoints every epoch."""
     dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
-    model = Net().to(dev)
+    from ..engine.native_mnist import native_mnist
+    model = native_mnist(Net(), dev)  # GPU: the fused HIP Net (csrc/mnist_ops.hip); CPU: the module
     loader = DataLoader(_mnist(True, dataset), batch_size=batch_size, shuffle=True)
     opt = torch.optim.SGD(model.parameters(), lr=learning_rate, momentum=momentum)
     for epoch in range(1, epochs + 1):
         train_one_epoch(model, dev, loader, opt, epoch)
         save_checkpoint(log_dir, model, opt, epoch)
-    return model
+    return getattr(model, "module", model)
 
 
 def test(log_dir: str, dataset=None, epoch: int = num_epochs, device: Optional[str] = None) -> float:
@@ -110,7 +112,12 @@ def main_fn(directory: str, train_dataset=None, test_dataset=None, epochs: int =
     ds = _mnist(True, train_dataset)
     sampler = ShardSampler(ds)
     loader = DataLoader(ds, batch_size=batch_size, sampler=sampler)
-    model = DistributedDataParallel(Net().to(info.device))
+    if info.device.type == "cuda":
+        # the fused HIP Net: broadcasts rank 0's weights and averages its flat gradient itself (DDP semantics)
+        from ..engine.native_mnist import native_mnist
+        model = native_mnist(Net(), info.device)
+    else:
+        model = DistributedDataParallel(Net().to(info.device))
     opt = torch.optim.SGD(model.parameters(), lr=learning_rate, momentum=momentum)
     for epoch in range(1, epochs + 1):
         sampler.set_epoch(epoch)

@@ -5,6 +5,9 @@ on ``engine.native_module`` (native HIP forward / backward through autograd).
 
   torch   channels_last model under autocast bf16 (what Accelerate's mixed_precision="bf16" runs)
   native  native_module(model, batch, hw): float NCHW input, bf16 HIP program, fp32 torch loss
+  prepare the notebook's own call with no flags: ``Accelerator().prepare(model, optimizer)`` (Ray config:
+          ``ray.train.torch.prepare_model(model)``) -- the frontends put the ResNet on the native
+          program by default (compiled for the first batch), the optimizer built before prepare
 
 Synthetic normalised float inputs + random labels on the device; one JSON line per (config, impl).
   python tools/bench_native_module.py [--steps 20] [--warmup 5]
@@ -36,29 +39,49 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--configs", default=",".join(CONFIGS))
+    ap.add_argument("--impls", default="torch,native,prepare")
     a = ap.parse_args()
     dev = torch.device("cuda")
     for name in a.configs.split(","):
         arch, s, nc, b, opt_name, ref = CONFIGS[name]
         x = torch.randn(b, 3, s, s, device=dev)
         y = torch.randint(0, nc, (b,), device=dev)
-        for impl in ("torch", "native"):
+        for impl in a.impls.split(","):
             torch.manual_seed(0)
             model = build_model(arch, num_classes=nc)
+            acc = None
             if impl == "native":
                 model = native_module(model, b, (s, s), dev).train()
+                xin = x
+            elif impl == "prepare":
+                from dbx_distributed_pytorch_examples_amd.frontends.accelerate import Accelerator
+                from dbx_distributed_pytorch_examples_amd.frontends.ray import prepare_model
+                opt0 = (torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4) if opt_name == "adam"
+                        else torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5))
+                if name.startswith("ray"):
+                    model = prepare_model(model).train()
+                else:
+                    acc = Accelerator(mixed_precision="bf16")
+                    model, opt0 = acc.prepare(model, opt0)
+                    model.train()
                 xin = x
             else:
                 model = model.to(dev).to(memory_format=torch.channels_last).train()
                 xin = x.contiguous(memory_format=torch.channels_last)
-            opt = (torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4) if opt_name == "adam"
-                   else torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5))
+            if impl == "prepare":
+                opt = opt0  # built before prepare, as the notebooks do
+            else:
+                opt = (torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4) if opt_name == "adam"
+                       else torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5))
 
             def step():
                 opt.zero_grad(set_to_none=True)
                 with torch.autocast("cuda", dtype=torch.bfloat16, enabled=(impl == "torch")):
                     loss = F.cross_entropy(model(xin), y, label_smoothing=0.1)
-                loss.backward()
+                if acc is not None:
+                    acc.backward(loss)
+                else:
+                    loss.backward()
                 opt.step()
             for _ in range(a.warmup):
                 step()

@@ -3,7 +3,7 @@
 set -o pipefail
 O=${1:-gpurun_out/fast_e2e}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_conv_fast_gpu.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_conv_fast_gpu.py tests/test_mnist_native_gpu.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc = 0 ] || { grep -E "Error|assert" $O/pytest.log | head -20; exit $rc; }
 for r in 1 2; do
   for f in 1 0; do
