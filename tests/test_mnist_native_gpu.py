@@ -59,10 +59,11 @@ def test_native_mnist_trains():
     torch.manual_seed(1)
     nm = native_mnist(Net(), torch.device("cuda"))
     opt = torch.optim.SGD(nm.parameters(), lr=0.05, momentum=0.5)
-    x = torch.randn(100, 1, 28, 28, device="cuda")
+    protos = torch.randn(10, 1, 28, 28, device="cuda")
     y = torch.randint(0, 10, (100,), device="cuda")
+    x = protos[y] + 0.5 * torch.randn(100, 1, 28, 28, device="cuda")  # learnable: class prototypes + noise
     losses = []
-    for _ in range(40):
+    for _ in range(60):
         opt.zero_grad()
         loss = F.nll_loss(nm(x), y)
         loss.backward()

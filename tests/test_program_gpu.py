@@ -75,6 +75,75 @@ def test_program_matches_autograd(arch, size, batch, fold, monkeypatch):
             assert _cos(b1, b2) > 0.99 or b2.abs().max() < 1e-3, n1
 
 
+class _Q(torch.autograd.Function):
+    """bf16 rounding of a stored activation (forward) and of a stored gradient (backward)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.bfloat16().float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.bfloat16().float()
+
+
+def _bf16_emulating(model):
+    """fp32 reference that rounds where the native program stores bf16: every conv / fc operand
+    (input, weight), every conv output, and every dgrad result flowing back into a conv input."""
+    def wrap(mod):
+        f = mod.forward
+
+        def fwd(x):
+            w0 = mod.weight.data
+            mod.weight.data = w0.bfloat16().float()
+            try:
+                y = f(_Q.apply(x))
+            finally:
+                mod.weight.data = w0
+            return _Q.apply(y) if isinstance(mod, torch.nn.Conv2d) else y
+        mod.forward = fwd
+    for m in model.modules():
+        if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear)):
+            wrap(m)
+    return model
+
+
+@pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 8), ("resnet18", 32, 16)])
+def test_program_grads_match_bf16_emulating_reference(arch, size, batch):
+    """Tight end-to-end check: every parameter gradient of one native step against autograd of a
+    reference that rounds to bf16 at the program's storage points -- cosine > 0.99 for every tensor
+    (BN gamma / beta included), so a wrong-but-correlated BN-backward term fails."""
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    torch.manual_seed(0)
+    model = build_model(arch, num_classes=100)
+    for n_, m_ in model.named_modules():
+        if n_.endswith("bn3") or (n_.endswith("bn2") and "layer" in n_ and arch != "resnet50"):
+            torch.nn.init.constant_(m_.weight, 0.2)
+    ref = _bf16_emulating(copy.deepcopy(model).to(dev).train())
+    tr = NativeTrainer(model, batch, (size, size), dev, optim=OptimConfig(lr=0.0, momentum=0.0, weight_decay=0.0),
+                       use_graphs=False)
+    p = tr.prog
+    g = torch.Generator().manual_seed(1)
+    img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).to(dev)
+    lab = torch.randint(0, p.num_classes, (batch,), generator=g).to(dev)
+    tr.step(img, lab)
+    torch.cuda.synchronize()
+    x = p.x4[..., :3].float().permute(0, 3, 1, 2).contiguous()
+    F.cross_entropy(ref(x), lab).backward()
+    named_ref = dict(ref.named_parameters())
+    cs = {}
+    for name, prm in model.named_parameters():
+        off = (prm.data_ptr() - p.master.data_ptr()) // 4
+        gflat = p.grad[off:off + prm.numel()]
+        gn = (gflat.view(prm.shape[0], prm.shape[2], prm.shape[3], prm.shape[1]).permute(0, 3, 1, 2)
+              if prm.dim() == 4 else gflat.view(prm.shape))
+        cs[name] = _cos(gn, named_ref[name].grad)
+    worst = sorted(cs.items(), key=lambda kv: kv[1])[:5]
+    print(f"[grad-cos] {arch}: worst {worst}")
+    assert worst[0][1] > 0.99, worst
+
+
 def test_program_trains_and_graph_replay():
     """Loss decreases on a fixed batch; graph replay reproduces eager training bit for bit (every
     reduction in the step is order-independent: fp64 statistics atomics, fixed-order split-K and

@@ -20,10 +20,13 @@ def main():
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--step-marker", default="sgd_kernel,adam_kernel")
     a = ap.parse_args()
-    ks = []
+    ks, qs = [], {}
     with open(a.trace) as f:
         for r in csv.DictReader(f):
-            ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+            s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            ks.append((s, e, r["Kernel_Name"]))
+            q = r.get("Queue_Id") or r.get("Stream_Id") or "?"
+            qs.setdefault(q, []).append((s, e, r["Kernel_Name"]))
     ks.sort()
     markers = tuple(m.strip() for m in a.step_marker.split(","))
     ends = [e for s, e, n in ks if any(m in n for m in markers)]
@@ -54,6 +57,28 @@ def main():
     print(f"{a.last} steps: wall {wall / 1e6 / a.last:.3f} ms/step, GPU busy (union) {busy / 1e6 / a.last:.3f} ms/step "
           f"({100 * busy / wall:.1f} %), kernel time summed {sumk / 1e6 / a.last:.3f} ms/step "
           f"(overlap {100 * (sumk - busy) / max(1, busy):.1f} %), {len(win) // a.last} kernels/step")
+    # per hardware queue: busy time inside the window (a queue busy ~100 % is the critical path;
+    # kernels of the other queues then only matter through the CUs they take from it)
+    for q, lst in sorted(qs.items(), key=lambda kv: -len(kv[1])):
+        w = sorted((s, e) for s, e, _ in lst if s >= t0 and e <= t1)
+        if not w:
+            continue
+        b, cs, ce = 0, w[0][0], w[0][1]
+        for s, e in w[1:]:
+            if s > ce:
+                b += ce - cs
+                cs, ce = s, e
+            else:
+                ce = max(ce, e)
+        b += ce - cs
+        top = {}
+        for s, e, n in lst:
+            if s >= t0 and e <= t1:
+                k = n.split("(")[0][:60]
+                top[k] = top.get(k, 0) + e - s
+        tops = ", ".join(f"{k} {v / 1e6 / a.last:.2f}" for k, v in sorted(top.items(), key=lambda kv: -kv[1])[:3])
+        print(f"queue {q}: {len(w) // a.last} kernels/step, busy {b / 1e6 / a.last:.3f} ms/step "
+              f"({100 * b / wall:.1f} % of wall); top: {tops}")
     idle = sum(g for g, _, _ in gaps)
     print(f"idle {idle / 1e6 / a.last:.3f} ms/step in {len(gaps) // a.last} gaps/step; largest:")
     short = lambda n: (n[:70] + "...") if len(n) > 73 else n  # noqa: E731
