@@ -2,6 +2,27 @@
 #pragma once
 typedef __bf16 bf16;
 namespace dbx {
+// BatchNorm finalize descriptor (device-resident, one per BN and direction): what bn_finalize
+// (mode 1: sharded sums -> scale / shift / saved mean, invstd / running stats) or bn_bwd_coeff
+// (mode 2: -> the backward coefficients [3][C] and dgamma / dbeta) would compute, done instead by the
+// last tile of the producing conv that touches each 64-channel group (bn_fin.h bn_fin_tail).
+struct BnFin {
+  unsigned* cnt;          // [C / 64] arrival counters (zeroed; the finalizing block resets its group's)
+  const double* stats;    // [nshard][2][C]
+  const float* gamma;     // nullable (1)
+  const float* beta;      // nullable (0), mode 1
+  float* running_mean;    // mode 1, nullable (no running-stat update)
+  float* running_var;
+  float* scale;           // mode 1 out
+  float* shift;
+  float* mean;            // mode 1: out (save_mean, nullable) ; mode 2: in
+  float* invstd;          // mode 1: out (save_invstd, nullable) ; mode 2: in
+  float* coeff;           // mode 2 out [3][C]
+  float* dgamma;          // mode 2 out (nullable)
+  float* dbeta;
+  int C, nshard, mode, accumulate;
+  float count, eps, momentum, pad_;
+};
 struct IGemmArgs {
   const bf16* x;          // A source, NHWC [N][IH][IW][IC]
   const bf16* w;          // B, [OC][KTOT] with KTOT = R*S*IC (STEM: 8*32)
@@ -51,6 +72,12 @@ struct IGemmArgs {
   // magic divisors (common.h mdiv) for pixel -> (n, oh, ow): ceil(2^40 / (OH*OW)), ceil(2^40 / OW);
   // 0 = not exact for this size (plain division)
   unsigned long long mag_ohw, mag_ow;
+  // in-launch BN finalize of the statistics this launch accumulates (stats: fin1; EPI: bstats1 ->
+  // fin1, bstats2 -> fin2; nullable). fin_final: this is the producer's last launch, whose arrivals
+  // complete the count fin_base (tiles of its earlier launches) + ceil(M / BM)
+  const BnFin* fin1;
+  const BnFin* fin2;
+  int fin_base, fin_final;
 };
 struct WgradArgs {
   const bf16* dy;        // [M][OC]
@@ -61,6 +88,13 @@ struct WgradArgs {
   int N, IH, IW, IC, OH, OW, OC, R, S, stride, pad;
   int M, KTOT, nsplit, m_per_split, relu_in;
   unsigned long long mag_ow, mag_ohw;  // ceil(2^40 / OW), ceil(2^40 / (OH*OW)): pixel -> (n, oh, ow)
+  // in-launch split-K reduction (conv_igemm.hip wgrad_store): dw != null -> the block that draws a
+  // tile's last ticket from cnt[tile] (zeroed; reset by that block) sums the tile's nsplit slabs in
+  // split order and writes dw = scale * sum (+ dw when accumulate); nsplit == 1 writes dw directly
+  float* dw;
+  unsigned* cnt;
+  float scale;
+  int accumulate;
 };
 // Fused backward of a bottleneck conv3 (1x1 stride-1, C -> K channels), conv_dwfused.hip
 struct DwFusedArgs {

@@ -83,9 +83,11 @@ static void check(int rc, const char* what) {
 }
 
 void register_runtime(py::module& m);  // csrc/runtime/mds_loader.cpp
+void register_comm(py::module& m);     // csrc/runtime/comm.cpp
 
 PYBIND11_MODULE(_C, m) {
   register_runtime(m);
+  register_comm(m);
   m.doc() = "dbx_distributed_pytorch_examples_amd native HIP kernels (gfx950)";
   m.def("conv_igemm", [](int mode, int bm, int bn, uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t in_scale,
                          uintptr_t in_shift, int relu_in, uintptr_t stats, int nshard, int N, int IH, int IW, int IC,
@@ -95,7 +97,7 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t bsc, uintptr_t bsh, uintptr_t mean1, uintptr_t inv1, uintptr_t mean2,
                          uintptr_t inv2, uintptr_t bstats1, uintptr_t bstats2, uintptr_t a_out, uintptr_t res,
                          uintptr_t res_scale, uintptr_t res_shift, uintptr_t tail_out, uintptr_t tail_bits,
-                         uintptr_t st, int dma) {
+                         uintptr_t st, int dma, uintptr_t fin1, uintptr_t fin2, int fin_base, int fin_final) {
     dbx::IGemmArgs a{P<const bf16*>(x), P<const bf16*>(w), P<bf16*>(y), P<const float*>(in_scale),
                      P<const float*>(in_shift), P<double*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
                      N * OH * OW, nshard > 0 ? nshard : 1, relu_in, nr, ns, r0, s0, tstep, dh0, dw0, osub, oph, opw,
@@ -103,7 +105,10 @@ PYBIND11_MODULE(_C, m) {
                      P<const bf16*>(ybn2), P<const float*>(bsc), P<const float*>(bsh), P<const float*>(mean1),
                      P<const float*>(inv1), P<const float*>(mean2), P<const float*>(inv2), P<double*>(bstats1),
                      P<double*>(bstats2), P<bf16*>(a_out), P<const bf16*>(res), P<const float*>(res_scale),
-                     P<const float*>(res_shift), P<bf16*>(tail_out), P<unsigned char*>(tail_bits), 0ull, 0ull};
+                     P<const float*>(res_shift), P<bf16*>(tail_out), P<unsigned char*>(tail_bits), 0ull, 0ull,
+                     P<const dbx::BnFin*>(fin1), P<const dbx::BnFin*>(fin2), fin_base, fin_final};
+    if ((fin1 || fin2) && !(stats || bstats1)) throw std::invalid_argument("conv_igemm: BN finalize without statistics");
+    if (fin2 && !bstats2) throw std::invalid_argument("conv_igemm: second BN finalize without its statistics");
     {  // magic divisors when exact: m < N*OH*OW, so m * OH*OW < 2^40 suffices
       const unsigned long long two40 = 1ull << 40, ohw = (unsigned long long)OH * OW;
       if (ohw > 0 && (unsigned long long)N * ohw * ohw < two40) {
@@ -116,13 +121,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_wgrad", [](int mode, int bm, int bn, uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t in_scale,
                          uintptr_t in_shift, int relu_in, int N, int IH, int IW, int IC, int OH, int OW, int OC, int R,
                          int S_, int stride, int pad, int KTOT, int nsplit, int m_per_split, uintptr_t st,
-                         unsigned lds_pad, int dma) {
+                         unsigned lds_pad, int dma, uintptr_t dw, uintptr_t cnt, float scale, int accumulate) {
     const unsigned long long two40 = 1ull << 40;
     const unsigned long long ohw = (unsigned long long)OH * OW;
     if ((unsigned long long)N * ohw * ohw >= two40) throw std::runtime_error("conv_wgrad: batch too large for mdiv");
     dbx::WgradArgs a{P<const bf16*>(dy), P<const bf16*>(x), P<float*>(ws), P<const float*>(in_scale),
                      P<const float*>(in_shift), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad, N * OH * OW, KTOT,
-                     nsplit, m_per_split, relu_in, (two40 + OW - 1) / OW, (two40 + ohw - 1) / ohw};
+                     nsplit, m_per_split, relu_in, (two40 + OW - 1) / OW, (two40 + ohw - 1) / ohw,
+                     P<float*>(dw), P<unsigned*>(cnt), scale, accumulate};
+    if (dw && nsplit > 1 && !cnt) throw std::invalid_argument("conv_wgrad: fused split-K reduction needs tile counters");
     check(dbx_conv_wgrad(mode, bm, bn, &a, in_scale != 0, S(st), lds_pad, dma), "conv_wgrad");
   });
   m.def("wgrad_patch3", [](uintptr_t dy, uintptr_t x, uintptr_t ws, long long ws_cap, int N, int IH, int IW, int IC,

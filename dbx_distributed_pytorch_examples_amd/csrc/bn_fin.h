@@ -1,0 +1,109 @@
+// BatchNorm finalize math shared by the standalone kernels (nn_ops.hip bn_finalize_kernel /
+// bn_bwd_coeff_kernel) and the in-launch finalize of the conv epilogue (bn_fin_tail): one
+// definition, so a fused and an unfused step produce the same bits.
+#pragma once
+#include "abi.h"
+
+namespace dbx {
+
+// forward: shard sums (s, q) of channel c -> scale / shift, saved mean / invstd, running stats
+__device__ __forceinline__ void bn_fwd_final(int c, double s, double q, float count, const float* gamma,
+                                             const float* beta, float eps, float momentum, float* running_mean,
+                                             float* running_var, float* scale, float* shift, float* save_mean,
+                                             float* save_invstd) {
+  const double mean = s / count;
+  double var = q / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * invstd;
+  shift[c] = b - (float)mean * g * invstd;
+  if (save_mean) save_mean[c] = (float)mean;
+  if (save_invstd) save_invstd[c] = invstd;
+  if (running_mean && momentum > 0.f) {
+    const double unbiased = count > 1.f ? var * count / (count - 1.0) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  }
+}
+
+// backward: shard sums (sum g, sum g*xhat) of channel c -> dy = k1*g + k2*y + k3, dgamma, dbeta
+__device__ __forceinline__ void bn_bwd_final(int C, int c, double sd, double qd, float count, const float* gamma,
+                                             const float* mean, const float* invstd, float* coeff, float* dgamma,
+                                             float* dbeta, int accumulate) {
+  const float s = (float)sd, q = (float)qd;
+  const float g = gamma ? gamma[c] : 1.f, is = invstd[c], mu = mean[c];
+  const float sg = s / count, sgx = q / count;
+  const float k1 = g * is;
+  const float k2 = -g * is * is * sgx;
+  const float k3 = -g * is * sg + g * is * is * sgx * mu;
+  coeff[c] = k1; coeff[C + c] = k2; coeff[2 * C + c] = k3;
+  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + q;
+  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + s;
+}
+
+// Shard sum of channel c in the standalone kernels' order (0 + shard 0 + shard 1 + ...: their
+// 32-way split holds one shard per lane for nshard <= 32, summed lane by lane).
+__device__ __forceinline__ void bn_fin_sums(const double* stats, int nshard, int C, int c, double& s, double& q) {
+  s = 0.0;
+  q = 0.0;
+  for (int k = 0; k < nshard; ++k) {
+    s += stats[(size_t)k * 2 * C + c];
+    q += stats[(size_t)k * 2 * C + C + c];
+  }
+}
+
+__device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c) {
+  double s, q;
+  bn_fin_sums(f.stats, f.nshard, f.C, c, s, q);
+  if (f.mode == 1)
+    bn_fwd_final(c, s, q, f.count, f.gamma, f.beta, f.eps, f.momentum, f.running_mean, f.running_var, f.scale,
+                 f.shift, f.mean, f.invstd);
+  else
+    bn_bwd_final(f.C, c, s, q, f.count, f.gamma, f.mean, f.invstd, f.coeff, f.dgamma, f.dbeta, f.accumulate);
+}
+
+// End of a conv tile epilogue whose launch carries BN finalize descriptors: the tile's statistics
+// atomics are published (agent-scope release) and counted per 64-channel group; the tile that
+// completes a group's count (all ceil(M / BM) M-tiles of the producer, over all its launches)
+// acquires and finalizes those 64 channels, then resets the group counter. The same hand-off as the
+// split-K reduction (cdna_hip_programming.md §5 item 2); the finalizing block reads 2 x nshard x 64
+// doubles. n0: first output channel of the tile (a multiple of 64).
+template <int BM, int BN>
+__device__ __forceinline__ void bn_fin_tail(const IGemmArgs& a, const int n0, bf16* lds) {
+  constexpr int G = BN / 64;
+  static_assert(G >= 1 && G * 64 == BN, "64-channel groups");
+  const int tid = threadIdx.x;
+  const int ng = a.fin2 ? 2 * G : G;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics atomics have completed
+  __syncthreads();                                   // ... every wave's; the LDS is free
+  int* flag = reinterpret_cast<int*>(lds);
+  if (tid < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (tid < ng) {
+      const BnFin* f = tid < G ? a.fin1 : a.fin2;
+      const unsigned total = a.fin_final ? (unsigned)(a.fin_base + (a.M + BM - 1) / BM) : 0xFFFFFFFFu;
+      const unsigned t = __hip_atomic_fetch_add(f->cnt + (n0 >> 6) + tid % G, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      last = t + 1u == total;
+      flag[tid] = last;
+    }
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k < ng; ++k) {
+    if (!flag[k]) continue;  // block-uniform
+    const BnFin* f = k < G ? a.fin1 : a.fin2;
+    const int g = (n0 >> 6) + k % G;
+    if (tid < 64) bn_fin_channel(*f, g * 64 + tid);
+    if (tid == 0) __hip_atomic_store(f->cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();  // flags read before the LDS is reused
+}
+
+}  // namespace dbx

@@ -30,6 +30,7 @@
 #include <type_traits>
 #include "common.h"
 #include "abi.h"
+#include "bn_fin.h"
 
 namespace dbx {
 
@@ -295,6 +296,9 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x4 (&acc)[
         atomicAdd(st2 + a.OC + n0 + tid, (double)q2);
       }
     }
+  }
+  if constexpr (STATS || EPI > 0) {
+    if (a.fin1) bn_fin_tail<BM, BN>(a, n0, lds);  // wave-uniform
   }
 }
 

@@ -14,6 +14,7 @@
 //   * softmax-cross-entropy, label smoothing, argmax/correct-count and dlogits in one kernel;
 //   * SGD-momentum / Adam(W) over the flat fp32 master buffer, writing the bf16 compute copy.
 #include "common.h"
+#include "bn_fin.h"
 
 namespace dbx {
 
@@ -51,20 +52,8 @@ __global__ void bn_finalize_kernel(const double* __restrict__ stats, int nshard,
   int c;
   shard_sums(stats, nshard, C, blockIdx.x * 8, s, q, active, c);
   if (!active) return;
-  const double mean = s / count;
-  double var = q / count - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-  scale[c] = g * invstd;
-  shift[c] = b - (float)mean * g * invstd;
-  if (save_mean) save_mean[c] = (float)mean;
-  if (save_invstd) save_invstd[c] = invstd;
-  if (running_mean && momentum > 0.f) {
-    const double unbiased = count > 1.f ? var * count / (count - 1.0) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
-  }
+  bn_fwd_final(c, s, q, count, gamma, beta, eps, momentum, running_mean, running_var, scale, shift, save_mean,
+               save_invstd);
 }
 
 // eval-mode BN: scale/shift from running stats
@@ -238,15 +227,7 @@ __global__ void bn_bwd_coeff_kernel(const double* __restrict__ stats, int nshard
   int c;
   shard_sums(stats, nshard, C, blockIdx.x * 8, sd, qd, active, c);
   if (!active) return;
-  const float s = (float)sd, q = (float)qd;
-  const float g = gamma ? gamma[c] : 1.f, is = invstd[c], mu = mean[c];
-  const float sg = s / count, sgx = q / count;
-  const float k1 = g * is;
-  const float k2 = -g * is * is * sgx;
-  const float k3 = -g * is * sg + g * is * is * sgx * mu;
-  coeff[c] = k1; coeff[C + c] = k2; coeff[2 * C + c] = k3;
-  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + q;
-  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + s;
+  bn_bwd_final(C, c, sd, qd, count, gamma, mean, invstd, coeff, dgamma, dbeta, accumulate);
 }
 
 template <int MASK, bool WRITE_G>

@@ -102,6 +102,15 @@ class NativeTrainer:
             # stream vs 14.43k / 14.40k without; the plain single graph is 14.53-14.56k either way
             # (profiles/r2s2_multirank/). Weight gradients then run in order on the main stream.
             self.prog.overlap_wgrad = False
+        # DBX_COMM=native: the DP bucket all-reduces go through the framework's own RCCL communicator
+        # (parallel/comm.py) on the comm stream, and the whole step -- backward segments, forked
+        # all-reduces, join, optimizer -- is captured as ONE graph instead of per-segment graphs
+        # with eager c10d collectives between replays
+        self.ncomm = None
+        if self.segmented and device.type == "cuda" and not zero_stage:
+            from ..parallel.comm import NativeComm, native_comm_available, native_comm_requested
+            if native_comm_requested() and native_comm_available():
+                self.ncomm = NativeComm(process_group, device)
         self.flip = None
         self.seg_ranges = self._segment_ranges()
         self.zero = None
@@ -257,6 +266,19 @@ class NativeTrainer:
 
     def _allreduce_range(self, lo: int, hi: int):
         g = self.prog.grad
+        if self.ncomm is not None:  # enqueued on the current (comm) stream; capturable
+            pos = lo
+            while pos < hi:
+                end = min(hi, pos + self.bucket_cap)
+                chunk = g[pos:end]
+                if self.ar_dtype == torch.float32:
+                    self.ncomm.all_reduce(chunk)
+                else:
+                    buf = chunk.to(self.ar_dtype)
+                    self.ncomm.all_reduce(buf)
+                    chunk.copy_(buf)
+                pos = end
+            return
         host_sync_for_gloo(g, self.pg)
         pos = lo
         while pos < hi:
@@ -309,7 +331,10 @@ class NativeTrainer:
     def _waits_comm(self, i: int, name: str) -> bool:
         # the optimizer phases consume the reduced gradients / norm; the first phase of a step
         # consumes the previous step's all-gathered parameters
-        return self.segmented and (i == 0 or name in ("optimizer", "opt_norm"))
+        # (inside the one-graph capture the comm stream joins only after its first fork: no wait on
+        # work recorded outside the capture)
+        first = i == 0 and not getattr(self, "_capturing_one", False)
+        return self.segmented and (first or name in ("optimizer", "opt_norm"))
 
     def _run_phases_eager(self):
         if self.dev.type != "cuda":  # CPU (reference ops; gloo collectives, synchronous)
@@ -347,7 +372,18 @@ class NativeTrainer:
         # global mode such a query from another thread invalidates the capture
         mode = "thread_local" if (dist.is_available() and dist.is_initialized()) else "global"
         with torch.cuda.stream(s):
-            if not self.segmented:
+            if self.ncomm is not None:
+                # one graph: the comm-stream fork / join of every bucket is recorded as graph edges
+                g = torch.cuda.CUDAGraph()
+                self._capturing_one = True
+                try:
+                    with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode=mode):
+                        self._run_phases_eager()
+                        torch.cuda.current_stream(self.dev).wait_stream(self.comm_stream)
+                finally:
+                    self._capturing_one = False
+                self.graphs = [g]
+            elif not self.segmented:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode=mode):
                     for _, fn, _ in self.phases:
@@ -364,7 +400,9 @@ class NativeTrainer:
 
     def _replay(self):
         cur = torch.cuda.current_stream(self.dev)
-        if not self.segmented:
+        if not self.segmented or self.ncomm is not None:
+            if self.ncomm is not None:
+                cur.wait_stream(self.comm_stream)  # eager warm-up collectives
             self.graphs[0].replay()
             return
         for i, ((name, _, post), g) in enumerate(zip(self._graph_phases(), self.graphs)):

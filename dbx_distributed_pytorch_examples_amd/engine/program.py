@@ -150,6 +150,10 @@ class ResNetProgram:
         self.dev = device
         self.in_ch = model.conv1.in_channels
         self.overlap_wgrad = os.environ.get("DBX_OVERLAP_WGRAD", "1") == "1"
+        # split-K weight-gradient reduction inside the wgrad launch where a tile's slabs are small
+        self.fuse_wgrad_reduce = os.environ.get("DBX_FUSE_WGRAD_REDUCE", "1") == "1"
+        # BN finalize / backward coefficients computed by the producing conv's last tiles (K.BnFin)
+        self.fuse_fin = os.environ.get("DBX_FUSE_BN_FIN", "1") == "1"
         self.wgrad_lds_pad = int(os.environ.get("DBX_WGRAD_LDS_PAD", "0"))
         # store block-internal BN outputs from the MASK_Y dgrad epilogue for the wgrads (A/B switch)
         self.act_writeback = os.environ.get("DBX_ACT_WRITEBACK", "1") == "1"
@@ -190,6 +194,7 @@ class ResNetProgram:
         self._build_layers()
         self._alloc_params()
         self._alloc_activations()
+        self.build_fins()
         self.training = True
 
     # ----------------------------------------------------------------------------------
@@ -426,6 +431,15 @@ class ResNetProgram:
             wsmax = max(wsmax, cv.OC * ktot)
         # split-K wgrad workspace: up to 64 splits of the largest layer, >= 64 MiB
         self.ws = torch.empty(max(64 * wsmax, 16 << 20), device=dev, dtype=torch.float32)
+        # per-conv tile counters of the in-launch split-K reduction (K.conv_wgrad cnt=): zeroed once,
+        # every launch leaves them zero again; keyed by the gradient view's address
+        body = [cv for cv in self.convs if not cv.stem]
+        sizes = [K.wgrad_tiles_max(cv.OC, cv.R * cv.S * cv.IC) for cv in body]
+        self.wg_cnt = torch.zeros(max(1, sum(sizes)), device=dev, dtype=torch.int32)
+        self._wg_cnt_of, pos = {}, 0
+        for cv, n in zip(body, sizes):
+            self._wg_cnt_of[cv.grad.data_ptr()] = self.wg_cnt[pos:pos + n]
+            pos += n
         # the fused conv3 backward runs on the main stream while side-stream weight gradients use
         # self.ws: its per-workgroup slabs get their own workspace (<= 1024 slabs + 64 partials)
         fused = [b.convs[-1] for i, b in enumerate(self.blocks) if self._fuse3(b, i == len(self.blocks) - 1)]
@@ -471,6 +485,36 @@ class ResNetProgram:
         # augment kernel (box paste) and the CE kernel (mixed soft targets)
         self.cutmix = False
         self.mix_perm = self.mix_box = self.mix_lam = self.labels2 = None
+
+    def build_fins(self) -> None:
+        """(Re)build every BN's finalize descriptors (K.BnFin: raw pointers to its statistics, affine
+        parameters, running stats and outputs) -- again whenever one of those tensors is reallocated."""
+        N = self.N
+        pairs = [(self.stem_bn, self.stem)]
+        for b in self.blocks:
+            pairs += list(zip(b.bns, b.convs))
+            if b.ds_conv is not None:
+                pairs.append((b.ds_bn, b.ds_conv))
+        for bn, cv in pairs:
+            mod = bn.mod
+            cnt = N * cv.OH * cv.OW
+            mom = mod.momentum if mod.momentum is not None else 0.1
+            bn.fin_f = bn.fin_b = None
+            if bn.C % 64:
+                continue
+            bn.fin_f = K.BnFin(K.BnFin.FWD, bn.stats, cnt, gamma=bn.gamma, beta=bn.beta, eps=mod.eps,
+                               momentum=mom if mod.track_running_stats else 0.0, running_mean=mod.running_mean,
+                               running_var=mod.running_var, scale=bn.scale, shift=bn.shift, mean=bn.mean,
+                               invstd=bn.invstd)
+            bn.fin_b = K.BnFin(K.BnFin.BWD, bn.bstats, cnt, gamma=bn.gamma, mean=bn.mean, invstd=bn.invstd,
+                               coeff=bn.coeff, dgamma=bn.dgamma, dbeta=bn.dbeta)
+
+    def _ff(self, bn):
+        """The forward finalize descriptor to hand the conv producing ``bn``'s statistics (training)."""
+        return bn.fin_f if self.training and self.fuse_fin else None
+
+    def _fused_fin(self, bn) -> bool:
+        return self.fuse_fin and bn.fin_f is not None
 
     def enable_cutmix(self) -> None:
         dev = self.dev
@@ -551,26 +595,30 @@ class ResNetProgram:
                     K.conv_fwd(pb.ys[-1], cv.w16, b.ys[0], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                                stats=b.bns[0].stats if tr else None, in_scale=pb.bns[-1].scale,
                                in_shift=pb.bns[-1].shift, relu_in=True, tail_res=res, tail_res_scale=rsc,
-                               tail_res_shift=rsh, tail_out=pb.out, tail_bits=pb.obits if tr else None)
+                               tail_res_shift=rsh, tail_out=pb.out, tail_bits=pb.obits if tr else None,
+                               fin=self._ff(b.bns[0]))
                     pending = None
                 elif i > 0 and b.mat[i - 1]:  # materialised BN output -> plain-operand (eight-wave) conv
                     K.bn_apply(b.ys[i - 1], prev_bn.scale, prev_bn.shift, b.acts[i - 1], relu=True)
                     K.conv_fwd(b.acts[i - 1], cv.w16, b.ys[i], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
-                               stats=b.bns[i].stats if tr else None)
+                               stats=b.bns[i].stats if tr else None, fin=self._ff(b.bns[i]))
                 else:
                     src = x if i == 0 else b.ys[i - 1]
                     K.conv_fwd(src, cv.w16, b.ys[i], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                                stats=b.bns[i].stats if tr else None,
                                in_scale=prev_bn.scale if prev_bn else None,
-                               in_shift=prev_bn.shift if prev_bn else None, relu_in=True)
-                self._bn_fwd(b.bns[i], N * cv.OH * cv.OW)
+                               in_shift=prev_bn.shift if prev_bn else None, relu_in=True,
+                               fin=self._ff(b.bns[i]))
+                if self._ff(b.bns[i]) is None:
+                    self._bn_fwd(b.bns[i], N * cv.OH * cv.OW)
                 prev_bn = b.bns[i]
             last = b.bns[-1]
             if b.ds_conv is not None:
                 dc = b.ds_conv
                 K.conv_fwd(x, dc.w16, b.yd, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad,
-                           stats=b.ds_bn.stats if tr else None)
-                self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
+                           stats=b.ds_bn.stats if tr else None, fin=self._ff(b.ds_bn))
+                if self._ff(b.ds_bn) is None:
+                    self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
                 res, rsc, rsh = b.yd, b.ds_bn.scale, b.ds_bn.shift
             else:
                 res, rsc, rsh = x, None, None
@@ -634,6 +682,8 @@ class ResNetProgram:
         self._side_pending = True
 
     def _wgrad(self, *args, **kw):
+        if self.fuse_wgrad_reduce:
+            kw["cnt"] = self._wg_cnt_of.get(args[2].data_ptr())
         if self.wgrad_lds_pad and self.dev.type == "cuda" and self.overlap_wgrad:
             kw["lds_pad"] = self.wgrad_lds_pad  # occupancy cap: leave room for the main stream's kernels
         self._side(lambda: K.conv_wgrad(*args, **kw))
@@ -685,11 +735,14 @@ class ResNetProgram:
             g = self.g_last
         else:
             g = self.blocks[i + 1].dx
-            K.bn_bwd_coeff(lbn.bstats, cnt_last, lbn.gamma, lbn.mean, lbn.invstd, lbn.coeff, lbn.dgamma, lbn.dbeta)
+            if not self._fused_fin(lbn):  # (else finished by block i+1's conv1 dgrad epilogue)
+                K.bn_bwd_coeff(lbn.bstats, cnt_last, lbn.gamma, lbn.mean, lbn.invstd, lbn.coeff, lbn.dgamma,
+                               lbn.dbeta)
         if b.ds_conv is not None:
             dc, dbn = b.ds_conv, b.ds_bn
-            K.bn_bwd_coeff(dbn.bstats, N * dc.OH * dc.OW, dbn.gamma, dbn.mean, dbn.invstd, dbn.coeff, dbn.dgamma,
-                           dbn.dbeta)
+            if last or not self._fused_fin(dbn):
+                K.bn_bwd_coeff(dbn.bstats, N * dc.OH * dc.OW, dbn.gamma, dbn.mean, dbn.invstd, dbn.coeff,
+                               dbn.dgamma, dbn.dbeta)
             if last:
                 K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE)
             elif (fuse3 or self._fold(lc)) and self._fold(dc, dense=True):
@@ -732,14 +785,16 @@ class ResNetProgram:
                 K.conv_dgrad(src, cv.wt16, b.das[j - 1], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                              epilogue=K.BNBwdEpilogue(K.MASK_Y, b.ys[j - 1], pbn.mean, pbn.invstd, pbn.bstats,
                                                       scale=pbn.scale, shift=pbn.shift,
-                                                      act_out=None if b.mat[j - 1] else act), **kw)
+                                                      act_out=None if b.mat[j - 1] else act,
+                                                      fin1=pbn.fin_b if self._fused_fin(pbn) else None), **kw)
             if act is not None:
                 self._wgrad(b.dys[j], act, cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad)
             elif kw and not pre:
                 self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                             in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
-            K.bn_bwd_coeff(pbn.bstats, N * pc.OH * pc.OW, pbn.gamma, pbn.mean, pbn.invstd, pbn.coeff, pbn.dgamma,
-                           pbn.dbeta)
+            if kw is None or not self._fused_fin(pbn):  # (else finished by the dgrad epilogue above)
+                K.bn_bwd_coeff(pbn.bstats, N * pc.OH * pc.OW, pbn.gamma, pbn.mean, pbn.invstd, pbn.coeff,
+                               pbn.dgamma, pbn.dbeta)
             if self._fold(pc):  # the next dgrad (conv j-1) applies it while staging
                 pend = dict(bwd_y=b.ys[j - 1], bwd_coeff=pbn.coeff, dy_out=b.dys[j - 1])
                 gin = b.das[j - 1]
@@ -771,7 +826,10 @@ class ResNetProgram:
                                   ybn2=pb.yd if pb.ds_conv is not None else None,
                                   mean2=pb.ds_bn.mean if pb.ds_conv is not None else None,
                                   inv2=pb.ds_bn.invstd if pb.ds_conv is not None else None,
-                                  stats2=pb.ds_bn.bstats if pb.ds_conv is not None else None)
+                                  stats2=pb.ds_bn.bstats if pb.ds_conv is not None else None,
+                                  fin1=pb.bns[-1].fin_b if self._fused_fin(pb.bns[-1]) else None,
+                                  fin2=(pb.ds_bn.fin_b if pb.ds_conv is not None and self._fused_fin(pb.ds_bn)
+                                        else None))
         K.conv_dgrad(src0, c0.wt16, b.dx, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad,
                      addsrc=addsrc, add_sub=sub, epilogue=epi, **kw0)
         if kw0:

@@ -49,6 +49,54 @@ def _dispatch(fn):
 NSHARD = _ref.NSHARD  # BN-statistics shards (spreads the epilogue atomics over NSHARD copies)
 
 
+class BnFin:
+    """In-launch BatchNorm finalize descriptor (csrc/abi.h BnFin, csrc/bn_fin.h): handed to the conv
+    that accumulates a BN's statistics (``conv_fwd(fin=)`` for the forward statistics, ``BNBwdEpilogue
+    (fin1=, fin2=)`` for the backward ones), it makes the producer's last tile of every 64-channel group
+    compute what ``bn_finalize`` (mode 1) / ``bn_bwd_coeff`` (mode 2) would, bit for bit -- one launch
+    and one graph node fewer per BN and direction. Producers that cannot (reference ops on the CPU,
+    multi-launch strided dgrads, the stem) call :meth:`run` instead, so after the producer returns the
+    finalize is done either way. The descriptor holds raw pointers: rebuild it if a tensor it names
+    is reallocated."""
+
+    FWD, BWD = 1, 2
+
+    def __init__(self, mode, stats, count, *, gamma=None, beta=None, eps=1e-5, momentum=0.0, running_mean=None,
+                 running_var=None, scale=None, shift=None, mean=None, invstd=None, coeff=None, dgamma=None,
+                 dbeta=None, accumulate=False):
+        C = (scale if mode == self.FWD else coeff).numel() // (1 if mode == self.FWD else 3)
+        if C % 64:
+            raise ValueError("BnFin needs a multiple of 64 channels")
+        self.mode, self.stats, self.count, self.C = mode, stats, float(count), C
+        self.gamma, self.beta, self.eps, self.momentum = gamma, beta, float(eps), float(momentum)
+        self.running_mean, self.running_var, self.scale, self.shift = running_mean, running_var, scale, shift
+        self.mean, self.invstd, self.coeff, self.dgamma, self.dbeta = mean, invstd, coeff, dgamma, dbeta
+        self.accumulate = bool(accumulate)
+        self.cnt = torch.zeros(C // 64, dtype=torch.int32, device=stats.device)
+        self.desc = None
+        if stats.is_cuda:
+            import numpy as np
+            ptrs = [self.cnt, stats, gamma, beta, running_mean, running_var, scale, shift, mean, invstd, coeff,
+                    dgamma, dbeta]
+            buf = np.zeros(136, dtype=np.uint8)
+            buf[:104].view(np.uint64)[:] = [_p(t) for t in ptrs]
+            buf[104:120].view(np.int32)[:] = [C, NSHARD, mode, int(accumulate)]
+            buf[120:136].view(np.float32)[:] = [count, eps, momentum, 0.0]
+            self.desc = torch.from_numpy(buf).to(stats.device)
+
+    def ptr(self) -> int:
+        return self.desc.data_ptr() if self.desc is not None else 0
+
+    def run(self) -> None:
+        """The standalone finalize launch (what the fused path replaces)."""
+        if self.mode == self.FWD:
+            bn_finalize(self.stats, self.count, self.gamma, self.beta, self.eps, self.momentum, self.running_mean,
+                        self.running_var, self.scale, self.shift, self.mean, self.invstd)
+        else:
+            bn_bwd_coeff(self.stats, self.count, self.gamma, self.mean, self.invstd, self.coeff, self.dgamma,
+                         self.dbeta, accumulate=self.accumulate)
+
+
 def new_stats(C: int, device=None) -> torch.Tensor:
     """Zeroed BN-statistics slab ``[NSHARD, 2, C]`` (flat, fp64: the epilogue atomics add fp32
     partials exactly, so statistics do not depend on tile completion order)."""
@@ -180,12 +228,13 @@ def _use_patch3(tile, mode: str) -> int:
 @_dispatch
 def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None,
              relu_in=True, tile=None, tail_res=None, tail_res_scale=None, tail_res_shift=None, tail_out=None,
-             tail_bits=None, _split=True):
+             tail_bits=None, fin: "BnFin" = None, _split=True, _fin=(0, 1)):
     """Y = conv(act(X), W); act = relu(X*in_scale + in_shift) with a BN prologue. "Tail" mode
     (``tail_res`` given; 1x1 stride-1 convs): act = relu(X*in_scale + in_shift + r), r = tail_res or
     tail_res*tail_res_scale + tail_res_shift -- the previous residual block's output computed on the
     fly -- and act / its 1-bit ReLU mask are stored to ``tail_out`` / ``tail_bits`` (bn_apply's
-    outputs), so that pass and the re-read of the block output disappear."""
+    outputs), so that pass and the re-read of the block output disappear. ``fin``: the BN finalize of
+    ``stats`` (:class:`BnFin`), done by the launch's last tiles (or by a finalize launch after it)."""
     N, IH, IW, IC = x.shape
     OH, OW = conv_out_hw(IH, IW, R, S, stride, pad)
     OC = w16.shape[0]
@@ -228,16 +277,20 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
         dma = 4
     elif dma == 4 and _split:
         n1 = fast_split(N, OH * OW, OC, bn)
-        kw = dict(R=R, S=S, stride=stride, pad=pad, stats=stats, _split=False)
-        if n1 > 0:
-            conv_fwd(x[:n1], w16, out[:n1], tile=(256, bn, 4), **kw)
+        kw = dict(R=R, S=S, stride=stride, pad=pad, stats=stats, fin=fin, _split=False)
+        if n1 > 0:  # (the fast launch's tiles count toward the finalize the leftover launch completes)
+            conv_fwd(x[:n1], w16, out[:n1], tile=(256, bn, 4), _fin=(0, int(n1 == N)), **kw)
         if n1 < N:  # the leftover images on small four-wave tiles (they fill the chip)
-            conv_fwd(x[n1:], w16, out[n1:], tile=pick_tile((N - n1) * OH * OW, OC, use_table=False), **kw)
+            conv_fwd(x[n1:], w16, out[n1:], tile=pick_tile((N - n1) * OH * OW, OC, use_table=False),
+                     _fin=(-(-n1 * OH * OW // 256), 1), **kw)
         return out
+    f1 = fin.ptr() if fin is not None and stats is not None else 0
     C().conv_igemm(mode, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
                    R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
-                   _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma)
+                   _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma, f1, 0, _fin[0], _fin[1])
+    if fin is not None and not f1 and _fin[1]:
+        fin.run()
     return out
 
 
@@ -292,11 +345,18 @@ class BNBwdEpilogue:
     BN fed by the same gradient: the downsample branch). Replaces a separate reduction pass."""
 
     def __init__(self, mode, ybn, mean1, inv1, stats1, mbits=None, scale=None, shift=None,
-                 ybn2=None, mean2=None, inv2=None, stats2=None, act_out=None):
+                 ybn2=None, mean2=None, inv2=None, stats2=None, act_out=None, fin1=None, fin2=None):
         self.mode, self.ybn, self.mean1, self.inv1, self.stats1 = mode, ybn, mean1, inv1, stats1
         self.act_out = act_out  # MASK_Y only: also store relu(ybn*scale+shift) (the BN output)
         self.mbits, self.scale, self.shift = mbits, scale, shift
         self.ybn2, self.mean2, self.inv2, self.stats2 = ybn2, mean2, inv2, stats2
+        # BnFin (mode BWD) of stats1 / stats2: the backward coefficients are final when the dgrad returns
+        self.fin1, self.fin2 = fin1, fin2
+
+    def run_fin(self):
+        for f in (self.fin1, self.fin2):
+            if f is not None:
+                f.run()
 
     def batch_slice(self, n0: int, n1: int, N: int) -> "BNBwdEpilogue":
         """The same epilogue over images [n0, n1) of an N-image batch (per-pixel tensors sliced)."""
@@ -304,7 +364,7 @@ class BNBwdEpilogue:
             return None if t is None else t.view(N, -1)[n0:n1]
         return BNBwdEpilogue(self.mode, sl(self.ybn), self.mean1, self.inv1, self.stats1, mbits=sl(self.mbits),
                              scale=self.scale, shift=self.shift, ybn2=sl(self.ybn2), mean2=self.mean2, inv2=self.inv2,
-                             stats2=self.stats2, act_out=sl(self.act_out))
+                             stats2=self.stats2, act_out=sl(self.act_out), fin1=self.fin1, fin2=self.fin2)
 
     def args(self):
         return (self.mode, _p(self.mbits), _p(self.ybn), _p(self.ybn2), _p(self.scale), _p(self.shift),
@@ -313,7 +373,8 @@ class BNBwdEpilogue:
 
 @_dispatch
 def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, addsrc=None, add_sub=1,
-               epilogue: "BNBwdEpilogue" = None, bwd_y=None, bwd_coeff=None, dy_out=None, _split=True):
+               epilogue: "BNBwdEpilogue" = None, bwd_y=None, bwd_coeff=None, dy_out=None, _split=True,
+               _fin=(0, 1)):
     """dX = conv_transpose(dY, W): dy [N,P,Q,K], wt16 [C, R*S*K] (CRSK), dx [N,H,W,C].
 
     Stride > 1 runs one dense launch per output phase (``dgrad_phases``): no MFMA work on the
@@ -323,6 +384,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
     ``bwd_y``/``bwd_coeff`` (1x1 stride-1 only): ``dy`` is the raw BN-output gradient g and the
     operand is the BN-backward apply k1*g + k2*bwd_y + k3 (coeff [3, K]) computed while staging;
     it is also stored to ``dy_out`` (for the weight gradient) -- bn_bwd_apply folded in.
+    The epilogue's ``fin1`` / ``fin2`` (:class:`BnFin`) are done when this returns.
     """
     N, P, Q, K = dy.shape
     _, H, W, Cc = dx.shape
@@ -354,8 +416,12 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             _chk(e.act_out, torch.bfloat16, "act_out", dx.numel())
         epi = e.args()
         act_ptr = _p(e.act_out)
+        fins = (e.fin1.ptr() if e.fin1 is not None else 0, e.fin2.ptr() if e.fin2 is not None and e.stats2 is not None else 0)
+        if fins[1] and not fins[0]:
+            fins = (0, 0)
     else:
         act_ptr = 0
+        fins = (0, 0)
     bwd = (0, 0, 0, 0, 0, 0)  # in_scale, in_shift, res, res_scale, res_shift, tail_out
     if bwd_y is not None:
         if not tail_supported(K, R, S, stride, pad):
@@ -371,7 +437,8 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
     if kind:
         C().conv_igemm(DGRAD_PATCH, 0, 0, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
                        N, P, Q, K, H, W, Cc, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, H, W,
-                       0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), kind - 1)
+                       0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), kind - 1, *fins, 0, 1)
+        _fin_rest(epilogue, fins)
         return dx
     if isinstance(tile, str):
         raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 dgrad at width 56 (no addend / fold)")
@@ -388,11 +455,14 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
     elif t_sel is not None and _tile_dma(t_sel)[2] == 4 and _split:
         bn = _tile_dma(t_sel)[1]
         n1 = fast_split(N, H * W, Cc, bn)
-        for (a0, a1, t) in ((0, n1, (256, bn, 4)), (n1, N, pick_tile((N - n1) * H * W, Cc, use_table=False))):
+        fins_of = ((0, int(n1 == N)), (-(-n1 * H * W // 256), 1))  # the leftover launch completes the count
+        for (a0, a1, t), fi in zip(((0, n1, (256, bn, 4)), (n1, N, pick_tile((N - n1) * H * W, Cc, use_table=False))),
+                                   fins_of):
             if a1 > a0:
                 conv_dgrad(dy[a0:a1], wt16, dx[a0:a1], R=R, S=S, stride=stride, pad=pad, accumulate=accumulate,
                            tile=t, addsrc=None if addsrc is None else addsrc[a0:a1], add_sub=add_sub,
-                           epilogue=None if epilogue is None else epilogue.batch_slice(a0, a1, N), _split=False)
+                           epilogue=None if epilogue is None else epilogue.batch_slice(a0, a1, N), _split=False,
+                           _fin=fi)
         return dx
     phases = dgrad_phases(H, W, R, S, stride, pad)
     if not accumulate and any(ph[5] == 0 or ph[7] == 0 for ph in phases):
@@ -400,6 +470,8 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             raise ValueError("fused BN epilogue needs every output pixel covered by one launch")
         dx.zero_()  # phases without taps receive no contribution
         accumulate = True
+    if len(phases) > 1:  # several launches of differing tiles: finalize with its own launch
+        fins = (0, 0)
     for (ph, pw, ohs, ows, r0, nr, s0, ns, dh0, dw0) in phases:
         if nr == 0 or ns == 0 or ohs == 0 or ows == 0:
             if epilogue is not None or addsrc is not None:
@@ -410,8 +482,21 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), bwd[0], bwd[1], 0, 0, NSHARD,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,
-                       _p(addsrc), add_sub, *epi, act_ptr, bwd[2], bwd[3], bwd[4], bwd[5], 0, stream_ptr(), dma)
+                       _p(addsrc), add_sub, *epi, act_ptr, bwd[2], bwd[3], bwd[4], bwd[5], 0, stream_ptr(), dma,
+                       *fins, _fin[0], _fin[1])
+    if _fin[1]:
+        _fin_rest(epilogue, fins)
     return dx
+
+
+def _fin_rest(epilogue, fins) -> None:
+    """Run the standalone finalize of every BnFin of ``epilogue`` the launch did not take."""
+    if epilogue is None:
+        return
+    if epilogue.fin1 is not None and not fins[0]:
+        epilogue.fin1.run()
+    if epilogue.fin2 is not None and not fins[1]:
+        epilogue.fin2.run()
 
 
 def stem_patch_supported(IH: int, IW: int, OC: int, R: int, S: int, stride: int, pad: int) -> bool:
@@ -442,7 +527,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
     bm = 0 if patch and stem_patch_supported(IH, IW, OC, R, S, stride, pad) else 128  # bm 0: patch kernel
     C().conv_igemm(STEM, bm, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
-                   *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr(), 0)
+                   *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr(), 0, 0, 0, 0, 1)
     return out
 
 
@@ -479,12 +564,35 @@ def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int
     return nsplit, ms
 
 
+_WG_FUSE_MAX = None
+
+
+def wgrad_fuse_max() -> int:
+    """Largest per-tile slab volume (nsplit x BM x BN x 4 bytes) reduced inside the weight-gradient
+    launch by the tile's last block (DBX_WGRAD_FUSE_MAX bytes; 0 = always a separate reduce)."""
+    global _WG_FUSE_MAX
+    if _WG_FUSE_MAX is None:
+        import os
+        _WG_FUSE_MAX = int(os.environ.get("DBX_WGRAD_FUSE_MAX", str(1 << 20)))
+    return _WG_FUSE_MAX
+
+
+def wgrad_tiles_max(OC: int, KTOT: int) -> int:
+    """Upper bound on the weight-gradient tile count of an OC x KTOT gradient (64 x 64 tiles): the
+    size of its in-launch reduction counter slice."""
+    return (OC // 64) * (KTOT // 64)
+
+
 @_dispatch
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True,
-               scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1):
+               scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None):
     """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace.
     ``dma``: operand path of the prologue-free kernels -- LDS-DMA ring depth 2 / 3, 0 = register
-    staged, -1 = the tune table's choice, else DBX_WGRAD_DMA, else 3 for 256-wide tiles / 2."""
+    staged, -1 = the tune table's choice, else DBX_WGRAD_DMA, else 3 for 256-wide tiles / 2.
+    ``cnt``: zeroed int32 tile counters (>= wgrad_tiles_max(OC, KTOT), owned by this call site):
+    when given and the split slabs of a tile are small (wgrad_fuse_max), the split-K reduction runs
+    inside the launch (the last block of each tile sums its slabs, bit-identical to wgrad_reduce)
+    and no separate reduce kernel is launched; one split writes dW directly."""
     N, OH, OW, OC = dy.shape
     _, IH, IW, IC = x.shape
     KTOT = 256 if stem else R * S * IC
@@ -536,10 +644,17 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
     nsplit, ms = wgrad_splits(M, OC, KTOT, bm, bn, ws.numel())
     if (nsplit + (min(64, nsplit) if nsplit > 8 else 0)) * OC * KTOT > ws.numel():
         raise ValueError("wgrad workspace too small")
+    fuse = (cnt is not None and not stem and (nsplit == 1 or nsplit * bm * bn * 4 <= wgrad_fuse_max()))
+    if fuse and nsplit > 1:
+        _chk(cnt, torch.int32, "cnt")
+        if cnt.numel() < (OC // bm) * (KTOT // bn):
+            raise ValueError("conv_wgrad: tile counter slice too small")
     C().conv_wgrad(STEM if stem else FWD, bm, bn, dy.data_ptr(), x.data_ptr(), ws.data_ptr(), _p(in_scale),
                    _p(in_shift), int(relu_in), N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, KTOT, nsplit, ms,
-                   stream_ptr(), int(lds_pad), int(dma))
-    C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsplit, float(scale), int(accumulate), stream_ptr())
+                   stream_ptr(), int(lds_pad), int(dma), dw.data_ptr() if fuse else 0,
+                   cnt.data_ptr() if fuse else 0, float(scale), int(accumulate))
+    if not fuse:
+        C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsplit, float(scale), int(accumulate), stream_ptr())
     return dw
 
 

@@ -46,7 +46,7 @@ def _add_stats(stats, y):
 
 
 def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None, relu_in=True, tile=None,
-             tail_res=None, tail_res_scale=None, tail_res_shift=None, tail_out=None, tail_bits=None):
+             tail_res=None, tail_res_scale=None, tail_res_shift=None, tail_out=None, tail_bits=None, fin=None):
     OC = w16.shape[0]
     IC = x.shape[-1]
     if tail_res is not None:  # previous block's output relu(bn3(x) + shortcut): bn_apply's semantics
@@ -61,11 +61,13 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     out.copy_(y.reshape(out.shape))
     if stats is not None:
         _add_stats(stats, out)
+        if fin is not None:  # the kernels' in-launch BN finalize, as its own step
+            fin.run()
     return out
 
 
 def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, addsrc=None, add_sub=1,
-               epilogue=None, bwd_y=None, bwd_coeff=None, dy_out=None):
+               epilogue=None, bwd_y=None, bwd_coeff=None, dy_out=None, _fin=(0, 1)):
     if bwd_y is not None:  # the operand is the BN-backward apply of (dy, bwd_y)
         d = dy_out if dy_out is not None else torch.empty_like(dy)
         bn_bwd_apply(dy, bwd_y, bwd_coeff, d, mask_mode=MASK_NONE)
@@ -102,6 +104,8 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             st2 = e.stats2.view(NSHARD, 2, Cc)
             st2[0, 0] += gf.sum(0)
             st2[0, 1] += (gf * ((e.ybn2.float() - e.mean2) * e.inv2).reshape(-1, Cc)).sum(0)
+        if hasattr(e, "run_fin"):  # the kernels' in-launch BN-backward finalize, as its own step
+            e.run_fin()
     dx.copy_(g.bfloat16())
     return dx
 
@@ -117,7 +121,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
 
 
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True, scale=1.0,
-               accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1):
+               accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None):
     N, OH, OW, OC = dy.shape
     IC = x.shape[-1]
     xf = _act_in(x, in_scale, in_shift, relu_in)

@@ -1,0 +1,125 @@
+"""In-launch BatchNorm finalize (csrc/bn_fin.h bn_fin_tail): the conv that accumulates a BN's
+statistics also finishes them in its last tile per 64-channel group. Bit-identical to the standalone
+bn_finalize / bn_bwd_coeff launches (same shard order, same math), across kernel families (four-wave
+igemm, the eight-wave kernel with its full-rounds batch split, the 3x3 patch kernel), and for whole
+training steps; counters return to zero."""
+import copy
+import math
+
+import pytest
+import torch
+
+from dbx_distributed_pytorch_examples_amd.ops import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _bn_state(C, dev="cuda"):
+    t = {k: torch.zeros(C, device=dev) for k in ("scale", "shift", "mean", "invstd")}
+    t["rm"] = torch.randn(C, device=dev)
+    t["rv"] = torch.rand(C, device=dev) + 0.5
+    t["gamma"] = torch.rand(C, device=dev) + 0.5
+    t["beta"] = torch.randn(C, device=dev)
+    return t
+
+
+@pytest.mark.parametrize("N,H,C,Kc,R,tile", [
+    (16, 14, 256, 256, 3, None),            # tune-table / default tiles
+    (40, 14, 256, 512, 1, (128, 128, 0)),   # four-wave
+    (200, 14, 256, 256, 3, (256, 256, 4)),  # eight-wave with the batch split (two launches)
+    (8, 56, 64, 64, 3, None),               # 64 -> 64 3x3 at 56: the patch kernel
+    (64, 4, 512, 512, 3, (64, 64, 0)),      # small map, many tiles per group
+])
+def test_fused_forward_finalize_bit_identical(N, H, C, Kc, R, tile):
+    torch.manual_seed(N + Kc)
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = (torch.randn(Kc, R * R * C, device="cuda") / math.sqrt(C * R * R)).bfloat16()
+    outs = []
+    for fused in (False, True):
+        y = torch.empty(N, H, H, Kc, device="cuda", dtype=torch.bfloat16)
+        st = K.new_stats(Kc, "cuda")
+        torch.manual_seed(7)
+        b = _bn_state(Kc)
+        fin = K.BnFin(K.BnFin.FWD, st, N * H * H, gamma=b["gamma"], beta=b["beta"], eps=1e-5, momentum=0.1,
+                      running_mean=b["rm"], running_var=b["rv"], scale=b["scale"], shift=b["shift"],
+                      mean=b["mean"], invstd=b["invstd"])
+        for rep in range(2):  # the second call reuses the (reset) counters
+            st.zero_()
+            kw = dict(R=R, S=R, stride=1, pad=R // 2, stats=st, tile=tile)
+            if fused:
+                K.conv_fwd(x, w, y, fin=fin, **kw)
+            else:
+                K.conv_fwd(x, w, y, **kw)
+                fin.run()
+        torch.cuda.synchronize()
+        assert int(fin.cnt.abs().sum()) == 0
+        outs.append(b)
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("mode,two", [(K.MASK_OUT, True), (K.MASK_OUT, False), (K.MASK_Y, False)])
+@pytest.mark.parametrize("tile", [None, (128, 128, 2)])
+def test_fused_backward_coeff_bit_identical(mode, two, tile):
+    torch.manual_seed(3)
+    N, H, C, Kc = 24, 14, 256, 512
+    dy = torch.randn(N, H, H, Kc, device="cuda").bfloat16()
+    wt = (torch.randn(C, Kc, device="cuda") / math.sqrt(Kc)).bfloat16()
+    ybn, ybn2 = (torch.randn(N, H, H, C, device="cuda").bfloat16() for _ in range(2))
+    mb = K.pack_mask_bits(torch.randn(N, H, H, C, device="cuda"))
+    res = []
+    for fused in (False, True):
+        torch.manual_seed(11)
+        bns = []
+        for _ in range(2):
+            d = {k: torch.randn(C, device="cuda") for k in ("mean", "gamma")}
+            d["invstd"] = torch.rand(C, device="cuda") + 0.5
+            d["sc"], d["sh"] = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+            d["coeff"] = torch.zeros(3 * C, device="cuda")
+            d["dg"], d["db"] = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+            d["st"] = K.new_stats(C, "cuda")
+            d["fin"] = K.BnFin(K.BnFin.BWD, d["st"], N * H * H, gamma=d["gamma"], mean=d["mean"], invstd=d["invstd"],
+                               coeff=d["coeff"], dgamma=d["dg"], dbeta=d["db"])
+            bns.append(d)
+        a, b = bns
+        dx = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
+        kw2 = dict(ybn2=ybn2, mean2=b["mean"], inv2=b["invstd"], stats2=b["st"]) if two else {}
+        e = (K.BNBwdEpilogue(K.MASK_OUT, ybn, a["mean"], a["invstd"], a["st"], mbits=mb, **kw2) if mode == K.MASK_OUT
+             else K.BNBwdEpilogue(K.MASK_Y, ybn, a["mean"], a["invstd"], a["st"], scale=a["sc"], shift=a["sh"]))
+        if fused:
+            e.fin1, e.fin2 = a["fin"], (b["fin"] if two else None)
+        K.conv_dgrad(dy, wt, dx, R=1, S=1, stride=1, pad=0, tile=tile, epilogue=e)
+        if not fused:
+            a["fin"].run()
+            if two:
+                b["fin"].run()
+        torch.cuda.synchronize()
+        assert int(a["fin"].cnt.abs().sum()) == 0
+        res.append([a[k] for k in ("coeff", "dg", "db")] + [b[k] for k in ("coeff", "dg", "db")])
+    for u, v in zip(*res):
+        assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("cifar_resnet18", 32, 64), ("resnet18", 32, 64)])
+def test_program_fused_fin_bit_identical(arch, size, batch, monkeypatch):
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    torch.manual_seed(0)
+    m1 = build_model(arch, num_classes=10)
+    m2 = copy.deepcopy(m1)
+    t1 = NativeTrainer(m1, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    monkeypatch.setenv("DBX_FUSE_BN_FIN", "0")
+    t2 = NativeTrainer(m2, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    assert t1.prog.fuse_fin and not t2.prog.fuse_fin
+    g = torch.Generator().manual_seed(1)
+    for i in range(5):
+        img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).cuda()
+        lab = torch.randint(0, 10, (batch,), generator=g).cuda()
+        t1.step(img, lab)
+        t2.step(img, lab)
+        assert t1.read_metrics()[0] == t2.read_metrics()[0], i
+    assert torch.equal(t1.prog.master, t2.prog.master)
+    for b1, b2 in zip(m1.buffers(), m2.buffers()):
+        assert torch.equal(b1, b2)
+    assert all(int(bn.fin_f.cnt.abs().sum()) == 0 and int(bn.fin_b.cnt.abs().sum()) == 0
+               for bn in t1.prog.bns if bn.fin_f is not None)

@@ -1,0 +1,114 @@
+"""Framework-owned RCCL communicator (csrc/runtime/comm.cpp, parallel/comm.py): collectives on a
+world-1 group on one GPU (exact results), capture inside a HIP graph, and the NativeTrainer's
+one-graph step with DBX_COMM=native bit-identical to the c10d segmented step. Multi-device RCCL
+runs only where >= 2 GPUs are visible."""
+import copy
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def world1(tmp_path):
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1)
+    yield
+    dist.destroy_process_group()
+
+
+def test_native_comm_world1_collectives(world1):
+    from dbx_distributed_pytorch_examples_amd.parallel.comm import NativeComm, native_comm_available
+    assert native_comm_available()
+    c = NativeComm()
+    x = torch.randn(1000, device="cuda")
+    ref = x.clone()
+    c.all_reduce(x)
+    c.all_reduce(x, op="avg")
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
+    out = torch.empty(1000, device="cuda", dtype=torch.bfloat16)
+    c.reduce_scatter(out, ref.bfloat16())
+    g = torch.empty_like(out)
+    c.all_gather(g, out)
+    c.broadcast(g)
+    torch.cuda.synchronize()
+    assert torch.equal(g, ref.bfloat16())
+    with pytest.raises(ValueError):
+        c.all_gather(torch.empty(3, device="cuda"), torch.empty(2, device="cuda"))
+    c.close()
+
+
+def test_native_comm_captured_in_graph(world1):
+    from dbx_distributed_pytorch_examples_amd.parallel.comm import NativeComm
+    c = NativeComm()
+    x = torch.zeros(4096, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        x.add_(1.0)
+        c.all_reduce(x)  # warm RCCL outside capture
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+            x.mul_(2.0)
+            c.all_reduce(x)
+            x.add_(1.0)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.all(x == 15.0)  # 1 -> 3 -> 7 -> 15
+    c.close()
+
+
+def test_trainer_native_comm_one_graph_matches_segmented(world1, monkeypatch):
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    monkeypatch.setenv("DBX_SEGMENTED_GRAPHS", "1")
+    torch.manual_seed(0)
+    m1 = build_model("resnet18", num_classes=10)
+    m2 = copy.deepcopy(m1)
+    monkeypatch.setenv("DBX_COMM", "native")
+    t1 = NativeTrainer(m1, 32, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    monkeypatch.setenv("DBX_COMM", "torch")
+    t2 = NativeTrainer(m2, 32, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    assert t1.ncomm is not None and t2.ncomm is None and t1.segmented and t2.segmented
+    g = torch.Generator().manual_seed(1)
+    for i in range(6):
+        img = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, generator=g).cuda()
+        lab = torch.randint(0, 10, (32,), generator=g).cuda()
+        t1.step(img, lab)
+        t2.step(img, lab)
+        l1, l2 = t1.read_metrics()[0], t2.read_metrics()[0]
+        assert l1 == l2, (i, l1, l2)
+    assert len(t1.graphs) == 1 and len(t2.graphs) > 1
+    assert torch.equal(t1.prog.master, t2.prog.master)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs >= 2 GPUs")
+def test_native_comm_two_ranks(tmp_path):
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import torch, torch.distributed as dist, os\n"
+        "from dbx_distributed_pytorch_examples_amd.parallel.comm import NativeComm\n"
+        "r = int(os.environ['RANK']); torch.cuda.set_device(r)\n"
+        "dist.init_process_group('gloo')\n"
+        "c = NativeComm()\n"
+        "x = torch.full((1 << 20,), float(r + 1), device='cuda'); c.all_reduce(x)\n"
+        "o = torch.empty(1 << 19, device='cuda'); c.reduce_scatter(o, torch.arange(1 << 20, device='cuda', dtype=torch.float32))\n"
+        "torch.cuda.synchronize()\n"
+        "assert torch.all(x == 3.0)\n"
+        "assert torch.equal(o, 2 * torch.arange(r << 19, (r + 1) << 19, device='cuda', dtype=torch.float32))\n"
+        "c.close(); dist.destroy_process_group(); print('OK', r)\n")
+    env = dict(os.environ, PYTHONPATH=os.getcwd())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", "29531", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count("OK") == 2

@@ -1,0 +1,79 @@
+"""In-launch split-K reduction of the weight gradient (conv_igemm.hip wgrad_store): bit-identical to
+the slab + wgrad_reduce path for one and several splits, scale / accumulate, both kernel families
+(register-staged and LDS-DMA), counters left at zero; plus the fp32 reference of the op."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dbx_distributed_pytorch_examples_amd.ops import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("N,H,C,Kc,R,tile,dma", [
+    (8, 8, 256, 512, 3, (128, 128), 2),    # few splits, LDS-DMA
+    (8, 8, 256, 512, 3, (128, 128), 0),    # register-staged
+    (2, 4, 512, 512, 3, (256, 128), 3),    # M = 32 rows: one split -> direct write
+    (16, 14, 128, 256, 1, (64, 64), 2),
+    (4, 7, 512, 2048, 1, (128, 256), 3),
+])
+@pytest.mark.parametrize("accumulate,scale", [(False, 1.0), (True, 0.5)])
+def test_fused_wgrad_reduce_bit_identical(N, H, C, Kc, R, tile, dma, accumulate, scale):
+    torch.manual_seed(N * H + C)
+    pad = R // 2
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    dy = torch.randn(N, H, H, Kc, device="cuda").bfloat16()
+    ws = torch.empty(64 * Kc * R * R * C + (16 << 20), device="cuda")
+    cnt = torch.zeros(K.wgrad_tiles_max(Kc, R * R * C), device="cuda", dtype=torch.int32)
+    base = torch.randn(Kc, R * R * C, device="cuda")
+    d0, d1 = base.clone(), base.clone()
+    kw = dict(R=R, S=R, stride=1, pad=pad, tile=tile, dma=dma, scale=scale, accumulate=accumulate)
+    # a first fused launch on other data leaves its slabs in the workspace (and in the caches): the
+    # second one must not read any of them (stale-line check) and reuses the reset counters
+    K.conv_wgrad(torch.randn_like(dy, dtype=torch.float32).bfloat16(), x, d1.clone(), ws, cnt=cnt, **kw)
+    K.conv_wgrad(dy, x, d1, ws, cnt=cnt, **kw)
+    K.conv_wgrad(dy, x, d0, ws, **kw)
+    torch.cuda.synchronize()
+    nsplit, _ = K.wgrad_splits(N * H * H, Kc, R * R * C, tile[0], tile[1], ws.numel())
+    if nsplit <= 8:  # single-level reduce on the two-kernel path: the same fp32 order
+        assert torch.equal(d0, d1)
+    else:
+        assert ((d0 - d1).norm() / d0.norm()).item() < 1e-6
+    assert int(cnt.abs().sum()) == 0
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Kc, C, R, R),
+                                      dy.float().permute(0, 3, 1, 2), padding=pad)
+    ref = ref.permute(0, 2, 3, 1).reshape(Kc, -1) * scale + (base if accumulate else 0)
+    assert ((d1 - ref).norm() / ref.norm()).item() < 1e-3
+
+
+def test_program_step_with_fused_reduce_matches_unfused(monkeypatch):
+    """A ResNet-18 CIFAR step (small maps: the fused path is taken) tracks the two-kernel path (which
+    sums many-split slabs in two levels: another fp32 order) to rounding noise, and the graph-replayed
+    fused step is bit-identical to the eager fused step."""
+    import copy
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    torch.manual_seed(0)
+    m1 = build_model("cifar_resnet18", num_classes=10)
+    m2 = copy.deepcopy(m1)
+    m3 = copy.deepcopy(m1)
+    t1 = NativeTrainer(m1, 64, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    t3 = NativeTrainer(m3, 64, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05), use_graphs=False)
+    monkeypatch.setenv("DBX_FUSE_WGRAD_REDUCE", "0")
+    t2 = NativeTrainer(m2, 64, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    assert t1.prog.fuse_wgrad_reduce and not t2.prog.fuse_wgrad_reduce
+    g = torch.Generator().manual_seed(1)
+    for i in range(6):
+        img = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, generator=g).cuda()
+        lab = torch.randint(0, 10, (64,), generator=g).cuda()
+        for t in (t1, t2, t3):
+            t.step(img, lab)
+        l1, l2, l3 = t1.read_metrics()[0], t2.read_metrics()[0], t3.read_metrics()[0]
+        assert l1 == l3, (i, l1, l3)
+        assert abs(l1 - l2) <= 1e-3 * abs(l2), (i, l1, l2)
+    assert torch.equal(t1.prog.master, t3.prog.master)
+    rel = ((t1.prog.master - t2.prog.master).norm() / t2.prog.master.norm()).item()
+    assert rel < 1e-4, rel
+    assert int(t1.prog.wg_cnt.abs().sum()) == 0
