@@ -18,6 +18,8 @@ int dbx_conv_igemm(int mode, int bm, int bn, const dbx::IGemmArgs* a, int pro, i
 int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, hipStream_t st, unsigned lds_pad,
                    int dma);
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
+int dbx_wgrad_reduce_gather(const float* ws, float* dw, int OC, int R, int S, int IC, int nsplit, float scale,
+                            int accumulate, hipStream_t st);
 int dbx_wgrad_patch3(const dbx::WgradArgs* a, long long ws_cap, hipStream_t st);
 int dbx_conv_dwfused(const dbx::DwFusedArgs* a, long long ws_cap, hipStream_t st);
 int dbx_stem_bwd(dbx::StemBwdArgs* a, long long ws_cap, int fused, hipStream_t st);
@@ -167,6 +169,11 @@ PYBIND11_MODULE(_C, m) {
     const int n = dbx_stem_bwd(&a, ws_cap, fused, S(st));
     if (n <= 0) check(n ? n : -1, "stem_bwd");
     return n;
+  });
+  m.def("wgrad_reduce_gather", [](uintptr_t ws, uintptr_t dw, int OC, int R, int S_, int IC, int nsplit, float scale,
+                                  int acc, uintptr_t st) {
+    check(dbx_wgrad_reduce_gather(P<const float*>(ws), P<float*>(dw), OC, R, S_, IC, nsplit, scale, acc, S(st)),
+          "wgrad_reduce_gather");
   });
   m.def("wgrad_reduce", [](uintptr_t ws, uintptr_t dw, long long n, int nsplit, float scale, int acc, uintptr_t st) {
     check(dbx_wgrad_reduce(P<const float*>(ws), P<float*>(dw), n, nsplit, scale, acc, S(st)), "wgrad_reduce");

@@ -11,6 +11,7 @@ __device__ __forceinline__ void bn_fwd_final(int c, double s, double q, float co
                                              const float* beta, float eps, float momentum, float* running_mean,
                                              float* running_var, float* scale, float* shift, float* save_mean,
                                              float* save_invstd) {
+#pragma clang fp contract(off)  // no context-dependent FMA contraction: fused == standalone bits
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -31,6 +32,7 @@ __device__ __forceinline__ void bn_fwd_final(int c, double s, double q, float co
 __device__ __forceinline__ void bn_bwd_final(int C, int c, double sd, double qd, float count, const float* gamma,
                                              const float* mean, const float* invstd, float* coeff, float* dgamma,
                                              float* dbeta, int accumulate) {
+#pragma clang fp contract(off)
   const float s = (float)sd, q = (float)qd;
   const float g = gamma ? gamma[c] : 1.f, is = invstd[c], mu = mean[c];
   const float sg = s / count, sgx = q / count;

@@ -487,6 +487,26 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
   }
 }
 
+// Final level of the stem weight-gradient reduction, writing only the real taps: the slabs hold
+// the stem's padded (OC, 8, 8, 4) layout; dw is the (OC, R, S, IC) gradient (KRSC) in the flat
+// buffer. Sums the splits in order (the same fp32 result as wgrad_reduce followed by a strided copy,
+// minus that copy's launch).
+__global__ void wgrad_reduce_gather_kernel(const float* __restrict__ ws, float* __restrict__ dw, int OC, int R, int S,
+                                           int IC, int nsplit, long long slab, float scale, int accumulate) {
+  const int n = OC * R * S * IC;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int oc = i / (R * S * IC), rem = i - oc * (R * S * IC);
+    const int r = rem / (S * IC), rem2 = rem - r * (S * IC);
+    const int s = rem2 / IC, c = rem2 - s * IC;
+    const long long src = (long long)oc * 256 + (r * 8 + s) * 4 + c;
+    float v = ws[src];
+    for (int k = 1; k < nsplit; ++k) v += ws[(long long)k * slab + src];
+    v *= scale;
+    if (accumulate) v += dw[i];
+    dw[i] = v;
+  }
+}
+
 }  // namespace dbx
 
 using namespace dbx;
@@ -615,6 +635,33 @@ extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, i
   WG(128, 256)
 #undef WG
   return -3;
+}
+
+// stem: reduce the (OC, 256) slabs into the (OC, R, S, IC) gradient (level 1 as dbx_wgrad_reduce)
+extern "C" int dbx_wgrad_reduce_gather(const float* ws, float* dw, int OC, int R, int S, int IC, int nsplit,
+                                       float scale, int accumulate, hipStream_t st) {
+  if (R > 8 || S > 8 || IC > 4) return -1;
+  const long long n = (long long)OC * 256;
+  const int n4 = (int)(n / 4);
+  const int gx = (n4 + 255) / 256;
+  const float* src = ws;
+  int parts = nsplit;
+  if (nsplit > 8 && (long long)gx * 4 < 1024) {
+    int G = 1024 / gx;
+    if (G > nsplit / 4) G = nsplit / 4;
+    if (G > 64) G = 64;
+    if (G < 2) G = 2;
+    const int spg = (nsplit + G - 1) / G;
+    G = (nsplit + spg - 1) / spg;
+    float* ws2 = const_cast<float*>(ws) + (size_t)nsplit * n;
+    hipLaunchKernelGGL(wgrad_reduce_l1_kernel, dim3(gx, G), dim3(256), 0, st, ws, ws2, n4, nsplit, spg);
+    src = ws2;
+    parts = G;
+  }
+  const int nout = OC * R * S * IC;
+  hipLaunchKernelGGL(wgrad_reduce_gather_kernel, dim3((nout + 255) / 256), dim3(256), 0, st, src, dw, OC, R, S, IC,
+                     parts, n, scale, accumulate);
+  return (int)hipGetLastError();
 }
 
 extern "C" int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale,

@@ -859,6 +859,35 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const T* __restrict__ 
                                                           const WDesc* __restrict__ desc, int nlayers) {
   const WDesc d = desc[blockIdx.y];
   const int tid = threadIdx.x;
+  // per-step utility work folded into this launch (one graph node instead of four):
+  //   tr == -2: the stem weight (K, R, S, C) at d.src -> bf16 (K, 8, 8, 4) at d.fwd, zero padded
+  //             (R = d.RS >> 4, S = d.RS & 15); tr == -3: zero d.K doubles at address d.src (the BN
+  //             statistics slabs); tr == -4: add 1 to d.K int64 counters at address d.src
+  //             (num_batches_tracked)
+  if (d.tr == -2) {
+    const int R = d.RS >> 4, S = d.RS & 15;
+    const long long n = (long long)d.K * 256;
+    for (long long i = (long long)blockIdx.x * 256 + tid; i < n; i += (long long)gridDim.x * 256) {
+      const int k = (int)(i >> 8), r = (int)(i >> 5) & 7, s = (int)(i >> 2) & 7, c = (int)i & 3;
+      const bool v = r < R && s < S && c < d.C;
+      wbuf[d.fwd + i] = v ? (bf16)master[d.src + (((long long)k * R + r) * S + s) * d.C + c] : (bf16)0.f;
+    }
+    return;
+  }
+  if (d.tr == -3) {
+    double* z = reinterpret_cast<double*>(d.src);
+    const long long n2 = (long long)d.K / 2;
+    for (long long i = (long long)blockIdx.x * 256 + tid; i < n2; i += (long long)gridDim.x * 256)
+      reinterpret_cast<f64x2*>(z)[i] = f64x2{0.0, 0.0};
+    if ((d.K & 1) && blockIdx.x == 0 && tid == 0) z[d.K - 1] = 0.0;
+    return;
+  }
+  if (d.tr == -4) {
+    long long* c = reinterpret_cast<long long*>(d.src);
+    if (blockIdx.x == 0)
+      for (int i = tid; i < d.K; i += 256) c[i] += 1;
+    return;
+  }
   if (d.tr < 0) {
     const long long n = (long long)d.K * d.RS * d.C;
     const long long n4 = n / 4;

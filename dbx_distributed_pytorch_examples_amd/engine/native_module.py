@@ -219,9 +219,7 @@ class NativeResNet(nn.Module):
 
     def _fwd_body(self):
         p = self.prog
-        p.prepare_weights()
-        if p.training:
-            p.nbt.add_(1)
+        p.prepare_weights(step=p.training)  # (training: + statistics zeroing, num_batches_tracked)
         p.forward(compute_grad=False, metrics=False)
 
     def _native_forward(self, x: torch.Tensor) -> torch.Tensor:

@@ -152,9 +152,9 @@ class NativeTrainer:
         segs = p._segments
 
         def fwd_phase():
-            p.prepare_weights()
+            # bf16 weights + BN-statistics zeroing + every BN's num_batches_tracked, one launch
+            p.prepare_weights(step=True)
             p.load_input_u8(self.flip)
-            p.nbt.add_(1)  # every BN's num_batches_tracked (views of one tensor)
             p.forward(smoothing=self.smoothing)
 
         phases: List[Tuple[str, Callable, Optional[Tuple[int, int]]]] = []

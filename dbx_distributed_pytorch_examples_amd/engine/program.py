@@ -195,6 +195,7 @@ class ResNetProgram:
         self._alloc_params()
         self._alloc_activations()
         self.build_fins()
+        self._pack_step_descs()
         self.training = True
 
     # ----------------------------------------------------------------------------------
@@ -367,22 +368,27 @@ class ResNetProgram:
         fc_off = n16
         n16 += self.fc.weight.numel()
         descs.append((self.fc_w_off, fc_off, -1, self.num_classes, 1, self.fc.in_features))
-        self.w16buf = torch.zeros(n16 + 16, device=dev, dtype=torch.bfloat16)
+        # the stem's (K, 8, 8, 4) zero-padded copy and the fc bias: in the same buffer, same launch
+        al = lambda v: (v + 63) // 64 * 64  # noqa: E731
+        st = self.stem
+        stem_off = n16 = al(n16)
+        n16 += st.OC * 256
+        descs.append((st.off, stem_off, -2, st.OC, st.R * 16 + st.S, st.IC))
+        fcb_off = n16 = al(n16)
+        n16 += self.num_classes
+        descs.append((self.fc_b_off, fcb_off, -1, self.num_classes, 1, 1))
+        self.w16buf = torch.zeros(al(n16) + 64, device=dev, dtype=torch.bfloat16)
         for cv in self.convs:
             if cv.stem:
-                cv.w16 = torch.zeros(cv.OC, 256, device=dev, dtype=torch.bfloat16)
+                cv.w16 = self.w16buf[stem_off:stem_off + cv.OC * 256].view(cv.OC, 256)
                 continue
             cv.w16 = self.w16buf[cv._w16_off:cv._w16_off + cv.numel].view(cv.OC, -1)
             cv.wt16 = self.w16buf[cv._wt16_off:cv._wt16_off + cv.numel].view(cv.IC, -1)
         self.fc_w16 = self.w16buf[fc_off:fc_off + self.fc.weight.numel()].view(self.num_classes, -1)
-        # WDesc {long long src, fwd, tr; int K, RS, C, pad} = 40 bytes
-        raw = []
-        for (src, f, t, k, rs, c) in descs:
-            raw.append(torch.tensor([src, f, t], dtype=torch.int64).view(torch.int32))
-            raw.append(torch.tensor([k, rs, c, 0], dtype=torch.int32))
-        self.wdesc = torch.cat(raw).to(dev)
+        self.fc_b16 = self.w16buf[fcb_off:fcb_off + self.num_classes]
+        self._wdescs = descs  # + the per-step entries (_pack_step_descs, after the activations exist)
+        self.wdesc = self._pack_wdesc(descs)
         self.n_wdesc = len(descs)
-        self.fc_b16 = torch.zeros(self.num_classes, device=dev, dtype=torch.bfloat16)
         self.stem_grad_tmp = torch.zeros(self.stem.OC, 256, device=dev, dtype=torch.float32)
 
     def _alloc_activations(self):
@@ -486,6 +492,24 @@ class ResNetProgram:
         self.cutmix = False
         self.mix_perm = self.mix_box = self.mix_lam = self.labels2 = None
 
+    def _pack_wdesc(self, descs) -> torch.Tensor:
+        # WDesc {long long src, fwd, tr; int K, RS, C, pad} = 40 bytes
+        raw = []
+        for (src, f, t, k, rs, c) in descs:
+            raw.append(torch.tensor([src, f, t], dtype=torch.int64).view(torch.int32))
+            raw.append(torch.tensor([k, rs, c, 0], dtype=torch.int32))
+        return torch.cat(raw).to(self.dev)
+
+    def _pack_step_descs(self) -> None:
+        """The training step's weight-prep launch also zeroes the BN statistics slabs and counts
+        num_batches_tracked (prepare_weights(step=True))."""
+        extra = [(self.stats_region.data_ptr(), 0, -3, self.stats_region.numel(), 0, 0)]
+        if self.nbt.numel():
+            extra.append((self.nbt.data_ptr(), 0, -4, self.nbt.numel(), 0, 0))
+        self.wdesc_step = self._pack_wdesc(self._wdescs + extra) if self.dev.type == "cuda" else None
+        self.n_wdesc_step = len(self._wdescs) + len(extra)
+        self._stats_zeroed = False
+
     def build_fins(self) -> None:
         """(Re)build every BN's finalize descriptors (K.BnFin: raw pointers to its statistics, affine
         parameters, running stats and outputs) -- again whenever one of those tensors is reallocated."""
@@ -527,15 +551,18 @@ class ResNetProgram:
     # ----------------------------------------------------------------------------------
     # per-step pieces
     # ----------------------------------------------------------------------------------
-    def prepare_weights(self):
-        """fp32 master -> bf16 compute copies (KRSC fwd, CRSK dgrad, fc, stem 8x8x4)."""
+    def prepare_weights(self, step: bool = False):
+        """fp32 master -> bf16 compute copies (KRSC fwd, CRSK dgrad, fc weight and bias, stem 8x8x4),
+        one launch. ``step``: a training step follows -- the same launch zeroes the BN statistics and
+        counts num_batches_tracked (the forward then skips its own zeroing)."""
         src = self.master if self.param16 is None else self.param16  # ZeRO: the all-gathered bf16 copy
+        if step and self.wdesc_step is not None:
+            K.weight_prep(src, self.w16buf, self.wdesc_step, self.n_wdesc_step)
+            self._stats_zeroed = True
+            return
         K.weight_prep(src, self.w16buf, self.wdesc, self.n_wdesc)
-        st = self.stem
-        w = src[st.off:st.off + st.numel].view(st.OC, st.R, st.S, st.IC)
-        stem16 = st.w16.view(st.OC, 8, 8, 4)
-        stem16[:, :st.R, :st.S, :st.IC].copy_(w)
-        self.fc_b16.copy_(src[self.fc_b_off:self.fc_b_off + self.num_classes])
+        if step:
+            self.nbt.add_(1)
 
     def bn_param_blocks(self) -> List[Tuple[int, int]]:
         """Contiguous [lo, hi) blocks of the flat buffer holding BatchNorm affine parameters (read in
@@ -576,8 +603,9 @@ class ResNetProgram:
         ``features_only``: stop after global average pooling and return ``self.pooled`` [N, C]
         (frozen-backbone feature extraction; the fc / loss are left to the caller)."""
         tr = self.training
-        if tr:
+        if tr and not self._stats_zeroed:
             self.stats_region.zero_()
+        self._stats_zeroed = False
         N = self.N
         st, sbn = self.stem, self.stem_bn
         K.conv_stem_fwd(self.x4, st.w16, self.y0, R=st.R, S=st.S, stride=st.stride, pad=st.pad,
@@ -885,10 +913,13 @@ class ResNetProgram:
             K.maxpool_bwd(dp, self.parg, self.da0, K=self.pool_k, stride=self.pool_s, pad=self.pool_p)
             self._bn_bwd(sbn, self.da0, self.y0, self.dy0, self.N * st.OH * st.OW, K.MASK_Y)
         def stem_wgrad():
-            K.conv_wgrad(self.dy0, self.x4, self.stem_grad_tmp, self.ws, R=st.R, S=st.S, stride=st.stride,
-                         pad=st.pad, stem=True)
-            g = self.grad[st.off:st.off + st.numel].view(st.OC, st.R, st.S, st.IC)
-            g.copy_(self.stem_grad_tmp.view(st.OC, 8, 8, 4)[:, :st.R, :st.S, :st.IC])
+            # reduced straight into the flat gradient's (OC, R, S, IC) slice when the stem tile kernel
+            # runs (no padded temporary + strided copy)
+            g = self.grad[st.off:st.off + st.numel]
+            out = K.conv_wgrad(self.dy0, self.x4, self.stem_grad_tmp, self.ws, R=st.R, S=st.S, stride=st.stride,
+                               pad=st.pad, stem=True, out_krsc=g)
+            if out is not g:
+                g.view(st.OC, st.R, st.S, st.IC).copy_(self.stem_grad_tmp.view(st.OC, 8, 8, 4)[:, :st.R, :st.S, :st.IC])
         self._side(stem_wgrad)
 
     def backward(self):

@@ -585,14 +585,16 @@ def wgrad_tiles_max(OC: int, KTOT: int) -> int:
 
 @_dispatch
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True,
-               scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None):
+               scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None, out_krsc=None):
     """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace.
     ``dma``: operand path of the prologue-free kernels -- LDS-DMA ring depth 2 / 3, 0 = register
     staged, -1 = the tune table's choice, else DBX_WGRAD_DMA, else 3 for 256-wide tiles / 2.
     ``cnt``: zeroed int32 tile counters (>= wgrad_tiles_max(OC, KTOT), owned by this call site):
     when given and the split slabs of a tile are small (wgrad_fuse_max), the split-K reduction runs
     inside the launch (the last block of each tile sums its slabs, bit-identical to wgrad_reduce)
-    and no separate reduce kernel is launched; one split writes dW directly."""
+    and no separate reduce kernel is launched; one split writes dW directly. ``out_krsc`` (stem
+    only): the reduction writes the real taps straight into this (OC, R, S, IC) gradient instead of
+    the padded (OC, 8, 8, 4) ``dw``."""
     N, OH, OW, OC = dy.shape
     _, IH, IW, IC = x.shape
     KTOT = 256 if stem else R * S * IC
@@ -619,6 +621,14 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         _chk(dy, torch.bfloat16, "dy", N * OH * OW * 64)
         n = C().stem_bwd(0, 0, dy.data_ptr(), 0, 0, 0, x.data_ptr(), ws.data_ptr(), ws.numel(), N, OH, OW, OC, 0, 0,
                          0, 1, 0, IH, IW, R, S, stride, pad, 0, stream_ptr())
+        if out_krsc is not None:  # (the image's real channels: x carries them padded to 4)
+            icr = out_krsc.numel() // (OC * R * S)
+            _chk(out_krsc, torch.float32, "out_krsc", OC * R * S * icr)
+            if not 1 <= icr <= IC:
+                raise ValueError("out_krsc: (OC, R, S, IC) with IC <= the padded input channels")
+            C().wgrad_reduce_gather(ws.data_ptr(), out_krsc.data_ptr(), OC, R, S, icr, n, float(scale),
+                                    int(accumulate), stream_ptr())
+            return out_krsc
         C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, n, float(scale), int(accumulate), stream_ptr())
         return dw
     if stem:

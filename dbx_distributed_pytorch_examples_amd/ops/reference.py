@@ -121,12 +121,16 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
 
 
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True, scale=1.0,
-               accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None):
+               accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None, out_krsc=None):
     N, OH, OW, OC = dy.shape
     IC = x.shape[-1]
     xf = _act_in(x, in_scale, in_shift, relu_in)
     g = torch.nn.grad.conv2d_weight(_nchw(xf), (OC, IC, R, S), _nchw(dy.float()), stride=stride, padding=pad)
     g = g.permute(0, 2, 3, 1) * scale  # KRSC
+    if stem and out_krsc is not None:  # the real input channels only (x is padded to 4)
+        icr = out_krsc.numel() // (OC * R * S)
+        out_krsc.copy_((g[..., :icr].reshape(-1) + (out_krsc if accumulate else 0)))
+        return out_krsc
     if stem:
         full = torch.zeros(OC, 8, 8, 4, dtype=torch.float32, device=dy.device)
         full[:, :R, :S, :IC] = g
@@ -474,6 +478,14 @@ def weight_prep(master, wbuf, desc_dev, nlayers):
         row = d[i]
         src, fwd, tr = (int(x) for x in row[:6].view(torch.int64))
         k, rs, c = int(row[6]), int(row[7]), int(row[8])
+        if tr == -2:  # stem (K, R, S, C) -> (K, 8, 8, 4) zero padded
+            R, S = rs >> 4, rs & 15
+            o = torch.zeros(k, 8, 8, 4, dtype=torch.bfloat16, device=wbuf.device)
+            o[:, :R, :S, :c] = master[src:src + k * R * S * c].float().view(k, R, S, c).bfloat16()
+            wbuf[fwd:fwd + k * 256].copy_(o.reshape(-1))
+            continue
+        if tr < -2:  # absolute-pointer utility entries (GPU only)
+            continue
         n = k * rs * c
         w = master[src:src + n].float()
         if fwd >= 0:
