@@ -3,6 +3,7 @@
 // definition, so a fused and an unfused step produce the same bits.
 #pragma once
 #include "abi.h"
+#include "common.h"
 
 namespace dbx {
 
@@ -45,19 +46,22 @@ __device__ __forceinline__ void bn_bwd_final(int C, int c, double sd, double qd,
 }
 
 // Shard sum of channel c in the standalone kernels' order (0 + shard 0 + shard 1 + ...: their
-// 32-way split holds one shard per lane for nshard <= 32, summed lane by lane).
-__device__ __forceinline__ void bn_fin_sums(const double* stats, int nshard, int C, int c, double& s, double& q) {
+// 32-way split holds one shard per lane for nshard <= 32, summed lane by lane). The in-launch
+// finalize reads the shards with agent-scope (sc1) loads: they bypass this CU's L1, and the shards'
+// lines are never in an L2 (the statistics atomics execute at the memory side and drop the line).
+__device__ __forceinline__ void bn_fin_sums_sc1(const double* stats, int nshard, int C, int c, double& s, double& q) {
   s = 0.0;
   q = 0.0;
   for (int k = 0; k < nshard; ++k) {
-    s += stats[(size_t)k * 2 * C + c];
-    q += stats[(size_t)k * 2 * C + C + c];
+    gf64* p = (gf64*)(stats + (size_t)k * 2 * C + c);
+    s += __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    q += __hip_atomic_load(p + C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 __device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c) {
   double s, q;
-  bn_fin_sums(f.stats, f.nshard, f.C, c, s, q);
+  bn_fin_sums_sc1(f.stats, f.nshard, f.C, c, s, q);
   if (f.mode == 1)
     bn_fwd_final(c, s, q, f.count, f.gamma, f.beta, f.eps, f.momentum, f.running_mean, f.running_var, f.scale,
                  f.shift, f.mean, f.invstd);
@@ -65,12 +69,14 @@ __device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c) {
     bn_bwd_final(f.C, c, s, q, f.count, f.gamma, f.mean, f.invstd, f.coeff, f.dgamma, f.dbeta, f.accumulate);
 }
 
-// End of a conv tile epilogue whose launch carries BN finalize descriptors: the tile's statistics
-// atomics are published (agent-scope release) and counted per 64-channel group; the tile that
-// completes a group's count (all ceil(M / BM) M-tiles of the producer, over all its launches)
-// acquires and finalizes those 64 channels, then resets the group counter. The same hand-off as the
-// split-K reduction (cdna_hip_programming.md §5 item 2); the finalizing block reads 2 x nshard x 64
-// doubles. n0: first output channel of the tile (a multiple of 64).
+// End of a conv tile epilogue whose launch carries BN finalize descriptors: once every wave's
+// statistics atomics have completed (they execute at the memory side: no L2 write-back, so no
+// release fence -- a buffer_wbl2 per tile would write back the tile's just-stored outputs, which
+// measured 1.6x slower steps), one lane per 64-channel group takes a ticket; the tile that completes
+// a group's count (all ceil(M / BM) M-tiles of the producer, over all its launches) finalizes those
+// 64 channels from sc1 loads of the shards (MI355X_MICROARCH.md "Valid forms", row 1: the last
+// adder loads after its add returned, the other waves after a barrier), then resets the counter.
+// The finalizing block reads 2 x nshard x 64 doubles. n0: first output channel of the tile.
 template <int BM, int BN>
 __device__ __forceinline__ void bn_fin_tail(const IGemmArgs& a, const int n0, bf16* lds) {
   constexpr int G = BN / 64;
@@ -80,22 +86,12 @@ __device__ __forceinline__ void bn_fin_tail(const IGemmArgs& a, const int n0, bf
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics atomics have completed
   __syncthreads();                                   // ... every wave's; the LDS is free
   int* flag = reinterpret_cast<int*>(lds);
-  if (tid < 64) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int last = 0;
-    if (tid < ng) {
-      const BnFin* f = tid < G ? a.fin1 : a.fin2;
-      const unsigned total = a.fin_final ? (unsigned)(a.fin_base + (a.M + BM - 1) / BM) : 0xFFFFFFFFu;
-      const unsigned t = __hip_atomic_fetch_add(f->cnt + (n0 >> 6) + tid % G, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-      last = t + 1u == total;
-      flag[tid] = last;
-    }
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+  if (tid < ng) {
+    const BnFin* f = tid < G ? a.fin1 : a.fin2;
+    const unsigned total = a.fin_final ? (unsigned)(a.fin_base + (a.M + BM - 1) / BM) : 0xFFFFFFFFu;
+    const unsigned t = __hip_atomic_fetch_add((gu32*)(f->cnt + (n0 >> 6) + tid % G), 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    flag[tid] = t + 1u == total;
   }
   __syncthreads();
   for (int k = 0; k < ng; ++k) {
@@ -103,7 +99,7 @@ __device__ __forceinline__ void bn_fin_tail(const IGemmArgs& a, const int n0, bf
     const BnFin* f = k < G ? a.fin1 : a.fin2;
     const int g = (n0 >> 6) + k % G;
     if (tid < 64) bn_fin_channel(*f, g * 64 + tid);
-    if (tid == 0) __hip_atomic_store(f->cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store((gu32*)(f->cnt + g), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();  // flags read before the LDS is reused
 }

@@ -11,6 +11,9 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
+// global-address-space views for inter-workgroup counters and sc1 loads (global_, never flat_ ops)
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) double gf64;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 #define DBX_LDS __attribute__((address_space(3)))

@@ -16,21 +16,85 @@ namespace dbx {
 
 // End of a weight-gradient tile: the fp32 partial slab ws[split][k][kk], or (a.dw set) the finished
 // gradient. With one split the tile is written to dw straight from the accumulators. Otherwise the
-// in-launch split-K reduction (cdna_hip_programming.md §5, "Projection GEMM at M = 256" item 2):
-// every wave drains its slab stores, one agent-scope release, a relaxed agent-scope ticket from
-// cnt[tile]; the block drawing nsplit-1 acquires and sums the nsplit slabs of the tile in split
-// order -- the same fp32 order as wgrad_reduce_kernel, so the result is bit-identical to the
-// two-kernel path -- then resets the counter for the next launch. Correct for any placement of a
-// tile's splits over XCDs. The host enables it only when a tile's slabs are small (the reducer reads
-// nsplit x BM x BN x 4 bytes alone).
+// in-launch split-K reduction (cdna_hip_programming.md §5, "Projection GEMM at M = 256" item 2, in
+// its write-through form): every block stores its partial tile with 16-B sc1 (write-through) buffer
+// stores in the accumulators' own lane order -- tile region ((split * ntile + tile) * BM * BN) -- so
+// no release fence (a buffer_wbl2 per block) is needed; each wave drains its stores, then one lane
+// takes a relaxed agent-scope ticket from cnt[tile]; the block drawing nsplit-1 loads the nsplit
+// partials of the tile with sc1 loads at the same lane positions (MI355X_MICROARCH.md "Valid forms",
+// row 1) and sums them in split order -- the same fp32 order per element as wgrad_reduce_kernel, so
+// the result is bit-identical to the two-kernel path when that sums in one level -- and writes dw;
+// then resets the counter. The host enables it only when a tile's partials are small (the reducer
+// reads nsplit x BM x BN x 4 bytes alone).
 template <int BM, int BN, int WM, int WN, int TM, int TN>
 __device__ __forceinline__ void wgrad_store(const WgradArgs& a, const f32x4 (&acc)[TM][TN], const int split,
                                             const int tile, const int k0, const int kk0, bf16* lds) {
-  constexpr int NT = 64 * WM * WN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
-  const bool direct = a.dw != nullptr && a.nsplit == 1;  // uniform
-  float* out = direct ? a.dw : a.ws + (size_t)split * a.OC * a.KTOT;
-  const float sc = direct ? a.scale : 1.f;
+  if (a.dw != nullptr && a.nsplit == 1) {  // uniform: the finished gradient straight from the tile
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = k0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
+          const int kk = kk0 + wn * (BN / WN) + j * 16 + (lane & 15);
+          const size_t e = (size_t)k * a.KTOT + kk;
+          float v = acc[i][j][r] * a.scale;
+          if (a.accumulate) v += a.dw[e];
+          a.dw[e] = v;
+        }
+    return;
+  }
+  if (a.dw == nullptr) {  // slab for the separate reduce kernel: ws[split][k][kk]
+    float* out = a.ws + (size_t)split * a.OC * a.KTOT;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = k0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
+          const int kk = kk0 + wn * (BN / WN) + j * 16 + (lane & 15);
+          out[(size_t)k * a.KTOT + kk] = acc[i][j][r];
+        }
+    return;
+  }
+  const int ntile = (a.OC / BM) * (a.KTOT / BN);
+  const rsrc_t ws = make_rsrc(a.ws, (unsigned long long)a.nsplit * ntile * BM * BN * 4);
+  // this thread's 16-B slot of accumulator (i, j) inside a tile region
+  auto slot = [&](int s, int i, int j) __attribute__((always_inline)) {
+    return (unsigned)((((size_t)s * ntile + tile) * BM * BN + ((size_t)(wid * TM + i) * TN + j) * 256 + lane * 4) * 4);
+  };
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
+                                                                acc[i][j]),
+                                             ws, slot(split, i, j), 0, 16);  // aux 16: sc1 (write-through)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has reached memory
+  __syncthreads();                                   // ... every wave's; LDS no longer read
+  int* flag = reinterpret_cast<int*>(lds);
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add((gu32*)(a.cnt + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = t == (unsigned)(a.nsplit - 1);
+  }
+  __syncthreads();
+  if (!flag[0]) return;  // block-uniform
+  f32x4 s[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      s[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ws, slot(0, i, j), 0, 16));
+  for (int k = 1; k < a.nsplit; ++k) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        s[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ws, slot(k, i, j), 0, 16));
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -40,56 +104,11 @@ __device__ __forceinline__ void wgrad_store(const WgradArgs& a, const f32x4 (&ac
         const int k = k0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
         const int kk = kk0 + wn * (BN / WN) + j * 16 + (lane & 15);
         const size_t e = (size_t)k * a.KTOT + kk;
-        float v = acc[i][j][r] * sc;
-        if (direct && a.accumulate) v += out[e];
-        out[e] = v;
+        float v = s[i][j][r] * a.scale;
+        if (a.accumulate) v += a.dw[e];
+        a.dw[e] = v;
       }
-  if (a.dw == nullptr || direct) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores have left
-  __syncthreads();                                   // ... every wave's; LDS no longer read
-  int* flag = reinterpret_cast<int*>(lds);
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == (unsigned)(a.nsplit - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    flag[0] = last;
-  }
-  __syncthreads();
-  if (!flag[0]) return;  // block-uniform
-  constexpr int C4 = BN / 4;               // float4 per tile row
-  constexpr int V = BM * C4 / NT;           // float4 per thread
-  static_assert(V * NT == BM * C4, "tile / thread count");
-  const size_t slab = (size_t)a.OC * a.KTOT;
-  size_t off[V];
-  f32x4 s[V];
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    const int idx = tid + v * NT;
-    off[v] = (size_t)(k0 + idx / C4) * a.KTOT + kk0 + (idx % C4) * 4;
-    s[v] = *reinterpret_cast<const f32x4*>(a.ws + off[v]);
-  }
-  for (int k = 1; k < a.nsplit; ++k) {
-    const float* w = a.ws + (size_t)k * slab;
-#pragma unroll
-    for (int v = 0; v < V; ++v) s[v] += *reinterpret_cast<const f32x4*>(w + off[v]);
-  }
-  f32x4 d[V];
-  if (a.accumulate) {
-#pragma unroll
-    for (int v = 0; v < V; ++v) d[v] = *reinterpret_cast<const f32x4*>(a.dw + off[v]);
-  }
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    f32x4 o = s[v] * a.scale;
-    if (a.accumulate) o += d[v];
-    *reinterpret_cast<f32x4*>(a.dw + off[v]) = o;
-  }
-  if (tid == 0) __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store((gu32*)(a.cnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // WM x WN waves (64*WM*WN threads), each owning a (BM/WM) x (BN/WN) block of dW.

@@ -151,9 +151,9 @@ class ResNetProgram:
         self.in_ch = model.conv1.in_channels
         self.overlap_wgrad = os.environ.get("DBX_OVERLAP_WGRAD", "1") == "1"
         # split-K weight-gradient reduction inside the wgrad launch where a tile's slabs are small
-        self.fuse_wgrad_reduce = os.environ.get("DBX_FUSE_WGRAD_REDUCE", "1") == "1"
+        self.fuse_wgrad_reduce = os.environ.get("DBX_FUSE_WGRAD_REDUCE", "0") == "1"
         # BN finalize / backward coefficients computed by the producing conv's last tiles (K.BnFin)
-        self.fuse_fin = os.environ.get("DBX_FUSE_BN_FIN", "1") == "1"
+        self.fuse_fin = os.environ.get("DBX_FUSE_BN_FIN", "0") == "1"
         self.wgrad_lds_pad = int(os.environ.get("DBX_WGRAD_LDS_PAD", "0"))
         # store block-internal BN outputs from the MASK_Y dgrad epilogue for the wgrads (A/B switch)
         self.act_writeback = os.environ.get("DBX_ACT_WRITEBACK", "1") == "1"

@@ -107,6 +107,7 @@ def test_program_fused_fin_bit_identical(arch, size, batch, monkeypatch):
     torch.manual_seed(0)
     m1 = build_model(arch, num_classes=10)
     m2 = copy.deepcopy(m1)
+    monkeypatch.setenv("DBX_FUSE_BN_FIN", "1")
     t1 = NativeTrainer(m1, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_FUSE_BN_FIN", "0")
     t2 = NativeTrainer(m2, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))

@@ -60,6 +60,7 @@ def test_program_step_with_fused_reduce_matches_unfused(monkeypatch):
     torch.manual_seed(0)
     m1 = build_model("cifar_resnet18", num_classes=10)
     m2, m3 = copy.deepcopy(m1), copy.deepcopy(m1)
+    monkeypatch.setenv("DBX_FUSE_WGRAD_REDUCE", "1")
     t1 = NativeTrainer(m1, 64, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     t3 = NativeTrainer(m3, 64, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05), use_graphs=False)
     monkeypatch.setenv("DBX_FUSE_WGRAD_REDUCE", "0")
