@@ -545,17 +545,23 @@ def _stem_wgrad_tile() -> bool:
     return _STEM_WGRAD
 
 
-def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int) -> Tuple[int, int]:
-    """Split the pixel reduction so that ~1024 workgroups stream (>= 8 K-blocks each); the
-    workspace holds nsplit slabs + up to 64 level-1 partial slabs of the reduction."""
+def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int,
+                 rounds: Optional[float] = None) -> Tuple[int, int]:
+    """Split the pixel reduction so that ``rounds`` rounds of workgroups stream over the CUs (>= 8
+    K-blocks each); the workspace holds nsplit slabs + up to 64 level-1 partial slabs of the
+    reduction. ``rounds``: the tune table's per-shape value, else DBX_WGRAD_ROUNDS (2); 0 = no split
+    (one workgroup per tile over all M rows, the gradient written directly)."""
     global _WG_ROUNDS
     if _WG_ROUNDS is None:
         import os
         _WG_ROUNDS = float(os.environ.get("DBX_WGRAD_ROUNDS", "2"))
+    r = _WG_ROUNDS if rounds is None else float(rounds)
+    if r <= 0:
+        return 1, max(64, (M + 63) // 64 * 64)
     tiles = (OC // bm) * (KTOT // bn)
-    # _WG_ROUNDS rounds of workgroups over the 256 CUs (8-wave (256-wide) tiles run one per CU,
-    # 4-wave two): fewer rounds = longer workgroups and proportionally smaller fp32 partial slabs
-    target = max(1, int(_WG_ROUNDS * (256 if max(bm, bn) >= 256 else 512)) // tiles)
+    # r rounds of workgroups over the CUs (8-wave (256-wide) tiles run one per CU, 4-wave two):
+    # fewer rounds = longer workgroups and proportionally smaller fp32 partial slabs
+    target = max(1, int(r * (num_cus() if max(bm, bn) >= 256 else 2 * num_cus())) // tiles)
     ms = max(512, ((M + target - 1) // target + 63) // 64 * 64)
     nsplit = (M + ms - 1) // ms
     while (nsplit + min(64, nsplit)) * OC * KTOT > max_ws_elems and nsplit > 1:
@@ -585,7 +591,8 @@ def wgrad_tiles_max(OC: int, KTOT: int) -> int:
 
 @_dispatch
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True,
-               scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None, out_krsc=None):
+               scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None, out_krsc=None,
+               rounds=None):
     """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace.
     ``dma``: operand path of the prologue-free kernels -- LDS-DMA ring depth 2 / 3, 0 = register
     staged, -1 = the tune table's choice, else DBX_WGRAD_DMA, else 3 for 256-wide tiles / 2.
@@ -644,6 +651,8 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
                 bm, bn = t[0], t[1]
                 if len(t) > 2 and dma < 0:  # measured operand path (tools/tune_conv.py)
                     dma = int(t[2])
+                if len(t) > 3 and rounds is None:  # measured split depth (tools/tune_conv.py --wgrad-rounds)
+                    rounds = float(t[3])
             else:
                 bm = 128 if OC % 128 == 0 else 64
                 bn = 128 if IC % 128 == 0 else 64
@@ -651,10 +660,11 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         _chk(in_scale, torch.float32, "in_scale", IC)
         _chk(in_shift, torch.float32, "in_shift", IC)
     M = N * OH * OW
-    nsplit, ms = wgrad_splits(M, OC, KTOT, bm, bn, ws.numel())
+    nsplit, ms = wgrad_splits(M, OC, KTOT, bm, bn, ws.numel(), rounds)
     if (nsplit + (min(64, nsplit) if nsplit > 8 else 0)) * OC * KTOT > ws.numel():
         raise ValueError("wgrad workspace too small")
-    fuse = (cnt is not None and not stem and (nsplit == 1 or nsplit * bm * bn * 4 <= wgrad_fuse_max()))
+    # one split: the kernel writes the finished gradient itself (no slab, no reduce launch)
+    fuse = not stem and (nsplit == 1 or (cnt is not None and nsplit * bm * bn * 4 <= wgrad_fuse_max()))
     if fuse and nsplit > 1:
         _chk(cnt, torch.int32, "cnt")
         if cnt.numel() < (OC // bm) * (KTOT // bn):
@@ -662,7 +672,7 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
     C().conv_wgrad(STEM if stem else FWD, bm, bn, dy.data_ptr(), x.data_ptr(), ws.data_ptr(), _p(in_scale),
                    _p(in_shift), int(relu_in), N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, KTOT, nsplit, ms,
                    stream_ptr(), int(lds_pad), int(dma), dw.data_ptr() if fuse else 0,
-                   cnt.data_ptr() if fuse else 0, float(scale), int(accumulate))
+                   cnt.data_ptr() if fuse and cnt is not None else 0, float(scale), int(accumulate))
     if not fuse:
         C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsplit, float(scale), int(accumulate), stream_ptr())
     return dw

@@ -1,0 +1,15 @@
+#!/bin/bash
+# one bench run per environment setting (interleaved per preset):  sweep_env.sh OUT "presets" setting...
+# a setting is a space-free list of VAR=VALUE joined by '+', or "base"
+set -o pipefail
+O=$1; PRESETS=$2; shift 2
+mkdir -p $O
+for p in $PRESETS; do
+  for st in "$@"; do
+    envs=""; [ "$st" != base ] && envs="${st//+/ }"
+    args="--steps 30 --warmup 10"; [ $p = headline ] && args="--steps 15 --warmup 5" || args="$args --preset $p"
+    f=$O/${p}_${st//[=+]/_}.log
+    env $envs timeout -k 10 300 python bench.py $args > $f 2>&1 || { tail -20 $f; exit 1; }
+    echo "$p $st: $(grep -o '"value": [0-9.]*' $f)"
+  done
+done

@@ -7,6 +7,7 @@ gets FLOP and minimum-HBM-byte estimates -> achieved TF/s and TB/s. Output: the 
 (conv fwd / dgrad / wgrad / BN passes / rest) and the top ops, sorted by time.
 
   BATCH=1024 python tools/op_breakdown.py [--steps 3] [--top 40]
+  ARCH=resnet18 SIZE=32 CLASSES=10 BATCH=256 python tools/op_breakdown.py   (the CIFAR preset)
 """
 import argparse
 import collections
@@ -111,10 +112,13 @@ def main():
     ap.add_argument("--top", type=int, default=45)
     a = ap.parse_args()
     B = int(os.environ.get("BATCH", 1024))
-    tr = NativeTrainer(build_model("resnet50"), B, (224, 224), torch.device("cuda"), optim=OptimConfig(),
+    arch = os.environ.get("ARCH", "resnet50")
+    hw = int(os.environ.get("SIZE", 224))
+    ncls = int(os.environ.get("CLASSES", 1000))
+    tr = NativeTrainer(build_model(arch, num_classes=ncls), B, (hw, hw), torch.device("cuda"), optim=OptimConfig(),
                        use_graphs=False)
     tr.prog.img_u8.copy_(torch.randint(0, 256, tr.prog.img_u8.shape, dtype=torch.uint8))
-    tr.prog.labels.copy_(torch.randint(0, 1000, (B,)))
+    tr.prog.labels.copy_(torch.randint(0, ncls, (B,)))
     for _ in range(2):
         tr.step()
     torch.cuda.synchronize()

@@ -61,6 +61,9 @@ def main():
     ap.add_argument("--modes", default="fwd,fwdt,dgrad0,dgrad1,dgrad2,dgrad1b,dgrad2b,wgrad")
     ap.add_argument("--dma", type=int, default=1,
                     help="also time the LDS-DMA operand paths of the fwd / dgrad kernels (tile x path)")
+    ap.add_argument("--wgrad-rounds", default="",
+                    help="comma list of split depths (workgroup rounds; 0 = no split) to time for each wgrad with "
+                         "its current table tile / operand path; the winner becomes the entry's 4th field")
     a = ap.parse_args()
     dev = "cuda"
     N = a.batch
@@ -127,11 +130,17 @@ def main():
         dw = torch.empty(Kc * R * R * C, device=dev)
         # wgrads read stored activations (no BN prologue) since the dgrad-epilogue write-back
         jobs.append(("wgrad", N * OH * OH, Kc, C, R, st,
-                     lambda t: K.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, tile=t[:2], dma=t[2])))
+                     lambda t: K.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, tile=t[:2], dma=t[2],
+                                            rounds=t[3] if len(t) > 3 else None)))
         for mode, M, OCm, Kin, Rk, sk, make in jobs:
             if mode not in a.modes.split(","):
                 continue
-            if mode == "wgrad":  # tile x operand path (LDS-DMA ring depth 3 / 2, 0 = register staged)
+            if mode == "wgrad" and a.wgrad_rounds:  # split depth for the entry's tile / operand path
+                cur = table.get(K.tune_key(mode, M, OCm, Kin, Rk, sk))
+                base = tuple(cur[:3]) if cur is not None and len(cur) >= 3 else (
+                    128 if Kc % 128 == 0 else 64, 128 if C % 128 == 0 else 64, 2)
+                cands = [base + (float(r),) for r in a.wgrad_rounds.split(",")]
+            elif mode == "wgrad":  # tile x operand path (LDS-DMA ring depth 3 / 2, 0 = register staged)
                 cands = [t + (d,) for t in WGRAD_TILES if Kc % t[0] == 0 and C % t[1] == 0 for d in (3, 2, 0)]
             else:  # tile x operand path: prologue convs 0 / 1 (weights by DMA), plain 0 / 2 / 3 (ring)
                 pro = mode in ("fwdt", "dgrad1b", "dgrad2b") or (mode == "fwd" and psc is not None)
@@ -148,6 +157,8 @@ def main():
                     f"{'x'.join(map(str, t))}={v:.3f}" for t, v in sorted(med.items())), flush=True)
             default = (K.pick_tile(M, OCm, use_table=False) + (0,) if mode != "wgrad" else
                        (128 if Kc % 128 == 0 else 64, 128 if C % 128 == 0 else 64, 0))
+            if mode == "wgrad" and a.wgrad_rounds:
+                default = cands[0][:3] + (2.0,)
             key = K.tune_key(mode, M, OCm, Kin, Rk, sk)
             table[key] = list(best) if (mode == "wgrad" or best[2]) else list(best[:2])
             lines.append(f"| {C}→{Kc} | {R}x{R} s{st} | {H} | {cnt} | {mode} | {'x'.join(map(str, best))} | {med[best]:.3f} | "
