@@ -111,8 +111,13 @@ def _bf16_emulating(model):
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 8), ("resnet18", 32, 16)])
 def test_program_grads_match_bf16_emulating_reference(arch, size, batch):
     """Tight end-to-end check: every parameter gradient of one native step against autograd of a
-    reference that rounds to bf16 at the program's storage points -- cosine > 0.99 for every tensor
-    (BN gamma / beta included), so a wrong-but-correlated BN-backward term fails."""
+    reference that rounds to bf16 at the program's storage points (BN gamma / beta included), held to
+    the rounding noise floor of the network itself: the native program must agree with the emulating
+    reference at least as well as plain fp32 autograd does (per tensor, within 0.03, capped at 0.99),
+    and at the median within 0.01. A fixed cosine bound cannot do this for ResNet-50: at b8 the
+    fp32-vs-emulating cosine of some BN biases is 0.87-0.91 (near-cancelling pixel sums), while the
+    native program sits at or above that floor on every tensor (tools/grad_noise.py,
+    profiles/r3s2_gradnoise/). A wrong-but-correlated BN-backward term drops below the floor."""
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
     torch.manual_seed(0)
@@ -120,6 +125,7 @@ def test_program_grads_match_bf16_emulating_reference(arch, size, batch):
     for n_, m_ in model.named_modules():
         if n_.endswith("bn3") or (n_.endswith("bn2") and "layer" in n_ and arch != "resnet50"):
             torch.nn.init.constant_(m_.weight, 0.2)
+    ref32 = copy.deepcopy(model).to(dev).train()
     ref = _bf16_emulating(copy.deepcopy(model).to(dev).train())
     tr = NativeTrainer(model, batch, (size, size), dev, optim=OptimConfig(lr=0.0, momentum=0.0, weight_decay=0.0),
                        use_graphs=False)
@@ -131,17 +137,22 @@ def test_program_grads_match_bf16_emulating_reference(arch, size, batch):
     torch.cuda.synchronize()
     x = p.x4[..., :3].float().permute(0, 3, 1, 2).contiguous()
     F.cross_entropy(ref(x), lab).backward()
-    named_ref = dict(ref.named_parameters())
-    cs = {}
+    F.cross_entropy(ref32(x), lab).backward()
+    named_ref, named32 = dict(ref.named_parameters()), dict(ref32.named_parameters())
+    cs, floor = {}, {}
     for name, prm in model.named_parameters():
         off = (prm.data_ptr() - p.master.data_ptr()) // 4
         gflat = p.grad[off:off + prm.numel()]
         gn = (gflat.view(prm.shape[0], prm.shape[2], prm.shape[3], prm.shape[1]).permute(0, 3, 1, 2)
               if prm.dim() == 4 else gflat.view(prm.shape))
         cs[name] = _cos(gn, named_ref[name].grad)
-    worst = sorted(cs.items(), key=lambda kv: kv[1])[:5]
-    print(f"[grad-cos] {arch}: worst {worst}")
-    assert worst[0][1] > 0.99, worst
+        floor[name] = _cos(named32[name].grad, named_ref[name].grad)
+    bad = sorted(((n, c, floor[n]) for n, c in cs.items() if c < min(0.99, floor[n]) - 0.03), key=lambda t: t[1])
+    med, med_floor = (sorted(d.values())[len(d) // 2] for d in (cs, floor))
+    print(f"[grad-cos] {arch}: median {med:.4f} (floor {med_floor:.4f}), worst "
+          f"{sorted(cs.items(), key=lambda kv: kv[1])[:3]}")
+    assert not bad, bad[:5]
+    assert med >= min(0.99, med_floor) - 0.01, (med, med_floor)
 
 
 def test_program_trains_and_graph_replay():
