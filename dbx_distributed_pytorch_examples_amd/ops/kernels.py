@@ -285,9 +285,13 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
                      _fin=(-(-n1 * OH * OW // 256), 1), **kw)
         return out
     f1 = fin.ptr() if fin is not None and stats is not None else 0
+    r0, nr = fwd_taps(IH, OH, R, stride, pad)
+    s0, ns = fwd_taps(IW, OW, S, stride, pad)
+    if nr == 0 or ns == 0:
+        raise ValueError("conv_fwd: no filter tap touches the input")
     C().conv_igemm(mode, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
-                   R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
+                   nr, ns, r0, s0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
                    _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma, f1, 0, _fin[0], _fin[1])
     if fin is not None and not f1 and _fin[1]:
         fin.run()
@@ -315,14 +319,51 @@ def tail_supported(IC: int, R: int, S: int, stride: int, pad: int) -> bool:
     return R == 1 and S == 1 and stride == 1 and pad == 0 and IC <= 1024 and IC % 64 == 0
 
 
+_PRUNE = None
+
+
+def _prune() -> bool:
+    """DBX_TAP_PRUNE (default 1): conv launches skip the filter taps that only ever see padding."""
+    global _PRUNE
+    if _PRUNE is None:
+        import os
+        _PRUNE = os.environ.get("DBX_TAP_PRUNE", "1") != "0"
+    return _PRUNE
+
+
+def fwd_taps(IH: int, OH: int, R: int, stride: int, pad: int) -> Tuple[int, int]:
+    """(r0, nr): the filter rows of a forward conv that touch the image for SOME output row, i.e.
+    0 <= oh*stride - pad + r < IH for an oh in [0, OH). The K loop skips the rest: on small maps
+    (ResNet-18 at 32x32: layer4 is 1x1, so a 3x3 conv is its centre tap) the other taps would only
+    multiply zero padding -- 8 of 9 K blocks of work and weight traffic."""
+    if not _prune():
+        return 0, R
+    lo = max(0, pad - (OH - 1) * stride)
+    hi = min(R - 1, IH - 1 + pad)
+    return (lo, hi - lo + 1) if hi >= lo else (0, 0)
+
+
+def _live_taps(n_out: int, d0: int, n_in: int, nt: int) -> Tuple[int, int]:
+    """Tap indices t in [0, nt) with 0 <= i + d0 - t < n_in for some i in [0, n_out) (the transposed
+    gather of a dgrad phase): (first, count)."""
+    if not _prune():
+        return 0, nt
+    lo = max(0, d0 - n_in + 1)
+    hi = min(nt - 1, n_out - 1 + d0)
+    return (lo, hi - lo + 1) if hi >= lo else (0, 0)
+
+
 def dgrad_phases(H: int, W: int, R: int, S: int, stride: int, pad: int):
     """Parity decomposition of a strided dgrad into stride-1 sub-problems.
 
     Output pixel h receives tap r only where (h + pad - r) % stride == 0, so for each output
     phase (ph, pw) only taps r = r0 + stride*t contribute and the gather is dense:
     ih = i + (ph + pad - r0) // stride - t over the phase's sub-grid i (h = i*stride + ph).
+    Taps whose gather never lands inside dY (small maps: only padding) are dropped from the range.
     Returns [(ph, pw, OHs, OWs, r0, nr, s0, ns, dh0, dw0)] (classes with no taps included, nr=0).
     """
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - S) // stride + 1
     out = []
     for ph in range(stride):
         for pw in range(stride):
@@ -332,7 +373,10 @@ def dgrad_phases(H: int, W: int, R: int, S: int, stride: int, pad: int):
             s0 = (pw + pad) % stride
             nr = max(0, (R - r0 + stride - 1) // stride)
             ns = max(0, (S - s0 + stride - 1) // stride)
-            out.append((ph, pw, ohs, ows, r0, nr, s0, ns, (ph + pad - r0) // stride, (pw + pad - s0) // stride))
+            dh0, dw0 = (ph + pad - r0) // stride, (pw + pad - s0) // stride
+            tr, nr = _live_taps(ohs, dh0, P, nr)
+            ts, ns = _live_taps(ows, dw0, Q, ns)
+            out.append((ph, pw, ohs, ows, r0 + stride * tr, nr, s0 + stride * ts, ns, dh0 - tr, dw0 - ts))
     return out
 
 

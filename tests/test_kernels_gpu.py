@@ -42,6 +42,11 @@ CONV_CASES = [
     (3, 7, 7, 512, 512, 3, 1, 1),
     (4, 9, 9, 64, 128, 3, 2, 1),
     (1, 5, 5, 128, 64, 3, 1, 1),
+    # small maps: the launches visit only the taps that touch data (fwd_taps / dgrad_phases)
+    (8, 1, 1, 512, 512, 3, 1, 1),
+    (8, 2, 2, 256, 512, 3, 2, 1),
+    (8, 2, 2, 256, 256, 3, 1, 1),
+    (4, 1, 2, 128, 64, 3, 1, 1),
 ]
 
 
