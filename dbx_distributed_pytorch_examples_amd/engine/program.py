@@ -187,6 +187,8 @@ class ResNetProgram:
         # csrc/conv_fast.hip): the forward materialises the input BN output relu(bn(y)) once (the
         # block's acts buffer, which backward needs anyway) and runs the conv without a prologue
         self.fast_mat = os.environ.get("DBX_FAST_MAT", "1") == "1"
+        # ... also the 1x1 conv3 of a bottleneck (short-K C -> 4C forward) where its plain shape has one
+        self.fast_mat1 = os.environ.get("DBX_FAST_MAT1", "0") == "1"
         self._wstream = None
         self._side_pending = False
         self.param_align = max(16, int(param_align))
@@ -864,8 +866,9 @@ class ResNetProgram:
             self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
 
     def _materialize(self, cv: ConvL) -> bool:
-        """Does conv ``cv`` (a block-internal 3x3) take a materialised BN output on the eight-wave kernel?"""
-        if not (self.fast_mat and self.dev.type == "cuda" and cv.R == 3 and cv.stride == 1):
+        """Does conv ``cv`` (a block-internal 3x3, or with DBX_FAST_MAT1 a bottleneck conv3) take a
+        materialised BN output on the eight-wave kernel?"""
+        if not (self.fast_mat and self.dev.type == "cuda" and cv.stride == 1 and (cv.R == 3 or (cv.R == 1 and self.fast_mat1))):
             return False
         t = K.pick_tile(self.N * cv.OH * cv.OW, cv.OC, "fwd0", cv.IC, cv.R, cv.stride)
         return len(t) > 2 and t[2] in (4, 5)

@@ -61,6 +61,11 @@ def main():
     ap.add_argument("--modes", default="fwd,fwdt,dgrad0,dgrad1,dgrad2,dgrad1b,dgrad2b,wgrad")
     ap.add_argument("--dma", type=int, default=1,
                     help="also time the LDS-DMA operand paths of the fwd / dgrad kernels (tile x path)")
+    ap.add_argument("--fast", type=float, default=0.0,
+                    help="eight-wave mode: time only the current table entry against the eight-wave kernel "
+                         "(csrc/conv_fast.hip, tile dma 4 / 5) on the plain-operand stride-1 fwd0 / dgrad1 / "
+                         "dgrad2 convs; an eight-wave tile replaces the entry only when it is this fraction "
+                         "faster (e.g. 0.04)")
     ap.add_argument("--wgrad-rounds", default="",
                     help="comma list of split depths (workgroup rounds; 0 = no split) to time for each wgrad with "
                          "its current table tile / operand path; the winner becomes the entry's 4th field")
@@ -93,7 +98,9 @@ def main():
         # the BN prologue only exists on inputs that are BN outputs inside a block (<= 512 channels);
         # block inputs (1x1 conv1 / downsample of 1024+ channels) are materialised activations
         psc, psh = (sc, sh) if C <= 512 else (None, None)
-        jobs = [("fwd", N * OH * OH, Kc, C, R, st,
+        jobs = [("fwd0", N * OH * OH, Kc, C, R, st,
+                 lambda t: K.conv_fwd(x, w2, y, R=R, S=R, stride=st, pad=pad, stats=stats, tile=t)),
+                ("fwd", N * OH * OH, Kc, C, R, st,
                  lambda t: K.conv_fwd(x, w2, y, R=R, S=R, stride=st, pad=pad, stats=stats, in_scale=psc,
                                       in_shift=psh, tile=t))]
         if R == 1 and st == 1 and Kc < C and K.tail_supported(C, R, R, st, pad):
@@ -135,7 +142,18 @@ def main():
         for mode, M, OCm, Kin, Rk, sk, make in jobs:
             if mode not in a.modes.split(","):
                 continue
-            if mode == "wgrad" and a.wgrad_rounds:  # split depth for the entry's tile / operand path
+            cur = table.get(K.tune_key(mode, M, OCm, Kin, Rk, sk))
+            if a.fast:
+                # plain operands, stride 1 (the eight-wave kernel's geometry); dgrad2's MASK_Y epilogue is
+                # 128-wide only (conv_fast.hip)
+                if mode not in ("fwd0", "dgrad1", "dgrad2") or sk != 1 or OCm % 128:
+                    continue
+                fb = (128,) if mode == "dgrad2" or OCm % 256 else (128, 256)
+                base = tuple(cur) if cur is not None else K.pick_tile(M, OCm, use_table=False)
+                cands = [base] + [(256, b, d) for b in fb for d in (4, 5)]
+            elif mode == "fwd0":
+                continue  # (only in --fast mode: the plain forward is tuned against the eight-wave kernel)
+            elif mode == "wgrad" and a.wgrad_rounds:  # split depth for the entry's tile / operand path
                 cur = table.get(K.tune_key(mode, M, OCm, Kin, Rk, sk))
                 base = tuple(cur[:3]) if cur is not None and len(cur) >= 3 else (
                     128 if Kc % 128 == 0 else 64, 128 if C % 128 == 0 else 64, 2)
@@ -160,7 +178,13 @@ def main():
             if mode == "wgrad" and a.wgrad_rounds:
                 default = cands[0][:3] + (2.0,)
             key = K.tune_key(mode, M, OCm, Kin, Rk, sk)
-            table[key] = list(best) if (mode == "wgrad" or best[2]) else list(best[:2])
+            if a.fast:
+                default = cands[0]
+                if best != cands[0] and med[best] > (1.0 - a.fast) * med[cands[0]]:
+                    best = cands[0]  # not a clear win: keep the entry
+                if best == cands[0] and cur is None:
+                    continue  # nothing to record
+            table[key] = list(best) if (mode == "wgrad" or (len(best) > 2 and best[2])) else list(best[:2])
             lines.append(f"| {C}→{Kc} | {R}x{R} s{st} | {H} | {cnt} | {mode} | {'x'.join(map(str, best))} | {med[best]:.3f} | "
                          f"{gf / med[best]:.0f} | {med.get(default, float('nan')):.3f} |")
             print(lines[-1], flush=True)
