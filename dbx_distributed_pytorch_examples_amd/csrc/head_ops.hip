@@ -6,7 +6,7 @@
 // small_gemm: C[M][N] = alpha * sum_k A(m, k) * B(k, n) (+ bias[n]) (+ C)
 //   A: TA = 0 -> [M][K] row-major (lda), TA = 1 -> [K][M] (lda)
 //   B: TB = 0 -> [N][K] (ldb),          TB = 1 -> [K][N] (ldb)
-// Tiles 64 x 64 x 32 per 4-wave workgroup (2 x 2 waves, 32 x 32 each = 2 x 2 v_mfma_f32_16x16x32_bf16),
+// Tiles 64 x 64 x 128 per 4-wave workgroup (2 x 2 waves, 32 x 32 each = 2 x 2 v_mfma_f32_16x16x32_bf16),
 // both operands staged into K-contiguous LDS images ([m][k], [n][k], XOR-swizzled 16-byte chunks) so
 // every fragment is one ds_read_b128; transposed sources are transposed by the staging store.
 // Shapes are arbitrary (masked edges): logits [B, 1000 | 200 | 10] = pooled [B, 2048 | 512] x W^T,
@@ -47,7 +47,11 @@ __device__ __forceinline__ float drop_scale(unsigned long long idx, unsigned lon
 
 template <int TA, int TB, bool OUT_F32, int DROP>
 __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
-  constexpr int BM = 64, BN = 64, BK = 32;
+  // 64 x 64 output tile, K staged 128 deep (4 MFMA k-steps per barrier pair) with the next stage's
+  // global loads issued into registers before this stage's MFMAs: the head GEMMs have few tiles
+  // (fc forward at batch 256 / 10 classes: 4 workgroups) and are latency-bound on the K loop, so
+  // the loop is cut to K / 128 iterations, each hiding the next stage's load latency.
+  constexpr int BM = 64, BN = 64, BK = 128, NCH = BK / 8, CPT = BM * NCH / 256;  // 4 chunks / thread
   __shared__ __attribute__((aligned(16))) bf16 sA[BM * BK];
   __shared__ __attribute__((aligned(16))) bf16 sB[BN * BK];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
@@ -58,13 +62,12 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // staging: 64 rows x 32 k = 256 chunks of 8 elements; thread -> (row = tid / 4, chunk = tid % 4)
-  // in the K-contiguous image; the swizzle spreads a row's 4 chunks (64 B) over the bank window
-  const int srow = tid >> 2, sch = tid & 3;
-  auto swz = [](int row, int ch) { return ch ^ ((row >> 1) & 3); };
-  // load 8 elements (k = k0 + 8*sch .. +7) of operand row `r` (m or n) into the LDS image
-  auto stage = [&](const bf16* P, int T, int ld, int rows, int r0, int k0, bf16* img, bool drop) {
-    const int r = r0 + srow, kk = k0 + sch * 8;
+  // staging: chunk q = tid + 256 c (c < 4) -> (row = q / 16, chunk = q % 16) of the K-contiguous
+  // image [64][128]; chunk ^ (row & 15) spreads 16 consecutive rows of one k chunk over all 64 banks
+  auto swz = [](int row, int ch) { return ch ^ (row & 15); };
+  // 8 elements (k = k0 + 8 ch .. +7) of operand row r0 + row (dropout applied, zeros past the edges)
+  auto load = [&](const bf16* P, int T, int ld, int rows, int r0, int k0, bool drop, int c) -> bf16x8 {
+    const int q = tid + 256 * c, r = r0 + (q >> 4), kk = k0 + (q & 15) * 8;
     bf16x8 v;
     const bool full = (r < rows) && (kk + 8 <= g.K);
     if (T == 0 && full && ((ld & 7) == 0)) {
@@ -86,29 +89,46 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
         v[j] = (bf16)((float)v[j] * drop_scale(e, g.seed, doff, g.thresh, g.inv_keep));
       }
     }
-    *reinterpret_cast<bf16x8*>(img + srow * BK + swz(srow, sch) * 8) = v;
+    return v;
   };
+  bf16x8 ra[CPT], rb[CPT];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      ra[c] = load(g.A, TA, g.lda, g.M, m0, k0, DROP == 1, c);
+      rb[c] = load(g.B, TB, g.ldb, g.N, n0, k0, DROP == 2, c);
+    }
+  };
+  fetch(0);
   for (int k0 = 0; k0 < g.K; k0 += BK) {
-    stage(g.A, TA, g.lda, g.M, m0, k0, sA, DROP == 1);
-    stage(g.B, TB, g.ldb, g.N, n0, k0, sB, DROP == 2);
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int q = tid + 256 * c, row = q >> 4, ch = q & 15;
+      *reinterpret_cast<bf16x8*>(sA + row * BK + swz(row, ch) * 8) = ra[c];
+      *reinterpret_cast<bf16x8*>(sB + row * BK + swz(row, ch) * 8) = rb[c];
+    }
     __syncthreads();
-    bf16x8 af[2], bfr[2];
-    const int ch = lane >> 4;  // k chunk 0..3 of this lane's 8 (16x16x32: k = 8*(lane>>4) + j)
+    if (k0 + BK < g.K) fetch(k0 + BK);  // block-uniform: in flight under this stage's MFMAs
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = wm * 32 + i * 16 + (lane & 15);
-      af[i] = *reinterpret_cast<const bf16x8*>(sA + r * BK + swz(r, ch) * 8);
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[2], bfr[2];
+      const int ch = ks * 4 + (lane >> 4);  // 16x16x32: lane's k = 8 * (lane >> 4) + j of this k-step
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm * 32 + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(sA + r * BK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 32 + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + r * BK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)  // C^T tile: a lane's 4 accumulators = 4 consecutive n of one m
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = wn * 32 + j * 16 + (lane & 15);
-      bfr[j] = *reinterpret_cast<const bf16x8*>(sB + r * BK + swz(r, ch) * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)  // C^T tile: a lane's 4 accumulators = 4 consecutive n of one m
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     __syncthreads();
   }
   // epilogue: acc[i][j][q] = C[m = wm*32 + i*16 + (lane & 15)][n = wn*32 + j*16 + 4*(lane >> 4) + q]
@@ -137,13 +157,24 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
   }
 }
 
-// db[n] (+)= sum_m X[m][n] (bf16 in, fp32 out, fixed summation order: deterministic)
-__global__ void colsum_kernel(const bf16* __restrict__ X, float* __restrict__ out, int M, int N, int accumulate) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+// db[n] (+)= sum_m X[m][n] (bf16 in, fp32 out). A workgroup owns 16 columns; its 16 row groups each
+// sum every 16th row in order, then the 16 partials are added in row-group order: a fixed
+// summation order (deterministic) with 16 independent chains instead of one serial pass over M.
+__global__ __launch_bounds__(256) void colsum_kernel(const bf16* __restrict__ X, float* __restrict__ out, int M, int N,
+                                                     int accumulate) {
+  __shared__ float part[16][17];
+  const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4, n = blockIdx.x * 16 + cl;
   float s = 0.f;
-  for (int m = 0; m < M; ++m) s += (float)X[(size_t)m * N + n];
-  out[n] = accumulate ? out[n] + s : s;
+  if (n < N)
+    for (int m = rg; m < M; m += 16) s += (float)X[(size_t)m * N + n];
+  part[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t += part[r][cl];
+    out[n] = accumulate ? out[n] + t : t;
+  }
 }
 
 // y = x * dropout-mask (the forward's h, for frozen-head training that keeps it; deterministic)
@@ -185,7 +216,7 @@ extern "C" int dbx_small_gemm(int ta, int tb, int out_f32, int drop, const dbx::
 }
 
 extern "C" int dbx_colsum(const bf16* X, float* out, int M, int N, int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256), dim3(256), 0, st, X, out, M, N, accumulate);
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 15) / 16), dim3(256), 0, st, X, out, M, N, accumulate);
   return (int)hipGetLastError();
 }
 

@@ -149,7 +149,8 @@ class ResNetProgram:
         self.norm_std = tuple(std) if std else None
         self.dev = device
         self.in_ch = model.conv1.in_channels
-        self.overlap_wgrad = os.environ.get("DBX_OVERLAP_WGRAD", "1") == "1"
+        ov = os.environ.get("DBX_OVERLAP_WGRAD")  # unset: decided by the step's size (_build_layers)
+        self.overlap_wgrad = ov != "0"
         # split-K weight-gradient reduction inside the wgrad launch where a tile's slabs are small
         self.fuse_wgrad_reduce = os.environ.get("DBX_FUSE_WGRAD_REDUCE", "0") == "1"
         # BN finalize / backward coefficients computed by the producing conv's last tiles (K.BnFin)
@@ -194,6 +195,21 @@ class ResNetProgram:
         self.param_align = max(16, int(param_align))
         self._want_param16 = param16
         self._build_layers()
+        if ov is None:
+            # The side stream pays off only when the kernels fill the GPU: a launch-bound step (small
+            # maps / batch) loses more to the cross-stream joins of the captured graph than it overlaps
+            # -- ResNet-18 CIFAR b256 (19 GFLOP forward) 215k img/s without vs 189-190k with; ResNet-50
+            # TinyImageNet b512 (343 GFLOP) 89.4k vs 90.7-91.1k; headline +0.4 %
+            # (profiles/r3s2_knobs/). Threshold: 100 GFLOP of forward convolution per step.
+            fwd = sum(2.0 * self.N * cv.OH * cv.OW * cv.OC * cv.R * cv.S * cv.IC for cv in self.convs)
+            self.overlap_wgrad = fwd >= 100e9
+        if not self.overlap_wgrad:
+            # without the side stream folding costs no overlap: fold every BN-backward apply it can
+            # (unless set explicitly) -- CIFAR b256 193.7k vs 189.5k img/s with overlap (r3s2_knobs)
+            if "DBX_FOLD_MIN_ELEMS" not in os.environ:
+                self.fold_min = 0
+            if "DBX_FOLD_MAX_RATIO" not in os.environ:
+                self.fold_max_ratio = 8.0
         self._alloc_params()
         self._alloc_activations()
         self.build_fins()

@@ -65,11 +65,15 @@ def test_small_gemm_dropout_mask_matches_reference_philox(which):
     assert 0.45 < kept < 0.55
 
 
-def test_colsum():
-    x = _bf(1000, 1000)
-    out = torch.empty(1000, device="cuda")
+@pytest.mark.parametrize("M,N", [(1000, 1000), (256, 10), (37, 70)])
+def test_colsum(M, N):
+    x = _bf(M, N)
+    out = torch.empty(N, device="cuda")
     K.colsum(x, out)
     assert torch.allclose(out, x.float().sum(0), atol=1e-3, rtol=1e-4)
+    base = out.clone()
+    K.colsum(x, out, accumulate=True)
+    assert torch.allclose(out, 2 * base, atol=1e-3, rtol=1e-4)
 
 
 def test_softmax_ce_cutmix_soft_targets_vs_reference():
