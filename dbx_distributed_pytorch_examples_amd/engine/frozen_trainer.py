@@ -39,6 +39,7 @@ from ..models.wrappers import FrozenBackboneClassifier
 from ..parallel.ddp import DistributedDataParallel
 from ..utils import debug as _debug
 from .autograd_trainer import build_torch_optimizer
+from .hyper import DeviceHyper
 from .program import ResNetProgram
 
 
@@ -89,6 +90,7 @@ class NativeHead:
         self.m = torch.zeros(n, device=device)
         self.v = torch.zeros(n, device=device) if optim.name in ("adam", "adamw") else None
         self.hyper = torch.zeros(4, device=device)
+        self._hyper_dev = DeviceHyper(self.hyper)
         self.step_count = 0
         self.drop_off = torch.zeros(1, device=device, dtype=torch.int32)  # Philox offset: +1 per step (device)
         self.seed = int(seed) * 0x9E3779B97F4A7C15 % (1 << 63) + 12345
@@ -106,9 +108,7 @@ class NativeHead:
         self.step_count += 1
         t = self.step_count
         vals = [o.lr, 1.0, 1.0, 0.0] if o.name == "sgd" else [o.lr, 1.0 - o.betas[0] ** t, 1.0 - o.betas[1] ** t, 0.0]
-        h = torch.tensor(vals, dtype=torch.float32)
-        self._hyper_host = h.pin_memory() if self.dev.type == "cuda" else h
-        self.hyper.copy_(self._hyper_host, non_blocking=True)
+        self._hyper_dev.set(vals)
 
     def fwd_bwd(self, feats: torch.Tensor, labels: torch.Tensor, metrics: torch.Tensor) -> None:
         """feats [n, F] bf16 (n <= batch), labels [n] int64: logits, CE (+ metrics), dW, db."""

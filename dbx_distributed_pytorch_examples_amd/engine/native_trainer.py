@@ -30,6 +30,7 @@ from ..ops import kernels as K
 from ..parallel.dist import host_sync_for_gloo
 from ..utils import debug as _debug
 from ..utils.profiling import PhaseTimer
+from .hyper import DeviceHyper
 from .program import ResNetProgram
 
 
@@ -78,6 +79,7 @@ class NativeTrainer:
         self.mom = torch.zeros(n, device=device)
         self.mom2 = torch.zeros(n, device=device) if optim.name in ("adam", "adamw") else None
         self.hyper = torch.zeros(4, device=device)      # lr, bc1, bc2 (device-side, graph-safe)
+        self._hyper_dev = DeviceHyper(self.hyper)
         self.clip_work = torch.zeros(4, device=device)
         self.step_count = 0
         # debug mode synchronizes after every kernel, which graph capture forbids; per-phase
@@ -322,8 +324,7 @@ class NativeTrainer:
             vals = [o.lr, 1.0, 1.0, 0.0]
         else:
             vals = [o.lr, 1.0 - o.betas[0] ** t, 1.0 - o.betas[1] ** t, 0.0]
-        self._hyper_host = torch.tensor(vals, dtype=torch.float32).pin_memory() if self.dev.type == "cuda" else torch.tensor(vals)
-        self.hyper.copy_(self._hyper_host, non_blocking=True)
+        self._hyper_dev.set(vals)
 
     def set_lr(self, lr: float):
         self.opt.lr = float(lr)
