@@ -481,6 +481,23 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_dma_kernel(const WgradA
 // range of group g into ws2[g][i]; level 2 sums the G group partials in order, scales, and writes
 // (or accumulates into) the fp32 gradient. Both levels are wide (n4 x G threads), so a 1024-split
 // reduction of a tiny 64x64 weight no longer serialises 1024 dependent loads in one thread.
+// s + slab(k0) + slab(k0 + 1) + ... + slab(k1 - 1), added strictly in that order (the fixed-order,
+// deterministic split-K sum) with the loads issued eight at a time ahead of their adds: the reduces
+// are latency-bound chains of dependent slab loads on the small (launch-bound) steps.
+template <class T, class F>
+__device__ __forceinline__ T sum_slabs_in_order(T s, int k0, int k1, F load) {
+  int k = k0;
+  for (; k + 8 <= k1; k += 8) {
+    T v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = load(k + j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j];
+  }
+  for (; k < k1; ++k) s += load(k);
+  return s;
+}
+
 __global__ void wgrad_reduce_l1_kernel(const float* __restrict__ ws, float* __restrict__ ws2, int n4, int nsplit,
                                        int spg) {
   const f32x4* w4 = reinterpret_cast<const f32x4*>(ws);
@@ -488,8 +505,8 @@ __global__ void wgrad_reduce_l1_kernel(const float* __restrict__ ws, float* __re
   const int g = blockIdx.y;
   const int s0 = g * spg, s1 = min(nsplit, s0 + spg);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int k = s0; k < s1; ++k) s += w4[(size_t)k * n4 + i];
+    const f32x4 s = sum_slabs_in_order(f32x4{0.f, 0.f, 0.f, 0.f}, s0, s1,
+                                       [&](int k) { return w4[(size_t)k * n4 + i]; });
     o4[(size_t)g * n4 + i] = s;
   }
 }
@@ -498,8 +515,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
   const f32x4* w4 = reinterpret_cast<const f32x4*>(ws);
   f32x4* o4 = reinterpret_cast<f32x4*>(dw);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
-    f32x4 s = w4[i];
-    for (int k = 1; k < nsplit; ++k) s += w4[(size_t)k * n4 + i];
+    f32x4 s = sum_slabs_in_order(w4[i], 1, nsplit, [&](int k) { return w4[(size_t)k * n4 + i]; });
     s *= scale;
     if (accumulate) s += o4[i];
     o4[i] = s;
@@ -518,8 +534,7 @@ __global__ void wgrad_reduce_gather_kernel(const float* __restrict__ ws, float* 
     const int r = rem / (S * IC), rem2 = rem - r * (S * IC);
     const int s = rem2 / IC, c = rem2 - s * IC;
     const long long src = (long long)oc * 256 + (r * 8 + s) * 4 + c;
-    float v = ws[src];
-    for (int k = 1; k < nsplit; ++k) v += ws[(long long)k * slab + src];
+    float v = sum_slabs_in_order(ws[src], 1, nsplit, [&](int k) { return ws[(long long)k * slab + src]; });
     v *= scale;
     if (accumulate) v += dw[i];
     dw[i] = v;
