@@ -35,6 +35,10 @@ import torch.nn as nn
 from ..models.resnet import BasicBlock, Bottleneck, CifarBlock, CifarResNet18, ResNet
 from ..ops import kernels as K
 
+# steps with less forward convolution than this run their weight gradients in order on the main
+# stream (see ResNetProgram.__init__): launch-bound steps lose more to cross-stream joins than they overlap
+OVERLAP_MIN_FWD_FLOPS = 100e9
+
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
@@ -201,8 +205,7 @@ class ResNetProgram:
             # -- ResNet-18 CIFAR b256 (19 GFLOP forward) 215k img/s without vs 189-190k with; ResNet-50
             # TinyImageNet b512 (343 GFLOP) 89.4k vs 90.7-91.1k; headline +0.4 %
             # (profiles/r3s2_knobs/). Threshold: 100 GFLOP of forward convolution per step.
-            fwd = sum(2.0 * self.N * cv.OH * cv.OW * cv.OC * cv.R * cv.S * cv.IC for cv in self.convs)
-            self.overlap_wgrad = fwd >= 100e9
+            self.overlap_wgrad = self.fwd_conv_flops() >= OVERLAP_MIN_FWD_FLOPS
         if not self.overlap_wgrad:
             # without the side stream folding costs no overlap: fold every BN-backward apply it can
             # (unless set explicitly) -- CIFAR b256 193.7k vs 189.5k img/s with overlap (r3s2_knobs)
@@ -880,6 +883,10 @@ class ResNetProgram:
                      addsrc=addsrc, add_sub=sub, epilogue=epi, **kw0)
         if kw0:
             self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
+
+    def fwd_conv_flops(self) -> float:
+        """FLOPs of the forward convolutions of one step (sizes the wgrad side-stream decision)."""
+        return sum(2.0 * self.N * cv.OH * cv.OW * cv.OC * cv.R * cv.S * cv.IC for cv in self.convs)
 
     def _materialize(self, cv: ConvL) -> bool:
         """Does conv ``cv`` (a block-internal 3x3, or with DBX_FAST_MAT1 a bottleneck conv3) take a
