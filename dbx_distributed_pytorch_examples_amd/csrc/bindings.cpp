@@ -99,7 +99,8 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t bsc, uintptr_t bsh, uintptr_t mean1, uintptr_t inv1, uintptr_t mean2,
                          uintptr_t inv2, uintptr_t bstats1, uintptr_t bstats2, uintptr_t a_out, uintptr_t res,
                          uintptr_t res_scale, uintptr_t res_shift, uintptr_t tail_out, uintptr_t tail_bits,
-                         uintptr_t st, int dma, uintptr_t fin1, uintptr_t fin2, int fin_base, int fin_final) {
+                         uintptr_t st, int dma, uintptr_t fin1, uintptr_t fin2, int fin_base, int fin_final,
+                         uintptr_t fin_in) {
     dbx::IGemmArgs a{P<const bf16*>(x), P<const bf16*>(w), P<bf16*>(y), P<const float*>(in_scale),
                      P<const float*>(in_shift), P<double*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
                      N * OH * OW, nshard > 0 ? nshard : 1, relu_in, nr, ns, r0, s0, tstep, dh0, dw0, osub, oph, opw,
@@ -108,7 +109,9 @@ PYBIND11_MODULE(_C, m) {
                      P<const float*>(inv1), P<const float*>(mean2), P<const float*>(inv2), P<double*>(bstats1),
                      P<double*>(bstats2), P<bf16*>(a_out), P<const bf16*>(res), P<const float*>(res_scale),
                      P<const float*>(res_shift), P<bf16*>(tail_out), P<unsigned char*>(tail_bits), 0ull, 0ull,
-                     P<const dbx::BnFin*>(fin1), P<const dbx::BnFin*>(fin2), fin_base, fin_final};
+                     P<const dbx::BnFin*>(fin1), P<const dbx::BnFin*>(fin2), fin_base, fin_final,
+                     P<const dbx::BnFin*>(fin_in)};
+    if (fin_in && !in_scale) throw std::invalid_argument("conv_igemm: input finalize without a BN prologue");
     if ((fin1 || fin2) && !(stats || bstats1)) throw std::invalid_argument("conv_igemm: BN finalize without statistics");
     if (fin2 && !bstats2) throw std::invalid_argument("conv_igemm: second BN finalize without its statistics");
     {  // magic divisors when exact: m < N*OH*OW, so m * OH*OW < 2^40 suffices

@@ -7,19 +7,31 @@
 
 namespace dbx {
 
+// forward: shard sums (s, q) of channel c -> the affine (scale, shift) and the batch moments
+__device__ __forceinline__ void bn_fwd_affine(int c, double s, double q, float count, const float* gamma,
+                                              const float* beta, float eps, float& scale, float& shift,
+                                              double& mean, double& var, float& invstd) {
+#pragma clang fp contract(off)  // no context-dependent FMA contraction: fused == standalone bits
+  mean = s / count;
+  var = q / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale = g * invstd;
+  shift = b - (float)mean * g * invstd;
+}
+
 // forward: shard sums (s, q) of channel c -> scale / shift, saved mean / invstd, running stats
 __device__ __forceinline__ void bn_fwd_final(int c, double s, double q, float count, const float* gamma,
                                              const float* beta, float eps, float momentum, float* running_mean,
                                              float* running_var, float* scale, float* shift, float* save_mean,
                                              float* save_invstd) {
-#pragma clang fp contract(off)  // no context-dependent FMA contraction: fused == standalone bits
-  const double mean = s / count;
-  double var = q / count - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-  scale[c] = g * invstd;
-  shift[c] = b - (float)mean * g * invstd;
+#pragma clang fp contract(off)
+  double mean, var;
+  float invstd, sc, sh;
+  bn_fwd_affine(c, s, q, count, gamma, beta, eps, sc, sh, mean, var, invstd);
+  scale[c] = sc;
+  shift[c] = sh;
   if (save_mean) save_mean[c] = (float)mean;
   if (save_invstd) save_invstd[c] = invstd;
   if (running_mean && momentum > 0.f) {
@@ -67,6 +79,27 @@ __device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c) {
                  f.shift, f.mean, f.invstd);
   else
     bn_bwd_final(f.C, c, s, q, f.count, f.gamma, f.mean, f.invstd, f.coeff, f.dgamma, f.dbeta, f.accumulate);
+}
+
+// Consumer-side forward finalize (IGemmArgs::fin_in): the prologue affine of channel c, summed over
+// the shards in the standalone kernels' order (plain loads: the statistics were completed by an
+// earlier launch); the storing workgroup also writes every bn_finalize output of the channel.
+__device__ __forceinline__ void bn_fin_consume(const BnFin& f, int c, bool store, float& scale, float& shift) {
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < f.nshard; ++k) {
+    s += f.stats[(size_t)k * 2 * f.C + c];
+    q += f.stats[(size_t)k * 2 * f.C + f.C + c];
+  }
+  if (store) {
+    bn_fwd_final(c, s, q, f.count, f.gamma, f.beta, f.eps, f.momentum, f.running_mean, f.running_var, f.scale,
+                 f.shift, f.mean, f.invstd);
+    scale = f.scale[c];
+    shift = f.shift[c];
+    return;
+  }
+  double mean, var;
+  float invstd;
+  bn_fwd_affine(c, s, q, f.count, f.gamma, f.beta, f.eps, scale, shift, mean, var, invstd);
 }
 
 // End of a conv tile epilogue whose launch carries BN finalize descriptors: once every wave's

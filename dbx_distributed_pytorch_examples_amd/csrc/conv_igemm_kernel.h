@@ -398,6 +398,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   int pcb[2] = {0, 0};                    // channel block of the staged set (prologue coefficients)
   if constexpr (PRO && MODE != STEM) {
     for (int c = tid; c < a.IC; c += NT) {
+      if (!TAIL && a.fin_in) {  // wave-uniform: the input BN finalized here (workgroup 0 stores it)
+        float sc, sh;
+        bn_fin_consume(*a.fin_in, c, blockIdx.x == 0, sc, sh);
+        sPro[c] = sc;
+        sPro[PRO_MAXC + c] = sh;
+        continue;
+      }
       sPro[c] = a.in_scale[c];
       sPro[PRO_MAXC + c] = a.in_shift[c];
       if constexpr (TAIL) {

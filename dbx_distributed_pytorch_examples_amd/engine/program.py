@@ -206,6 +206,11 @@ class ResNetProgram:
             # TinyImageNet b512 (343 GFLOP) 89.4k vs 90.7-91.1k; headline +0.4 %
             # (profiles/r3s2_knobs/). Threshold: 100 GFLOP of forward convolution per step.
             self.overlap_wgrad = self.fwd_conv_flops() >= OVERLAP_MIN_FWD_FLOPS
+        # consumer-side forward BN finalize (K.conv_fwd fin_in) for the launch-bound steps: each
+        # workgroup of the consuming conv re-reads the statistics shards (2 x NSHARD x C doubles), so
+        # it pays only where launches, not bytes, dominate
+        fi = os.environ.get("DBX_FIN_IN")
+        self.fin_in = (fi == "1") if fi is not None else self.fwd_conv_flops() < OVERLAP_MIN_FWD_FLOPS
         if not self.overlap_wgrad:
             # without the side stream folding costs no overlap: fold every BN-backward apply it can
             # (unless set explicitly) -- CIFAR b256 193.7k vs 189.5k img/s with overlap (r3s2_knobs)
@@ -638,6 +643,7 @@ class ResNetProgram:
         pending = None  # previous block whose output this block's conv1 computes (tail prologue)
         for bi, b in enumerate(self.blocks):
             prev_bn = None
+            deferred = None  # BN of conv i-1 whose finalize conv i's prologue performs (fin_in)
             for i, cv in enumerate(b.convs):
                 if i == 0 and pending is not None:
                     pb, res, rsc, rsh = pending
@@ -657,9 +663,14 @@ class ResNetProgram:
                                stats=b.bns[i].stats if tr else None,
                                in_scale=prev_bn.scale if prev_bn else None,
                                in_shift=prev_bn.shift if prev_bn else None, relu_in=True,
-                               fin=self._ff(b.bns[i]))
+                               fin=self._ff(b.bns[i]), fin_in=deferred.fin_f if deferred is not None else None)
+                deferred = None
                 if self._ff(b.bns[i]) is None:
-                    self._bn_fwd(b.bns[i], N * cv.OH * cv.OW)
+                    if (tr and self.fin_in and i + 1 < len(b.convs) and not b.mat[i]
+                            and b.bns[i].fin_f is not None):
+                        deferred = b.bns[i]  # finalized by the next conv's prologue
+                    else:
+                        self._bn_fwd(b.bns[i], N * cv.OH * cv.OW)
                 prev_bn = b.bns[i]
             last = b.bns[-1]
             if b.ds_conv is not None:

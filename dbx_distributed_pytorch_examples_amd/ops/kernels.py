@@ -228,13 +228,16 @@ def _use_patch3(tile, mode: str) -> int:
 @_dispatch
 def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None,
              relu_in=True, tile=None, tail_res=None, tail_res_scale=None, tail_res_shift=None, tail_out=None,
-             tail_bits=None, fin: "BnFin" = None, _split=True, _fin=(0, 1)):
+             tail_bits=None, fin: "BnFin" = None, _split=True, _fin=(0, 1), fin_in: "BnFin" = None):
     """Y = conv(act(X), W); act = relu(X*in_scale + in_shift) with a BN prologue. "Tail" mode
     (``tail_res`` given; 1x1 stride-1 convs): act = relu(X*in_scale + in_shift + r), r = tail_res or
     tail_res*tail_res_scale + tail_res_shift -- the previous residual block's output computed on the
     fly -- and act / its 1-bit ReLU mask are stored to ``tail_out`` / ``tail_bits`` (bn_apply's
     outputs), so that pass and the re-read of the block output disappear. ``fin``: the BN finalize of
-    ``stats`` (:class:`BnFin`), done by the launch's last tiles (or by a finalize launch after it)."""
+    ``stats`` (:class:`BnFin`), done by the launch's last tiles (or by a finalize launch after it).
+    ``fin_in``: the forward finalize of the INPUT's BN (whose outputs are ``in_scale`` / ``in_shift``),
+    done inside this launch's prologue where the kernel supports it, else by its standalone launch
+    first -- either way it is complete when this returns."""
     N, IH, IW, IC = x.shape
     OH, OW = conv_out_hw(IH, IW, R, S, stride, pad)
     OC = w16.shape[0]
@@ -285,6 +288,12 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
                      _fin=(-(-n1 * OH * OW // 256), 1), **kw)
         return out
     f1 = fin.ptr() if fin is not None and stats is not None else 0
+    fi = 0
+    if fin_in is not None:
+        if mode == FWD and in_scale is not None and tail_res is None and dma in (0, 1) and fin_in.desc is not None:
+            fi = fin_in.ptr()  # the implicit-GEMM prologue finalizes it (csrc/bn_fin.h bn_fin_consume)
+        else:
+            fin_in.run()
     r0, nr = fwd_taps(IH, OH, R, stride, pad)
     s0, ns = fwd_taps(IW, OW, S, stride, pad)
     if nr == 0 or ns == 0:
@@ -292,7 +301,7 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     C().conv_igemm(mode, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
                    nr, ns, r0, s0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
-                   _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma, f1, 0, _fin[0], _fin[1])
+                   _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma, f1, 0, _fin[0], _fin[1], fi)
     if fin is not None and not f1 and _fin[1]:
         fin.run()
     return out
@@ -481,7 +490,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
     if kind:
         C().conv_igemm(DGRAD_PATCH, 0, 0, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
                        N, P, Q, K, H, W, Cc, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, H, W,
-                       0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), kind - 1, *fins, 0, 1)
+                       0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), kind - 1, *fins, 0, 1, 0)
         _fin_rest(epilogue, fins)
         return dx
     if isinstance(tile, str):
@@ -527,7 +536,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,
                        _p(addsrc), add_sub, *epi, act_ptr, bwd[2], bwd[3], bwd[4], bwd[5], 0, stream_ptr(), dma,
-                       *fins, _fin[0], _fin[1])
+                       *fins, _fin[0], _fin[1], 0)
     if _fin[1]:
         _fin_rest(epilogue, fins)
     return dx
@@ -571,7 +580,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
     bm = 0 if patch and stem_patch_supported(IH, IW, OC, R, S, stride, pad) else 128  # bm 0: patch kernel
     C().conv_igemm(STEM, bm, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
-                   *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr(), 0, 0, 0, 0, 1)
+                   *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr(), 0, 0, 0, 0, 1, 0)
     return out
 
 
