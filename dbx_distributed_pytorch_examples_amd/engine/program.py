@@ -206,11 +206,11 @@ class ResNetProgram:
             # TinyImageNet b512 (343 GFLOP) 89.4k vs 90.7-91.1k; headline +0.4 %
             # (profiles/r3s2_knobs/). Threshold: 100 GFLOP of forward convolution per step.
             self.overlap_wgrad = self.fwd_conv_flops() >= OVERLAP_MIN_FWD_FLOPS
-        # consumer-side forward BN finalize (K.conv_fwd fin_in) for the launch-bound steps: each
-        # workgroup of the consuming conv re-reads the statistics shards (2 x NSHARD x C doubles), so
-        # it pays only where launches, not bytes, dominate
-        fi = os.environ.get("DBX_FIN_IN")
-        self.fin_in = (fi == "1") if fi is not None else self.fwd_conv_flops() < OVERLAP_MIN_FWD_FLOPS
+        # consumer-side forward BN finalize (K.conv_fwd fin_in, DBX_FIN_IN=1): each workgroup of the
+        # consuming conv re-reads the statistics shards (2 x NSHARD x C doubles). Off: measured slower
+        # than the finalize launch it removes even on the launch-bound CIFAR step (212-214k vs 222k
+        # img/s; TinyImageNet 87.6k vs 89.5-89.9k, profiles/r3s2_finin/)
+        self.fin_in = os.environ.get("DBX_FIN_IN", "0") == "1"
         if not self.overlap_wgrad:
             # without the side stream folding costs no overlap: fold every BN-backward apply it can
             # (unless set explicitly) -- CIFAR b256 193.7k vs 189.5k img/s with overlap (r3s2_knobs)

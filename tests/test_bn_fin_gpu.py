@@ -140,7 +140,7 @@ def test_program_consumer_fin_in_bit_identical(arch, size, batch, monkeypatch):
     t1 = NativeTrainer(m1, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_FIN_IN", "0")
     t2 = NativeTrainer(m2, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
-    assert t1.prog.fin_in and not t2.prog.fin_in
+    assert t1.prog.fin_in and not t2.prog.fin_in  # (off by default: an A/B switch)
     g = torch.Generator().manual_seed(1)
     for i in range(5):
         img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).cuda()
