@@ -196,6 +196,10 @@ class ResNetProgram:
         self.fast_mat1 = os.environ.get("DBX_FAST_MAT1", "0") == "1"
         self._wstream = None
         self._side_pending = False
+        # DBX_OVERLAP_WGRAD=2: the side stream forks once per backward segment (batched) instead of
+        # once per weight gradient
+        self.side_batch = os.environ.get("DBX_OVERLAP_WGRAD") == "2" and not self.fuse_stem_bwd  # (shares self.ws)
+        self._side_q = []
         self.param_align = max(16, int(param_align))
         self._want_param16 = param16
         self._build_layers()
@@ -721,7 +725,9 @@ class ResNetProgram:
             segs.append((f"layer{li}", (lambda idx=idx: [self._bwd_block(i) for i in idx])))
         segs.append(("stem", self._bwd_stem))
         # every segment ends with its weight gradients complete on the main stream (join)
-        self._segments = [(n, (lambda fn=fn: (fn(), self._join_side()))) for n, fn in segs]
+        last = len(segs) - 1
+        self._segments = [(n, (lambda fn=fn, k=k: (fn(), self._join_side(final=k == last))))
+                          for k, (n, fn) in enumerate(segs)]
         return self._segments
 
     # --------------------------------------------------------------------------------------
@@ -733,6 +739,9 @@ class ResNetProgram:
     def _side(self, fn):
         if self.dev.type != "cuda" or not self.overlap_wgrad:
             fn()
+            return
+        if self.side_batch:  # launched as one batch at the segment's end (_join_side)
+            self._side_q.append(fn)
             return
         if self._wstream is None:
             self._wstream = torch.cuda.Stream(device=self.dev)
@@ -748,7 +757,26 @@ class ResNetProgram:
             kw["lds_pad"] = self.wgrad_lds_pad  # occupancy cap: leave room for the main stream's kernels
         self._side(lambda: K.conv_wgrad(*args, **kw))
 
-    def _join_side(self):
+    def _join_side(self, final: bool = True):
+        if self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad:
+            # batched side stream: the segment's weight gradients fork ONCE, after its data gradients,
+            # and run under the NEXT segment's backward; joined one segment later (at most one batch in
+            # flight: they share self.ws) and at the end of the backward
+            cur = torch.cuda.current_stream(self.dev)
+            if self._side_pending:
+                cur.wait_stream(self._wstream)
+                self._side_pending = False
+            if self._side_q:
+                if self._wstream is None:
+                    self._wstream = torch.cuda.Stream(device=self.dev)
+                self._wstream.wait_stream(cur)
+                with torch.cuda.stream(self._wstream):
+                    for fn in self._side_q:
+                        fn()
+                self._side_q = []
+                self._side_pending = True
+            if not final:
+                return
         if self._side_pending:
             torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
             self._side_pending = False
