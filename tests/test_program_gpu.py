@@ -465,6 +465,9 @@ def test_batched_side_stream_bit_identical(arch, size, batch, monkeypatch):
     torch.manual_seed(0)
     m1 = build_model(arch, num_classes=10)
     m2 = copy.deepcopy(m1)
+    # the same BN-backward fold schedule on both sides (without the side stream it defaults to fold-all)
+    monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(1 << 25))
+    monkeypatch.setenv("DBX_FOLD_MAX_RATIO", "1")
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "2")
     t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "0")
