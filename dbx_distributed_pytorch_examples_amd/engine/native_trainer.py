@@ -104,6 +104,10 @@ class NativeTrainer:
             # stream vs 14.43k / 14.40k without; the plain single graph is 14.53-14.56k either way
             # (profiles/r2s2_multirank/). Weight gradients then run in order on the main stream.
             self.prog.overlap_wgrad = False
+        if self.segmented:
+            # per-segment all-reduces need each segment's weight gradients final at its end: no batched
+            # side stream (it joins a segment late)
+            self.prog.side_batch = False
         # DBX_COMM=native: the DP bucket all-reduces go through the framework's own RCCL communicator
         # (parallel/comm.py) on the comm stream, and the whole step -- backward segments, forked
         # all-reduces, join, optimizer -- is captured as ONE graph instead of per-segment graphs

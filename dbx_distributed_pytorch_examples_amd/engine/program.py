@@ -35,10 +35,6 @@ import torch.nn as nn
 from ..models.resnet import BasicBlock, Bottleneck, CifarBlock, CifarResNet18, ResNet
 from ..ops import kernels as K
 
-# steps with less forward convolution than this run their weight gradients in order on the main
-# stream (see ResNetProgram.__init__): launch-bound steps lose more to cross-stream joins than they overlap
-OVERLAP_MIN_FWD_FLOPS = 100e9
-
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
@@ -153,8 +149,13 @@ class ResNetProgram:
         self.norm_std = tuple(std) if std else None
         self.dev = device
         self.in_ch = model.conv1.in_channels
-        ov = os.environ.get("DBX_OVERLAP_WGRAD")  # unset: decided by the step's size (_build_layers)
-        self.overlap_wgrad = ov != "0"
+        # weight gradients on a side stream (DBX_OVERLAP_WGRAD unset / "2": batched, one fork per backward
+        # segment -- see self.side_batch; "1": one fork per weight gradient; "0": in order on the main
+        # stream). Per-gradient forks cost more than they overlap on launch-bound steps (ResNet-18 CIFAR
+        # b256 189k img/s vs 222k in order) while one fork per segment wins at every size: CIFAR
+        # 229-230k, TinyImageNet 95.3-95.5k vs 90.6-91.5k, headline 16.07-16.15k vs 15.94-15.99k
+        # (profiles/r3s2_batched/)
+        self.overlap_wgrad = os.environ.get("DBX_OVERLAP_WGRAD", "2") != "0"
         # split-K weight-gradient reduction inside the wgrad launch where a tile's slabs are small
         self.fuse_wgrad_reduce = os.environ.get("DBX_FUSE_WGRAD_REDUCE", "0") == "1"
         # BN finalize / backward coefficients computed by the producing conv's last tiles (K.BnFin)
@@ -196,20 +197,14 @@ class ResNetProgram:
         self.fast_mat1 = os.environ.get("DBX_FAST_MAT1", "0") == "1"
         self._wstream = None
         self._side_pending = False
-        # DBX_OVERLAP_WGRAD=2: the side stream forks once per backward segment (batched) instead of
-        # once per weight gradient
-        self.side_batch = os.environ.get("DBX_OVERLAP_WGRAD") == "2" and not self.fuse_stem_bwd  # (shares self.ws)
+        # DBX_OVERLAP_WGRAD unset / 2: the side stream forks once per backward segment (batched) instead
+        # of once per weight gradient. Callers that need every segment's gradients final at its end
+        # (per-segment all-reduces: NativeTrainer / native_module at world > 1) turn it off.
+        self.side_batch = os.environ.get("DBX_OVERLAP_WGRAD", "2") == "2" and not self.fuse_stem_bwd  # (shares self.ws)
         self._side_q = []
         self.param_align = max(16, int(param_align))
         self._want_param16 = param16
         self._build_layers()
-        if ov is None:
-            # The side stream pays off only when the kernels fill the GPU: a launch-bound step (small
-            # maps / batch) loses more to the cross-stream joins of the captured graph than it overlaps
-            # -- ResNet-18 CIFAR b256 (19 GFLOP forward) 215k img/s without vs 189-190k with; ResNet-50
-            # TinyImageNet b512 (343 GFLOP) 89.4k vs 90.7-91.1k; headline +0.4 %
-            # (profiles/r3s2_knobs/). Threshold: 100 GFLOP of forward convolution per step.
-            self.overlap_wgrad = self.fwd_conv_flops() >= OVERLAP_MIN_FWD_FLOPS
         # consumer-side forward BN finalize (K.conv_fwd fin_in, DBX_FIN_IN=1): each workgroup of the
         # consuming conv re-reads the statistics shards (2 x NSHARD x C doubles). Off: measured slower
         # than the finalize launch it removes even on the launch-bound CIFAR step (212-214k vs 222k

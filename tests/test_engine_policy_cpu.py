@@ -1,10 +1,10 @@
-"""Size-dependent engine policies: the wgrad side stream threshold, and the per-step hyper-parameter
-refresh (no copy when unchanged)."""
+"""Engine policies: the weight-gradient side-stream modes, the per-step hyper-parameter refresh (no
+copy when unchanged), and the step FLOP count."""
 import pytest
 import torch
 
 from dbx_distributed_pytorch_examples_amd.engine.hyper import DeviceHyper
-from dbx_distributed_pytorch_examples_amd.engine.program import OVERLAP_MIN_FWD_FLOPS, ResNetProgram
+from dbx_distributed_pytorch_examples_amd.engine.program import ResNetProgram
 from dbx_distributed_pytorch_examples_amd.models import build_model
 
 
@@ -15,15 +15,21 @@ def _flops(arch, size, batch, classes=10):
     return p.fwd_conv_flops()
 
 
-@pytest.mark.parametrize("arch,size,batch,overlap", [("resnet18", 32, 256, False),   # CIFAR preset: launch-bound
-                                                     ("resnet50", 32, 128, False),   # Accelerate / Composer loops
-                                                     ("resnet50", 64, 512, True),    # TinyImageNet preset
-                                                     ("resnet50", 224, 1024, True)])  # headline
-def test_wgrad_overlap_threshold(arch, size, batch, overlap):
-    f = _flops(arch, size, batch)
-    assert (f >= OVERLAP_MIN_FWD_FLOPS) == overlap, f
-    if arch == "resnet50" and size == 224:  # ~4.1 GMAC / image forward
-        assert abs(f / batch / 2 - 4.09e9) / 4.09e9 < 0.05
+def test_fwd_conv_flops():
+    f = _flops("resnet50", 224, 1024)
+    assert abs(f / 1024 / 2 - 4.09e9) / 4.09e9 < 0.05  # ~4.1 GMAC / image of forward convolution
+    assert _flops("resnet18", 32, 256) < _flops("resnet50", 64, 512) < f
+
+
+def test_side_stream_defaults(monkeypatch):
+    """Default: the batched side stream (one fork per backward segment); 1 = per-gradient forks; 0 = off."""
+    for env, overlap, batch in ((None, True, True), ("2", True, True), ("1", True, False), ("0", False, False)):
+        if env is None:
+            monkeypatch.delenv("DBX_OVERLAP_WGRAD", raising=False)
+        else:
+            monkeypatch.setenv("DBX_OVERLAP_WGRAD", env)
+        p = ResNetProgram(build_model("resnet18", num_classes=10), 2, (32, 32), torch.device("cpu"))
+        assert (p.overlap_wgrad, p.side_batch) == (overlap, batch), env
 
 
 def test_device_hyper_copies_only_changes():
