@@ -201,6 +201,9 @@ class ResNetProgram:
         # of once per weight gradient. Callers that need every segment's gradients final at its end
         # (per-segment all-reduces: NativeTrainer / native_module at world > 1) turn it off.
         self.side_batch = os.environ.get("DBX_OVERLAP_WGRAD", "2") == "2" and not self.fuse_stem_bwd  # (shares self.ws)
+        # "3": one fork per residual block (after its data gradients), every segment joined at its end:
+        # overlap that keeps segment-final gradients (the per-segment all-reduces at world > 1)
+        self.side_block = os.environ.get("DBX_OVERLAP_WGRAD") == "3" and not self.fuse_stem_bwd
         self._side_q = []
         self.param_align = max(16, int(param_align))
         self._want_param16 = param16
@@ -717,7 +720,7 @@ class ResNetProgram:
         segs.append(("head", self._bwd_head))
         for li in (4, 3, 2, 1):
             idx = list(reversed(stages[li]))
-            segs.append((f"layer{li}", (lambda idx=idx: [self._bwd_block(i) for i in idx])))
+            segs.append((f"layer{li}", (lambda idx=idx: [(self._bwd_block(i), self._block_flush()) for i in idx])))
         segs.append(("stem", self._bwd_stem))
         # every segment ends with its weight gradients complete on the main stream (join)
         last = len(segs) - 1
@@ -735,7 +738,7 @@ class ResNetProgram:
         if self.dev.type != "cuda" or not self.overlap_wgrad:
             fn()
             return
-        if self.side_batch:  # launched as one batch at the segment's end (_join_side)
+        if self.side_batch or self.side_block:  # launched as one batch (_flush_side)
             self._side_q.append(fn)
             return
         if self._wstream is None:
@@ -752,26 +755,36 @@ class ResNetProgram:
             kw["lds_pad"] = self.wgrad_lds_pad  # occupancy cap: leave room for the main stream's kernels
         self._side(lambda: K.conv_wgrad(*args, **kw))
 
+    def _flush_side(self):
+        """Fork the side stream once from the main stream and launch the queued weight gradients on it."""
+        if not self._side_q:
+            return
+        if self._wstream is None:
+            self._wstream = torch.cuda.Stream(device=self.dev)
+        self._wstream.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self._wstream):
+            for fn in self._side_q:
+                fn()
+        self._side_q = []
+        self._side_pending = True
+
+    def _block_flush(self):
+        if self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
+            self._flush_side()  # this block's weight gradients, under the next block's data gradients
+
     def _join_side(self, final: bool = True):
         if self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad:
             # batched side stream: the segment's weight gradients fork ONCE, after its data gradients,
             # and run under the NEXT segment's backward; joined one segment later (at most one batch in
             # flight: they share self.ws) and at the end of the backward
-            cur = torch.cuda.current_stream(self.dev)
             if self._side_pending:
-                cur.wait_stream(self._wstream)
+                torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
                 self._side_pending = False
-            if self._side_q:
-                if self._wstream is None:
-                    self._wstream = torch.cuda.Stream(device=self.dev)
-                self._wstream.wait_stream(cur)
-                with torch.cuda.stream(self._wstream):
-                    for fn in self._side_q:
-                        fn()
-                self._side_q = []
-                self._side_pending = True
+            self._flush_side()
             if not final:
                 return
+        elif self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
+            self._flush_side()  # (the stem / head segments queue theirs here), joined below
         if self._side_pending:
             torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
             self._side_pending = False

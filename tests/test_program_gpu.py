@@ -456,10 +456,12 @@ def test_composer_trainer_runs_on_native_module():
     assert 0.0 <= hist[-1]["metrics/eval/Accuracy"] <= 1.0
 
 
+@pytest.mark.parametrize("mode", ["2", "3"])
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64)])
-def test_batched_side_stream_bit_identical(arch, size, batch, monkeypatch):
+def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch):
     """DBX_OVERLAP_WGRAD=2 (weight gradients forked once per backward segment, joined one segment
-    later) trains bit-identically to the in-order schedule, eager and graph-replayed."""
+    later) and =3 (forked once per block, joined at the segment's end) train bit-identically to the
+    in-order schedule, eager and graph-replayed."""
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
     torch.manual_seed(0)
@@ -468,11 +470,12 @@ def test_batched_side_stream_bit_identical(arch, size, batch, monkeypatch):
     # the same BN-backward fold schedule on both sides (without the side stream it defaults to fold-all)
     monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(1 << 25))
     monkeypatch.setenv("DBX_FOLD_MAX_RATIO", "1")
-    monkeypatch.setenv("DBX_OVERLAP_WGRAD", "2")
+    monkeypatch.setenv("DBX_OVERLAP_WGRAD", mode)
     t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "0")
     t2 = NativeTrainer(m2, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
-    assert t1.prog.side_batch and t1.prog.overlap_wgrad and not t2.prog.overlap_wgrad
+    assert (t1.prog.side_batch if mode == "2" else t1.prog.side_block) and t1.prog.overlap_wgrad
+    assert not t2.prog.overlap_wgrad
     g = torch.Generator().manual_seed(3)
     for i in range(5):
         img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).to(dev)
