@@ -290,6 +290,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const bf16* __restri
 // ----------------------------------------------------------------------------------------
 // MaxPool 3x3 s2 p1 (NHWC) with BN-apply + ReLU prologue; argmax (0..8) saved as uint8.
 // ----------------------------------------------------------------------------------------
+// KF > 0: the window size as a constant (the ResNet stem's 3x3 / stride-2 pool) -- all KF x KF loads
+// of a window issued before any compare (out-of-image taps masked, no branches between the loads) and
+// 32-bit pixel arithmetic (host-checked M < 2^31); the compares run in the generic path's (r, s) order
+// with the same strict '>', so the argmax (and its ties) are identical.
+template <int KF>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ sc,
                                    const float* __restrict__ sh, bf16* __restrict__ out,
                                    unsigned char* __restrict__ arg, bf16* __restrict__ ymax, int N, int H, int W,
@@ -305,15 +310,46 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16* __restrict
   }
   const long long M = (long long)N * P * Q;
   for (long long pix = (long long)blockIdx.x * rm.rpb + rm.r0; pix < M; pix += (long long)gridDim.x * rm.rpb) {
-    const int q = (int)(pix % Q);
-    const long long t = pix / Q;
-    const int p = (int)(t % P);
-    const int n = (int)(t / P);
+    int q, p, n;
+    if constexpr (KF > 0) {
+      const int pi = (int)pix, t = pi / Q;
+      q = pi - t * Q; n = t / P; p = t - n * P;
+    } else {
+      q = (int)(pix % Q);
+      const long long t = pix / Q;
+      p = (int)(t % P);
+      n = (int)(t / P);
+    }
     float best[8], braw[8];
     unsigned char bi[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; braw[j] = 0.f; bi[j] = 0; }
-    for (int r = 0; r < K; ++r) {
+    if constexpr (KF > 0) {
+      u32x4 win[KF * KF];
+      bool ok[KF * KF];
+#pragma unroll
+      for (int r = 0; r < KF; ++r)
+#pragma unroll
+        for (int ss = 0; ss < KF; ++ss) {
+          const int hh = p * stride - pad + r, w = q * stride - pad + ss;
+          const bool v = (unsigned)hh < (unsigned)H && (unsigned)w < (unsigned)W;
+          ok[r * KF + ss] = v;
+          win[r * KF + ss] = *reinterpret_cast<const u32x4*>(
+              x + (((size_t)n * H + (v ? hh : 0)) * W + (v ? w : 0)) * C + c0);
+        }
+#pragma unroll
+      for (int k = 0; k < KF * KF; ++k) {
+        float f[8];
+        unpack8(win[k], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float v = f[j] * s[j] + h[j];
+          if (relu) v = fmaxf(v, 0.f);
+          if (ok[k] && v > best[j]) { best[j] = v; braw[j] = f[j]; bi[j] = (unsigned char)k; }
+        }
+      }
+    }
+    for (int r = 0; r < (KF > 0 ? 0 : K); ++r) {
       const int hh = p * stride - pad + r;
       if (hh < 0 || hh >= H) continue;
       for (int ss = 0; ss < K; ++ss) {
@@ -1022,8 +1058,13 @@ extern "C" int dbx_maxpool_fwd(const bf16* x, const float* sc, const float* sh, 
                                hipStream_t st) {
   if (C % 8) return -1;
   if (C / 8 > 256) return -1;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * P * Q, 256 / (C / 8), 4096)), dim3(256), 0, st,
-                     x, sc, sh, out, arg, ymax, N, H, W, C, P, Q, K, stride, pad, relu);
+  const dim3 grid(grid_for((long long)N * P * Q, 256 / (C / 8), 4096));
+  if (K == 3 && (long long)N * P * Q < (1ll << 31))
+    hipLaunchKernelGGL(maxpool_fwd_kernel<3>, grid, dim3(256), 0, st, x, sc, sh, out, arg, ymax, N, H, W, C, P, Q, K,
+                       stride, pad, relu);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<0>, grid, dim3(256), 0, st, x, sc, sh, out, arg, ymax, N, H, W, C, P, Q, K,
+                       stride, pad, relu);
   RET_LAST;
 }
 extern "C" int dbx_maxpool_bwd(const bf16* dout, const unsigned char* arg, bf16* dx, int N, int H, int W, int C, int P,
