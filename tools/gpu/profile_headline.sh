@@ -1,12 +1,12 @@
 #!/bin/bash
-# rocprofv3 kernel trace + stats of the headline ResNet-50 b1024 step: serialised (wgrad on the main
+# stream: per-kernel times add up to the step, DBX_OVERLAP_WGRAD=0) and the default batched side stream (2);
 # stream: per-kernel times add up to the step) and default; then per-kernel top list + timeline gaps.
 set -o pipefail
 O=${1:-gpurun_out/prof_headline}
 mkdir -p $O
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-for ov in 0 1; do
+for ov in 0 2; do
   (cd /tmp && DBX_OVERLAP_WGRAD=$ov timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/rp_ov$ov -o run --output-format csv -- python3 $R/bench.py --steps 6 --warmup 3 > $R/$O/rp_ov$ov.log 2>&1) || { echo "rocprof ov=$ov failed"; tail -5 $O/rp_ov$ov.log; exit 1; }
   grep -o '"value": [0-9.]*' $O/rp_ov$ov.log
   f=$(find $O/rp_ov$ov -name "*kernel_stats.csv" | head -1)
