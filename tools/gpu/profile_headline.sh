@@ -1,6 +1,6 @@
 #!/bin/bash
-# stream: per-kernel times add up to the step, DBX_OVERLAP_WGRAD=0) and the default batched side stream (2);
-# stream: per-kernel times add up to the step) and default; then per-kernel top list + timeline gaps.
+# rocprofv3 kernel trace + stats of the headline ResNet-50 b1024 step: serialised (wgrad on the main
+# stream, DBX_OVERLAP_WGRAD=0: per-kernel times add up to the step) and the default batched side stream (2); then per-kernel top list + timeline gaps.
 set -o pipefail
 O=${1:-gpurun_out/prof_headline}
 mkdir -p $O
