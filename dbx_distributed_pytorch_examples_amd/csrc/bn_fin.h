@@ -61,13 +61,27 @@ __device__ __forceinline__ void bn_bwd_final(int C, int c, double sd, double qd,
 // 32-way split holds one shard per lane for nshard <= 32, summed lane by lane). The in-launch
 // finalize reads the shards with agent-scope (sc1) loads: they bypass this CU's L1, and the shards'
 // lines are never in an L2 (the statistics atomics execute at the memory side and drop the line).
+// The loads are issued 16 shards at a time before their in-order adds: one memory round trip per 16
+// shards instead of one per shard (the shards live at the memory side, ~1-2 us away).
 __device__ __forceinline__ void bn_fin_sums_sc1(const double* stats, int nshard, int C, int c, double& s, double& q) {
   s = 0.0;
   q = 0.0;
-  for (int k = 0; k < nshard; ++k) {
-    gf64* p = (gf64*)(stats + (size_t)k * 2 * C + c);
-    s += __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    q += __hip_atomic_load(p + C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k0 = 0; k0 < nshard; k0 += 16) {
+    double sv[16], qv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = k0 + j < nshard ? k0 + j : k0;  // (past the end: a valid address, not added)
+      gf64* p = (gf64*)(stats + (size_t)k * 2 * C + c);
+      sv[j] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      qv[j] = __hip_atomic_load(p + C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (k0 + j < nshard) {
+        s += sv[j];
+        q += qv[j];
+      }
+    }
   }
 }
 
@@ -86,9 +100,21 @@ __device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c) {
 // earlier launch); the storing workgroup also writes every bn_finalize output of the channel.
 __device__ __forceinline__ void bn_fin_consume(const BnFin& f, int c, bool store, float& scale, float& shift) {
   double s = 0.0, q = 0.0;
-  for (int k = 0; k < f.nshard; ++k) {
-    s += f.stats[(size_t)k * 2 * f.C + c];
-    q += f.stats[(size_t)k * 2 * f.C + f.C + c];
+  for (int k0 = 0; k0 < f.nshard; k0 += 16) {  // loads batched ahead of the in-order adds
+    double sv[16], qv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = k0 + j < f.nshard ? k0 + j : k0;
+      sv[j] = f.stats[(size_t)k * 2 * f.C + c];
+      qv[j] = f.stats[(size_t)k * 2 * f.C + f.C + c];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (k0 + j < f.nshard) {
+        s += sv[j];
+        q += qv[j];
+      }
+    }
   }
   if (store) {
     bn_fwd_final(c, s, q, f.count, f.gamma, f.beta, f.eps, f.momentum, f.running_mean, f.running_var, f.scale,
