@@ -66,6 +66,7 @@ class SchedulerConfig:
     name: str = "none"                 # none | cosine | warmup_linear | warmup_cosine | step | warmup_lr
     warmup_steps: int = 0
     warmup_min_lr: float = 0.0
+    warmup_type: str = "log"           # DeepSpeed WarmupLR: "log" (its default) | "linear"
     total_steps: int = 0
     t_max_epochs: int = 0              # CosineAnnealingLR(T_max=epochs), per-epoch stepping
     step_size: int = 30
@@ -82,6 +83,17 @@ class ZeroConfig:
     reduce_scatter: bool = True
     offload_optimizer: bool = False    # fp32 master shard + moments in pinned host memory, CPU step (stage 3 path)
     offload_param: bool = False        # + no persistent device parameter shard
+    allgather_partitions: bool = True
+    sub_group_size: int = 1_000_000_000
+    # stage 3 (parallel/fsdp.py): parameters smaller than the persistence threshold stay replicated
+    # (never gathered / released); the prefetch size bounds how many parameter elements the next units'
+    # all-gathers may run ahead of the forward; live / reuse distance are recorded (DeepSpeed
+    # memory-pressure knobs with no effect at ResNet sizes on 288 GB HBM)
+    stage3_prefetch_bucket_size: int = 50_000_000
+    stage3_param_persistence_threshold: int = 100_000
+    stage3_max_live_parameters: int = 1_000_000_000
+    stage3_max_reuse_distance: int = 1_000_000_000
+    stage3_gather_16bit_weights_on_model_save: bool = False
 
 
 @dataclass
@@ -123,6 +135,9 @@ class TrainConfig:
     resume: str = ""                   # path or "latest"
     experiment: str = "dbx_amd"
     run_name: str = ""
+    model_name: str = "model"          # MLflow model artifact name (the notebooks' per-file names)
+    wall_clock_breakdown: bool = False # DeepSpeed wall_clock_breakdown: per-phase timers (utils/profiling.py)
+    tensorboard_dir: str = ""          # DeepSpeed tensorboard.output_path when enabled (recorded; MLflow is the sink)
     optim: OptimizerConfig = field(default_factory=OptimizerConfig)
     sched: SchedulerConfig = field(default_factory=SchedulerConfig)
     zero: ZeroConfig = field(default_factory=ZeroConfig)
@@ -227,24 +242,96 @@ def parse_duration(s: Union[str, int], steps_per_epoch: int, batch_size: int = 1
     return int(v) // max(1, batch_size)
 
 
-def from_deepspeed(ds: Dict[str, Any], base: Optional[TrainConfig] = None) -> TrainConfig:
-    """Map the DeepSpeed config schema subset used by `02_deepspeed/deepspeed_config.py:5-105`."""
+def _ds_auto(v: Any) -> bool:
+    return isinstance(v, str) and v.strip().lower() == "auto"
+
+
+def _ds_bool(v: Any, default: bool = False) -> bool:
+    """DeepSpeed booleans: JSON true/false, or the strings "true"/"false" the reference writes
+    (`deepspeed_config.py:19-21` has ``"enabled": "true"``); "auto" = ``default``."""
+    if v is None or _ds_auto(v):
+        return default
+    if isinstance(v, str):
+        s = v.strip().lower()
+        if s in ("true", "1", "yes", "on"):
+            return True
+        if s in ("false", "0", "no", "off", ""):
+            return False
+        raise ValueError(f"not a DeepSpeed boolean: {v!r}")
+    return bool(v)
+
+
+def _ds_num(v: Any, auto: Union[int, float]) -> Union[int, float]:
+    """A DeepSpeed number: int, float, numeric string ("5e8"), or "auto" -> ``auto``."""
+    if _ds_auto(v):
+        return auto
+    return float(v) if isinstance(v, str) else v
+
+
+# DeepSpeed's own optimizer defaults (torch.optim.AdamW / Adam / SGD): a key the dict omits takes
+# these, never a TrainConfig default
+_DS_OPT_DEFAULTS = {"adamw": {"weight_decay": 0.01}, "adam": {"weight_decay": 0.0},
+                    "sgd": {"weight_decay": 0.0, "momentum": 0.0}}
+
+
+def from_deepspeed(ds: Dict[str, Any], base: Optional[TrainConfig] = None, world_size: Optional[int] = None,
+                   model_numel: Optional[int] = None) -> TrainConfig:
+    """Map a DeepSpeed config dict (the schema `02_deepspeed/deepspeed_config.py:5-105` uses) onto a
+    :class:`TrainConfig`. The reference dicts load verbatim:
+
+    * ``"auto"`` values are resolved the way DeepSpeed's integration resolves them, with the model
+      in place of a transformer's hidden size: ``train_batch_size`` = micro x accumulation x world,
+      ``reduce_bucket_size`` / ``allgather_bucket_size`` = the whole gradient (``model_numel``; one
+      bucket -- ResNet gradients are <= 102 MB), ``stage3_prefetch_bucket_size`` = 0.9 x that,
+      ``stage3_param_persistence_threshold`` = DeepSpeed's default 1e5;
+    * string booleans (``"true"`` / ``"false"``) are parsed, not truth-tested;
+    * an explicit ``train_batch_size`` is checked against micro x accumulation x world (as DeepSpeed
+      does) or, without a micro batch, defines it;
+    * optimizer keys the dict omits take the optimizer's defaults (AdamW weight decay 0.01), not
+      the TrainConfig's;
+    * WarmupLR keeps its ``warmup_type`` ("log" when absent, DeepSpeed's default).
+    """
     cfg = copy.deepcopy(base) if base is not None else TrainConfig()
-    if "train_micro_batch_size_per_gpu" in ds:
-        cfg.batch_size = int(ds["train_micro_batch_size_per_gpu"])
-    if "gradient_accumulation_steps" in ds:
-        cfg.grad_accum = int(ds["gradient_accumulation_steps"])
-    if "gradient_clipping" in ds:
+    if world_size is None:
+        world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    ga = ds.get("gradient_accumulation_steps", 1)
+    ga = 1 if _ds_auto(ga) else int(float(ga))
+    cfg.grad_accum = ga
+    mb = ds.get("train_micro_batch_size_per_gpu")
+    if mb is not None and not _ds_auto(mb):
+        cfg.batch_size = int(float(mb))
+    tbs = ds.get("train_batch_size")
+    if tbs is not None and not _ds_auto(tbs):
+        tbs = int(float(tbs))
+        if mb is None or _ds_auto(mb):
+            if tbs % (ga * world_size):
+                raise ValueError(f"train_batch_size {tbs} is not divisible by accumulation {ga} x world {world_size}")
+            cfg.batch_size = tbs // (ga * world_size)
+        elif tbs != cfg.batch_size * ga * world_size:
+            raise ValueError(f"train_batch_size {tbs} != micro batch {cfg.batch_size} x accumulation {ga} x "
+                             f"world {world_size}")
+    if "gradient_clipping" in ds and not _ds_auto(ds["gradient_clipping"]):
         cfg.optim.grad_clip = float(ds["gradient_clipping"])
-    if ds.get("bf16", {}).get("enabled"):
-        cfg.precision = "bf16"
-    elif ds.get("fp16", {}).get("enabled"):
-        cfg.precision = "bf16"  # MI355X path computes in bf16; fp16 loss-scaling not needed
+    if _ds_bool(ds.get("bf16", {}).get("enabled")) or _ds_bool(ds.get("fp16", {}).get("enabled")):
+        cfg.precision = "bf16"  # fp16 dicts too: the MI355X path computes in bf16 (no loss scaling needed)
+    elif "bf16" in ds or "fp16" in ds:
+        cfg.precision = "fp32"
+    if "steps_per_print" in ds:
+        cfg.log_every = int(float(ds["steps_per_print"]))
+    if "wall_clock_breakdown" in ds:
+        cfg.wall_clock_breakdown = _ds_bool(ds["wall_clock_breakdown"])
+    tb = ds.get("tensorboard") or {}
+    if _ds_bool(tb.get("enabled")):
+        cfg.tensorboard_dir = str(tb.get("output_path", ""))
     opt = ds.get("optimizer")
     if opt:
         t = opt.get("type", "AdamW").lower()
-        cfg.optim.name = {"adamw": "adamw", "adam": "adam", "sgd": "sgd"}.get(t, "adamw")
-        p = opt.get("params", {})
+        if t not in ("adamw", "adam", "sgd", "lars"):
+            raise ValueError(f"unsupported DeepSpeed optimizer type {opt.get('type')!r}")
+        cfg.optim.name = t
+        p = dict(_DS_OPT_DEFAULTS.get(t, {}))
+        p.update({"betas": (0.9, 0.999), "eps": 1e-8} if t in ("adamw", "adam") else {})
+        p.update({k: v for k, v in opt.get("params", {}).items() if not _ds_auto(v)})
         if "lr" in p:
             cfg.optim.lr = float(p["lr"])
         if "betas" in p:
@@ -258,27 +345,45 @@ def from_deepspeed(ds: Dict[str, Any], base: Optional[TrainConfig] = None) -> Tr
     sch = ds.get("scheduler")
     if sch:
         t = sch.get("type", "")
-        p = sch.get("params", {})
+        p = {k: v for k, v in sch.get("params", {}).items() if not _ds_auto(v)}
         if t == "WarmupLR":
             cfg.sched.name = "warmup_lr"
-            cfg.sched.warmup_steps = int(p.get("warmup_num_steps", 0))
+            cfg.sched.warmup_steps = int(float(p.get("warmup_num_steps", 1000)))
             cfg.sched.warmup_min_lr = float(p.get("warmup_min_lr", 0.0))
+            cfg.sched.warmup_type = str(p.get("warmup_type", "log"))
+            if cfg.sched.warmup_type not in ("log", "linear"):
+                raise ValueError(f"WarmupLR warmup_type must be 'log' or 'linear', got {cfg.sched.warmup_type!r}")
             if "warmup_max_lr" in p:
                 cfg.optim.lr = float(p["warmup_max_lr"])
         elif t in ("WarmupDecayLR", "WarmupCosineLR"):
             cfg.sched.name = "warmup_linear" if t == "WarmupDecayLR" else "warmup_cosine"
-            cfg.sched.warmup_steps = int(p.get("warmup_num_steps", 0))
-            cfg.sched.total_steps = int(p.get("total_num_steps", 0))
+            cfg.sched.warmup_steps = int(float(p.get("warmup_num_steps", 0)))
+            cfg.sched.warmup_type = str(p.get("warmup_type", "log"))
+            cfg.sched.total_steps = int(float(p.get("total_num_steps", 0)))
+        elif t:
+            raise ValueError(f"unsupported DeepSpeed scheduler type {t!r}")
     z = ds.get("zero_optimization")
-    if z:
-        cfg.zero.stage = int(z.get("stage", 0))
-        for k in ("reduce_bucket_size", "allgather_bucket_size"):
+    if z is not None:
+        zc = cfg.zero
+        zc.stage = int(float(z.get("stage", 0)))
+        whole = int(model_numel) if model_numel else zc.reduce_bucket_size
+        for k in ("reduce_bucket_size", "allgather_bucket_size", "sub_group_size", "stage3_max_live_parameters",
+                  "stage3_max_reuse_distance"):
             if k in z:
-                setattr(cfg.zero, k, int(float(z[k])))
-        for k in ("overlap_comm", "contiguous_gradients", "reduce_scatter"):
+                setattr(zc, k, int(_ds_num(z[k], whole if "bucket" in k else getattr(zc, k))))
+        if "stage3_prefetch_bucket_size" in z:
+            zc.stage3_prefetch_bucket_size = int(_ds_num(z["stage3_prefetch_bucket_size"], 0.9 * whole))
+        if "stage3_param_persistence_threshold" in z:
+            zc.stage3_param_persistence_threshold = int(_ds_num(z["stage3_param_persistence_threshold"], 100_000))
+        for k in ("overlap_comm", "contiguous_gradients", "reduce_scatter", "allgather_partitions",
+                  "stage3_gather_16bit_weights_on_model_save"):
             if k in z:
-                setattr(cfg.zero, k, bool(z[k]))
-        cfg.zero.offload_optimizer = bool(z.get("offload_optimizer", {}).get("device", "none") not in ("none", None))
-        cfg.zero.offload_param = bool(z.get("offload_param", {}).get("device", "none") not in ("none", None))
+                setattr(zc, k, _ds_bool(z[k], getattr(zc, k)))
+
+        def _dev(key):
+            d = z.get(key) or {}
+            return str(d.get("device", "none")).lower() not in ("none", "") if isinstance(d, dict) else _ds_bool(d)
+        zc.offload_optimizer = _dev("offload_optimizer") or _ds_bool(z.get("cpu_offload"))
+        zc.offload_param = _dev("offload_param")
     cfg.deepspeed_applied = True  # train() then skips the launcher's DBX_DEEPSPEED_CONFIG env copy
     return cfg

@@ -33,6 +33,7 @@ struct Api {
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
   ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
   ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*comm_get_async_error)(ncclComm_t, ncclResult_t*) = nullptr;
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*reduce_scatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
@@ -59,6 +60,7 @@ static Api& api() {
     DBX_SYM(comm_destroy, "ncclCommDestroy");
     DBX_SYM(comm_abort, "ncclCommAbort");
     DBX_SYM(comm_count, "ncclCommCount");
+    DBX_SYM(comm_get_async_error, "ncclCommGetAsyncError");
     DBX_SYM(all_reduce, "ncclAllReduce");
     DBX_SYM(reduce_scatter, "ncclReduceScatter");
     DBX_SYM(all_gather, "ncclAllGather");
@@ -171,6 +173,30 @@ void register_comm(py::module& m) {
       else a.comm_destroy(c->comm);
     }
     delete c;
+  });
+  // failure handling (parallel/comm_guard.py): the communicator's asynchronous error state -- a peer
+  // that died or a network / xGMI failure surfaces here while the kernels are still queued -- and an
+  // abort that can be issued from the watchdog thread while the main thread is blocked on the
+  // device: ncclCommAbort makes the communicator's queued kernels return, so the stream drains
+  // (the handle is then inert; a later comm_destroy only frees it)
+  m.def("comm_async_error", [](uintptr_t h) -> py::tuple {
+    auto* c = reinterpret_cast<Communicator*>(h);
+    Api& a = need();
+    if (!c || !c->comm) return py::make_tuple(-1, std::string("communicator aborted"));
+    if (!a.comm_get_async_error) return py::make_tuple(0, std::string("ncclCommGetAsyncError unavailable"));
+    ncclResult_t st = ncclSuccess;
+    ncclResult_t r = a.comm_get_async_error(c->comm, &st);
+    if (r != ncclSuccess) st = r;
+    return py::make_tuple(static_cast<int>(st), std::string(a.error_string ? a.error_string(st) : ""));
+  });
+  m.def("comm_abort", [](uintptr_t h) {
+    auto* c = reinterpret_cast<Communicator*>(h);
+    Api& a = need();
+    if (!c || !c->comm || !a.comm_abort) return;
+    ncclComm_t comm = c->comm;
+    c->comm = nullptr;
+    py::gil_scoped_release nogil;
+    a.comm_abort(comm);
   });
   m.def("comm_rank", [](uintptr_t h) { return reinterpret_cast<Communicator*>(h)->rank; });
   m.def("comm_size", [](uintptr_t h) { return reinterpret_cast<Communicator*>(h)->size; });

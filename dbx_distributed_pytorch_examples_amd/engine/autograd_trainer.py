@@ -91,8 +91,10 @@ class AutogradTrainer:
     def __init__(self, model: nn.Module, device: torch.device, optim, label_smoothing: float = 0.0,
                  bucket_cap_mb: float = 64.0, channels_last: bool = True, zero_stage: int = 0,
                  cutmix_alpha: float = 0.0, grad_accum: int = 1, allreduce_dtype=torch.float32,
-                 offload_optimizer: bool = False, offload_param: bool = False):
+                 offload_optimizer: bool = False, offload_param: bool = False, bf16: bool = True,
+                 stage3: Optional[dict] = None):
         self.dev = device
+        self.bf16 = bool(bf16) and device.type == "cuda"  # autocast bf16 (DeepSpeed bf16.enabled)
         self.model = model.to(device)
         if device.type == "cuda" and channels_last:
             self.model = self.model.to(memory_format=torch.channels_last)
@@ -100,7 +102,7 @@ class AutogradTrainer:
         if self.sharded:  # ZeRO-3: parameters, gradients and optimizer state sharded (parallel/fsdp.py)
             from ..parallel.fsdp import ShardedDataParallel
             self.ddp = ShardedDataParallel(self.model, optim, offload_optimizer=offload_optimizer,
-                                           offload_param=offload_param)
+                                           offload_param=offload_param, **(stage3 or {}))
             zero_stage = 0
         else:
             from .native_module import NativeResNet
@@ -163,7 +165,7 @@ class AutogradTrainer:
         last_micro = (self.micro + 1) % self.grad_accum == 0
         ctx = self.ddp.no_sync() if not last_micro else _null()
         with ctx:
-            with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.dev.type == "cuda"):
+            with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.bf16):
                 out = self.ddp(x) if not _is_composer(self.model) else self.ddp((x, y))
             loss = self._loss(out, x, y, target) / self.grad_accum
             loss.backward()
@@ -205,7 +207,7 @@ class AutogradTrainer:
         x, y = x.to(self.dev), y.to(self.dev)
         if self.dev.type == "cuda" and x.dim() == 4:
             x = x.contiguous(memory_format=torch.channels_last)
-        with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.dev.type == "cuda"):
+        with torch.autocast(self.dev.type, dtype=torch.bfloat16, enabled=self.bf16):
             out = self.model((x, y)) if _is_composer(self.model) else self.model(x)
         out = out.float()
         m = unwrap(self.model)

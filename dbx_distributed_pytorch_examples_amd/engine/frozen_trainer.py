@@ -232,6 +232,15 @@ class FrozenFeatureTrainer:
         self._graph.replay()
         return self._feats
 
+    @torch.no_grad()
+    def params_changed(self) -> None:
+        """The model's parameters were rewritten (``load_state_dict`` on resume): refresh the derived
+        copies -- the native head's bf16 compute copy (in place: captured graphs read it) and the
+        backbone program's converted weights."""
+        if self.nhead is not None:
+            self.nhead.p16.copy_(self.nhead.master)
+        self.prog.prepare_weights()
+
     @property
     def step_count(self) -> int:
         return self.nhead.step_count if self.nhead is not None else 0

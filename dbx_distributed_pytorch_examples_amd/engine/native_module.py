@@ -26,7 +26,11 @@ already ARE views of the program's flat fp32 master, so any torch optimizer step
   backward segment on a comm stream while the remaining segments' backward runs (the segment
   boundaries NativeTrainer uses: head+layer4 | layer3 | layer2 | layer1 | stem), so most of the
   all-reduce hides under the backward; do not wrap the result in DDP as well
-  (``frontends.accelerate`` knows this);
+  (``frontends.accelerate`` knows this). A ``torch.nn.parallel.DistributedDataParallel`` wrap (what
+  the real HF ``Accelerator.prepare`` does at world > 1) is neutralised at the first forward: its
+  reducer never sees this module's gradients (they are set, not accumulated by autograd), so it is
+  switched to ``no_sync`` permanently and stops broadcasting buffers -- the module's own overlapped
+  all-reduce is the one gradient synchronisation;
 * on the GPU the program's forward (train / eval) and backward are each captured as a HIP graph
   after two eager calls and replayed (the user loop is otherwise launch-bound at CIFAR sizes);
   the input / dlogits copies into the static buffers and the all-reduce stay outside the graphs.
@@ -181,7 +185,25 @@ class NativeResNet(nn.Module):
         return self
 
     # ------------------------------------------------------------------------------
+    def _neutralize_outer_ddp(self) -> None:
+        """Inside a torch DDP wrapper's forward: make that wrapper inert (see the module docstring)."""
+        from torch.nn.parallel import DistributedDataParallel as TorchDDP
+        get = getattr(TorchDDP, "_get_active_ddp_module", None)
+        d = get() if get is not None else None
+        if d is None or d.module is not self or getattr(d, "_dbx_inert", False):
+            return
+        # _post_forward (after this forward returns) then skips reducer.prepare_for_backward, and
+        # every later forward skips the reducer and the buffer broadcast
+        d.require_backward_grad_sync = False
+        d.require_forward_param_sync = False
+        d.broadcast_buffers = False
+        d._dbx_inert = True
+        import warnings
+        warnings.warn("native_module wrapped in torch DistributedDataParallel: the wrapper is made inert; the "
+                      "native module all-reduces its own gradients (overlapped with its backward)", stacklevel=3)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        self._neutralize_outer_ddp()
         if (self.prog is None and x.dim() == 4 and x.is_cuda and self.training and torch.is_grad_enabled()
                 and x.shape[1] == self.model.conv1.in_channels):
             self._build(x.shape[0], tuple(x.shape[2:]))  # lazy: the first training batch's shape

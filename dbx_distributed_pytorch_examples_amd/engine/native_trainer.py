@@ -111,9 +111,9 @@ class NativeTrainer:
         # DBX_COMM=native: the DP bucket all-reduces go through the framework's own RCCL communicator
         # (parallel/comm.py) on the comm stream, and the whole step -- backward segments, forked
         # all-reduces, join, optimizer -- is captured as ONE graph instead of per-segment graphs
-        # with eager c10d collectives between replays
+        # with eager c10d collectives between replays (ZeRO's reduce-scatter / all-gather included)
         self.ncomm = None
-        if self.segmented and device.type == "cuda" and not zero_stage:
+        if self.segmented and device.type == "cuda":
             from ..parallel.comm import NativeComm, native_comm_available, native_comm_requested
             if native_comm_requested() and native_comm_available():
                 self.ncomm = NativeComm(process_group, device)
@@ -123,7 +123,8 @@ class NativeTrainer:
         if zero_stage:
             from ..parallel.zero import SegmentedZero
             self.zero = SegmentedZero(self.prog, optim, self.seg_ranges, self.prog.bn_param_blocks(),
-                                      stage=zero_stage, process_group=process_group)
+                                      stage=zero_stage, process_group=process_group, comm=self.ncomm,
+                                      collectives=self.segmented)
             self.mom = self.zero.m  # shard-sized optimizer state only
             self.mom2 = self.zero.v
         self.lars = self._lars_segments() if optim.name == "lars" else None

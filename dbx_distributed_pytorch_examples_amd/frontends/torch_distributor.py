@@ -140,12 +140,15 @@ def main_fn(directory: str, train_dataset=None, test_dataset=None, epochs: int =
 
 
 def train_func(*, train_dataset, test_dataset, batch_size: int = 32, epochs: int = 5, mlflow_run_id=None,
-               arch: str = "resnet18", frozen_backbone: bool = True, learning_rate: float = 1e-3, **cfg_kw):
-    """ResNet train_func of the TD notebooks: Adam(lr), CE, per-epoch train/val metrics on rank 0."""
+               arch: str = "resnet18", frozen_backbone: bool = True, learning_rate: float = 1e-3,
+               model_name: str = "cifar_torch_distributor_resnet", **cfg_kw):
+    """ResNet train_func of the TD notebooks: Adam(lr), CE, per-epoch train/val metrics on rank 0; the
+    model is logged as ``model_name`` (both `02_cifar_…:267` and `03_tiny_imagenet_…:251` use
+    "cifar_torch_distributor_resnet")."""
     num_classes = getattr(test_dataset, "num_classes", None) or getattr(train_dataset, "num_classes", 10)
     model = (FrozenBackboneClassifier(arch, num_classes) if frozen_backbone else build_model(arch, num_classes=num_classes))
     cfg = TrainConfig(model=arch, num_classes=num_classes, batch_size=batch_size, epochs=epochs, log_every=10,
-                      experiment=os.environ.get("MLFLOW_EXPERIMENT_NAME", "torch_distributor"))
+                      experiment=os.environ.get("MLFLOW_EXPERIMENT_NAME", "torch_distributor"), model_name=model_name)
     cfg.optim.name, cfg.optim.lr, cfg.optim.weight_decay = "adam", learning_rate, 0.0
     for k, v in cfg_kw.items():
         setattr(cfg, k, v)
@@ -156,15 +159,18 @@ def train_func(*, train_dataset, test_dataset, batch_size: int = 32, epochs: int
 
 def train_func_mds(*, batch_size: int = 128, epochs: int = 5, mlflow_run_id=None, patience: int = 4,
                    remote: Optional[str] = None, local: Optional[str] = None, remote_val: Optional[str] = None,
-                   num_classes: int = 200, arch: str = "resnet50", image_size: int = 64, frozen_backbone: bool = False):
-    """03a: train from MDS shards (rank-partitioned StreamingDataset), per-epoch eval, early stop."""
+                   num_classes: int = 200, arch: str = "resnet50", image_size: int = 64, frozen_backbone: bool = True,
+                   model_name: str = "cifar_torch_distributor_resnet_mds"):
+    """03a: train from MDS shards (rank-partitioned StreamingDataset), per-epoch eval, early stop. As in
+    the notebook (`03a_…_mds.py:321-340`) the default trains a Dropout(0.5)+Linear head on a frozen
+    ResNet-50 (``frozen_backbone=False``: the whole network); logged as ``model_name`` (`:466`)."""
     from ..data.mds import StreamingDataset
     ds = StreamingDataset(remote=remote, local=local, shuffle=True, batch_size=batch_size)
     ev = StreamingDataset(remote=remote_val, local=(local + "_val") if (local and remote_val) else remote_val) \
         if remote_val else None
     model = FrozenBackboneClassifier(arch, num_classes) if frozen_backbone else build_model(arch, num_classes=num_classes)
     cfg = TrainConfig(model=arch, num_classes=num_classes, batch_size=batch_size, epochs=epochs, patience=patience,
-                      experiment=os.environ.get("MLFLOW_EXPERIMENT_NAME", "torch_distributor_mds"))
+                      experiment=os.environ.get("MLFLOW_EXPERIMENT_NAME", "torch_distributor_mds"), model_name=model_name)
     cfg.data.image_size = image_size
     cfg.data.dataset = "mds"
     cfg.optim.name, cfg.optim.lr, cfg.optim.weight_decay = "adam", 1e-3, 0.0

@@ -155,7 +155,9 @@ class Launcher:
                     done[i] = True
                 elif not p.is_alive():
                     if p.exitcode != 0:
-                        errors.append(f"rank {i}: exited with code {p.exitcode}")
+                        from .parallel.comm_guard import EXIT_COMM_FAILURE
+                        why = " (collective failure: comm watchdog)" if p.exitcode == EXIT_COMM_FAILURE else ""
+                        errors.append(f"rank {i}: exited with code {p.exitcode}{why}")
                     done[i] = True
             if errors:
                 break
@@ -286,7 +288,7 @@ def run_subprocess_ranks(nproc: int, cmd: List[str], nnodes: int = 1, node_rank:
             bad = [i for i, c in enumerate(codes) if c not in (None, 0)]
             if bad:
                 failed = f"rank(s) {bad} exited with {[codes[i] for i in bad]}"
-                code = next(c for c in codes if c not in (None, 0))
+                code = max(c for c in codes if c not in (None, 0))  # the worst rank's code (defined for any order)
                 break
             if all(c == 0 for c in codes):
                 break

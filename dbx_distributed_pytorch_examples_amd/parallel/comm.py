@@ -63,7 +63,7 @@ class NativeComm:
     def __init__(self, process_group=None, device: Optional[torch.device] = None):
         if not dist.is_initialized():
             raise RuntimeError("NativeComm needs an initialised torch.distributed process group for its bootstrap")
-        self.group = process_group
+        self.pg = process_group
         self.size = dist.get_world_size(process_group)
         self.rank = dist.get_rank(process_group)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
@@ -108,7 +108,7 @@ class NativeComm:
                                _stream_ptr(stream))
         return t
 
-    def group(self):
+    def fused_group(self):
         """Context manager fusing the collectives issued inside into one RCCL launch group."""
         comm = self
 
@@ -119,6 +119,20 @@ class NativeComm:
             def __exit__(self_, *exc):
                 comm._c.comm_group_end()
         return _G()
+
+    def async_error(self):
+        """(code, message) of the communicator's asynchronous error state (``ncclCommGetAsyncError``):
+        code 0 = healthy, 7 (``ncclInProgress``) = still initialising, -1 = aborted, else a failure."""
+        if not getattr(self, "_h", 0):
+            return -1, "communicator closed"
+        code, msg = self._c.comm_async_error(self._h)
+        return int(code), str(msg)
+
+    def abort(self) -> None:
+        """``ncclCommAbort`` (safe from another thread while this one waits on the device): queued
+        collectives of this communicator return, so the streams drain; the communicator is unusable after."""
+        if getattr(self, "_h", 0):
+            self._c.comm_abort(self._h)
 
     def close(self, abort: bool = False) -> None:
         if getattr(self, "_h", 0):

@@ -51,8 +51,11 @@ def env_int(name: str, default: int) -> int:
 
 
 def init_distributed(backend: Optional[str] = None, device: Optional[str] = None,
-                     timeout_s: float = 1800.0) -> DistInfo:
+                     timeout_s: Optional[float] = None) -> DistInfo:
     """Initialise (idempotently) the default process group from env:// variables.
+
+    ``timeout_s``: the c10d collective timeout (default ``DBX_COMM_TIMEOUT``, else 1800 s) -- a
+    blocked collective raises after it (see ``parallel.comm_guard``).
 
     ``device``: "cuda" / "cpu" / None (auto). With world_size 1 and no MASTER_ADDR the
     process group is skipped entirely (pure single-process mode).
@@ -60,6 +63,8 @@ def init_distributed(backend: Optional[str] = None, device: Optional[str] = None
     global _INFO
     if _INFO is not None and (not _INFO.distributed or dist.is_initialized()):
         return _INFO
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("DBX_COMM_TIMEOUT", "1800"))
     rank = env_int("RANK", 0)
     world = env_int("WORLD_SIZE", 1)
     local_rank = env_int("LOCAL_RANK", 0)

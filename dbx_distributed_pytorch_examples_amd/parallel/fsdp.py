@@ -25,6 +25,13 @@ Design (one process per GPU, RCCL collectives on the compute stream):
   the step runs on the CPU (gradient shard D2H, updated shard H2D); with ``offload_param`` no
   persistent device copy of the shard is kept either (it is uploaded at each gather).
 
+DeepSpeed ``stage3_*`` knobs: ``persistence_threshold`` keeps units with fewer parameter elements
+than it replicated (gathered once, re-gathered after each optimizer step, never released:
+DeepSpeed's ``stage3_param_persistence_threshold``, at unit rather than parameter granularity);
+``prefetch_elems`` lets a unit's forward pre-hook issue the asynchronous all-gathers of the units
+after it, up to that many elements ahead (``stage3_prefetch_bucket_size``), so their transfer
+overlaps the current unit's compute.
+
 Buffers (BatchNorm running statistics) stay replicated, broadcast from rank 0 at construction, as
 DeepSpeed and torch FSDP do. ``state_dict()`` / ``load_state_dict()`` on the wrapped module work
 on full tensors (hooks gather first; every rank must call them, as with any collective).
@@ -80,8 +87,11 @@ def _tensors(out):
 
 
 class _Unit:
-    def __init__(self, owner: "ShardedDataParallel", name: str, params: List[nn.Parameter], reshard: bool):
+    def __init__(self, owner: "ShardedDataParallel", name: str, params: List[nn.Parameter], reshard: bool,
+                 persistent: bool = False):
         self.owner, self.name, self.reshard = owner, name, reshard
+        self.persistent = persistent
+        self.work = None  # in-flight asynchronous all-gather (prefetch)
         params = [p for p in params if p.requires_grad] + [p for p in params if not p.requires_grad]
         self.params = params
         self.trainable = [p for p in params if p.requires_grad]
@@ -117,11 +127,21 @@ class _Unit:
         self.gathered = True
         self.pinned = False
         self.ready = 0
-        self.release()
+        self.release(force=True)
+        if persistent:
+            self.gather()
 
     # -- parameter materialisation -----------------------------------------------------------
-    def gather(self):
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+            self._src = None
+
+    def gather(self, async_op: bool = False):
         if self.gathered:
+            if not async_op:
+                self.wait()
             return
         o = self.owner
         st = self.full.untyped_storage()
@@ -131,14 +151,17 @@ class _Unit:
             src = self.master.to(o.device, non_blocking=True)
         if o.world > 1:
             host_sync_for_gloo(src)
-            dist.all_gather_into_tensor(self.full, src, group=o.pg)
+            w = dist.all_gather_into_tensor(self.full, src, group=o.pg, async_op=async_op)
+            if async_op:
+                self.work, self._src = w, src  # the source stays alive until the gather completes
         else:
             self.full.copy_(src)
         self.gathered = True
 
-    def release(self):
-        if not self.gathered or self.pinned:
+    def release(self, force: bool = False):
+        if not self.gathered or ((self.pinned or self.persistent) and not force):
             return
+        self.wait()
         # queued kernels may still read the storage; the caching allocator orders its reuse on this
         # stream, the only one that touches it
         self.full.untyped_storage().resize_(0)
@@ -186,8 +209,10 @@ class ShardedDataParallel(nn.Module):
     eps, grad_clip (the TrainConfig ``OptimConfig``)."""
 
     def __init__(self, module: nn.Module, optim, process_group=None, units: Optional[List[nn.Module]] = None,
-                 offload_optimizer: bool = False, offload_param: bool = False, reshard_after_forward: bool = True):
+                 offload_optimizer: bool = False, offload_param: bool = False, reshard_after_forward: bool = True,
+                 persistence_threshold: int = 0, prefetch_elems: int = 0):
         super().__init__()
+        self.prefetch_elems = int(prefetch_elems)
         if optim.name not in ("sgd", "adam", "adamw"):
             raise ValueError(f"ZeRO-3 supports sgd / adam / adamw, not {optim.name!r}")
         self.module = module
@@ -212,7 +237,8 @@ class ShardedDataParallel(nn.Module):
             ps = [p for p in m.parameters() if id(p) not in owned]
             owned.update(id(p) for p in ps)
             if ps:
-                u = _Unit(self, names.get(id(m), "?"), ps, reshard_after_forward)
+                persistent = sum(p.numel() for p in ps) < persistence_threshold
+                u = _Unit(self, names.get(id(m), "?"), ps, reshard_after_forward, persistent)
                 self.units.append(u)
                 self._hook_unit(m, u)
         rest = [p for p in module.parameters() if id(p) not in owned]
@@ -231,6 +257,7 @@ class ShardedDataParallel(nn.Module):
     def _hook_unit(self, m: nn.Module, u: _Unit):
         def pre(_m, _inp):
             u.gather()
+            self._prefetch_after(u)
 
         def post(_m, _inp, out):
             if torch.is_grad_enabled():
@@ -243,6 +270,19 @@ class ShardedDataParallel(nn.Module):
         m.register_forward_hook(post)
         for p in u.trainable:
             p.register_post_accumulate_grad_hook(lambda _p: u.on_grad())
+
+    def _prefetch_after(self, u: _Unit):
+        """Issue the asynchronous all-gathers of the units after ``u`` (forward order) within the
+        prefetch budget; their own pre-hooks wait for them."""
+        if self.prefetch_elems <= 0 or self.world == 1:
+            return
+        budget = self.prefetch_elems
+        i = self.units.index(u)
+        for v in self.units[i + 1:]:
+            if v.n > budget:
+                break
+            budget -= v.n
+            v.gather(async_op=True)
 
     def _root_pre(self, _m, _inp):
         if torch.is_grad_enabled():
@@ -339,7 +379,9 @@ class ShardedDataParallel(nn.Module):
                 u.dev_shard[:u.k].copy_(p, non_blocking=True)
         for u in self._all():  # materialised copies are stale now (other ranks updated their shards)
             u.pinned = False
-            u.release()
+            u.release(force=True)
+            if u.persistent:
+                u.gather()
 
     def optim_state_dict(self) -> Dict:
         return {"stage": 3, "step": self.step_count, "rank": self.rank, "world": self.world,
@@ -359,7 +401,9 @@ class ShardedDataParallel(nn.Module):
             if u.dev_shard is not None and u.dev_shard is not u.master:
                 u.dev_shard.copy_(p)
             u.pinned = False
-            u.release()
+            u.release(force=True)
+            if u.persistent:
+                u.gather()
 
     def materialised_bytes(self) -> int:
         return sum(u.full.untyped_storage().nbytes() for u in self._all())

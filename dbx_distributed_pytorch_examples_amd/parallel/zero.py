@@ -32,6 +32,7 @@ tools/dist_gpu_check.py). Stage 3 (parameter sharding) and CPU offload live in `
 from __future__ import annotations
 
 import math
+import os
 import warnings
 from typing import List, Optional, Tuple
 
@@ -188,7 +189,13 @@ class SegmentedZero:
     so) and is extended to the next such multiple. ``bn_ranges``: [lo, hi) blocks of fp32
     parameters that must stay exact (the BatchNorm affines)."""
 
-    def __init__(self, prog, optim, seg_ranges, bn_ranges, stage: int = 1, process_group=None):
+    def __init__(self, prog, optim, seg_ranges, bn_ranges, stage: int = 1, process_group=None, comm=None,
+                 collectives: Optional[bool] = None):
+        """``comm``: a :class:`~.comm.NativeComm` -- the collectives are then enqueued on the caller's
+        stream through the framework's RCCL communicator (capturable into the step's one graph)
+        instead of c10d. ``collectives``: take the reduce-scatter / all-gather path even at world 1
+        (default: when a process group exists and DBX_SEGMENTED_GRAPHS=1 -- the one-GPU RCCL
+        rehearsal, where every collective is an identity but runs through RCCL)."""
         if optim.name not in ("sgd", "adam", "adamw"):
             raise ValueError(f"sharded optimizer supports sgd / adam / adamw, not {optim.name!r}")
         if stage == 3:
@@ -199,6 +206,11 @@ class SegmentedZero:
         self.prog, self.o, self.pg = prog, optim, process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        self.comm = comm
+        if collectives is None:
+            collectives = self.world > 1 or (dist.is_available() and dist.is_initialized()
+                                             and os.environ.get("DBX_SEGMENTED_GRAPHS", "0") == "1")
+        self.coll = bool(collectives)  # the sharded exchange path (reduce-scatter / all-gather) is taken
         W, r = self.world, self.rank
         align = 16 * W
         dev = prog.master.device
@@ -221,15 +233,15 @@ class SegmentedZero:
         self.shard_n = off
         self.m = torch.zeros(off, device=dev)
         self.v = torch.zeros(off, device=dev) if optim.name in ("adam", "adamw") else None
-        self.gsh = torch.zeros(off, device=dev) if W > 1 else None          # reduce-scatter output
-        self.p16sh = torch.zeros(off, device=dev, dtype=torch.bfloat16) if W > 1 else None  # all-gather input
+        self.gsh = torch.zeros(off, device=dev) if self.coll else None          # reduce-scatter output
+        self.p16sh = torch.zeros(off, device=dev, dtype=torch.bfloat16) if self.coll else None  # all-gather input
         self.param16 = prog.param16
         self.work = torch.zeros(4, device=dev)  # [0:2] fp64 sum of squares, [2] clip factor, [3] norm
         self.step_count = 0
         # exact fp32 exchange of the BN affine blocks: this rank's pieces summed with zeros elsewhere
         self.bn_ranges = [tuple(b) for b in bn_ranges]
         nbn = sum(hi - lo for lo, hi in self.bn_ranges)
-        self.bnbuf = torch.zeros(max(1, nbn), device=dev) if W > 1 else None
+        self.bnbuf = torch.zeros(max(1, nbn), device=dev) if self.coll else None
         self._bn_own = []  # (buf_off, master_lo, length) of the owned pieces
         bo = 0
         for lo, hi in self.bn_ranges:
@@ -244,7 +256,28 @@ class SegmentedZero:
     # ---- helpers ------------------------------------------------------------------------
     def _gpart(self, part):
         lo, hi, per, own, so = part
-        return self.prog.grad[own:own + per] if self.world == 1 else self.gsh[so:so + per]
+        return self.prog.grad[own:own + per] if not self.coll else self.gsh[so:so + per]
+
+    # the three collectives: the framework communicator (current stream, capturable) or c10d
+    def _rs(self, out, inp):
+        if self.comm is not None:
+            self.comm.reduce_scatter(out, inp)
+        else:
+            _reduce_scatter_sum(out, inp, self.rank, self.pg)
+
+    def _ag(self, out, inp):
+        if self.comm is not None:
+            self.comm.all_gather(out, inp)
+        else:
+            host_sync_for_gloo(inp, self.pg)
+            dist.all_gather_into_tensor(out, inp, group=self.pg)
+
+    def _ar(self, t):
+        if self.comm is not None:
+            self.comm.all_reduce(t)
+        else:
+            host_sync_for_gloo(t, self.pg)
+            dist.all_reduce(t, group=self.pg)
 
     def refresh_param16(self) -> None:
         """bf16 copy of the FULL fp32 master (every rank holds it: after the constructor broadcast
@@ -255,32 +288,28 @@ class SegmentedZero:
     # ---- collectives (issued between graph replays, on the comm stream) -------------------
     def reduce_range(self, lo: int, hi: int) -> None:
         """Reduce-scatter every part inside the backward range [lo, hi)."""
-        if self.world == 1:
+        if not self.coll:
             return
         for part in self.parts:
             plo, phi, per, own, so = part
             if lo <= plo < hi:
-                _reduce_scatter_sum(self.gsh[so:so + per], self.prog.grad[plo:phi], self.rank, self.pg)
+                self._rs(self.gsh[so:so + per], self.prog.grad[plo:phi])
 
     def allreduce_norm(self) -> None:
-        if self.world > 1:
-            s = self.work[0:2].view(torch.float64)
-            host_sync_for_gloo(s, self.pg)
-            dist.all_reduce(s, group=self.pg)
+        if self.coll:
+            self._ar(self.work[0:2].view(torch.float64))
 
     def gather(self) -> None:
         """bf16 all-gather of the updated shards into param16; exact fp32 exchange of the BN blocks."""
-        if self.world == 1:
+        if not self.coll:
             return
-        host_sync_for_gloo(self.p16sh, self.pg)
         for (lo, hi, per, own, so) in self.parts:
-            dist.all_gather_into_tensor(self.param16[lo:hi], self.p16sh[so:so + per], group=self.pg)
+            self._ag(self.param16[lo:hi], self.p16sh[so:so + per])
         if self.bn_ranges:  # every rank joins, owner of a BN piece or not
             self.bnbuf.zero_()
             for bo, ml, n in self._bn_own:
                 self.bnbuf[bo:bo + n].copy_(self.prog.master[ml:ml + n])
-            host_sync_for_gloo(self.bnbuf, self.pg)
-            dist.all_reduce(self.bnbuf, group=self.pg)
+            self._ar(self.bnbuf)
             bo = 0
             for lo, hi in self.bn_ranges:
                 self.prog.master[lo:hi].copy_(self.bnbuf[bo:bo + hi - lo])
@@ -289,13 +318,12 @@ class SegmentedZero:
     @torch.no_grad()
     def gather_master(self) -> None:
         """Full fp32 master on every rank (collective; before checkpoints / state_dict)."""
-        if self.world == 1:
+        if not self.coll:
             return
         m = self.prog.master
-        host_sync_for_gloo(m, self.pg)
         for (lo, hi, per, own, so) in self.parts:
             buf = torch.empty(hi - lo, device=m.device)
-            dist.all_gather_into_tensor(buf, m[own:own + per].contiguous(), group=self.pg)
+            self._ag(buf, m[own:own + per].contiguous())
             m[lo:hi].copy_(buf)
 
     # ---- graph-capturable compute -------------------------------------------------------------
@@ -320,7 +348,7 @@ class SegmentedZero:
             lo, hi, per, own, so = part
             p = self.prog.master[own:own + per]
             g = self._gpart(part)
-            p16 = self.param16[own:own + per] if W == 1 else self.p16sh[so:so + per]
+            p16 = self.param16[own:own + per] if not self.coll else self.p16sh[so:so + per]
             m = self.m[so:so + per]
             if o.name == "sgd":
                 K.sgd_step(p, g, m, p16, lr=lr, momentum=o.momentum, dampening=getattr(o, "dampening", 0.0),

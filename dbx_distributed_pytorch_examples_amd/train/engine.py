@@ -51,6 +51,7 @@ class TrainResult:
     steps: int = 0
     images_per_sec: float = 0.0
     engine: str = ""
+    resumed_epoch: int = 0   # > 0: this run resumed from the checkpoint of that epoch
 
 
 def _log(msg: str):
@@ -208,6 +209,7 @@ class _Autograd:
                                   bucket_cap_mb=cfg.bucket_cap_mb, zero_stage=cfg.zero.stage,
                                   cutmix_alpha=cfg.data.cutmix_alpha, grad_accum=cfg.grad_accum,
                                   offload_optimizer=cfg.zero.offload_optimizer, offload_param=cfg.zero.offload_param,
+                                  bf16=cfg.precision == "bf16", stage3=_stage3_kw(cfg.zero),
                                   allreduce_dtype=torch.bfloat16 if cfg.allreduce_dtype == "bf16" else torch.float32)
         self.loader, self.sampler = make_loader(ds, cfg.batch_size, cfg.data.shuffle, cfg.seed,
                                                 num_workers=cfg.data.num_workers if dev.type == "cuda" else 0,
@@ -252,6 +254,12 @@ class _Autograd:
         return self.tr.model
 
 
+def _stage3_kw(z) -> Dict[str, Any]:
+    """The ZeRO-3 knobs parallel/fsdp.py honours (DeepSpeed ``stage3_*`` keys)."""
+    return {"persistence_threshold": z.stage3_param_persistence_threshold,
+            "prefetch_elems": z.stage3_prefetch_bucket_size}
+
+
 def _pick_engine(cfg: TrainConfig, model, ds, dev) -> str:
     from ..engine.program import supports
     from ..models.wrappers import FrozenBackboneClassifier
@@ -259,6 +267,8 @@ def _pick_engine(cfg: TrainConfig, model, ds, dev) -> str:
         return cfg.engine
     if cfg.zero.stage == 3 or cfg.zero.offload_optimizer or cfg.zero.offload_param:
         return "autograd"  # parameter sharding / offload: parallel/fsdp.py on the autograd engine
+    if cfg.precision != "bf16":
+        return "autograd"  # the native kernels compute in bf16 (fp32 master weights)
     frozen = isinstance(model, FrozenBackboneClassifier) and supports(model.resnet) and \
         not any(p.requires_grad for p in model.resnet.parameters() if p is not None and
                 not any(p is q for q in model.resnet.fc.parameters()))
@@ -313,6 +323,8 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
     epochs = math.ceil(total / max(1, spe))
     sched = sched_from_config(cfg.sched, cfg.optim.lr, total, spe)
     res = TrainResult(model=model, engine=engine)
+    from ..parallel import comm_guard
+    watchdog = comm_guard.for_runner(runner, dev)  # a hung / failed peer ends this rank (launcher restarts)
     # --- resume ----------------------------------------------------------------------------
     start_epoch, step = 0, 0
     if cfg.checkpoint_dir and (cfg.resume == "latest" or int(os.environ.get("DBX_RESTART_COUNT", "0")) > 0):
@@ -325,6 +337,7 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
             start_epoch, step = int(st.get("epoch", 0)), int(st.get("step", 0))
             _restore_shard_state(runner, cfg.checkpoint_dir, start_epoch)
             res.history = list(st.get("history", []))
+            res.resumed_epoch = start_epoch
             _log(f"[train] resumed from {path} (epoch {start_epoch}, step {step})")
     elif cfg.resume and cfg.resume != "latest":
         st = torch.load(cfg.resume, map_location="cpu", weights_only=True)
@@ -348,21 +361,47 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
     for epoch in range(start_epoch, epochs):
         t0 = time.perf_counter()
         n_local = 0  # samples actually stepped this epoch (early stop / short final batch)
-        for bi, batch in enumerate(runner.epoch_batches(epoch)):
-            if step >= total:
+        t_wait = t_wall = 0.0  # wall_clock_breakdown: host time waiting for batches / per logging window
+        t_mark = time.perf_counter()
+        n_win = 0
+        it = iter(runner.epoch_batches(epoch))
+        while step < total:
+            t_b = time.perf_counter()
+            batch = next(it, None)
+            if batch is None:
                 break
+            t_wait += time.perf_counter() - t_b
             runner.set_lr(sched(step))
             fault.heartbeat(step)
             if fault.maybe_inject(step):
                 raise FloatingPointError(f"injected NaN loss at step {step}")
+            if watchdog is not None:
+                watchdog.step_begin(step)
             runner.step(batch)
+            if watchdog is not None:
+                watchdog.step_end()
             step += 1
+            n_win += 1
             n_local += runner.batch_samples(batch)
             imgs += cfg.batch_size * ddist.get_world_size()
-            if cfg.log_every and step % cfg.log_every == 0 and is_main:
-                print(f"[TRAINING] [RANK {ddist.get_rank()}] step {step}/{total} (epoch {epoch + 1})", flush=True)
+            if cfg.log_every and step % cfg.log_every == 0:
+                if cfg.wall_clock_breakdown:  # DeepSpeed's per-window timing (synchronised at the window end)
+                    if dev.type == "cuda":
+                        torch.cuda.synchronize()
+                    t_wall = time.perf_counter() - t_mark
+                    if is_main:
+                        print(f"[wall_clock_breakdown] steps {step - n_win + 1}-{step}: "
+                              f"{1e3 * t_wall / n_win:.2f} ms/step, data wait {1e3 * t_wait / n_win:.2f} ms/step, "
+                              f"compute+sync {1e3 * (t_wall - t_wait) / n_win:.2f} ms/step", flush=True)
+                    t_wait, n_win, t_mark = 0.0, 0, time.perf_counter()
+                if is_main:
+                    print(f"[TRAINING] [RANK {ddist.get_rank()}] step {step}/{total} (epoch {epoch + 1})", flush=True)
+        if watchdog is not None:
+            watchdog.step_begin(step)  # the epoch-end collectives are bounded too
         loss_sum, correct = runner.read_metrics()
         loss_sum, correct, n = ddist.all_reduce_sum([loss_sum, correct, float(n_local)])
+        if watchdog is not None:
+            watchdog.step_end()
         if not fault.check_finite(loss_sum):
             raise FloatingPointError(f"non-finite training loss in epoch {epoch + 1}")
         rec = {"epoch": epoch + 1, "train_loss": loss_sum / max(1.0, n), "train_accuracy": correct / max(1.0, n),
@@ -399,6 +438,8 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
             break
     if torch.cuda.is_available() and dev.type == "cuda":
         torch.cuda.synchronize()
+    if watchdog is not None:
+        watchdog.close()
     el = time.perf_counter() - t_start
     _sync_master(runner)  # the returned / logged model holds the full parameters on every rank
     res.steps = step
@@ -406,7 +447,7 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
     res.model = runner.model
     if is_main and log_mlflow:
         mlflow.log_metric("images_per_sec", res.images_per_sec)
-        mlflow.pytorch.log_model(res.model, "model")
+        mlflow.pytorch.log_model(res.model, cfg.model_name or "model")
         mlflow.log_dict({"history": res.history}, "training_history.json")
         mlflow.end_run()
     return res

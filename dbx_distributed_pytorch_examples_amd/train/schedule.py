@@ -19,7 +19,7 @@ def linear_scaled_lr(base_lr: float, global_batch: int, reference_batch: int = 2
 class LRSchedule:
     def __init__(self, name: str, base_lr: float, total_steps: int = 0, warmup_steps: int = 0,
                  warmup_min_lr: float = 0.0, steps_per_epoch: int = 1, t_max_epochs: int = 0,
-                 step_size: int = 30, gamma: float = 0.1, min_lr: float = 0.0):
+                 step_size: int = 30, gamma: float = 0.1, min_lr: float = 0.0, warmup_type: str = "log"):
         self.name = name
         self.base = base_lr
         self.total = max(1, total_steps)
@@ -28,12 +28,16 @@ class LRSchedule:
         self.spe = max(1, steps_per_epoch)
         self.tmax = t_max_epochs
         self.step_size, self.gamma, self.min_lr = step_size, gamma, min_lr
+        self.warmup_type = warmup_type
 
     def __call__(self, step: int) -> float:
         """LR for optimizer step ``step`` (0-based)."""
         if self.warm and step < self.warm:
-            if self.name == "warmup_lr":  # DeepSpeed WarmupLR: log warmup then constant
-                frac = math.log(step + 1) / math.log(self.warm)
+            if self.name == "warmup_lr":  # DeepSpeed WarmupLR: log (default) or linear warmup, then constant
+                if self.warmup_type == "linear":
+                    frac = step / self.warm
+                else:
+                    frac = math.log(step + 1) / math.log(self.warm) if self.warm > 1 else 1.0
                 return self.wmin + (self.base - self.wmin) * frac
             return self.base * (step + 1) / self.warm
         n = self.name
@@ -58,4 +62,5 @@ def from_config(sched_cfg, base_lr: float, total_steps: int, steps_per_epoch: in
     return LRSchedule(sched_cfg.name, base_lr, total_steps=sched_cfg.total_steps or total_steps,
                       warmup_steps=sched_cfg.warmup_steps, warmup_min_lr=sched_cfg.warmup_min_lr,
                       steps_per_epoch=steps_per_epoch, t_max_epochs=sched_cfg.t_max_epochs,
-                      step_size=sched_cfg.step_size, gamma=sched_cfg.gamma)
+                      step_size=sched_cfg.step_size, gamma=sched_cfg.gamma,
+                      warmup_type=getattr(sched_cfg, "warmup_type", "log"))

@@ -4,7 +4,8 @@
   ``launch.Launcher``); the launcher's watchdog kills the job when a rank stops advancing.
 * :func:`maybe_inject` — deterministic fault injection for tests: ``DBX_FAULT="rank:step:kind"``
   with kind ``exit`` (os._exit(3)), ``raise`` (RuntimeError), ``hang`` (sleep forever),
-  ``nan`` (returns True so the caller poisons its loss). Only fires on attempt
+  ``nan`` (returns True so the caller poisons its loss), ``comm_hang`` (keeps beating but never
+  issues another collective: the peers' ``parallel.comm_guard`` watchdog must end the job). Only fires on attempt
   ``DBX_FAULT_ATTEMPT`` (default 0) so a restarted job can run clean.
 * :func:`check_finite` — cross-rank divergence / NaN guard (one all-reduce of a flag).
 """
@@ -55,6 +56,10 @@ def maybe_inject(step: int) -> bool:
     if kind == "hang":
         while True:
             time.sleep(60)
+    if kind == "comm_hang":
+        while True:  # alive to the heartbeat watchdog, silent to the collectives
+            heartbeat(step)
+            time.sleep(0.5)
     if kind == "nan":
         return True
     raise ValueError(f"unknown fault kind {kind!r}")

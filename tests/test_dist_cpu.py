@@ -406,19 +406,92 @@ def _native_zero_vs_dp(optim, clip):
         tr.sync_master()
         out[z] = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
         if z:
-            nbytes, shard = tr.zero.bytes_per_step, tr.zero.m.numel()
+            nbytes, shard, coll = tr.zero.bytes_per_step, tr.zero.m.numel(), tr.zero.coll
     ddist.destroy()
     rel = ((out[0] - out[1]).norm() / out[0].norm()).item()
-    return torch.equal(out[0], out[1]), rel, nbytes, shard, out[0].numel()
+    return torch.equal(out[0], out[1]), rel, nbytes, shard, out[0].numel(), coll
 
 
-@pytest.mark.parametrize("world,optim,clip", [(2, "sgd", 0.0), (2, "adamw", 0.3), (4, "adamw", 0.0)])
+@pytest.mark.parametrize("world,optim,clip", [(1, "adamw", 0.3), (2, "sgd", 0.0), (2, "adamw", 0.3),
+                                              (4, "adamw", 0.0)])
 def test_native_zero1_matches_dp(world, optim, clip):
-    equal, rel, nbytes, shard, n = Launcher(world, use_gpu=False).run(_native_zero_vs_dp, optim, clip)
-    if world == 2:  # a two-term fp32 sum does not depend on the collective's reduction order
+    # world 1: a one-rank process group with the segmented multi-rank path forced (the one-GPU
+    # rehearsal configuration): the reduce-scatter / all-gather exchange runs as identities
+    env = {"DBX_FORCE_PG": "1", "DBX_SEGMENTED_GRAPHS": "1"} if world == 1 else None
+    equal, rel, nbytes, shard, n, coll = Launcher(world, use_gpu=False, env=env).run(_native_zero_vs_dp, optim, clip)
+    assert coll
+    if world <= 2:  # a two-term fp32 sum does not depend on the collective's reduction order
         assert equal, f"ZeRO-1 parameters differ from data parallel (rel {rel})"
     else:  # reduce-scatter vs all-reduce may sum the 4 ranks in another order: last-bit differences
         assert rel < 1e-6, rel
     assert shard <= n // world + 16 * world * 6  # optimizer state is sharded
     # reduce-scatter fp32 + all-gather bf16: ~ (w-1)/w * 6 bytes per parameter (DDP all-reduce alone: 8)
-    assert nbytes < (world - 1) / world * 6.2 * n
+    assert nbytes < (world - 1) / world * 6.2 * n or world == 1
+
+
+def _comm_hang_train(ckpt_dir):
+    """train() with checkpoints; rank 1 stops issuing collectives at step 3 (epoch 2) on the first
+    attempt. The comm watchdog (or the bounded c10d timeout) must end rank 0, the launcher restarts
+    the job, and the second attempt resumes from the epoch-1 checkpoint."""
+    from dbx_distributed_pytorch_examples_amd.config import TrainConfig
+    from dbx_distributed_pytorch_examples_amd.data.datasets import SyntheticImages
+    from dbx_distributed_pytorch_examples_amd.train.engine import train
+    cfg = TrainConfig(model="tiny", num_classes=5, batch_size=4, epochs=2, log_every=0, checkpoint_dir=ckpt_dir,
+                      engine="autograd")
+    cfg.optim.lr = 0.01
+    cfg.data.num_workers = 0
+    torch.manual_seed(0)
+    res = train(cfg, model=TinyNet(), train_dataset=SyntheticImages(16, 8, 3, 5, seed=1,
+                                                                     transform=_to_tensor), log_mlflow=False)
+    return int(os.environ["DBX_RESTART_COUNT"]), res.resumed_epoch, res.steps, len(res.history)
+
+
+def _to_tensor(img):
+    import numpy as np
+    return torch.from_numpy(np.array(img)).permute(2, 0, 1).float() / 255
+
+
+def test_comm_hang_is_aborted_and_job_resumes(tmp_path):
+    import time
+    t = time.time()
+    out = Launcher(2, use_gpu=False, max_restarts=1, heartbeat_timeout=120,
+                   env={"DBX_FAULT": "1:3:comm_hang", "DBX_COMM_TIMEOUT": "5"}).run(
+        _comm_hang_train, str(tmp_path))
+    restarts, resumed_epoch, steps, hist = out
+    assert restarts == 1 and resumed_epoch == 1 and steps == 4 and hist == 2, out
+    assert time.time() - t < 90  # detected within the 5 s bound, not the 30 min default
+
+
+def test_comm_watchdog_unit():
+    """CommWatchdog.check: an RCCL async error or an over-age step is reported; fire() aborts the
+    communicators and exits with EXIT_COMM_FAILURE."""
+    from dbx_distributed_pytorch_examples_amd.parallel.comm_guard import EXIT_COMM_FAILURE, CommWatchdog
+
+    class FakeComm:
+        def __init__(self):
+            self.code, self.aborted = 0, False
+
+        def async_error(self):
+            return self.code, "remote process exited" if self.code else ""
+
+        def abort(self):
+            self.aborted = True
+    exits = []
+    c = FakeComm()
+    wd = CommWatchdog(timeout_s=0.3, poll_s=0.05, comms=[c], exit_fn=exits.append)
+    wd.step_begin(0)
+    wd.step_end()
+    assert wd.check() is None
+    c.code = 6  # ncclRemoteError
+    import time
+    for _ in range(100):
+        if exits:
+            break
+        time.sleep(0.05)
+    assert exits == [EXIT_COMM_FAILURE] and c.aborted and "async error 6" in wd.fired
+    wd2 = CommWatchdog(timeout_s=0.2, poll_s=10, comms=[], exit_fn=exits.append)
+    wd2.step_begin(7)
+    time.sleep(0.3)
+    assert "step 7" in wd2.check()
+    wd.close()
+    wd2.close()

@@ -43,13 +43,22 @@ def test_dist_check_gloo_two_ranks_one_gpu():
     assert "dist_gpu_check OK: world=2 backend=gloo" in r.stdout
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_dist_check_rccl(world):
+@pytest.mark.parametrize("comm", ["torch", "native"])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_dist_check_rccl(world, comm):
+    """DP gradient == sum of per-rank gradients, graph == eager, ZeRO-1 == DP over RCCL, through
+    c10d (comm=torch) or the framework communicator + one-graph step (comm=native). World 1 is
+    the one-GPU rehearsal (one-rank RCCL group, segmented multi-rank path forced): every RCCL-only
+    branch -- c10d reduce_scatter_tensor / all_gather_into_tensor in parallel/zero.py included --
+    runs there."""
     if _ndev() < world:
         pytest.skip(f"RCCL world {world} needs {world} GPUs ({_ndev()} visible)")
-    r = _launch(world, "tools/dist_gpu_check.py")
+    env = {"DBX_COMM": comm}
+    if world == 1:
+        env.update({"DBX_FORCE_PG": "1", "DBX_SEGMENTED_GRAPHS": "1"})
+    r = _launch(world, "tools/dist_gpu_check.py", env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert f"dist_gpu_check OK: world={world} backend=nccl" in r.stdout
+    assert f"dist_gpu_check OK: world={world} backend=nccl comm={comm}" in r.stdout
 
 
 def _bench_line(stdout: str) -> dict:

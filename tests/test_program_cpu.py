@@ -143,6 +143,33 @@ def test_frozen_backbone_native_features_and_head_step():
     assert all(torch.equal(a, b) for a, b in zip(backbone_before, after))
 
 
+def test_frozen_native_head_params_changed_on_resume():
+    """A resume rewrites the fp32 head master through load_state_dict after the trainer exists:
+    params_changed() refreshes the native head's bf16 compute copy, so evaluation uses the loaded
+    weights (the copy was made once, at construction)."""
+    from dbx_distributed_pytorch_examples_amd.config import OptimizerConfig
+    from dbx_distributed_pytorch_examples_amd.engine.frozen_trainer import FrozenFeatureTrainer
+    from dbx_distributed_pytorch_examples_amd.models import FrozenBackboneClassifier
+    torch.manual_seed(0)
+    m = FrozenBackboneClassifier("resnet18", num_classes=5)
+    tr = FrozenFeatureTrainer(m, 4, (32, 32), torch.device("cpu"), OptimizerConfig(name="adam", lr=1e-2))
+    assert tr.nhead is not None
+    g = torch.Generator().manual_seed(1)
+    img = torch.randint(0, 256, (4, 32, 32, 3), dtype=torch.uint8, generator=g)
+    lab = torch.randint(0, 5, (4,), generator=g)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    for k in sd:
+        if k.startswith("resnet.fc") and sd[k].is_floating_point():
+            sd[k] = torch.randn_like(sd[k])
+    m.load_state_dict(sd)
+    tr.params_changed()
+    feats = tr._features(img, lab, None, None)
+    got = tr.evaluate_batch(img, lab).float()
+    m.resnet.fc.eval()
+    want = m.resnet.fc(feats.float())
+    assert torch.allclose(got, want, rtol=2e-2, atol=2e-2), (got - want).abs().max()
+
+
 @pytest.mark.parametrize("fold", [0, 1 << 40])
 def test_fused_conv3_backward_schedule(fold, monkeypatch):
     """DBX_FUSE_DW: the bottleneck conv3 backward as one op (K.conv_dwfused) gives the gradients of

@@ -10,6 +10,12 @@ Checks (all on the segmented-graph + comm-stream path that world > 1 takes):
      eager path bit for bit;
   3. ZeRO-1 (reduce-scatter + sharded update + bf16 all-gather) matches plain data parallel.
   python -m dbx_distributed_pytorch_examples_amd.launch --nproc-per-node 2 tools/dist_gpu_check.py
+
+World 1 (the one-GPU RCCL rehearsal): ``DBX_FORCE_PG=1 DBX_SEGMENTED_GRAPHS=1`` under the launcher
+creates a one-rank RCCL group and forces the segmented multi-rank path, so every RCCL-only branch
+(c10d reduce_scatter_tensor / all_gather_into_tensor in parallel/zero.py, the comm-stream bucket
+all-reduces, with DBX_COMM=native the framework communicator and the one-graph step) executes;
+the checks hold bit-exactly (every collective is an identity).
 """
 import os
 import sys
@@ -42,6 +48,10 @@ def run(use_graphs, zero=0, steps=4, bucket_mb=1.0, pg=None, optim="sgd"):
     opt = OptimConfig(lr=0.05) if optim == "sgd" else OptimConfig(name="adamw", lr=1e-3, weight_decay=0.01)
     tr = NativeTrainer(m, B, (32, 32), info.device, optim=opt, use_graphs=use_graphs,
                        bucket_cap_mb=bucket_mb, zero_stage=zero, process_group=pg)
+    if COMM == "native" and pg is None and info.device.type == "cuda" and info.backend == "nccl":
+        assert tr.ncomm is not None, "DBX_COMM=native did not create the framework communicator"
+    if zero:
+        assert tr.zero.coll, "ZeRO did not take the collective (reduce-scatter / all-gather) path"
     for img, lab in batches(steps):
         tr.step(img, lab)
     tr.sync_master()  # ZeRO: every rank updated only its shard of the fp32 master
@@ -57,8 +67,10 @@ def params(tr):
 
 info = ddist.init_distributed()
 W = info.world_size
-assert W >= 2, info
-exact = W == 2
+assert W >= 2 or (dist.is_initialized() and os.environ.get("DBX_SEGMENTED_GRAPHS") == "1"), \
+    f"{info}: world 1 needs DBX_FORCE_PG=1 DBX_SEGMENTED_GRAPHS=1 (under the launcher)"
+exact = W <= 2
+COMM = os.environ.get("DBX_COMM", "torch")
 
 # 1. DP gradient == sum of per-rank single-process gradients (one step, eager)
 singles = [dist.new_group([r]) for r in range(W)]
@@ -102,6 +114,6 @@ for optim in ("sgd", "adamw"):
     relz[optim] = ((w_zero - w_dp).norm() / w_dp.norm()).item()
     assert (relz[optim] == 0.0) if exact else (relz[optim] < 1e-6), f"ZeRO-1 vs DP mismatch ({optim}) {relz[optim]}"
 if info.rank == 0:
-    print(f"dist_gpu_check OK: world={W} backend={info.backend} loss={loss:.3f} grad-vs-sum={relg:.2e} "
+    print(f"dist_gpu_check OK: world={W} backend={info.backend} comm={COMM} loss={loss:.3f} grad-vs-sum={relg:.2e} "
           f"graph-vs-eager={rel:.2e} zero1-vs-dp sgd={relz['sgd']:.2e} adamw={relz['adamw']:.2e}", flush=True)
 ddist.destroy()
