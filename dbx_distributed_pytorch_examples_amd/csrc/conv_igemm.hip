@@ -27,12 +27,15 @@ namespace dbx {
 // then resets the counter. The host enables it only when a tile's partials are small (the reducer
 // reads nsplit x BM x BN x 4 bytes alone).
 template <int BM, int BN, int WM, int WN, int TM, int TN>
-__device__ __forceinline__ void wgrad_store(const WgradArgs& a, const f32x4 (&acc)[TM][TN], const int split,
+__device__ __forceinline__ void wgrad_store(const WgradArgs& a, f32x4 (&acc)[TM][TN], const int split,
                                             const int tile, const int k0, const int kk0, bf16* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
   if (a.dw != nullptr && a.nsplit == 1) {  // uniform: the finished gradient straight from the tile
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      // one accumulator row at a time: without the fence the compiler hoists every dw load of the
+      // accumulate path ahead of the stores (TM x TN x 4 more live registers: spills at 256 x 256)
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -44,6 +47,7 @@ __device__ __forceinline__ void wgrad_store(const WgradArgs& a, const f32x4 (&ac
           if (a.accumulate) v += a.dw[e];
           a.dw[e] = v;
         }
+    }
     return;
   }
   if (a.dw == nullptr) {  // slab for the separate reduce kernel: ws[split][k][kk]
@@ -82,7 +86,7 @@ __device__ __forceinline__ void wgrad_store(const WgradArgs& a, const f32x4 (&ac
   }
   __syncthreads();
   if (!flag[0]) return;  // block-uniform
-  f32x4 s[TM][TN];
+  f32x4 (&s)[TM][TN] = acc;  // the partials are stored: reuse the accumulator registers for the sum
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -107,6 +111,7 @@ __device__ __forceinline__ void wgrad_store(const WgradArgs& a, const f32x4 (&ac
         float v = s[i][j][r] * a.scale;
         if (a.accumulate) v += a.dw[e];
         a.dw[e] = v;
+        asm volatile("" ::: "memory");
       }
   if (tid == 0) __hip_atomic_store((gu32*)(a.cnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -347,10 +352,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_kernel(const WgradArgs 
 // NBUF-deep ring: block kb+NBUF-1 is issued while block kb is computed; at the top of each step
 // the wave waits until only the younger blocks' DMAs are in flight, then one barrier publishes
 // every wave's part of block kb and retires the buffer the next issue overwrites.
-template <int BM, int BN, int WM, int WN, int NBUF>
-__global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_dma_kernel(const WgradArgs a) {
+// BKM: pixels per ring slot (64, or 32 for the 256 x 256 tile: its 4-slot ring keeps three 32-pixel
+// stages in flight in 128 KiB, one barrier per stage). The 256 x 256 tile runs 2 x 4 waves of 128 x 64
+// (8 x 4 MFMA tiles: 0.375 fragment reads per MFMA instead of 0.5, half the staged bytes per FLOP of
+// 256 x 128) at one workgroup per CU with the whole register file.
+template <int BM, int BN, int WM, int WN, int NBUF, int BKM = 64>
+__global__ __launch_bounds__(64 * WM * WN, (BM * BN >= 256 * 256) ? 1 : 2) void wgrad_dma_kernel(const WgradArgs a) {
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
-  constexpr int BKM = 64;
+  static_assert(BKM == 32 || BKM == 64, "pixels per stage");
   constexpr int NCA = BM / 8, NCB = BN / 8;
   constexpr int DA = BKM * NCA / NT, DB = BKM * NCB / NT;  // DMA instructions per wave and block
   constexpr int ND = DA + DB;
@@ -432,18 +441,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_dma_kernel(const WgradA
     const bf16* cA = lds + s * IMG;
     const bf16* cB = cA + BKM * BM;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[TM], bfr[TN];
+    for (int ks = 0; ks < BKM / 32; ++ks) {
       const int row = ks * 32 + 8 * g + q, row2 = row + 4;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
+      auto frag_a = [&](int i) __attribute__((always_inline)) {
         const int col = wm * (BM / WM) + i * 16 + 4 * p;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (DBX_LDS s16x4*)(cA + row * BM + (tr_swz(row, col >> 3, NCA) << 3) + (col & 7)));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (DBX_LDS s16x4*)(cA + row2 * BM + (tr_swz(row2, col >> 3, NCA) << 3) + (col & 7)));
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      };
+      bf16x8 bfr[TN];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = wn * (BN / WN) + j * 16 + 4 * p;
@@ -453,11 +461,32 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void wgrad_dma_kernel(const WgradA
             (DBX_LDS s16x4*)(cB + row2 * BN + (tr_swz(row2, col >> 3, NCB) << 3) + (col & 7)));
         bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
+      if constexpr (BM * BN >= 256 * 256) {
+        // 128 accumulators per lane: A fragments two at a time (register budget), the MFMA bursts at
+        // raised priority ahead of the sibling wave's fragment reads and DMA issue
+        bf16x8 a0 = frag_a(0), a1 = frag_a(1);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; i += 2) {
+          const bf16x8 c0 = a0, c1 = a1;
+          if (i + 2 < TM) { a0 = frag_a(i + 2); a1 = frag_a(i + 3); }
+          __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c0, bfr[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i + 1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c1, bfr[j], acc[i + 1][j], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+      } else {
+        bf16x8 af[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = frag_a(i);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     }
   };
 
@@ -620,14 +649,24 @@ static void launch_wgrad_t(const WgradArgs& a, int nblk, hipStream_t st, unsigne
   hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, FWD, PRO, DEPTH>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
 }
 
+// dma: 2 / 3 = 64-pixel stages in a 2- / 3-slot ring; 4 = 32-pixel stages in a 4-slot ring (the
+// 256 x 256 tile's deep ring in 128 KiB)
 template <int BM, int BN>
-static void launch_wgrad_dma_t(const WgradArgs& a, int nblk, hipStream_t st, unsigned lds_pad, int nbuf) {
-  constexpr int WM = (BM == 256) ? 4 : 2;
+static void launch_wgrad_dma_t(const WgradArgs& a, int nblk, hipStream_t st, unsigned lds_pad, int dma) {
+  constexpr bool BIG = BM == 256 && BN == 256;  // 2 x 4 waves of 128 x 64
+  constexpr int WM = BIG ? 2 : (BM == 256) ? 4 : 2;
   constexpr int WN = (BN == 256) ? 4 : 2;
-  if (nbuf == 2)
-    hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 2>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
-  else
-    hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 3>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
+  if constexpr (BIG) {
+    if (dma == 4)
+      hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 4, 32>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
+    else
+      hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 2, 64>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
+  } else {
+    if (dma == 2)
+      hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 2>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
+    else
+      hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 3>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
+  }
 }
 
 // lds_pad: extra dynamic LDS per workgroup (bytes) -- an occupancy cap, so that a weight gradient
@@ -652,8 +691,15 @@ extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, i
     const char* e = getenv("DBX_WGRAD_DMA");
     return e ? atoi(e) : -1;
   }();
-  const int dreq = dma_req >= 0 ? dma_req : dma_env >= 0 ? dma_env : ((bm == 256 || bn == 256) ? 3 : 2);
-  const int dma = (dreq == 2 || dreq == 3) ? dreq : 0;
+  const int dreq = dma_req >= 0 ? dma_req : dma_env >= 0 ? dma_env : (bm == 256 && bn == 256) ? 4
+                   : ((bm == 256 || bn == 256) ? 3 : 2);
+  int dma = (dreq == 2 || dreq == 3 || dreq == 4) ? dreq : 0;
+  if (bm == 256 && bn == 256) {
+    if (pro) return -3;      // the 256 x 256 tile is LDS-DMA only (no register-staged prologue variant)
+    if (dma == 0) dma = 4;
+  } else if (dma == 4) {
+    dma = 3;
+  }
 #define WG(BM_, BN_)                                                                             \
   if (bm == BM_ && bn == BN_) {                                                                  \
     if (pro) launch_wgrad_t<BM_, BN_, true>(a, nblk, st, lds_pad);                               \
@@ -667,6 +713,10 @@ extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, i
   WG(64, 64)
   WG(256, 128)
   WG(128, 256)
+  if (bm == 256 && bn == 256) {
+    launch_wgrad_dma_t<256, 256>(a, nblk, st, lds_pad, dma);
+    return (int)hipGetLastError();
+  }
 #undef WG
   return -3;
 }

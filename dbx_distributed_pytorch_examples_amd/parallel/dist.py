@@ -80,7 +80,7 @@ def init_distributed(backend: Optional[str] = None, device: Optional[str] = None
         # which is how the multi-rank GPU path is exercised on a single-GPU box
         backend = os.environ.get("DBX_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     # DBX_FORCE_PG=1 (under a launcher) creates the process group even at world 1: a one-GPU box
-    # can then rehearse the RCCL code path (tools/gpu/archive/gpu_rccl_rehearsal.sh)
+    # can then rehearse the RCCL code path (tools/dist_gpu_check.py at world 1, tests/test_multirank_gpu.py)
     force_pg = os.environ.get("DBX_FORCE_PG", "0") == "1" and "MASTER_PORT" in os.environ
     if world > 1 or force_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

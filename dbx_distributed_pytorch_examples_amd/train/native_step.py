@@ -68,7 +68,13 @@ def _mds_step(args, info, tr):
     from ..data.mds import MDSWriter, StreamingDataset
     from ..parallel import dist as ddist
     s, B = args.image_size, args.batch
-    n = args.mds_samples or max(8 * B, (args.steps + args.warmup + 2) * B)
+    # a fixed pool (the loader re-iterates epochs): 8 batches per rank, not (steps + warmup) batches
+    n = args.mds_samples or 8 * B
+    free = shutil.disk_usage(tempfile.gettempdir()).free
+    est = n * (s * s * 3 + 64)  # zstd of random pixels does not compress
+    if est * info.local_world_size > 0.8 * free:
+        raise SystemExit(f"--data mds: ~{est * info.local_world_size / 2**30:.1f} GiB of shards would not fit the "
+                         f"{free / 2**30:.1f} GiB free under {tempfile.gettempdir()} (set TMPDIR or --mds-samples)")
     root = ddist.broadcast_object(tempfile.mkdtemp(prefix="dbx_bench_mds_") if info.rank == 0 else None)
     part = os.path.join(root, f"part{info.rank}")
     rng = np.random.default_rng(100 + info.rank)

@@ -33,7 +33,7 @@ import torch
 _ROCTX = None
 _ROCTX_TRIED = False
 
-# counter groups that fit one pass each (rocprofv3 --pmc); see tools/gpu/archive/gpu_pmc.sh
+# counter groups that fit one pass each (rocprofv3 --pmc); see tools/gpu/pmc_step.sh
 PMC_GROUPS = {
     "mfma": ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_MFMA",
              "SQ_INSTS_LDS"],

@@ -451,6 +451,31 @@ def test_conv_wgrad_split(shape):
             assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2, (tile, dma)
 
 
+@pytest.mark.parametrize("shape", [(8, 28, 28, 256, 512, 1, 2, 0), (4, 14, 14, 256, 256, 3, 1, 1),
+                                   (16, 14, 14, 256, 1024, 1, 1, 0), (8, 7, 7, 512, 512, 3, 1, 1)])
+@pytest.mark.parametrize("dma", [4, 2])
+@pytest.mark.parametrize("rounds", [0.0, 1.0, 4.0])
+def test_conv_wgrad_256x256(shape, dma, rounds):
+    """The 256 x 256 weight-gradient tile (2 x 4 waves of 128 x 64; dma 4: 32-pixel stages in a
+    4-slot LDS-DMA ring, dma 2: 64-pixel stages in 2 slots) against fp32, unsplit (written straight
+    to dW), split with the separate reduce, and split with the in-launch reduction (tile counters)."""
+    k = K()
+    N, H, W, IC, OC, R, st, pad = shape
+    torch.manual_seed(9)
+    x = torch.randn(N, H, W, IC, device=dev).bfloat16()
+    OH, OW = k.conv_out_hw(H, W, R, R, st, pad)
+    dy = torch.randn(N, OH, OW, OC, device=dev).bfloat16()
+    dw = torch.empty(OC, R * R * IC, device=dev)
+    ws = torch.empty(64 * 1024 * 1024, device=dev)
+    ref = torch.nn.grad.conv2d_weight(nchw(x.float()), (OC, IC, R, R), nchw(dy.float()), stride=st, padding=pad)
+    for cnt in (None, torch.zeros(k.wgrad_tiles_max(OC, R * R * IC), dtype=torch.int32, device=dev)):
+        dw.fill_(float("nan"))
+        k.conv_wgrad(dy, x, dw, ws, R=R, S=R, stride=st, pad=pad, tile=(256, 256), dma=dma, rounds=rounds, cnt=cnt)
+        assert relerr(dw.view(OC, R, R, IC), ref.permute(0, 2, 3, 1)) < 1e-2, (dma, rounds, cnt is not None)
+        if cnt is not None:
+            assert int(cnt.abs().sum()) == 0  # counters reset for the next launch
+
+
 def test_stem_wgrad_split():
     k = K()
     N, H, W = 8, 64, 64

@@ -70,3 +70,33 @@ def test_native_mnist_trains():
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < 0.5 * losses[0], losses[::10]
+
+
+def test_native_mnist_two_forwards_and_accumulation():
+    """Torch autograd semantics: two training forwards, then their backwards, give the sum of the
+    two single-step gradients (each forward keeps its own saved activations; the second backward
+    adds into the un-zeroed gradients)."""
+    from dbx_distributed_pytorch_examples_amd.engine.native_mnist import NativeMNIST
+    torch.manual_seed(4)
+    nm = NativeMNIST(Net(), torch.device("cuda")).train()
+    xa, xb = torch.randn(16, 1, 28, 28, device="cuda"), torch.randn(8, 1, 28, 28, device="cuda")
+    ya, yb = torch.randint(0, 10, (16,), device="cuda"), torch.randint(0, 10, (8,), device="cuda")
+
+    def grads():
+        return torch.cat([p.grad.reshape(-1).clone() for p in nm.parameters()])
+
+    s0, o0 = nm._seed, nm._offset
+    F.nll_loss(nm(xa), ya).backward()
+    ga = grads()
+    for p in nm.parameters():
+        p.grad = None
+    F.nll_loss(nm(xb), yb).backward()
+    gb = grads()
+    for p in nm.parameters():
+        p.grad = None
+    nm._offset = o0  # the same dropout streams as above
+    la = F.nll_loss(nm(xa), ya)
+    lb = F.nll_loss(nm(xb), yb)  # second forward before the first backward
+    la.backward()
+    lb.backward()  # accumulates
+    assert torch.allclose(grads(), ga + gb, rtol=1e-5, atol=1e-6)

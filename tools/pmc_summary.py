@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise per-kernel PMC counters from rocprofv3 ``--pmc`` passes (tools/gpu/archive/gpu_pmc_step.sh).
+"""Summarise per-kernel PMC counters from rocprofv3 ``--pmc`` passes (tools/gpu/pmc_step.sh).
 
   python tools/pmc_summary.py gpurun_out/pmc_step [--top 40]
 
