@@ -97,16 +97,21 @@ class NativeTrainer:
                                             and dist.is_available() and dist.is_initialized())
         self.comm_stream = (torch.cuda.Stream(device=device, priority=-1)
                             if self.segmented and device.type == "cuda" else None)
-        if self.segmented and os.environ.get("DBX_OVERLAP_WGRAD") is None:
-            # Next to the comm stream and RCCL's own stream, the wgrad side stream costs more than
-            # it overlaps: measured over a world-1 RCCL process group on one MI355X (ResNet-50
-            # b1024, 2 interleaved rounds) segmented step 14.03k / 14.06k img/s with the side
-            # stream vs 14.43k / 14.40k without; the plain single graph is 14.53-14.56k either way
-            # (profiles/r2s2_multirank/). Weight gradients then run in order on the main stream.
+        # Weight gradients next to the per-segment collectives. The batched side stream (one fork per
+        # backward segment, joined one segment later: DBX_OVERLAP_WGRAD=2, the world-1 default) stays
+        # on with LATE posts: segment k's gradient range is final only after segment k+1 joins it, so
+        # its all-reduce / reduce-scatter is issued after phase k+1 (the last phase posts the last two
+        # ranges). DBX_SEG_SIDE=0 restores the round-3 layout: weight gradients in order on the main
+        # stream and every range posted right after its own phase (per-gradient forks next to the
+        # comm stream cost more than they overlapped: profiles/r2s2_multirank/).
+        seg_side = os.environ.get("DBX_SEG_SIDE", "1") == "1"
+        if self.segmented and os.environ.get("DBX_OVERLAP_WGRAD") is None and not seg_side:
             self.prog.overlap_wgrad = False
-        if self.segmented:
-            # per-segment all-reduces need each segment's weight gradients final at its end: no batched
-            # side stream (it joins a segment late)
+        self.late_posts = bool(self.segmented and device.type == "cuda" and self.prog.overlap_wgrad
+                               and self.prog.side_batch)
+        if self.segmented and not self.late_posts:
+            # per-segment collectives right after their own phase need each segment's weight gradients
+            # final at its end: no batched side stream (it joins a segment late)
             self.prog.side_batch = False
         # DBX_COMM=native: the DP bucket all-reduces go through the framework's own RCCL communicator
         # (parallel/comm.py) on the comm stream, and the whole step -- backward segments, forked
@@ -170,7 +175,13 @@ class NativeTrainer:
         phases.append(("fwd+" + first_name, lambda: (fwd_phase(), first_fn()), self.seg_ranges[0]))
         for (name, fn), rg in zip(segs[1:], self.seg_ranges[1:]):
             phases.append((name, fn, rg))
-        if self.segmented:
+        if self.segmented and self.late_posts:
+            # batched side stream: phase k completes segment k-1's weight gradients (see __init__)
+            rgs = [ph[2] for ph in phases]
+            shifted = [None] + rgs[:-1]
+            shifted[-1] = [r for r in (rgs[-2], rgs[-1]) if r is not None] if len(rgs) > 1 else rgs[-1]
+            phases = [(n, fn, post) for (n, fn, _), post in zip(phases, shifted)]
+        elif self.segmented:
             phases = self._merge_phases(phases)
         z = self.zero
         # ZeRO + clipping with collectives: the shard's sum of squares is all-reduced between phases
@@ -266,6 +277,9 @@ class NativeTrainer:
             return
         if callable(post):
             post()
+        elif isinstance(post, list):  # late posts: several gradient ranges after one phase
+            for rg in post:
+                self._post(rg)
         elif self.zero is not None:
             self.zero.reduce_range(*post)
         else:

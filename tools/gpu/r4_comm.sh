@@ -15,10 +15,11 @@ for p in resnet18_cifar10 resnet50_tiny_imagenet headline; do
   args="--steps 30 --warmup 10 --preset $p"; [ $p = headline ] && args="--steps 15 --warmup 5"
   timeout -k 10 300 python bench.py $args > $O/${p}_plain.log 2>&1 || { tail -20 $O/${p}_plain.log; exit 1; }
   echo "$p plain: $(grep -o '"value": [0-9.]*' $O/${p}_plain.log)"
-  for c in torch native; do
+  for c in torch native torch_noside; do
     port=$((port + 1))
-    DBX_FORCE_PG=1 DBX_SEGMENTED_GRAPHS=1 DBX_COMM=$c timeout -k 10 300 $L --master-port $port bench.py --gpus 1 $args \
-      > $O/${p}_seg_$c.log 2>&1 || { tail -20 $O/${p}_seg_$c.log; exit 1; }
+    side=1; cm=$c; [ $c = torch_noside ] && { side=0; cm=torch; }
+    DBX_FORCE_PG=1 DBX_SEGMENTED_GRAPHS=1 DBX_COMM=$cm DBX_SEG_SIDE=$side timeout -k 10 300 $L --master-port $port \
+      bench.py --gpus 1 $args > $O/${p}_seg_$c.log 2>&1 || { tail -20 $O/${p}_seg_$c.log; exit 1; }
     echo "$p segmented comm=$c: $(grep -o '"value": [0-9.]*' $O/${p}_seg_$c.log)"
   done
 done
