@@ -474,7 +474,53 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // BN-apply (+ReLU) prologue on the staged A chunks. Kept apart from load_a so the global loads
   // of block kb+1 stay in flight across block kb's MFMAs (the transform waits on the data).
   auto pro_a = [&](int S) __attribute__((always_inline)) {
-    if constexpr (PRO && MODE != STEM) {
+    if constexpr (TAIL && MODE != STEM) {
+      // TAIL: four affine vectors per channel; transformed one 4-channel half at a time, in place
+      // (the half's result replaces the half's raw dwords), so 16 instead of 32 coefficient
+      // registers are live next to the two staged sets: the 128 x 128 / 256 x 128 tail variants
+      // spilled inside the K loop with all eight vectors resident
+      const int c0 = pcb[S] + ach * 8;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 ps = *reinterpret_cast<const f32x4*>(sPro + c0 + 4 * h);
+        const f32x4 ph = *reinterpret_cast<const f32x4*>(sPro + PRO_MAXC + c0 + 4 * h);
+        const f32x4 pr = *reinterpret_cast<const f32x4*>(sPro + 2 * PRO_MAXC + c0 + 4 * h);
+        const f32x4 pq = *reinterpret_cast<const f32x4*>(sPro + 3 * PRO_MAXC + c0 + 4 * h);
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) {
+          float f[4], g[4];
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const unsigned xv = ra[S][i][2 * h + d], rv = rr[S][i][2 * h + d];
+            f[2 * d] = __uint_as_float(xv << 16); f[2 * d + 1] = __uint_as_float(xv & 0xFFFF0000u);
+            g[2 * d] = __uint_as_float(rv << 16); g[2 * d + 1] = __uint_as_float(rv & 0xFFFF0000u);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f[j] = f[j] * ps[j] + ph[j];
+            f[j] += g[j] * pr[j] + pq[j];  // + shortcut (identity: rs = 1, rh = 0), as bn_apply computes it
+          }
+          ra[S][i][2 * h] = pack2(f[0], f[1]);
+          ra[S][i][2 * h + 1] = pack2(f[2], f[3]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        u32x4 t = ra[S][i];
+        if constexpr (MODE != DGRAD) t = relu_bf16x8(t);  // forward PRO implies ReLU (host-checked)
+        const bool vi = (avalid[S] >> i) & 1u;
+        ra[S][i] = vi ? t : zero4;  // padding taps stay exactly zero
+        // block output + 1-bit mask (bit j: element j > 0) written back by the first N tile
+        const unsigned off = (wlive[S] && vi) ? apix[i] + wtoff[S] : kOOB;
+        buf_store16(toutr, off, t);
+        if constexpr (MODE == DGRAD) continue;
+        unsigned bits = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          bits |= (((t[q] & 0xFFFFu) ? 1u : 0u) << (2 * q)) | (((t[q] >> 16) ? 1u : 0u) << (2 * q + 1));
+        buf_store8(tbitr, off == kOOB ? kOOB : (off >> 4), (unsigned char)bits);
+      }
+    } else if constexpr (PRO && MODE != STEM) {
       const int c0 = pcb[S] + ach * 8;  // this thread's 8 channels (the same for all its rows)
       const f32x4 ps0 = *reinterpret_cast<const f32x4*>(sPro + c0);
       const f32x4 ps1 = *reinterpret_cast<const f32x4*>(sPro + c0 + 4);
