@@ -23,13 +23,30 @@
 
 namespace dbx {
 
-template <int BN, int MODE, bool STATS, bool ACCUM, int EPI, int NBUF>
+// LDS image swizzle of a [rows][BK] bf16 stage: the 16-B chunk ch of row `row` sits at chunk
+// position ch ^ fswz(row). BK = 64 (128-B rows): (row >> 1) & 7. BK = 32 (64-B rows, four rows per
+// 256-B bank window): chunk bit 1 flipped for rows 8-15 of every 16 -- each ds_read_b128 lane group
+// (rows 0-3 / 12-15 at one chunk, rows 4-11 at the next) then covers 16 distinct 16-B slots of the
+// window: conflict-free (the same check as tools/lds_banks.py, by hand: the four row quads map to
+// chunk xors 0, 0, 2, 2, so {c, c^2, c^1, c^3} are distinct for every c).
+template <int BK>
+__device__ __forceinline__ int fswz(int row) {
+  return BK == 64 ? ((row >> 1) & 7) : (((row >> 3) & 1) << 1);
+}
+
+// BK: channels per ring stage -- 64 (NBUF 2 / 3), or 32 for the deep ring: with the 256 x 256 tile
+// a 4-slot ring of 32-channel stages keeps three stages (3 x 1024 MFMA cycles per SIMD) in flight in
+// the 128 KiB two 64-channel slots took (cdna_hip_programming.md §5, the 256^2 template's half-tile
+// prefetch).
+template <int BN, int MODE, bool STATS, bool ACCUM, int EPI, int NBUF, int BK = 64>
 __global__ __launch_bounds__(512, 1) void fast_igemm_kernel(const IGemmArgs a) {
-  constexpr int BM = 256, BK = 64, NT = 512, NW = 8;
+  constexpr int BM = 256, NT = 512, NW = 8;
   constexpr int WM = BN == 256 ? 2 : 4, WN = NW / WM;
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
-  constexpr int RPP = NT / 8;          // tile rows per DMA pass (8 lanes x 16 B per 64-wide row)
+  constexpr int CPR = BK / 8;          // 16-B chunks per tile row
+  constexpr int RPP = NT / CPR;        // tile rows per DMA pass (CPR lanes x 16 B per row)
   constexpr int A_CH = BM / RPP, B_CH = BN / RPP;
+  static_assert(BK == 64 || BK == 32, "stage depth");
   constexpr int ND = A_CH + B_CH;      // DMA instructions per wave and K block
   constexpr int LDS_AB = NBUF * (BM + BN) * BK;
   constexpr int LDS_EP = BM * (BN + 8) + 2 * (3 * NW * BN);
@@ -47,13 +64,13 @@ __global__ __launch_bounds__(512, 1) void fast_igemm_kernel(const IGemmArgs a) {
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- A rows of this thread's DMA lanes: decompose the output pixel once -------------------
-  const int ach = tid & 7;
-  const int lch = ach ^ ((tid >> 4) & 7);  // LDS position (row, ach) receives chunk lch (swizzle)
+  const int ach = tid & (CPR - 1);
+  const int lch = ach ^ fswz<BK>(tid / CPR);  // LDS position (row, ach) receives chunk lch (swizzle; RPP % 16 == 0)
   int ahb[A_CH], awb[A_CH];
   unsigned apix[A_CH];
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
-    const int m = m0 + (tid >> 3) + RPP * i;
+    const int m = m0 + tid / CPR + RPP * i;
     const int ohw = a.OH * a.OW;
     int n = mdiv_or(m, a.mag_ohw, ohw);
     const int pq = m - n * ohw;
@@ -89,7 +106,7 @@ __global__ __launch_bounds__(512, 1) void fast_igemm_kernel(const IGemmArgs a) {
     const unsigned db = lds0 + 2u * (unsigned)(NBUF * BM * BK + slot * BN * BK) + 1024u * (unsigned)wid;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      const int n = n0 + (tid >> 3) + RPP * i;
+      const int n = n0 + tid / CPR + RPP * i;
       lds_dma16(wsrd, live ? 2u * (unsigned)(n * KTOT + koff) : kOOB, db + 1024u * (unsigned)(NW * i));
     }
     ++lk;
@@ -102,9 +119,9 @@ __global__ __launch_bounds__(512, 1) void fast_igemm_kernel(const IGemmArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment reads of one K block from ring slot `slot`: both k32 steps up front (FS = 2), or one
-  // set reused per k step (FS = 1, fewer registers)
-  constexpr int FS = 2;
+  // fragment reads of one stage from ring slot `slot`: both k32 steps of a 64-channel stage up front
+  // (FS = 2), the one step of a 32-channel stage (FS = 1)
+  constexpr int FS = BK / 32;
   bf16x8 fa[FS][TM], fb[FS][TN];
   auto read_frags = [&](int slot, int ks0, int nks) __attribute__((always_inline)) {
     const bf16* cA = sA + slot * BM * BK;
@@ -116,12 +133,12 @@ __global__ __launch_bounds__(512, 1) void fast_igemm_kernel(const IGemmArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * (BN / WN) + j * 16 + (lane & 15);
-        fb[ks][j] = *reinterpret_cast<const bf16x8*>(cB + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
+        fb[ks][j] = *reinterpret_cast<const bf16x8*>(cB + row * BK + ((ch ^ fswz<BK>(row)) << 3));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * (BM / WM) + i * 16 + (lane & 15);
-        fa[ks][i] = *reinterpret_cast<const bf16x8*>(cA + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
+        fa[ks][i] = *reinterpret_cast<const bf16x8*>(cA + row * BK + ((ch ^ fswz<BK>(row)) << 3));
       }
     }
   };
@@ -147,16 +164,9 @@ __global__ __launch_bounds__(512, 1) void fast_igemm_kernel(const IGemmArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     issue(cur == 0 ? NBUF - 1 : cur - 1);
-    if constexpr (FS == 2) {
-      read_frags(cur, 0, 2);
-      mma_step(0);
-      mma_step(1);
-    } else {
-      read_frags(cur, 0, 1);
-      mma_step(0);
-      read_frags(cur, 1, 1);
-      mma_step(1);
-    }
+    read_frags(cur, 0, FS);
+#pragma unroll
+    for (int kq = 0; kq < FS; ++kq) mma_step(kq);
     cur = cur + 1 == NBUF ? 0 : cur + 1;
   }
   dma_wait<0>();  // no DMA may still write the LDS the epilogue stages through
@@ -169,11 +179,19 @@ __global__ __launch_bounds__(512, 1) void fast_igemm_kernel(const IGemmArgs a) {
 
 using namespace dbx;
 
+// DBX_FAST_STAGE=32: the deep ring of 32-channel stages (4 slots at BN 256, 6 at BN 128) instead of
+// 64-channel stages (2 / 3 slots); A/B switch, read at each launch (graph capture records the choice)
 template <int BN, int MODE, bool STATS, bool ACCUM, int EPI>
 static int launch_fast(const IGemmArgs& a, hipStream_t st) {
-  constexpr int NBUF = BN == 256 ? 2 : 3;
+  const char* e = getenv("DBX_FAST_STAGE");
+  const bool deep = e && atoi(e) == 32;
   const int ntile = (a.OC / BN) * ((a.M + 255) / 256);
-  hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, NBUF>), dim3(ntile), dim3(512), 0, st, a);
+  if (deep)
+    hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, BN == 256 ? 4 : 6, 32>), dim3(ntile), dim3(512),
+                       0, st, a);
+  else
+    hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, BN == 256 ? 2 : 3, 64>), dim3(ntile),
+                       dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -1,14 +1,11 @@
 #!/bin/bash
-# Round 4: the world-1 RCCL rehearsal of every RCCL-only branch (c10d and framework communicator,
-# DP and ZeRO-1), then the segmented multi-rank step vs the single-graph step on the three presets:
-# plain (no process group) | segmented c10d (DBX_COMM=torch) | one-graph framework comm (DBX_COMM=native).
+# The multi-rank step (world-1 RCCL group, segmented path forced) vs the single graph on the three
+# presets: plain | segmented c10d (late posts + side stream) | one-graph framework comm | segmented
+# c10d without the side stream (round-3 layout).
 set -o pipefail
 O=${1:-gpurun_out/r4_comm}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_multirank_gpu.py tests/test_comm_gpu.py -x -v --timeout 300 \
-  --timeout-method thread -k "dist_check_rccl or comm" > $O/pytest_rccl.log 2>&1
-rc=$?; tail -15 $O/pytest_rccl.log; [ $rc = 0 ] || exit $rc
 L="python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1"
 port=29640
 for p in resnet18_cifar10 resnet50_tiny_imagenet headline; do
