@@ -23,17 +23,6 @@
 
 namespace dbx {
 
-// LDS image swizzle of a [rows][BK] bf16 stage: the 16-B chunk ch of row `row` sits at chunk
-// position ch ^ fswz(row). BK = 64 (128-B rows): (row >> 1) & 7. BK = 32 (64-B rows, four rows per
-// 256-B bank window): chunk bit 1 flipped for rows 8-15 of every 16 -- each ds_read_b128 lane group
-// (rows 0-3 / 12-15 at one chunk, rows 4-11 at the next) then covers 16 distinct 16-B slots of the
-// window: conflict-free (the same check as tools/lds_banks.py, by hand: the four row quads map to
-// chunk xors 0, 0, 2, 2, so {c, c^2, c^1, c^3} are distinct for every c).
-template <int BK>
-__device__ __forceinline__ int fswz(int row) {
-  return BK == 64 ? ((row >> 1) & 7) : (((row >> 3) & 1) << 1);
-}
-
 // BK: channels per ring stage -- 64 (NBUF 2 / 3), or 32 for the deep ring: with the 256 x 256 tile
 // a 4-slot ring of 32-channel stages keeps three stages (3 x 1024 MFMA cycles per SIMD) in flight in
 // the 128 KiB two 64-channel slots took (cdna_hip_programming.md §5, the 256^2 template's half-tile

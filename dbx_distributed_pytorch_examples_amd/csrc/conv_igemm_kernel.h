@@ -36,6 +36,17 @@ namespace dbx {
 
 enum ConvMode { FWD = 0, DGRAD = 1, STEM = 2, FWD_PATCH = 3, DGRAD_PATCH = 4 };
 
+// LDS image swizzle of a [rows][BK] bf16 operand stage: the 16-B chunk ch of row `row` sits at chunk
+// position ch ^ fswz<BK>(row). BK = 64 (128-B rows): (row >> 1) & 7. BK = 32 (64-B rows, four rows
+// per 256-B bank window): chunk bit 1 flipped for rows 8-15 of every 16 -- each ds_read_b128 lane
+// group (rows 0-3 and 12-15 at one chunk, rows 4-11 at the next) then covers 16 distinct 16-B slots
+// of the window: conflict-free (the four row quads map to chunk xors 0, 0, 2, 2, so {c, c^2, c^1,
+// c^3} are distinct for every c).
+template <int BK>
+__device__ __forceinline__ int fswz(int row) {
+  return BK == 64 ? ((row >> 1) & 7) : (((row >> 3) & 1) << 1);
+}
+
 
 // ---- epilogue (shared by igemm_kernel and the 3x3 patch kernel) ---------------------------------
 // acc: this wave's (BM/WM) x (BN/WN) accumulators of the tile starting at output row m0 / channel n0;
@@ -314,18 +325,22 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x4 (&acc)[
 // prologue). A DMA wave-instruction fills 8 tile rows x 128 B; the XOR swizzle moves to the
 // source side (LDS position (row, slot) receives chunk slot ^ ((row >> 1) & 7) of that row), so
 // the fragment reads are unchanged. The DMA variants run one tile per workgroup (no persistence).
+// DMA 4: both operands by LDS-DMA in 32-channel stages through a 4-slot ring -- the LDS of the
+// 2-slot 64-channel ring (two workgroups per CU stay resident) with three stages instead of one in
+// flight behind the MFMAs of the current stage.
 template <int BM, int BN, int WM, int WN, int MODE, bool PRO, bool STATS, bool ACCUM, int EPI, bool TAIL = false,
           int DMA = 0>
 __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs a) {
   static_assert(DMA == 0 || (MODE != STEM && (DMA == 1 || (!PRO && !TAIL))), "DMA operand path");
   constexpr int NT = 64 * WM * WN;        // threads; WM x WN waves, each owns a (BM/WM) x (BN/WN) tile
   constexpr int NW = WM * WN;
-  constexpr int BK = 64;
-  constexpr int RPP = NT / 8;             // tile rows covered per staging pass (8 x 16B per 64-wide row)
+  constexpr int BK = DMA == 4 ? 32 : 64;  // channels per K block (stage)
+  constexpr int CPR = BK / 8;             // 16-B chunks per tile row
+  constexpr int RPP = NT / CPR;           // tile rows covered per staging pass
   constexpr int A_CH = BM * BK / 8 / NT;  // 16-byte chunks per thread (A)
   constexpr int B_CH = BN * BK / 8 / NT;
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);  // 16x16 MFMA tiles per wave
-  constexpr int NBUF = DMA == 3 ? 3 : 2;      // LDS operand buffers (ring slots)
+  constexpr int NBUF = DMA == 3 ? 3 : DMA == 4 ? 4 : 2;  // LDS operand buffers (ring slots)
   constexpr int LDS_AB = NBUF * (BM + BN) * BK;  // bf16 elements
   constexpr int LDS_C = BM * (BN + 8);
   constexpr int LDS_RED = 2 * (3 * NW * BN);  // fp32 reduction scratch (in bf16 units)
@@ -350,10 +365,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   int lk = 0, lcb = 0, lts = 0, ltr = 0;  // next K block to load (see advance())
 
   // ---- per-thread A rows: decompose output pixel once per tile ---------------------
-  const int ach = tid & 7;
-  // LDS-DMA: the chunk this lane fetches for each of its rows (row = tid/8 + RPP*i: RPP is a
-  // multiple of 16, so the swizzle term (row >> 1) & 7 is the same for all i)
-  const int lch = ach ^ ((tid >> 4) & 7);
+  const int ach = tid & (CPR - 1);
+  // LDS-DMA: the chunk this lane fetches for each of its rows (row = tid/CPR + RPP*i: RPP is a
+  // multiple of 16, so the swizzle term is the same for all i)
+  const int lch = ach ^ fswz<BK>(tid / CPR);
   const int acha = DMA >= 2 ? lch : ach;  // A chunk loaded by this thread
   const bf16* abase[A_CH];   // STEM mode: image base
   int ahb[A_CH], awb[A_CH];  // top-left input coordinate of the row's receptive field
@@ -365,7 +380,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     lk = lcb = lts = ltr = 0;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      const int m = lm0 + (tid >> 3) + RPP * i;
+      const int m = lm0 + tid / CPR + RPP * i;
       const int ohw = a.OH * a.OW;
       int n = mdiv_or(m, a.mag_ohw, ohw);
       const int pq = m - n * ohw;
@@ -579,7 +594,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     const bool live = lk < KB;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      const int n = ln0 + (tid >> 3) + RPP * i;
+      const int n = ln0 + tid / CPR + RPP * i;
       DBX_DCHECK(!live || (n < a.OC && koff + 8 <= KTOT));
       rb[S][i] = buf_load16(wr, live ? 2u * (unsigned)(n * KTOT + koff) : kOOB);
     }
@@ -587,16 +602,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   auto store_a = [&](int buf, int S) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      const int row = (tid >> 3) + RPP * i;
-      *reinterpret_cast<u32x4*>(sA + buf * BM * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = ra[S][i];
+      const int row = tid / CPR + RPP * i;
+      *reinterpret_cast<u32x4*>(sA + buf * BM * BK + row * BK + ((ach ^ fswz<BK>(row)) << 3)) = ra[S][i];
     }
   };
   auto store_ab = [&](int buf, int S) __attribute__((always_inline)) {
     store_a(buf, S);
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      const int row = (tid >> 3) + RPP * i;
-      *reinterpret_cast<u32x4*>(sB + buf * BN * BK + row * BK + ((ach ^ ((row >> 1) & 7)) << 3)) = rb[S][i];
+      const int row = tid / CPR + RPP * i;
+      *reinterpret_cast<u32x4*>(sB + buf * BN * BK + row * BK + ((ach ^ fswz<BK>(row)) << 3)) = rb[S][i];
     }
   };
   // ---- LDS-DMA operand path (DMA > 0) ----
@@ -613,7 +628,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     const unsigned dst = lds0 + 2u * (unsigned)(NBUF * BM * BK + buf * BN * BK) + 1024u * (unsigned)wid;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      const int n = ln0 + (tid >> 3) + RPP * i;
+      const int n = ln0 + tid / CPR + RPP * i;
       lds_dma16(wsrd, live ? 2u * (unsigned)(n * KTOT + koff) : kOOB, dst + 1024u * (unsigned)(NW * i));
     }
     ++bk;
@@ -640,18 +655,18 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     const bf16* cA = sA + buf * BM * BK;
     const bf16* cB = sB + buf * BN * BK;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 af[TM], bfr[TN];
       const int ch = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * (BM / WM) + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(cA + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
+        af[i] = *reinterpret_cast<const bf16x8*>(cA + row * BK + ((ch ^ fswz<BK>(row)) << 3));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * (BN / WN) + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(cB + row * BK + ((ch ^ ((row >> 1) & 7)) << 3));
+        bfr[j] = *reinterpret_cast<const bf16x8*>(cB + row * BK + ((ch ^ fswz<BK>(row)) << 3));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -825,8 +840,10 @@ static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
 // plain operands -> DMA 0, 2 or 3 (ring depth; a request of 1 means 2)
 #define DBX_DMA_PRO(CALL, ...) \
   return dma ? CALL<__VA_ARGS__, 1>(a, st) : CALL<__VA_ARGS__, 0>(a, st)
+// (tile code 6 = the 4-slot ring of 32-channel stages, kernel DMA 4)
 #define DBX_DMA_PLAIN(CALL, ...)                         \
-  return dma == 3 ? CALL<__VA_ARGS__, 3>(a, st)          \
+  return dma == 6 ? CALL<__VA_ARGS__, 4>(a, st)          \
+         : dma == 3 ? CALL<__VA_ARGS__, 3>(a, st)        \
          : dma ? CALL<__VA_ARGS__, 2>(a, st) : CALL<__VA_ARGS__, 0>(a, st)
 
 }  // namespace dbx

@@ -184,7 +184,8 @@ def _fast_enabled() -> bool:
 def _tile_dma(t) -> Tuple[int, int, int]:
     """(bm, bn[, dma]) -> (bm, bn, dma). ``dma`` is the conv operand path (conv_igemm_kernel.h):
     0 register-staged, 1 weights by LDS-DMA (prologue convs), 2 / 3 both operands by LDS-DMA
-    through a 2- / 3-slot ring. DBX_CONV_DMA overrides every choice (A/B runs)."""
+    through a 2- / 3-slot ring of 64-channel stages, 6 through a 4-slot ring of 32-channel stages
+    (4 / 5: the eight-wave kernel). DBX_CONV_DMA overrides every choice (A/B runs)."""
     global _DMA_ENV
     if _DMA_ENV is None:
         import os

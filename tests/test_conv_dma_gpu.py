@@ -46,7 +46,7 @@ def test_fwd_dma_bit_exact(case, prologue):
     sc = sh = None
     if prologue:
         sc, sh = torch.rand(IC, device=dev) + 0.5, torch.randn(IC, device=dev) * 0.1
-    dmas = (1,) if prologue else (2, 3)
+    dmas = (1,) if prologue else (2, 3, 6)  # 6: 4-slot ring of 32-channel stages
 
     def run(tile, dma):
         y = torch.full((N, OH, OW, OC), float("nan"), device=dev, dtype=torch.bfloat16)
@@ -107,7 +107,7 @@ def test_dgrad_dma_bit_exact(case, variant):
         if variant == "epi1_add" and st > 1:
             continue  # (a full-resolution addend with a strided dgrad is not a ResNet pattern)
         base = run(tile, 0)
-        for dma in (2, 3):
+        for dma in (2, 3, 6):
             _same(base, run(tile, dma), (tile, dma, variant))
 
 

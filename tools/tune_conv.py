@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 from dbx_distributed_pytorch_examples_amd.ops import kernels as K  # noqa: E402
 
 TILES = [(128, 128), (128, 64), (64, 64), (256, 128), (128, 256), (256, 64)]
-WGRAD_TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (256, 128), (128, 256)]
+WGRAD_TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (256, 128), (128, 256), (256, 256)]
 
 
 def convs_of(model_name, image, num_classes=1000):
@@ -159,10 +159,13 @@ def main():
                     128 if Kc % 128 == 0 else 64, 128 if C % 128 == 0 else 64, 2)
                 cands = [base + (float(r),) for r in a.wgrad_rounds.split(",")]
             elif mode == "wgrad":  # tile x operand path (LDS-DMA ring depth 3 / 2, 0 = register staged)
-                cands = [t + (d,) for t in WGRAD_TILES if Kc % t[0] == 0 and C % t[1] == 0 for d in (3, 2, 0)]
-            else:  # tile x operand path: prologue convs 0 / 1 (weights by DMA), plain 0 / 2 / 3 (ring)
+                # (256 x 256: LDS-DMA only -- 4 = 32-pixel stages in a 4-slot ring, 2 = 64-pixel stages)
+                cands = [t + (d,) for t in WGRAD_TILES if Kc % t[0] == 0 and C % t[1] == 0
+                         for d in ((4, 2) if t == (256, 256) else (3, 2, 0))]
+            else:  # tile x operand path: prologue convs 0 / 1 (weights by DMA), plain 0 / 2 / 3 (ring) /
+                # 6 (4-slot ring of 32-channel stages)
                 pro = mode in ("fwdt", "dgrad1b", "dgrad2b") or (mode == "fwd" and psc is not None)
-                dmas = ((0, 1) if pro else (0, 2, 3)) if a.dma else (0,)
+                dmas = ((0, 1) if pro else (0, 2, 3, 6)) if a.dma else (0,)
                 cands = [t + (d,) for t in TILES if OCm % t[1] == 0 for d in dmas]
             res = {t: [] for t in cands}
             for _ in range(a.rounds):
