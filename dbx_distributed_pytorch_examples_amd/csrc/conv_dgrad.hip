@@ -6,7 +6,7 @@ using namespace dbx;
 template <int BM, int BN>
 static int dispatch_dgrad(const IGemmArgs& a, bool accum, int epi, int dma, hipStream_t st) {
   if (a.res) {  // BN-backward apply prologue (1x1 stride-1 dgrads of the bottleneck)
-    constexpr int TM = (BM == 128 && BN == 256) ? 256 : BM, TN = (BM == 128 && BN == 256) ? 128 : BN;
+    constexpr int TM = BM, TN = BN;  // (128 x 256 fits since the half-split tail prologue: no remap)
     if (accum) {
       if (epi == 1) DBX_DMA_PRO(launch_igemm_t, TM, TN, DGRAD, true, false, true, 1, true);
       if (epi == 0) DBX_DMA_PRO(launch_igemm_t, TM, TN, DGRAD, true, false, true, 0, true);

@@ -582,8 +582,10 @@ extern "C" int dbx_stem_patch(const IGemmArgs* args, int stats, hipStream_t st);
 template <int BM, int BN>
 static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, int dma, hipStream_t st) {
   if (a.res) {
-    // the staged shortcut chunks push the 128x256 tile past 256 VGPRs: same-area 256x128 instead
-    constexpr int TM = (BM == 128 && BN == 256) ? 256 : BM, TN = (BM == 128 && BN == 256) ? 128 : BN;
+    // 128 x 256 runs as itself: the half-split tail prologue fits it in 256 VGPRs without spills (it
+    // was remapped to the same-area 256 x 128 before: one N tile covers a 256-channel conv1, so the
+    // shortcut / BN3 operands are read and transformed once instead of twice)
+    constexpr int TM = BM, TN = BN;
     if (stats) DBX_DMA_PRO(launch_igemm_t, TM, TN, FWD, true, true, false, 0, true);
     DBX_DMA_PRO(launch_igemm_t, TM, TN, FWD, true, false, false, 0, true);
   }
