@@ -652,11 +652,13 @@ def test_conv_fwd_tail_prologue(case, tile):
 
 @pytest.mark.parametrize("tile", [(64, 64), (128, 64), (128, 128), (256, 64), (256, 128), (128, 256)])
 @pytest.mark.parametrize("variant", ["epi2", "epi1_acc", "acc", "plain"])
-def test_dgrad_bwd_apply_prologue(variant, tile):
+@pytest.mark.parametrize("cc", [128, 256])
+def test_dgrad_bwd_apply_prologue(variant, tile, cc):
     """1x1 dgrad whose operand is the BN-backward apply k1*g + k2*y + k3 computed while staging ==
-    bn_bwd_apply followed by the plain dgrad (same epilogue); the applied operand is stored."""
+    bn_bwd_apply followed by the plain dgrad (same epilogue); the applied operand is stored.
+    (cc 256: the 128 x 256 tile covers every output channel in one N tile)"""
     k = K()
-    N, H, W, Kc, Cc = 2, 14, 14, 256, 128
+    N, H, W, Kc, Cc = 2, 14, 14, 256, cc
     if Cc % tile[1]:
         pytest.skip("tile wider than C")
     torch.manual_seed(31)
