@@ -16,7 +16,7 @@ timeout -k 10 400 python -u tools/bench_wgrad_big.py --batch 1024 --rounds 3 > $
 rc=$?; cut -c1-330 $O/bench_wgrad_big.txt; [ $rc = 0 ] || exit $rc
 T=dbx_distributed_pytorch_examples_amd/ops/tune_table.json
 cp $T $O/tune_table.json
-timeout -k 10 400 python -u tools/tune_conv.py --batch 1024 --rounds 3 --iters 3 --modes dgrad0,dgrad1,dgrad2,fwd \
+timeout -k 10 400 python -u tools/tune_conv.py --batch 1024 --rounds 3 --iters 3 --modes dgrad0,dgrad1,dgrad2,fwd,fwdt,dgrad1b,dgrad2b \
   --out $O/tune_table.json --report $O/tune_plain.md > $O/tune_plain.log 2>&1 || { tail -20 $O/tune_plain.log; exit 1; }
 DBX_FAST_STAGE=32 timeout -k 10 300 python -u tools/tune_conv.py --batch 1024 --rounds 3 --iters 3 --fast 0.03 \
   --modes fwd0,dgrad1,dgrad2 --out $O/tune_table.json --report $O/tune_fast32.md > $O/tune_fast32.log 2>&1 \
