@@ -97,22 +97,6 @@ class NativeTrainer:
                                             and dist.is_available() and dist.is_initialized())
         self.comm_stream = (torch.cuda.Stream(device=device, priority=-1)
                             if self.segmented and device.type == "cuda" else None)
-        # Weight gradients next to the per-segment collectives. The batched side stream (one fork per
-        # backward segment, joined one segment later: DBX_OVERLAP_WGRAD=2, the world-1 default) stays
-        # on with LATE posts: segment k's gradient range is final only after segment k+1 joins it, so
-        # its all-reduce / reduce-scatter is issued after phase k+1 (the last phase posts the last two
-        # ranges). DBX_SEG_SIDE=0 restores the round-3 layout: weight gradients in order on the main
-        # stream and every range posted right after its own phase (per-gradient forks next to the
-        # comm stream cost more than they overlapped: profiles/r2s2_multirank/).
-        seg_side = os.environ.get("DBX_SEG_SIDE", "1") == "1"
-        if self.segmented and os.environ.get("DBX_OVERLAP_WGRAD") is None and not seg_side:
-            self.prog.overlap_wgrad = False
-        self.late_posts = bool(self.segmented and device.type == "cuda" and self.prog.overlap_wgrad
-                               and self.prog.side_batch)
-        if self.segmented and not self.late_posts:
-            # per-segment collectives right after their own phase need each segment's weight gradients
-            # final at its end: no batched side stream (it joins a segment late)
-            self.prog.side_batch = False
         # DBX_COMM=native: the DP bucket all-reduces go through the framework's own RCCL communicator
         # (parallel/comm.py) on the comm stream, and the whole step -- backward segments, forked
         # all-reduces, join, optimizer -- is captured as ONE graph instead of per-segment graphs
@@ -122,6 +106,25 @@ class NativeTrainer:
             from ..parallel.comm import NativeComm, native_comm_available, native_comm_requested
             if native_comm_requested() and native_comm_available():
                 self.ncomm = NativeComm(process_group, device)
+        # Weight gradients next to the per-segment collectives. In the ONE-graph step (framework
+        # communicator) the batched side stream (one fork per backward segment, joined one segment
+        # later: DBX_OVERLAP_WGRAD=2, the world-1 default) stays on with LATE posts: segment k's
+        # gradient range is final only after segment k+1 joins it, so its all-reduce / reduce-scatter
+        # is issued after phase k+1 (the last phase posts the last two ranges). Per-segment graphs
+        # (c10d collectives between replays) cannot carry a fork across a graph boundary (a capture
+        # must end joined), so there -- and with DBX_SEG_SIDE=0 -- the round-3 layout stays: weight
+        # gradients in order on the main stream, every range posted right after its own phase
+        # (per-gradient forks next to the comm stream cost more than they overlapped:
+        # profiles/r2s2_multirank/).
+        seg_side = os.environ.get("DBX_SEG_SIDE", "1") == "1" and (self.ncomm is not None or not self.use_graphs)
+        if self.segmented and os.environ.get("DBX_OVERLAP_WGRAD") is None and not seg_side:
+            self.prog.overlap_wgrad = False
+        self.late_posts = bool(self.segmented and device.type == "cuda" and seg_side and self.prog.overlap_wgrad
+                               and self.prog.side_batch)
+        if self.segmented and not self.late_posts:
+            # per-segment collectives right after their own phase need each segment's weight gradients
+            # final at its end: no batched side stream (it joins a segment late)
+            self.prog.side_batch = False
         self.flip = None
         self.seg_ranges = self._segment_ranges()
         self.zero = None
