@@ -42,7 +42,10 @@ def build_native_step(args, info):
     return step, {**extra, "memory_format": "nhwc", "graphs": use_graphs,
                   "ddp": (f"flat-bucket {'RCCL' if info.backend == 'nccl' else info.backend} all-reduce, "
                           f"{tr.bucket_cap * 4 >> 20} MiB chunks, "
-                          f"{str(ar_dtype).split('.')[-1]}, overlapped per backward segment") if tr.world > 1 else "none",
+                          f"{str(ar_dtype).split('.')[-1]}, overlapped per backward segment"
+                          + (" (framework RCCL communicator, whole step one HIP graph, weight-gradient side stream "
+                             "with late posts)" if tr.ncomm is not None else " (c10d between per-segment graphs)"))
+                  if tr.world > 1 else "none",
                   "kernels": "dbx HIP (conv implicit-GEMM MFMA + fused BN/ReLU/pool/CE/SGD)"}
 
 
