@@ -599,6 +599,7 @@ static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, int dma, hipSt
 
 
 extern "C" int dbx_conv_fast(int mode, int bn, const IGemmArgs* args, int stats, int accum, int epi, hipStream_t st);
+extern "C" int dbx_conv_rowtile(int mode, const IGemmArgs* args, int stats, int accum, int epi, hipStream_t st);
 
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
                               int accum, int epi, hipStream_t st, int dma) {
@@ -606,6 +607,10 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
   if (dma == 4) {  // eight-wave 256-row kernel (conv_fast.hip): plain operands, stride-1 data gradients
     if (bm != 256 || pro || mode == STEM || (mode == DGRAD && (a.osub != 1 || a.add_sub > 1))) return -65;
     return dbx_conv_fast(mode, bn, args, stats, accum, epi, st);
+  }
+  if (dma == 7) {  // row-tile kernel (conv_rowtile.hip): 1x1 stride-1 BN-prologue forwards / folded dgrads
+    if (mode != FWD && mode != DGRAD) return -70;
+    return dbx_conv_rowtile(mode, args, stats, accum, epi, st);
   }
   if (mode == FWD_PATCH || mode == DGRAD_PATCH) {  // 3x3 weights-stationary patch kernel (conv_patch3.hip)
     if (pro && !a.relu_in) return -7;

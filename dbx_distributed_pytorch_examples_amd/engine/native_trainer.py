@@ -101,10 +101,10 @@ class NativeTrainer:
         # (parallel/comm.py) on the comm stream, and the whole step -- backward segments, forked
         # all-reduces, join, optimizer -- is captured as ONE graph instead of per-segment graphs
         # with eager c10d collectives between replays (ZeRO's reduce-scatter / all-gather included)
-        # (RCCL process groups only: under gloo -- several ranks sharing one GPU in the one-box tests --
-        # an RCCL communicator would refuse the duplicate device)
+        # (RCCL process groups, or a one-rank group: under gloo several ranks share one GPU in the
+        # one-box tests, and an RCCL communicator would refuse the duplicate device)
         self.ncomm = None
-        if self.segmented and device.type == "cuda" and dist.get_backend(process_group) == "nccl":
+        if self.segmented and device.type == "cuda" and (self.world == 1 or dist.get_backend(process_group) == "nccl"):
             from ..parallel.comm import NativeComm, native_comm_available, native_comm_requested
             if native_comm_requested() and native_comm_available():
                 self.ncomm = NativeComm(process_group, device)

@@ -185,7 +185,8 @@ def _tile_dma(t) -> Tuple[int, int, int]:
     """(bm, bn[, dma]) -> (bm, bn, dma). ``dma`` is the conv operand path (conv_igemm_kernel.h):
     0 register-staged, 1 weights by LDS-DMA (prologue convs), 2 / 3 both operands by LDS-DMA
     through a 2- / 3-slot ring of 64-channel stages, 6 through a 4-slot ring of 32-channel stages
-    (4 / 5: the eight-wave kernel). DBX_CONV_DMA overrides every choice (A/B runs)."""
+    (4 / 5: the eight-wave kernel; 7: the row-tile kernel of 1x1 stride-1 BN-prologue forwards and
+    folded dgrads, csrc/conv_rowtile.hip -- bm / bn are its own). DBX_CONV_DMA overrides every choice (A/B runs)."""
     global _DMA_ENV
     if _DMA_ENV is None:
         import os

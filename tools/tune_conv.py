@@ -162,11 +162,13 @@ def main():
                 # (256 x 256: LDS-DMA only -- 4 = 32-pixel stages in a 4-slot ring, 2 = 64-pixel stages)
                 cands = [t + (d,) for t in WGRAD_TILES if Kc % t[0] == 0 and C % t[1] == 0
                          for d in ((4, 2) if t == (256, 256) else (3, 2, 0))]
-            else:  # tile x operand path: prologue convs 0 / 1 (weights by DMA), plain 0 / 2 / 3 (ring) /
-                # 6 (4-slot ring of 32-channel stages)
+            else:  # tile x operand path: prologue convs 0 / 1 (weights by DMA) / 7 (1x1 row tile), plain
+                # 0 / 2 / 3 (ring) / 6 (4-slot ring of 32-channel stages)
                 pro = mode in ("fwdt", "dgrad1b", "dgrad2b") or (mode == "fwd" and psc is not None)
                 dmas = ((0, 1) if pro else (0, 2, 3, 6)) if a.dma else (0,)
                 cands = [t + (d,) for t in TILES if OCm % t[1] == 0 for d in dmas]
+                if pro and a.dma and Rk == 1 and sk == 1 and Kin <= 512 and OCm % 128 == 0 and mode != "fwd0":
+                    cands.append((128, 128, 7))  # row-tile kernel (conv_rowtile.hip): A resident, weights streamed
             res = {t: [] for t in cands}
             for _ in range(a.rounds):
                 for t in cands:
