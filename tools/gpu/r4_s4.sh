@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 4: numerics of the row-tile kernel (tile code 7) and the world-1 framework-communicator test;
 # a re-tune of the BN-prologue 1x1 entries (fwd / fwdt / dgrad1b / dgrad2b) with the row tile as a
-# candidate into a COPY of the tune table; the headline with the repo table vs the copy.
+# candidate into a COPY of the tune table; the headline with the repo table vs the copy (and the copy
+# with every conv1 data gradient folded: DBX_FOLD_MAX_RATIO=8).
 set -o pipefail
 O=${1:-gpurun_out/r4_s4}
 mkdir -p $O
@@ -21,4 +22,7 @@ for r in 1 2; do
   DBX_TUNE_TABLE=$O/tune_table.json timeout -k 10 300 python bench.py --steps 20 --warmup 5 \
     > $O/headline_rt_$r.log 2>&1 || { tail -20 $O/headline_rt_$r.log; exit 1; }
   echo "headline rowtile r$r: $(grep -o '"value": [0-9.]*' $O/headline_rt_$r.log)"
+  DBX_FOLD_MAX_RATIO=8 DBX_TUNE_TABLE=$O/tune_table.json timeout -k 10 300 python bench.py --steps 20 --warmup 5 \
+    > $O/headline_rtf_$r.log 2>&1 || { tail -20 $O/headline_rtf_$r.log; exit 1; }
+  echo "headline rowtile+fold-all r$r: $(grep -o '"value": [0-9.]*' $O/headline_rtf_$r.log)"
 done
