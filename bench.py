@@ -182,7 +182,7 @@ def main(argv=None) -> int:
             "seq_len": None,
             "parallelism": f"dp{n}" + (f"+zero{args.zero}" if args.zero else ""),
             "world_size_seen": seen,
-            "backend": info.backend if n > 1 else "none",
+            "backend": info.backend,  # "none" without a process group (a world-1 run unless DBX_FORCE_PG=1)
             "impl": args.impl,
             "optimizer": {"sgd": "SGD momentum 0.9 nesterov=False wd 5e-5",
                           "lars": "LARS (eta 1e-3) + SGD momentum 0.9 wd 5e-5"}.get(args.optim, "AdamW wd 0.01")

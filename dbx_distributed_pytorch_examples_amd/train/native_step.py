@@ -45,7 +45,7 @@ def build_native_step(args, info):
                           f"{str(ar_dtype).split('.')[-1]}, overlapped per backward segment"
                           + (" (framework RCCL communicator, whole step one HIP graph, weight-gradient side stream "
                              "with late posts)" if tr.ncomm is not None else " (c10d between per-segment graphs)"))
-                  if tr.world > 1 else "none",
+                  if tr.world > 1 or getattr(tr, "segmented", False) else "none",
                   "kernels": "dbx HIP (conv implicit-GEMM MFMA + fused BN/ReLU/pool/CE/SGD)"}
 
 
