@@ -34,9 +34,9 @@ int dbx_bn_bwd_reduce(const bf16*, const bf16*, const bf16*, const float*, const
 int dbx_bn_bwd_coeff(const double*, int, int, float, const float*, const float*, const float*, float*, float*, float*,
                      int, hipStream_t);
 int dbx_bn_bwd_apply(const bf16*, const bf16*, const bf16*, const float*, const float*, const float*, bf16*, bf16*,
-                     long long, int, int, hipStream_t);
+                     long long, int, int, hipStream_t, const dbx::BnFin*);
 int dbx_bn_bwd_apply2(const bf16*, const bf16*, const float*, bf16*, const bf16*, const float*, bf16*, long long, int,
-                      hipStream_t);
+                      hipStream_t, const dbx::BnFin*, const dbx::BnFin*);
 int dbx_maxpool_fwd(const bf16*, const float*, const float*, bf16*, unsigned char*, bf16*, int, int, int, int, int,
                     int, int, int, int, int, hipStream_t);
 int dbx_maxpool_bwd(const bf16*, const unsigned char*, bf16*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -220,16 +220,17 @@ PYBIND11_MODULE(_C, m) {
           "bn_bwd_coeff");
   });
   m.def("bn_bwd_apply", [](uintptr_t dout, uintptr_t mref, uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t coeff,
-                           uintptr_t dy, uintptr_t gout, long long n, int C, int mask_mode, uintptr_t st) {
+                           uintptr_t dy, uintptr_t gout, long long n, int C, int mask_mode, uintptr_t st, uintptr_t fin) {
     check(dbx_bn_bwd_apply(P<const bf16*>(dout), P<const bf16*>(mref), P<const bf16*>(y), P<const float*>(sc),
                            P<const float*>(sh), P<const float*>(coeff), P<bf16*>(dy), P<bf16*>(gout), n, C, mask_mode,
-                           S(st)),
+                           S(st), P<const dbx::BnFin*>(fin)),
           "bn_bwd_apply");
   });
   m.def("bn_bwd_apply2", [](uintptr_t g, uintptr_t y1, uintptr_t c1, uintptr_t dy1, uintptr_t y2, uintptr_t c2,
-                            uintptr_t dy2, long long n, int C, uintptr_t st) {
+                            uintptr_t dy2, long long n, int C, uintptr_t st, uintptr_t fin1, uintptr_t fin2) {
     check(dbx_bn_bwd_apply2(P<const bf16*>(g), P<const bf16*>(y1), P<const float*>(c1), P<bf16*>(dy1),
-                            P<const bf16*>(y2), P<const float*>(c2), P<bf16*>(dy2), n, C, S(st)),
+                            P<const bf16*>(y2), P<const float*>(c2), P<bf16*>(dy2), n, C, S(st),
+                            P<const dbx::BnFin*>(fin1), P<const dbx::BnFin*>(fin2)),
           "bn_bwd_apply2");
   });
   m.def("maxpool_fwd", [](uintptr_t x, uintptr_t sc, uintptr_t sh, uintptr_t out, uintptr_t arg, uintptr_t ymax, int N,

@@ -42,16 +42,22 @@ __device__ __forceinline__ void bn_fwd_final(int c, double s, double q, float co
 }
 
 // backward: shard sums (sum g, sum g*xhat) of channel c -> dy = k1*g + k2*y + k3, dgamma, dbeta
+__device__ __forceinline__ void bn_bwd_k(double sd, double qd, float count, float g, float is, float mu, float& k1,
+                                         float& k2, float& k3) {
+#pragma clang fp contract(off)
+  const float s = (float)sd, q = (float)qd;
+  const float sg = s / count, sgx = q / count;
+  k1 = g * is;
+  k2 = -g * is * is * sgx;
+  k3 = -g * is * sg + g * is * is * sgx * mu;
+}
 __device__ __forceinline__ void bn_bwd_final(int C, int c, double sd, double qd, float count, const float* gamma,
                                              const float* mean, const float* invstd, float* coeff, float* dgamma,
                                              float* dbeta, int accumulate) {
 #pragma clang fp contract(off)
   const float s = (float)sd, q = (float)qd;
-  const float g = gamma ? gamma[c] : 1.f, is = invstd[c], mu = mean[c];
-  const float sg = s / count, sgx = q / count;
-  const float k1 = g * is;
-  const float k2 = -g * is * is * sgx;
-  const float k3 = -g * is * sg + g * is * is * sgx * mu;
+  float k1, k2, k3;
+  bn_bwd_k(sd, qd, count, gamma ? gamma[c] : 1.f, invstd[c], mean[c], k1, k2, k3);
   coeff[c] = k1; coeff[C + c] = k2; coeff[2 * C + c] = k3;
   if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + q;
   if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + s;
@@ -126,6 +132,36 @@ __device__ __forceinline__ void bn_fin_consume(const BnFin& f, int c, bool store
   double mean, var;
   float invstd;
   bn_fwd_affine(c, s, q, f.count, f.gamma, f.beta, f.eps, scale, shift, mean, var, invstd);
+}
+
+// Consumer-side backward finalize (the BN-backward apply passes, DBX_COEFF_IN): channel c's
+// coefficients k1, k2, k3 from the shards in the standalone kernel's order (plain loads: the moments
+// were completed by an earlier launch) and bn_bwd_k's arithmetic -- bit-identical to bn_bwd_coeff;
+// the storing thread also writes coeff / dgamma / dbeta (exactly one per channel and launch).
+__device__ __forceinline__ void bn_bwd_consume(const BnFin& f, int c, bool store, float& k1, float& k2, float& k3) {
+  double s = 0.0, q = 0.0;
+  for (int k0 = 0; k0 < f.nshard; k0 += 16) {
+    double sv[16], qv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = k0 + j < f.nshard ? k0 + j : k0;
+      sv[j] = f.stats[(size_t)k * 2 * f.C + c];
+      qv[j] = f.stats[(size_t)k * 2 * f.C + f.C + c];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (k0 + j < f.nshard) {
+        s += sv[j];
+        q += qv[j];
+      }
+    }
+  }
+  if (store) {
+    bn_bwd_final(f.C, c, s, q, f.count, f.gamma, f.mean, f.invstd, f.coeff, f.dgamma, f.dbeta, f.accumulate);
+    k1 = f.coeff[c]; k2 = f.coeff[f.C + c]; k3 = f.coeff[2 * f.C + c];
+    return;
+  }
+  bn_bwd_k(s, q, f.count, f.gamma ? f.gamma[c] : 1.f, f.invstd[c], f.mean[c], k1, k2, k3);
 }
 
 // End of a conv tile epilogue whose launch carries BN finalize descriptors: once every wave's

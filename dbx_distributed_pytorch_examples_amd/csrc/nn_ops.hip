@@ -230,18 +230,32 @@ __global__ void bn_bwd_coeff_kernel(const double* __restrict__ stats, int nshard
   bn_bwd_final(C, c, sd, qd, count, gamma, mean, invstd, coeff, dgamma, dbeta, accumulate);
 }
 
+// The coefficients of a thread's 8 channels: loaded (bn_bwd_coeff ran before), or (fin set,
+// DBX_COEFF_IN) finalized here from the BN's moment shards -- bit-identical; the row-0 threads of
+// block 0 store coeff / dgamma / dbeta. Saves the bn_bwd_coeff launch in front of the apply.
+__device__ __forceinline__ void bwd_coeff8(const float* coeff, const BnFin* fin, int C, int c0, bool store, float* k1,
+                                           float* k2, float* k3) {
+  if (fin == nullptr) {
+    load8f(coeff + c0, k1);
+    load8f(coeff + C + c0, k2);
+    load8f(coeff + 2 * C + c0, k3);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bn_bwd_consume(*fin, c0 + j, store, k1[j], k2[j], k3[j]);
+}
+
 template <int MASK, bool WRITE_G>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ mref,
                                     const bf16* __restrict__ y, const float* __restrict__ sc,
                                     const float* __restrict__ sh, const float* __restrict__ coeff,
-                                    bf16* __restrict__ dy, bf16* __restrict__ gout, long long M, int C) {
+                                    bf16* __restrict__ dy, bf16* __restrict__ gout, long long M, int C,
+                                    const BnFin* __restrict__ fin) {
   const RowMap rm(C);
   if (rm.r0 >= rm.rpb) return;
   const int c0 = rm.cg * 8;
   float k1[8], k2[8], k3[8], scr[8] = {0}, shr[8] = {0};
-  load8f(coeff + c0, k1);
-  load8f(coeff + C + c0, k2);
-  load8f(coeff + 2 * C + c0, k3);
+  bwd_coeff8(coeff, fin, C, c0, blockIdx.x == 0 && rm.r0 == 0, k1, k2, k3);
   if (MASK == 2) { load8f(sc + c0, scr); load8f(sh + c0, shr); }
   for (long long m = (long long)blockIdx.x * rm.rpb + rm.r0; m < M; m += (long long)gridDim.x * rm.rpb) {
     const long long e = m * C + c0;
@@ -260,17 +274,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
 __global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const bf16* __restrict__ g_in, const bf16* __restrict__ y1,
                                                             const float* __restrict__ coeff1, bf16* __restrict__ dy1,
                                                             const bf16* __restrict__ y2, const float* __restrict__ coeff2,
-                                                            bf16* __restrict__ dy2, long long M, int C) {
+                                                            bf16* __restrict__ dy2, long long M, int C,
+                                                            const BnFin* __restrict__ fin1, const BnFin* __restrict__ fin2) {
   const RowMap rm(C);
   if (rm.r0 >= rm.rpb) return;
   const int c0 = rm.cg * 8;
   float a1[8], a2[8], a3[8], b1[8], b2[8], b3[8];
-  load8f(coeff1 + c0, a1);
-  load8f(coeff1 + C + c0, a2);
-  load8f(coeff1 + 2 * C + c0, a3);
-  load8f(coeff2 + c0, b1);
-  load8f(coeff2 + C + c0, b2);
-  load8f(coeff2 + 2 * C + c0, b3);
+  const bool store = blockIdx.x == 0 && rm.r0 == 0;
+  bwd_coeff8(coeff1, fin1, C, c0, store, a1, a2, a3);
+  bwd_coeff8(coeff2, fin2, C, c0, store, b1, b2, b3);
   for (long long m = (long long)blockIdx.x * rm.rpb + rm.r0; m < M; m += (long long)gridDim.x * rm.rpb) {
     const long long e = m * C + c0;
     float g[8], u[8], v[8], o1[8], o2[8];
@@ -1034,11 +1046,11 @@ extern "C" int dbx_bn_bwd_coeff(const double* stats, int nshard, int C, float co
 }
 extern "C" int dbx_bn_bwd_apply(const bf16* dout, const bf16* mref, const bf16* y, const float* sc, const float* sh,
                                 const float* coeff, bf16* dy, bf16* gout, long long n, int C, int mask_mode,
-                                hipStream_t st) {
+                                hipStream_t st, const BnFin* fin) {
   if (n % C || C % 8 || C / 8 > 256) return -1;
   const long long M = n / C;
   const dim3 g(grid_for(M, 256 / (C / 8), 4096)), b(256);
-#define BB(MK, WG) hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, WG>), g, b, 0, st, dout, mref, y, sc, sh, coeff, dy, gout, M, C)
+#define BB(MK, WG) hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, WG>), g, b, 0, st, dout, mref, y, sc, sh, coeff, dy, gout, M, C, fin)
   if (mask_mode == 0) { if (gout) BB(0, true); else BB(0, false); }
   else if (mask_mode == 1) { if (gout) BB(1, true); else BB(1, false); }
   else { if (gout) BB(2, true); else BB(2, false); }
@@ -1046,11 +1058,12 @@ extern "C" int dbx_bn_bwd_apply(const bf16* dout, const bf16* mref, const bf16* 
   RET_LAST;
 }
 extern "C" int dbx_bn_bwd_apply2(const bf16* g, const bf16* y1, const float* c1, bf16* dy1, const bf16* y2,
-                                 const float* c2, bf16* dy2, long long n, int C, hipStream_t st) {
+                                 const float* c2, bf16* dy2, long long n, int C, hipStream_t st, const BnFin* fin1,
+                                 const BnFin* fin2) {
   if (n % C || C % 8 || C / 8 > 256) return -1;
   const long long M = n / C;
   hipLaunchKernelGGL(bn_bwd_apply2_kernel, dim3(grid_for(M, 256 / (C / 8), 4096)), dim3(256), 0, st, g, y1, c1, dy1,
-                     y2, c2, dy2, M, C);
+                     y2, c2, dy2, M, C, fin1, fin2);
   RET_LAST;
 }
 extern "C" int dbx_maxpool_fwd(const bf16* x, const float* sc, const float* sh, bf16* out, unsigned char* arg,

@@ -213,6 +213,9 @@ class ResNetProgram:
         # than the finalize launch it removes even on the launch-bound CIFAR step (212-214k vs 222k
         # img/s; TinyImageNet 87.6k vs 89.5-89.9k, profiles/r3s2_finin/)
         self.fin_in = os.environ.get("DBX_FIN_IN", "0") == "1"
+        # consumer-side backward finalize: a BN-backward apply pass computes its coefficients from the
+        # moment shards itself (K.bn_bwd_apply fin=) instead of a bn_bwd_coeff launch in front of it
+        self.coeff_in = os.environ.get("DBX_COEFF_IN", "0") == "1"
         if not self.overlap_wgrad:
             # without the side stream folding costs no overlap: fold every BN-backward apply it can
             # (unless set explicitly) -- CIFAR b256 193.7k vs 189.5k img/s with overlap (r3s2_knobs)
@@ -798,12 +801,25 @@ class ResNetProgram:
         K.small_gemm(self.dlogits, self.fc_w16, self.dpooled, ta=False, tb=True, M=N, N=F, K=Cn)
         K.avgpool_bwd(self.dpooled, self.dlast)
 
+    def _cin(self, bn, count=None) -> bool:
+        """Does ``bn``'s next BN-backward apply pass finalize the coefficients inside its launch
+        (DBX_COEFF_IN: no bn_bwd_coeff launch in front of it)?"""
+        f = bn.fin_b
+        return (self.coeff_in and f is not None and f.desc is not None
+                and (count is None or float(count) == f.count))
+
+    def _coeff(self, bn, count) -> None:
+        """The standalone backward finalize of ``bn`` (its consumer needs ``bn.coeff`` in memory)."""
+        K.bn_bwd_coeff(bn.bstats, count, bn.gamma, bn.mean, bn.invstd, bn.coeff, bn.dgamma, bn.dbeta)
+
     def _bn_bwd(self, bn: BNL, dout, y, dy, count, mask_mode, mref=None, gout=None):
         K.bn_bwd_reduce(dout, y, bn.mean, bn.invstd, bn.bstats, mask_mode=mask_mode, mref=mref,
                         scale=bn.scale, shift=bn.shift)
-        K.bn_bwd_coeff(bn.bstats, count, bn.gamma, bn.mean, bn.invstd, bn.coeff, bn.dgamma, bn.dbeta)
+        fin = bn.fin_b if self._cin(bn, count) else None
+        if fin is None:
+            self._coeff(bn, count)
         K.bn_bwd_apply(dout, y, bn.coeff, dy, mask_mode=mask_mode, mref=mref, scale=bn.scale, shift=bn.shift,
-                       gout=gout)
+                       gout=gout, fin=fin)
 
     def _bwd_block(self, i: int):
         """Backward of block i. On entry its output gradient is already masked by the block's
@@ -825,39 +841,59 @@ class ResNetProgram:
             if b.ds_conv is not None:
                 K.bn_bwd_reduce(self.dlast, b.yd, b.ds_bn.mean, b.ds_bn.invstd, b.ds_bn.bstats,
                                 mask_mode=K.MASK_OUT, mref=b.out)
-            K.bn_bwd_coeff(lbn.bstats, cnt_last, lbn.gamma, lbn.mean, lbn.invstd, lbn.coeff, lbn.dgamma, lbn.dbeta)
+            fin = lbn.fin_b if self._cin(lbn, cnt_last) else None
+            if fin is None:
+                self._coeff(lbn, cnt_last)
             K.bn_bwd_apply(self.dlast, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_OUT, mref=b.out,
-                           gout=self.g_last)
+                           gout=self.g_last, fin=fin)
             g = self.g_last
         else:
             g = self.blocks[i + 1].dx
-            if not self._fused_fin(lbn):  # (else finished by block i+1's conv1 dgrad epilogue)
-                K.bn_bwd_coeff(lbn.bstats, cnt_last, lbn.gamma, lbn.mean, lbn.invstd, lbn.coeff, lbn.dgamma,
-                               lbn.dbeta)
+        # backward finalizes still to run for the tail BNs (else finished by block i+1's conv1 dgrad
+        # epilogue): run standalone before a consumer that reads the coefficients from memory, or
+        # handed to the apply pass that consumes them (DBX_COEFF_IN)
+        todo = {} if last else ({id(lbn): (lbn, cnt_last)} if not self._fused_fin(lbn) else {})
+
+        def ready(bn):  # the coefficients are in memory before the next launch
+            if id(bn) in todo:
+                self._coeff(*todo.pop(id(bn)))
+
+        def fin_of(bn):  # the apply pass finalizes them itself (or they are ready)
+            if id(bn) in todo and self._cin(*todo[id(bn)]):
+                todo.pop(id(bn))
+                return bn.fin_b
+            ready(bn)
+            return None
+
         if b.ds_conv is not None:
             dc, dbn = b.ds_conv, b.ds_bn
             if last or not self._fused_fin(dbn):
-                K.bn_bwd_coeff(dbn.bstats, N * dc.OH * dc.OW, dbn.gamma, dbn.mean, dbn.invstd, dbn.coeff,
-                               dbn.dgamma, dbn.dbeta)
+                todo[id(dbn)] = (dbn, N * dc.OH * dc.OW)
             if last:
-                K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE)
+                K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE, fin=fin_of(dbn))
             elif (fuse3 or self._fold(lc)) and self._fold(dc, dense=True):
                 # both tail BN applies folded into the dgrads of conv3 and of the downsample conv
+                ready(lbn)
+                ready(dbn)
                 pend = dict(bwd_y=b.ys[-1], bwd_coeff=lbn.coeff, dy_out=b.dys[-1])
                 gin = g
                 ds_fold = dict(bwd_y=b.yd, bwd_coeff=dbn.coeff, dy_out=b.dyd)
             elif fuse3:  # conv3's inside the fused kernel, the downsample BN's as its own pass
-                K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE)
+                K.bn_bwd_apply(g, b.yd, dbn.coeff, b.dyd, mask_mode=K.MASK_NONE, fin=fin_of(dbn))
+                ready(lbn)
                 pend = dict(bwd_y=b.ys[-1], bwd_coeff=lbn.coeff, dy_out=b.dys[-1])
                 gin = g
             else:  # both tail BNs from one read of the block-output gradient
-                K.bn_bwd_apply2(g, b.ys[-1], lbn.coeff, b.dys[-1], b.yd, dbn.coeff, b.dyd)
+                f1, f2 = fin_of(lbn), fin_of(dbn)
+                K.bn_bwd_apply2(g, b.ys[-1], lbn.coeff, b.dys[-1], b.yd, dbn.coeff, b.dyd, fin1=f1, fin2=f2)
         elif not last:
             if fuse3 or self._fold(lc):  # folded into conv3's dgrad prologue (it stores dys[-1] for the wgrad)
+                ready(lbn)
                 pend = dict(bwd_y=b.ys[-1], bwd_coeff=lbn.coeff, dy_out=b.dys[-1])
                 gin = g
             else:
-                K.bn_bwd_apply(g, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_NONE)
+                K.bn_bwd_apply(g, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_NONE, fin=fin_of(lbn))
+        assert not todo, "a tail BN's backward finalize was left pending"
         # inner convs, last to second: dgrad epilogue masks with the previous BN's ReLU and
         # accumulates that BN's backward statistics
         for j in range(nconv - 1, 0, -1):
@@ -888,14 +924,19 @@ class ResNetProgram:
             elif kw and not pre:
                 self._wgrad(b.dys[j], b.ys[j - 1], cv.grad, self.ws, R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                             in_scale=pbn.scale, in_shift=pbn.shift, relu_in=True)
+            pcount = N * pc.OH * pc.OW
+            fold = self._fold(pc)
+            fin = None
             if kw is None or not self._fused_fin(pbn):  # (else finished by the dgrad epilogue above)
-                K.bn_bwd_coeff(pbn.bstats, N * pc.OH * pc.OW, pbn.gamma, pbn.mean, pbn.invstd, pbn.coeff,
-                               pbn.dgamma, pbn.dbeta)
-            if self._fold(pc):  # the next dgrad (conv j-1) applies it while staging
+                if not fold and self._cin(pbn, pcount):
+                    fin = pbn.fin_b  # finalized by the apply pass below
+                else:
+                    self._coeff(pbn, pcount)
+            if fold:  # the next dgrad (conv j-1) applies it while staging
                 pend = dict(bwd_y=b.ys[j - 1], bwd_coeff=pbn.coeff, dy_out=b.dys[j - 1])
                 gin = b.das[j - 1]
             else:
-                K.bn_bwd_apply(b.das[j - 1], b.ys[j - 1], pbn.coeff, b.dys[j - 1], mask_mode=K.MASK_NONE)
+                K.bn_bwd_apply(b.das[j - 1], b.ys[j - 1], pbn.coeff, b.dys[j - 1], mask_mode=K.MASK_NONE, fin=fin)
         # first conv: wgrad (after the dgrad when that stores dys[0]), then the block-input gradient
         # = dgrad(conv1) + shortcut gradient
         c0 = b.convs[0]

@@ -866,26 +866,39 @@ def bn_bwd_coeff(stats, count, gamma, mean, invstd, coeff, dgamma=None, dbeta=No
 
 
 @_dispatch
-def bn_bwd_apply(dout, y, coeff, dy, *, mask_mode, mref=None, scale=None, shift=None, gout=None):
+def bn_bwd_apply(dout, y, coeff, dy, *, mask_mode, mref=None, scale=None, shift=None, gout=None, fin=None):
+    """dy = k1*g + k2*y + k3 with g = dout masked by ``mask_mode``. ``fin`` (:class:`BnFin`, mode BWD):
+    the coefficients are finalized inside this launch from the BN's moment shards (the bn_bwd_coeff
+    launch it replaces, bit for bit; ``coeff`` / dgamma / dbeta are stored on the way)."""
     Cc = y.shape[-1]
     _chk(dy, torch.bfloat16, "dy", y.numel())
     if gout is not None:
         _chk(gout, torch.bfloat16, "gout", y.numel())
+    if fin is not None and fin.desc is None:  # (no device descriptor: the standalone launch first)
+        fin.run()
+        fin = None
     C().bn_bwd_apply(dout.data_ptr(), _p(mref), y.data_ptr(), _p(scale), _p(shift), coeff.data_ptr(),
-                     dy.data_ptr(), _p(gout), y.numel(), Cc, mask_mode, stream_ptr())
+                     dy.data_ptr(), _p(gout), y.numel(), Cc, mask_mode, stream_ptr(), fin.ptr() if fin else 0)
 
 
 @_dispatch
-def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2):
+def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2, fin1=None, fin2=None):
     """Two unmasked BN-backward applies sharing the gradient g (one read of g):
-    dy1 = k1*g + k2*y1 + k3 (coeff1), dy2 likewise with y2 / coeff2."""
+    dy1 = k1*g + k2*y1 + k3 (coeff1), dy2 likewise with y2 / coeff2; ``fin1`` / ``fin2`` as in
+    :func:`bn_bwd_apply`."""
     Cc = y1.shape[-1]
     for t, nm in ((g, "g"), (y1, "y1"), (dy1, "dy1"), (y2, "y2"), (dy2, "dy2")):
         _chk(t, torch.bfloat16, nm, y1.numel())
     _chk(coeff1, torch.float32, "coeff1", 3 * Cc)
     _chk(coeff2, torch.float32, "coeff2", 3 * Cc)
+    fins = []
+    for f in (fin1, fin2):
+        if f is not None and f.desc is None:
+            f.run()
+            f = None
+        fins.append(f.ptr() if f else 0)
     C().bn_bwd_apply2(g.data_ptr(), y1.data_ptr(), coeff1.data_ptr(), dy1.data_ptr(), y2.data_ptr(),
-                      coeff2.data_ptr(), dy2.data_ptr(), y1.numel(), Cc, stream_ptr())
+                      coeff2.data_ptr(), dy2.data_ptr(), y1.numel(), Cc, stream_ptr(), *fins)
 
 
 @_dispatch

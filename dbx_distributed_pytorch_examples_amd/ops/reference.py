@@ -244,7 +244,9 @@ def bn_bwd_coeff(stats, count, gamma, mean, invstd, coeff, dgamma=None, dbeta=No
         dbeta.copy_(s + (dbeta if accumulate else 0))
 
 
-def bn_bwd_apply(dout, y, coeff, dy, *, mask_mode, mref=None, scale=None, shift=None, gout=None):
+def bn_bwd_apply(dout, y, coeff, dy, *, mask_mode, mref=None, scale=None, shift=None, gout=None, fin=None):
+    if fin is not None:  # (the kernel finalizes the coefficients in-launch; here: the finalize first)
+        fin.run()
     C = y.shape[-1]
     g = _g(dout, y, mask_mode, mref, scale, shift)
     if gout is not None:
@@ -253,9 +255,9 @@ def bn_bwd_apply(dout, y, coeff, dy, *, mask_mode, mref=None, scale=None, shift=
     dy.copy_((k[0] * g + k[1] * y.float() + k[2]).bfloat16())
 
 
-def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2):
-    bn_bwd_apply(g, y1, coeff1, dy1, mask_mode=0)
-    bn_bwd_apply(g, y2, coeff2, dy2, mask_mode=0)
+def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2, fin1=None, fin2=None):
+    bn_bwd_apply(g, y1, coeff1, dy1, mask_mode=0, fin=fin1)
+    bn_bwd_apply(g, y2, coeff2, dy2, mask_mode=0, fin=fin2)
 
 
 def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True, ymax=None):

@@ -154,3 +154,93 @@ def test_program_consumer_fin_in_bit_identical(arch, size, batch, monkeypatch):
     for bn1, bn2 in zip(t1.prog.bns, t2.prog.bns):
         for k in ("scale", "shift", "mean", "invstd"):
             assert torch.equal(getattr(bn1, k), getattr(bn2, k)), (bn1.name, k)
+
+
+@pytest.mark.parametrize("C,mask", [(64, K.MASK_NONE), (256, K.MASK_OUT), (512, K.MASK_Y), (2048, K.MASK_NONE)])
+def test_apply_consumer_coeff_bit_identical(C, mask):
+    """The BN-backward apply pass finalizing its own coefficients from the moment shards (fin=) ==
+    bn_bwd_coeff + the apply, bit for bit: the output, coeff, dgamma and dbeta."""
+    torch.manual_seed(C)
+    M = 3000
+    g, y, mref = (torch.randn(M, C, device="cuda").bfloat16() for _ in range(3))
+    sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+    st = K.new_stats(C, "cuda")
+    st.copy_(torch.randn_like(st) * 100)
+    res = []
+    for consumer in (False, True):
+        torch.manual_seed(5)
+        mean, gamma = torch.randn(C, device="cuda"), torch.randn(C, device="cuda")
+        inv = torch.rand(C, device="cuda") + 0.5
+        coeff, dg, db = torch.zeros(3 * C, device="cuda"), torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+        fin = K.BnFin(K.BnFin.BWD, st, M, gamma=gamma, mean=mean, invstd=inv, coeff=coeff, dgamma=dg, dbeta=db)
+        dy = torch.empty_like(g)
+        gout = torch.empty_like(g)
+        kw = dict(mask_mode=mask, mref=mref if mask == K.MASK_OUT else None, scale=sc if mask == K.MASK_Y else None,
+                  shift=sh if mask == K.MASK_Y else None, gout=gout if mask != K.MASK_NONE else None)
+        if consumer:
+            K.bn_bwd_apply(g, y, coeff, dy, fin=fin, **kw)
+        else:
+            fin.run()
+            K.bn_bwd_apply(g, y, coeff, dy, **kw)
+        torch.cuda.synchronize()
+        res.append((dy, coeff, dg, db, gout))
+    for u, v in zip(*res):
+        assert torch.equal(u, v)
+
+
+def test_apply2_consumer_coeff_bit_identical():
+    torch.manual_seed(9)
+    M, C = 2000, 256
+    g, y1, y2 = (torch.randn(M, C, device="cuda").bfloat16() for _ in range(3))
+    st1, st2 = K.new_stats(C, "cuda"), K.new_stats(C, "cuda")
+    st1.copy_(torch.randn_like(st1) * 50)
+    st2.copy_(torch.randn_like(st2) * 50)
+    res = []
+    for consumer in (False, True):
+        torch.manual_seed(2)
+        fins, outs = [], []
+        for st in (st1, st2):
+            d = dict(mean=torch.randn(C, device="cuda"), gamma=torch.randn(C, device="cuda"),
+                     invstd=torch.rand(C, device="cuda") + 0.5, coeff=torch.zeros(3 * C, device="cuda"),
+                     dgamma=torch.zeros(C, device="cuda"), dbeta=torch.zeros(C, device="cuda"))
+            fins.append(K.BnFin(K.BnFin.BWD, st, M, **d))
+            outs += [d["coeff"], d["dgamma"], d["dbeta"]]
+        dy1, dy2 = torch.empty_like(g), torch.empty_like(g)
+        if consumer:
+            K.bn_bwd_apply2(g, y1, fins[0].coeff, dy1, y2, fins[1].coeff, dy2, fin1=fins[0], fin2=fins[1])
+        else:
+            fins[0].run()
+            fins[1].run()
+            K.bn_bwd_apply2(g, y1, fins[0].coeff, dy1, y2, fins[1].coeff, dy2)
+        torch.cuda.synchronize()
+        res.append([dy1, dy2] + outs)
+    for u, v in zip(*res):
+        assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64), ("cifar_resnet18", 32, 32)])
+def test_program_consumer_coeff_bit_identical(arch, size, batch, monkeypatch):
+    """Backward finalizes done by the BN-backward apply passes (DBX_COEFF_IN=1) == the standalone
+    bn_bwd_coeff launches, over eager and graph-replayed steps (weights, BN buffers, coefficients)."""
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    torch.manual_seed(0)
+    m1 = build_model(arch, num_classes=10)
+    m2 = copy.deepcopy(m1)
+    monkeypatch.setenv("DBX_COEFF_IN", "1")
+    t1 = NativeTrainer(m1, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    monkeypatch.setenv("DBX_COEFF_IN", "0")
+    t2 = NativeTrainer(m2, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    assert t1.prog.coeff_in and not t2.prog.coeff_in
+    g = torch.Generator().manual_seed(1)
+    for i in range(5):
+        img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).cuda()
+        lab = torch.randint(0, 10, (batch,), generator=g).cuda()
+        t1.step(img, lab)
+        t2.step(img, lab)
+        assert t1.read_metrics()[0] == t2.read_metrics()[0], i
+    assert torch.equal(t1.prog.master, t2.prog.master)
+    for b1, b2 in zip(m1.buffers(), m2.buffers()):
+        assert torch.equal(b1, b2)
+    for bn1, bn2 in zip(t1.prog.bns, t2.prog.bns):
+        assert torch.equal(bn1.coeff, bn2.coeff), bn1.name
