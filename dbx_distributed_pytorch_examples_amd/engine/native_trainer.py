@@ -105,9 +105,9 @@ class NativeTrainer:
         # one-box tests, and an RCCL communicator would refuse the duplicate device)
         self.ncomm = None
         if self.segmented and device.type == "cuda" and (self.world == 1 or dist.get_backend(process_group) == "nccl"):
-            from ..parallel.comm import NativeComm, native_comm_available, native_comm_requested
-            if native_comm_requested() and native_comm_available():
-                self.ncomm = NativeComm(process_group, device)
+            from ..parallel.comm import native_comm_requested, open_verified_comm
+            if native_comm_requested():
+                self.ncomm = open_verified_comm(process_group, device)
         # Weight gradients next to the per-segment collectives. In the ONE-graph step (framework
         # communicator) the batched side stream (one fork per backward segment, joined one segment
         # later: DBX_OVERLAP_WGRAD=2, the world-1 default) stays on with LATE posts: segment k's

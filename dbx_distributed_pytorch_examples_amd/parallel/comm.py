@@ -53,6 +53,30 @@ def native_comm_requested() -> bool:
     return os.environ.get("DBX_COMM", "native") == "native"
 
 
+def open_verified_comm(process_group=None, device: Optional[torch.device] = None) -> "Optional[NativeComm]":
+    """A :class:`NativeComm` over ``process_group`` that has passed a check all-reduce and all-gather
+    on every rank -- or None on EVERY rank (the caller keeps the c10d collectives) when the
+    communicator cannot be created or returns wrong sums anywhere. The decision is itself agreed over
+    the c10d group, so no rank takes the framework path while another falls back."""
+    import warnings
+    ok, nc, err = native_comm_available(), None, "RCCL not loadable"
+    if ok:
+        try:
+            nc = NativeComm(process_group, device)
+            ok, err = nc.verify(), "check collectives returned wrong values"
+        except Exception as e:  # noqa: BLE001 -- any failure means: stay on c10d
+            ok, nc, err = False, None, f"{type(e).__name__}: {e}"
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                        device=dev if dist.get_backend(process_group) == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=process_group)
+    if int(flag.item()) == 1:
+        return nc
+    if not ok:
+        warnings.warn(f"framework RCCL communicator unavailable ({err}): using c10d collectives")
+    return None
+
+
 def _stream_ptr(stream: Optional[torch.cuda.Stream]) -> int:
     s = stream if stream is not None else torch.cuda.current_stream()
     return int(s.cuda_stream)
@@ -78,6 +102,17 @@ class NativeComm:
         with torch.cuda.device(self.device):
             self._h = c.comm_init(obj[0], self.size, self.rank)
         self._c = c
+
+    def verify(self) -> bool:
+        """Check collectives on the current stream (synchronised): an all-reduce of rank + 1 and an
+        all-gather of the ranks must give the exact expected values on this rank."""
+        t = torch.full((64,), float(self.rank + 1), device=self.device)
+        self.all_reduce(t)
+        g = torch.empty(self.size * 8, dtype=torch.int32, device=self.device)
+        self.all_gather(g, torch.full((8,), self.rank, dtype=torch.int32, device=self.device))
+        torch.cuda.synchronize(self.device)
+        want = torch.arange(self.size, dtype=torch.int32).repeat_interleave(8)
+        return bool((t.cpu() == self.size * (self.size + 1) / 2).all()) and torch.equal(g.cpu(), want)
 
     # ---- collectives (in place where the RCCL API allows it) -----------------------------------
     def all_reduce(self, t: torch.Tensor, op: str = "sum", stream=None) -> torch.Tensor:

@@ -112,3 +112,11 @@ def test_native_comm_two_ranks(tmp_path):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.count("OK") == 2
+
+
+def test_open_verified_comm_world1(world1):
+    """The trainer's entry: the communicator passes its check collectives and is returned on every
+    rank (here the one rank of a gloo group on one GPU)."""
+    from dbx_distributed_pytorch_examples_amd.parallel.comm import open_verified_comm
+    c = open_verified_comm(None, torch.device("cuda"))
+    assert c is not None and c.verify()

@@ -495,3 +495,19 @@ def test_comm_watchdog_unit():
     assert "step 7" in wd2.check()
     wd.close()
     wd2.close()
+
+
+def test_open_verified_comm_falls_back_together(tmp_path):
+    """Without RCCL (CPU / gloo) every rank gets None from open_verified_comm -- the agreed c10d
+    fallback -- with a warning, instead of some ranks taking the framework-communicator path."""
+    import warnings
+    import torch.distributed as tdist
+    from dbx_distributed_pytorch_examples_amd.parallel.comm import open_verified_comm
+    tdist.init_process_group("gloo", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1)
+    try:
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            assert open_verified_comm(None, torch.device("cpu")) is None
+        assert any("c10d" in str(x.message) for x in w)
+    finally:
+        tdist.destroy_process_group()
