@@ -134,36 +134,6 @@ __device__ __forceinline__ void bn_fin_consume(const BnFin& f, int c, bool store
   bn_fwd_affine(c, s, q, f.count, f.gamma, f.beta, f.eps, scale, shift, mean, var, invstd);
 }
 
-// Consumer-side backward finalize (the BN-backward apply passes, DBX_COEFF_IN): channel c's
-// coefficients k1, k2, k3 from the shards in the standalone kernel's order (plain loads: the moments
-// were completed by an earlier launch) and bn_bwd_k's arithmetic -- bit-identical to bn_bwd_coeff;
-// the storing thread also writes coeff / dgamma / dbeta (exactly one per channel and launch).
-__device__ __forceinline__ void bn_bwd_consume(const BnFin& f, int c, bool store, float& k1, float& k2, float& k3) {
-  double s = 0.0, q = 0.0;
-  for (int k0 = 0; k0 < f.nshard; k0 += 16) {
-    double sv[16], qv[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int k = k0 + j < f.nshard ? k0 + j : k0;
-      sv[j] = f.stats[(size_t)k * 2 * f.C + c];
-      qv[j] = f.stats[(size_t)k * 2 * f.C + f.C + c];
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (k0 + j < f.nshard) {
-        s += sv[j];
-        q += qv[j];
-      }
-    }
-  }
-  if (store) {
-    bn_bwd_final(f.C, c, s, q, f.count, f.gamma, f.mean, f.invstd, f.coeff, f.dgamma, f.dbeta, f.accumulate);
-    k1 = f.coeff[c]; k2 = f.coeff[f.C + c]; k3 = f.coeff[2 * f.C + c];
-    return;
-  }
-  bn_bwd_k(s, q, f.count, f.gamma ? f.gamma[c] : 1.f, f.invstd[c], f.mean[c], k1, k2, k3);
-}
-
 // End of a conv tile epilogue whose launch carries BN finalize descriptors: once every wave's
 // statistics atomics have completed (they execute at the memory side: no L2 write-back, so no
 // release fence -- a buffer_wbl2 per tile would write back the tile's just-stored outputs, which

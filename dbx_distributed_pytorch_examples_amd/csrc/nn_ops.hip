@@ -231,18 +231,42 @@ __global__ void bn_bwd_coeff_kernel(const double* __restrict__ stats, int nshard
 }
 
 // The coefficients of a thread's 8 channels: loaded (bn_bwd_coeff ran before), or (fin set,
-// DBX_COEFF_IN) finalized here from the BN's moment shards -- bit-identical; the row-0 threads of
-// block 0 store coeff / dgamma / dbeta. Saves the bn_bwd_coeff launch in front of the apply.
-__device__ __forceinline__ void bwd_coeff8(const float* coeff, const BnFin* fin, int C, int c0, bool store, float* k1,
+// DBX_COEFF_IN) finalized by the block into LDS first -- every thread derives a share of the C
+// channels from the moment shards (bn_bwd_k's math, the standalone kernel's shard order: bit-identical;
+// block 0 also stores coeff / dgamma / dbeta) -- which saves the bn_bwd_coeff launch in front of the
+// apply. All threads of the block must call it (barrier inside).
+__device__ __forceinline__ void bwd_coeff8(const float* coeff, const BnFin* fin, int C, int c0, float* sk, float* k1,
                                            float* k2, float* k3) {
   if (fin == nullptr) {
-    load8f(coeff + c0, k1);
-    load8f(coeff + C + c0, k2);
-    load8f(coeff + 2 * C + c0, k3);
+    if (c0 >= 0) {
+      load8f(coeff + c0, k1);
+      load8f(coeff + C + c0, k2);
+      load8f(coeff + 2 * C + c0, k3);
+    }
     return;
   }
+  const BnFin& f = *fin;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < f.nshard; ++k) {  // (k-ordered adds from 0.0: the standalone order)
+      s += f.stats[(size_t)k * 2 * C + c];
+      q += f.stats[(size_t)k * 2 * C + C + c];
+    }
+    float a, b, d;
+    if (blockIdx.x == 0) {
+      bn_bwd_final(C, c, s, q, f.count, f.gamma, f.mean, f.invstd, f.coeff, f.dgamma, f.dbeta, f.accumulate);
+      a = f.coeff[c]; b = f.coeff[C + c]; d = f.coeff[2 * C + c];
+    } else {
+      bn_bwd_k(s, q, f.count, f.gamma ? f.gamma[c] : 1.f, f.invstd[c], f.mean[c], a, b, d);
+    }
+    sk[c] = a; sk[C + c] = b; sk[2 * C + c] = d;
+  }
+  __syncthreads();
+  if (c0 >= 0) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) bn_bwd_consume(*fin, c0 + j, store, k1[j], k2[j], k3[j]);
+    for (int j = 0; j < 8; ++j) { k1[j] = sk[c0 + j]; k2[j] = sk[C + c0 + j]; k3[j] = sk[2 * C + c0 + j]; }
+  }
+  __syncthreads();  // (sk reusable by a second call)
 }
 
 template <int MASK, bool WRITE_G>
@@ -251,11 +275,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
                                     const float* __restrict__ sh, const float* __restrict__ coeff,
                                     bf16* __restrict__ dy, bf16* __restrict__ gout, long long M, int C,
                                     const BnFin* __restrict__ fin) {
+  __shared__ float sk[3 * 2048];
   const RowMap rm(C);
-  if (rm.r0 >= rm.rpb) return;
   const int c0 = rm.cg * 8;
   float k1[8], k2[8], k3[8], scr[8] = {0}, shr[8] = {0};
-  bwd_coeff8(coeff, fin, C, c0, blockIdx.x == 0 && rm.r0 == 0, k1, k2, k3);
+  bwd_coeff8(coeff, fin, C, rm.r0 < rm.rpb ? c0 : -1, sk, k1, k2, k3);
+  if (rm.r0 >= rm.rpb) return;
   if (MASK == 2) { load8f(sc + c0, scr); load8f(sh + c0, shr); }
   for (long long m = (long long)blockIdx.x * rm.rpb + rm.r0; m < M; m += (long long)gridDim.x * rm.rpb) {
     const long long e = m * C + c0;
@@ -276,13 +301,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const bf16* __restri
                                                             const bf16* __restrict__ y2, const float* __restrict__ coeff2,
                                                             bf16* __restrict__ dy2, long long M, int C,
                                                             const BnFin* __restrict__ fin1, const BnFin* __restrict__ fin2) {
+  __shared__ float sk[3 * 2048];
   const RowMap rm(C);
-  if (rm.r0 >= rm.rpb) return;
-  const int c0 = rm.cg * 8;
+  const int c0 = rm.cg * 8, cv = rm.r0 < rm.rpb ? c0 : -1;
   float a1[8], a2[8], a3[8], b1[8], b2[8], b3[8];
-  const bool store = blockIdx.x == 0 && rm.r0 == 0;
-  bwd_coeff8(coeff1, fin1, C, c0, store, a1, a2, a3);
-  bwd_coeff8(coeff2, fin2, C, c0, store, b1, b2, b3);
+  bwd_coeff8(coeff1, fin1, C, cv, sk, a1, a2, a3);
+  bwd_coeff8(coeff2, fin2, C, cv, sk, b1, b2, b3);
+  if (rm.r0 >= rm.rpb) return;
   for (long long m = (long long)blockIdx.x * rm.rpb + rm.r0; m < M; m += (long long)gridDim.x * rm.rpb) {
     const long long e = m * C + c0;
     float g[8], u[8], v[8], o1[8], o2[8];
@@ -1049,7 +1074,8 @@ extern "C" int dbx_bn_bwd_apply(const bf16* dout, const bf16* mref, const bf16* 
                                 hipStream_t st, const BnFin* fin) {
   if (n % C || C % 8 || C / 8 > 256) return -1;
   const long long M = n / C;
-  const dim3 g(grid_for(M, 256 / (C / 8), 4096)), b(256);
+  // (with the in-launch finalize every block derives all C coefficients: fewer, fatter blocks)
+  const dim3 g(grid_for(M, 256 / (C / 8), fin ? 512 : 4096)), b(256);
 #define BB(MK, WG) hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, WG>), g, b, 0, st, dout, mref, y, sc, sh, coeff, dy, gout, M, C, fin)
   if (mask_mode == 0) { if (gout) BB(0, true); else BB(0, false); }
   else if (mask_mode == 1) { if (gout) BB(1, true); else BB(1, false); }
@@ -1062,7 +1088,7 @@ extern "C" int dbx_bn_bwd_apply2(const bf16* g, const bf16* y1, const float* c1,
                                  const BnFin* fin2) {
   if (n % C || C % 8 || C / 8 > 256) return -1;
   const long long M = n / C;
-  hipLaunchKernelGGL(bn_bwd_apply2_kernel, dim3(grid_for(M, 256 / (C / 8), 4096)), dim3(256), 0, st, g, y1, c1, dy1,
+  hipLaunchKernelGGL(bn_bwd_apply2_kernel, dim3(grid_for(M, 256 / (C / 8), (fin1 || fin2) ? 512 : 4096)), dim3(256), 0, st, g, y1, c1, dy1,
                      y2, c2, dy2, M, C, fin1, fin2);
   RET_LAST;
 }

@@ -80,7 +80,7 @@ class BnFin:
                     dgamma, dbeta]
             buf = np.zeros(136, dtype=np.uint8)
             buf[:104].view(np.uint64)[:] = [_p(t) for t in ptrs]
-            buf[104:120].view(np.int32)[:] = [C, NSHARD, mode, int(accumulate)]
+            buf[104:120].view(np.int32)[:] = [C, stats.numel() // (2 * C), mode, int(accumulate)]
             buf[120:136].view(np.float32)[:] = [count, eps, momentum, 0.0]
             self.desc = torch.from_numpy(buf).to(stats.device)
 
@@ -97,14 +97,31 @@ class BnFin:
                          self.dbeta, accumulate=self.accumulate)
 
 
-def new_stats(C: int, device=None) -> torch.Tensor:
-    """Zeroed BN-statistics slab ``[NSHARD, 2, C]`` (flat, fp64: the epilogue atomics add fp32
-    partials exactly, so statistics do not depend on tile completion order)."""
-    return torch.zeros(NSHARD * 2 * C, device=device, dtype=torch.float64)
+def new_stats(C: int, device=None, nshard: Optional[int] = None) -> torch.Tensor:
+    """Zeroed BN-statistics slab ``[nshard, 2, C]`` (flat, fp64: the epilogue atomics add fp32
+    partials exactly, so statistics do not depend on tile completion order). ``nshard`` (default
+    NSHARD, at most 32): the copies the producer's atomics are spread over; every kernel reads the
+    count off the slab's size, so each BN may have its own."""
+    return torch.zeros((nshard or NSHARD) * 2 * C, device=device, dtype=torch.float64)
 
 
 def _p(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+def _nsh(stats, C: int) -> int:
+    """Shard count of a BN-statistics slab ``[nshard, 2, C]`` (fp64), from its size; NSHARD when absent."""
+    if stats is None:
+        return NSHARD
+    n = stats.numel() // (2 * C)
+    if n < 1 or n > 32 or n * 2 * C != stats.numel():
+        raise ValueError(f"statistics slab of {stats.numel()} elements is not [nshard <= 32, 2, {C}]")
+    return n
+
+
+def _chk_stats(t: torch.Tensor, name: str, C: int) -> int:
+    _chk(t, torch.float64, name)
+    return _nsh(t, C)
 
 
 def _chk(t: torch.Tensor, dtype, name: str, numel: Optional[int] = None):
@@ -249,7 +266,7 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     if IC % 64 or OC % 64:
         raise ValueError(f"conv_fwd needs IC,OC % 64 == 0 (got {IC},{OC})")
     if stats is not None:
-        _chk(stats, torch.float64, "stats", NSHARD * 2 * OC)
+        _chk_stats(stats, "stats", OC)
     if in_scale is not None:
         _chk(in_scale, torch.float32, "in_scale", IC)
         _chk(in_shift, torch.float32, "in_shift", IC)
@@ -301,7 +318,7 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     if nr == 0 or ns == 0:
         raise ValueError("conv_fwd: no filter tap touches the input")
     C().conv_igemm(mode, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
-                   int(relu_in), _p(stats), NSHARD, N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
+                   int(relu_in), _p(stats), _nsh(stats, OC), N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
                    nr, ns, r0, s0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
                    _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma, f1, 0, _fin[0], _fin[1], fi)
     if fin is not None and not f1 and _fin[1]:
@@ -456,15 +473,17 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             raise ValueError("addsrc subsampling must divide the output size")
         accumulate = True
     epi = (0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+    nsh = NSHARD
     if epilogue is not None:
         e = epilogue
         _chk(e.ybn, torch.bfloat16, "ybn", dx.numel())
-        _chk(e.stats1, torch.float64, "stats1", NSHARD * 2 * Cc)
+        nsh = _chk_stats(e.stats1, "stats1", Cc)
         if e.mode == MASK_OUT:
             _chk(e.mbits, torch.uint8, "mbits", dx.numel() // 8)
         if e.ybn2 is not None:
             _chk(e.ybn2, torch.bfloat16, "ybn2", dx.numel())
-            _chk(e.stats2, torch.float64, "stats2", NSHARD * 2 * Cc)
+            if _chk_stats(e.stats2, "stats2", Cc) != nsh:
+                raise ValueError("stats1 / stats2 must have the same shard count")
         if e.act_out is not None:
             if e.mode != MASK_Y:
                 raise ValueError("act_out needs the MASK_Y epilogue")
@@ -490,7 +509,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
     kind = (_use_patch3(tile, "dgrad") if not accumulate and bwd_y is None and (epilogue is None or epilogue.mode == MASK_Y)
             and patch3_supported(K, Cc, R, S, stride, pad, H, W) else 0)
     if kind:
-        C().conv_igemm(DGRAD_PATCH, 0, 0, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, NSHARD,
+        C().conv_igemm(DGRAD_PATCH, 0, 0, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, nsh,
                        N, P, Q, K, H, W, Cc, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, H, W,
                        0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), kind - 1, *fins, 0, 1, 0)
         _fin_rest(epilogue, fins)
@@ -534,7 +553,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             continue
         bm, bn, dma = _tile_dma(tile or pick_tile(N * ohs * ows, Cc, f"dgrad{epilogue.mode if epilogue else 0}"
                                                   + ("b" if bwd_y is not None else ""), K, R, stride))
-        C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), bwd[0], bwd[1], 0, 0, NSHARD,
+        C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), bwd[0], bwd[1], 0, 0, nsh,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,
                        _p(addsrc), add_sub, *epi, act_ptr, bwd[2], bwd[3], bwd[4], bwd[5], 0, stream_ptr(), dma,
@@ -573,14 +592,14 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
     _chk(w16s, torch.bfloat16, "w16s", OC * 256)
     _chk(out, torch.bfloat16, "out", N * OH * OW * OC)
     if stats is not None:
-        _chk(stats, torch.float64, "stats", NSHARD * 2 * OC)
+        _chk_stats(stats, "stats", OC)
     if R > 8 or S > 8:
         raise ValueError("stem kernel supports R,S <= 8")
     if patch is None:
         import os
         patch = os.environ.get("DBX_STEM_PATCH", "1") == "1"
     bm = 0 if patch and stem_patch_supported(IH, IW, OC, R, S, stride, pad) else 128  # bm 0: patch kernel
-    C().conv_igemm(STEM, bm, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), NSHARD,
+    C().conv_igemm(STEM, bm, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), _nsh(stats, OC),
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
                    *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr(), 0, 0, 0, 0, 1, 0)
     return out
@@ -789,14 +808,14 @@ def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2
     _chk(da, torch.bfloat16, "da", M * Cc)
     _chk(dw, torch.float32, "dw", Kc * Cc)
     _chk(ws, torch.float32, "ws")
-    _chk(bstats2, torch.float64, "bstats2", NSHARD * 2 * Cc)
+    nsh2 = _chk_stats(bstats2, "bstats2", Cc)
     for t, nm in ((scale2, "scale2"), (shift2, "shift2"), (mean2, "mean2"), (invstd2, "invstd2")):
         _chk(t, torch.float32, nm, Cc)
     if not dwfused_supported(Cc, Kc, M):
         raise ValueError(f"conv_dwfused: unsupported geometry C={Cc} K={Kc} M={M}")
     n = C().conv_dwfused(g.data_ptr(), y3.data_ptr(), coeff.data_ptr(), wt16.data_ptr(), y2.data_ptr(),
                          scale2.data_ptr(), shift2.data_ptr(), mean2.data_ptr(), invstd2.data_ptr(), da.data_ptr(),
-                         bstats2.data_ptr(), ws.data_ptr(), ws.numel(), M, Kc, Cc, NSHARD, stream_ptr())
+                         bstats2.data_ptr(), ws.data_ptr(), ws.numel(), M, Kc, Cc, nsh2, stream_ptr())
     C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), Kc * Cc, n, 1.0, 0, stream_ptr())
     return da
 
@@ -808,7 +827,7 @@ def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2
 def bn_finalize(stats, count, gamma, beta, eps, momentum, running_mean, running_var, scale, shift,
                 save_mean, save_invstd):
     Cc = scale.numel()
-    C().bn_finalize(stats.data_ptr(), NSHARD, Cc, float(count), _p(gamma), _p(beta), float(eps), float(momentum),
+    C().bn_finalize(stats.data_ptr(), _nsh(stats, Cc), Cc, float(count), _p(gamma), _p(beta), float(eps), float(momentum),
                     _p(running_mean), _p(running_var), scale.data_ptr(), shift.data_ptr(), _p(save_mean),
                     _p(save_invstd), stream_ptr())
 
@@ -823,8 +842,8 @@ def bn_eval_coeff(gamma, beta, eps, running_mean, running_var, scale, shift):
 def channel_stats(y, stats):
     Cc = y.shape[-1]
     _chk(y, torch.bfloat16, "y")
-    _chk(stats, torch.float64, "stats", NSHARD * 2 * Cc)
-    C().channel_stats(y.data_ptr(), y.numel() // Cc, Cc, stats.data_ptr(), NSHARD, stream_ptr())
+    nsh = _chk_stats(stats, "stats", Cc)
+    C().channel_stats(y.data_ptr(), y.numel() // Cc, Cc, stats.data_ptr(), nsh, stream_ptr())
 
 
 @_dispatch
@@ -851,17 +870,17 @@ def bn_bwd_reduce(dout, y, mean, invstd, stats, *, mask_mode, mref=None, scale=N
     Cc = y.shape[-1]
     _chk(dout, torch.bfloat16, "dout", y.numel())
     _chk(y, torch.bfloat16, "y")
-    _chk(stats, torch.float64, "stats", NSHARD * 2 * Cc)
+    nsh = _chk_stats(stats, "stats", Cc)
     if mask_mode == MASK_OUT:
         _chk(mref, torch.bfloat16, "mref", y.numel())
     C().bn_bwd_reduce(dout.data_ptr(), _p(mref), y.data_ptr(), _p(scale), _p(shift), mean.data_ptr(),
-                      invstd.data_ptr(), y.numel() // Cc, Cc, stats.data_ptr(), NSHARD, mask_mode, stream_ptr())
+                      invstd.data_ptr(), y.numel() // Cc, Cc, stats.data_ptr(), nsh, mask_mode, stream_ptr())
 
 
 @_dispatch
 def bn_bwd_coeff(stats, count, gamma, mean, invstd, coeff, dgamma=None, dbeta=None, accumulate=False):
     Cc = mean.numel()
-    C().bn_bwd_coeff(stats.data_ptr(), NSHARD, Cc, float(count), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
+    C().bn_bwd_coeff(stats.data_ptr(), _nsh(stats, Cc), Cc, float(count), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
                      coeff.data_ptr(), _p(dgamma), _p(dbeta), int(accumulate), stream_ptr())
 
 
@@ -948,9 +967,9 @@ def pool_bn_bwd_reduce(dpool, arg, y, scale, shift, mean, invstd, stats, *, K=3,
     masked by relu(y*scale+shift) > 0; stats += [sum g, sum g*xhat]. The pooled-gradient
     tensor at the pool input resolution is never materialised."""
     N, H, W, Cc, Pp, Q = _pool_bn_bwd_check(dpool, arg, y, K, stride)
-    _chk(stats, torch.float64, "stats", NSHARD * 2 * Cc)
+    nsh = _chk_stats(stats, "stats", Cc)
     C().pool_bn_bwd(dpool.data_ptr(), arg.data_ptr(), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
-                    mean.data_ptr(), invstd.data_ptr(), 0, 0, stats.data_ptr(), NSHARD, N, H, W, Cc, Pp, Q, K,
+                    mean.data_ptr(), invstd.data_ptr(), 0, 0, stats.data_ptr(), nsh, N, H, W, Cc, Pp, Q, K,
                     stride, pad, 0, stream_ptr())
 
 
@@ -960,7 +979,7 @@ def pool_bn_bwd_apply(dpool, arg, y, scale, shift, coeff, dy, *, K=3, stride=2, 
     N, H, W, Cc, Pp, Q = _pool_bn_bwd_check(dpool, arg, y, K, stride)
     _chk(dy, torch.bfloat16, "dy", y.numel())
     C().pool_bn_bwd(dpool.data_ptr(), arg.data_ptr(), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
-                    coeff.data_ptr(), coeff.data_ptr() + 4 * Cc, coeff.data_ptr() + 8 * Cc, dy.data_ptr(), 0, NSHARD,
+                    coeff.data_ptr(), coeff.data_ptr() + 4 * Cc, coeff.data_ptr() + 8 * Cc, dy.data_ptr(), 0, 1,
                     N, H, W, Cc, Pp, Q, K, stride, pad, 1, stream_ptr())
 
 

@@ -40,7 +40,7 @@ def _act_in(x, in_scale, in_shift, relu_in):
 def _add_stats(stats, y):
     C = y.shape[-1]
     yf = y.float().reshape(-1, C)
-    st = stats.view(NSHARD, 2, C)
+    st = stats.view(-1, 2, C)
     st[0, 0] += yf.sum(0)
     st[0, 1] += (yf * yf).sum(0)
 
@@ -100,11 +100,11 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
                 e.act_out.copy_(torch.relu(t).bfloat16())
         g = g.bfloat16().float()
         gf = g.reshape(-1, Cc)
-        st = e.stats1.view(NSHARD, 2, Cc)
+        st = e.stats1.view(-1, 2, Cc)
         st[0, 0] += gf.sum(0)
         st[0, 1] += (gf * ((y - e.mean1) * e.inv1).reshape(-1, Cc)).sum(0)
         if e.ybn2 is not None:
-            st2 = e.stats2.view(NSHARD, 2, Cc)
+            st2 = e.stats2.view(-1, 2, Cc)
             st2[0, 0] += gf.sum(0)
             st2[0, 1] += (gf * ((e.ybn2.float() - e.mean2) * e.inv2).reshape(-1, Cc)).sum(0)
         if hasattr(e, "run_fin"):  # the kernels' in-launch BN-backward finalize, as its own step
@@ -161,7 +161,7 @@ def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2
 def bn_finalize(stats, count, gamma, beta, eps, momentum, running_mean, running_var, scale, shift, save_mean,
                 save_invstd):
     C = scale.numel()
-    st = stats.view(NSHARD, 2, C).double().sum(0)
+    st = stats.view(-1, 2, C).double().sum(0)
     mean = st[0] / count
     var = (st[1] / count - mean * mean).clamp_min(0)
     invstd = 1.0 / torch.sqrt(var + eps)
@@ -223,14 +223,14 @@ def bn_bwd_reduce(dout, y, mean, invstd, stats, *, mask_mode, mref=None, scale=N
     C = y.shape[-1]
     g = _g(dout, y, mask_mode, mref, scale, shift).reshape(-1, C)
     xhat = ((y.float() - mean) * invstd).reshape(-1, C)
-    st = stats.view(NSHARD, 2, C)
+    st = stats.view(-1, 2, C)
     st[0, 0] += g.sum(0)
     st[0, 1] += (g * xhat).sum(0)
 
 
 def bn_bwd_coeff(stats, count, gamma, mean, invstd, coeff, dgamma=None, dbeta=None, accumulate=False):
     C = mean.numel()
-    st = stats.view(NSHARD, 2, C).sum(0).float()
+    st = stats.view(-1, 2, C).sum(0).float()
     s, q = st[0], st[1]
     g = gamma if gamma is not None else torch.ones_like(mean)
     sg, sgx = s / count, q / count
@@ -319,7 +319,7 @@ def pool_bn_bwd_reduce(dpool, arg, y, scale, shift, mean, invstd, stats, *, K=3,
     C = y.shape[-1]
     g = _pool_g(dpool, arg, y, scale, shift, K, stride, pad).reshape(-1, C)
     xhat = ((y.float() - mean) * invstd).reshape(-1, C)
-    st = stats.view(NSHARD, 2, C)
+    st = stats.view(-1, 2, C)
     st[0, 0] += g.sum(0).double()
     st[0, 1] += (g * xhat).sum(0).double()
 
