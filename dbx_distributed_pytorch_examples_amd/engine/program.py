@@ -215,20 +215,21 @@ class ResNetProgram:
         self.fin_in = os.environ.get("DBX_FIN_IN", "0") == "1"
         # Launch-bound small steps (< 0.5 TFLOP of forward conv work: the CIFAR / TinyImageNet presets)
         # keep 4 statistics shards per BN instead of NSHARD, which makes the consumer-side forward
-        # finalize cheap enough to replace the bn_finalize launches: CIFAR 234.7-236.6k vs 229.1-231.0k,
-        # TinyImageNet 96.9-97.0k vs 95.4-96.0k img/s; the b1024 headline keeps NSHARD and standalone
-        # finalizes (16.14k with them vs 16.38-16.40k, profiles/r4_s6/). DBX_NSHARD / DBX_FIN_IN set
-        # explicitly win.
+        # finalize cheap enough to replace the bn_finalize launches: CIFAR 233.7-236.6k vs 229.1-231.0k,
+        # TinyImageNet 96.9-97.1k vs 95.4-96.0k img/s; the b1024 headline keeps NSHARD and standalone
+        # finalizes (16.14k with them vs 16.38-16.40k; profiles/r4_s6/, r4_s7/). DBX_NSHARD / DBX_FIN_IN
+        # set explicitly win.
         self.small_step = self.fwd_conv_flops() < 5e11
         self.nshard = 4 if (self.small_step and "DBX_NSHARD" not in os.environ) else K.NSHARD
         if self.small_step and "DBX_FIN_IN" not in os.environ:
             self.fin_in = True
         # consumer-side backward finalize: a BN-backward apply pass computes its coefficients from the
         # moment shards itself (K.bn_bwd_apply fin=) instead of a bn_bwd_coeff launch in front of it
-        # (on by default with the 4-shard slabs of the small steps; at NSHARD = 32 every block of the
-        # apply would re-read 64 doubles per channel)
+        # (on by default for the smallest steps, < 50 GFLOP of forward conv work, with 4-shard slabs:
+        # CIFAR 238.2-238.6k vs 233.7k img/s without it; TinyImageNet 96.5k vs 97.1k, so off there;
+        # at NSHARD = 32 every block of an apply would re-read 64 doubles per channel: profiles/r4_s7/)
         self.coeff_in = (os.environ["DBX_COEFF_IN"] == "1" if "DBX_COEFF_IN" in os.environ
-                         else self.small_step and self.nshard <= 4)
+                         else self.fwd_conv_flops() < 5e10 and self.nshard <= 4)
         if not self.overlap_wgrad:
             # without the side stream folding costs no overlap: fold every BN-backward apply it can
             # (unless set explicitly) -- CIFAR b256 193.7k vs 189.5k img/s with overlap (r3s2_knobs)
