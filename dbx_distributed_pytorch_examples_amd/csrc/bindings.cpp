@@ -28,7 +28,7 @@ int dbx_bn_finalize(const double*, int, int, float, const float*, const float*, 
 int dbx_bn_eval_coeff(int, const float*, const float*, float, const float*, const float*, float*, float*, hipStream_t);
 int dbx_channel_stats(const bf16*, long long, int, double*, int, hipStream_t);
 int dbx_bn_apply(const bf16*, const float*, const float*, const bf16*, const float*, const float*, bf16*, long long, int,
-                 int, int, unsigned char*, hipStream_t);
+                 int, int, unsigned char*, hipStream_t, const dbx::BnFin*, const dbx::BnFin*);
 int dbx_bn_bwd_reduce(const bf16*, const bf16*, const bf16*, const float*, const float*, const float*, const float*,
                       long long, int, double*, int, int, hipStream_t);
 int dbx_bn_bwd_coeff(const double*, int, int, float, const float*, const float*, const float*, float*, float*, float*,
@@ -199,10 +199,11 @@ PYBIND11_MODULE(_C, m) {
     check(dbx_channel_stats(P<const bf16*>(y), M, C, P<double*>(stats), nshard, S(st)), "channel_stats");
   });
   m.def("bn_apply", [](uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t res, uintptr_t rsc, uintptr_t rsh,
-                       uintptr_t out, long long n, int C, int res_mode, int relu, uintptr_t mbits, uintptr_t st) {
+                       uintptr_t out, long long n, int C, int res_mode, int relu, uintptr_t mbits, uintptr_t st,
+                       uintptr_t fin, uintptr_t rfin) {
     check(dbx_bn_apply(P<const bf16*>(y), P<const float*>(sc), P<const float*>(sh), P<const bf16*>(res),
                        P<const float*>(rsc), P<const float*>(rsh), P<bf16*>(out), n, C, res_mode, relu,
-                       P<unsigned char*>(mbits), S(st)),
+                       P<unsigned char*>(mbits), S(st), P<const dbx::BnFin*>(fin), P<const dbx::BnFin*>(rfin)),
           "bn_apply");
   });
   m.def("bn_bwd_reduce", [](uintptr_t dout, uintptr_t mref, uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t mean,

@@ -116,18 +116,56 @@ __device__ __forceinline__ void load8f(const float* p, float* v) {
   v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
 
+// The forward affine (scale, shift) of a thread's 8 channels: loaded (bn_finalize ran before), or
+// (fin set) finalized by the block into LDS first: every thread derives a share of the C channels from
+// the statistics shards (the standalone kernel's shard order and math: bit-identical); block 0 also
+// stores scale / shift / saved moments / running statistics. All threads of the block must call it.
+__device__ __forceinline__ void fwd_affine8(const float* sc, const float* sh, const BnFin* fin, int C, int c0,
+                                            float* sk, float* s, float* h) {
+  if (fin == nullptr) {
+    if (c0 >= 0) { load8f(sc + c0, s); load8f(sh + c0, h); }
+    return;
+  }
+  const BnFin& f = *fin;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double sd = 0.0, qd = 0.0;
+    for (int k = 0; k < f.nshard; ++k) {
+      sd += f.stats[(size_t)k * 2 * C + c];
+      qd += f.stats[(size_t)k * 2 * C + C + c];
+    }
+    float a, b;
+    if (blockIdx.x == 0) {
+      bn_fwd_final(c, sd, qd, f.count, f.gamma, f.beta, f.eps, f.momentum, f.running_mean, f.running_var, f.scale,
+                   f.shift, f.mean, f.invstd);
+      a = f.scale[c]; b = f.shift[c];
+    } else {
+      double mean, var;
+      float invstd;
+      bn_fwd_affine(c, sd, qd, f.count, f.gamma, f.beta, f.eps, a, b, mean, var, invstd);
+    }
+    sk[c] = a; sk[C + c] = b;
+  }
+  __syncthreads();
+  if (c0 >= 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[j] = sk[c0 + j]; h[j] = sk[C + c0 + j]; }
+  }
+  __syncthreads();
+}
+
 template <int RES, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ sc,
                                 const float* __restrict__ sh, const bf16* __restrict__ res,
                                 const float* __restrict__ rsc, const float* __restrict__ rsh,
-                                bf16* __restrict__ out, unsigned char* __restrict__ mbits, long long M, int C) {
+                                bf16* __restrict__ out, unsigned char* __restrict__ mbits, long long M, int C,
+                                const BnFin* __restrict__ fin, const BnFin* __restrict__ rfin) {
+  __shared__ float sk[2 * 2048];
   const RowMap rm(C);
-  if (rm.r0 >= rm.rpb) return;
-  const int c0 = rm.cg * 8;
+  const int c0 = rm.cg * 8, cv = rm.r0 < rm.rpb ? c0 : -1;
   float s[8], h[8], a[8], b[8];
-  load8f(sc + c0, s);
-  load8f(sh + c0, h);
-  if (RES == 2) { load8f(rsc + c0, a); load8f(rsh + c0, b); }
+  fwd_affine8(sc, sh, fin, C, cv, sk, s, h);
+  if (RES == 2) fwd_affine8(rsc, rsh, rfin, C, cv, sk, a, b);
+  if (rm.r0 >= rm.rpb) return;
   for (long long m = (long long)blockIdx.x * rm.rpb + rm.r0; m < M; m += (long long)gridDim.x * rm.rpb) {
     const long long e = m * C + c0;
     float f[8];
@@ -1040,11 +1078,13 @@ extern "C" int dbx_channel_stats(const bf16* y, long long M, int C, double* stat
 }
 extern "C" int dbx_bn_apply(const bf16* y, const float* sc, const float* sh, const bf16* res, const float* rsc,
                             const float* rsh, bf16* out, long long n, int C, int res_mode, int relu,
-                            unsigned char* mbits, hipStream_t st) {
+                            unsigned char* mbits, hipStream_t st, const BnFin* fin, const BnFin* rfin) {
   if (n % C || C % 8 || C / 8 > 256) return -1;
+  if (rfin && res_mode != 2) return -2;
   const long long M = n / C;
-  const dim3 g(grid_for(M, 256 / (C / 8), 4096)), b(256);
-#define BA(R, A) hipLaunchKernelGGL((bn_apply_kernel<R, A>), g, b, 0, st, y, sc, sh, res, rsc, rsh, out, mbits, M, C)
+  // (with an in-launch finalize every block derives all C channels' affine: fewer, fatter blocks)
+  const dim3 g(grid_for(M, 256 / (C / 8), (fin || rfin) ? 512 : 4096)), b(256);
+#define BA(R, A) hipLaunchKernelGGL((bn_apply_kernel<R, A>), g, b, 0, st, y, sc, sh, res, rsc, rsh, out, mbits, M, C, fin, rfin)
   if (res_mode == 0) { if (relu) BA(0, true); else BA(0, false); }
   else if (res_mode == 1) { if (relu) BA(1, true); else BA(1, false); }
   else { if (relu) BA(2, true); else BA(2, false); }

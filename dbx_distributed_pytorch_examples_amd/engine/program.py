@@ -660,6 +660,7 @@ class ResNetProgram:
                       scale=sbn.scale, shift=sbn.shift, relu=True, ymax=self.pymax if tr else None)
         x = self.p0
         pending = None  # previous block whose output this block's conv1 computes (tail prologue)
+        out_fin = None  # the last BN's forward finalize, done by the block-output bn_apply (fin_in)
         for bi, b in enumerate(self.blocks):
             prev_bn = None
             deferred = None  # BN of conv i-1 whose finalize conv i's prologue performs (fin_in)
@@ -684,30 +685,39 @@ class ResNetProgram:
                                in_shift=prev_bn.shift if prev_bn else None, relu_in=True,
                                fin=self._ff(b.bns[i]), fin_in=deferred.fin_f if deferred is not None else None)
                 deferred = None
+                nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
+                c1 = nxt.convs[0] if nxt is not None else None
+                tail = (self.fuse_tail and c1 is not None
+                        and K.tail_supported(b.out_shape[2], c1.R, c1.S, c1.stride, c1.pad))
                 if self._ff(b.bns[i]) is None:
                     if (tr and self.fin_in and i + 1 < len(b.convs) and not b.mat[i]
                             and b.bns[i].fin_f is not None):
                         deferred = b.bns[i]  # finalized by the next conv's prologue
+                    elif tr and self.fin_in and i + 1 == len(b.convs) and not tail and b.bns[i].fin_f is not None:
+                        out_fin = b.bns[i].fin_f  # finalized by the block-output bn_apply below
                     else:
                         self._bn_fwd(b.bns[i], N * cv.OH * cv.OW)
                 prev_bn = b.bns[i]
             last = b.bns[-1]
+            res_fin = None
             if b.ds_conv is not None:
                 dc = b.ds_conv
                 K.conv_fwd(x, dc.w16, b.yd, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad,
                            stats=b.ds_bn.stats if tr else None, fin=self._ff(b.ds_bn))
                 if self._ff(b.ds_bn) is None:
-                    self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
+                    if tr and self.fin_in and not tail and b.ds_bn.fin_f is not None:
+                        res_fin = b.ds_bn.fin_f  # finalized by the block-output bn_apply below
+                    else:
+                        self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
                 res, rsc, rsh = b.yd, b.ds_bn.scale, b.ds_bn.shift
             else:
                 res, rsc, rsh = x, None, None
-            nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
-            c1 = nxt.convs[0] if nxt is not None else None
-            if self.fuse_tail and c1 is not None and K.tail_supported(b.out_shape[2], c1.R, c1.S, c1.stride, c1.pad):
+            if tail:
                 pending = (b, res, rsc, rsh)  # b.out (+ its mask) is written by the next block's conv1
             else:
                 K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=res, res_scale=rsc, res_shift=rsh,
-                           relu=True, mbits=b.obits if tr else None)
+                           relu=True, mbits=b.obits if tr else None, fin=out_fin, res_fin=res_fin)
+            out_fin = None
             x = b.out
         K.avgpool_fwd(x, self.pooled)
         if features_only:

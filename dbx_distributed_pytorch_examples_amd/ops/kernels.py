@@ -847,9 +847,13 @@ def channel_stats(y, stats):
 
 
 @_dispatch
-def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True, mbits=None):
+def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True, mbits=None, fin=None,
+             res_fin=None):
     """out = relu(y*scale + shift [+ res | + res*res_scale + res_shift]); ``mbits`` (uint8,
-    numel/8): also store the 1-bit ReLU mask (bit j of byte i = element 8i+j > 0) for backward."""
+    numel/8): also store the 1-bit ReLU mask (bit j of byte i = element 8i+j > 0) for backward.
+    ``fin`` / ``res_fin`` (:class:`BnFin`, mode FWD): the forward finalize of the BN giving scale / shift
+    (res_scale / res_shift) is done inside this launch (the bn_finalize launch it replaces, bit for bit;
+    its outputs are stored on the way)."""
     Cc = y.shape[-1]
     _chk(y, torch.bfloat16, "y")
     _chk(out, torch.bfloat16, "out", y.numel())
@@ -859,8 +863,16 @@ def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, 
         mode = 2 if res_scale is not None else 1
     if mbits is not None:
         _chk(mbits, torch.uint8, "mbits", y.numel() // 8)
+    fins = []
+    for f in (fin, res_fin if mode == 2 else None):
+        if f is not None and f.desc is None:
+            f.run()
+            f = None
+        fins.append(f.ptr() if f else 0)
+    if res_fin is not None and mode != 2:
+        res_fin.run()
     C().bn_apply(y.data_ptr(), scale.data_ptr(), shift.data_ptr(), _p(res), _p(res_scale), _p(res_shift),
-                 out.data_ptr(), y.numel(), Cc, mode, int(relu), _p(mbits), stream_ptr())
+                 out.data_ptr(), y.numel(), Cc, mode, int(relu), _p(mbits), stream_ptr(), *fins)
     return out
 
 

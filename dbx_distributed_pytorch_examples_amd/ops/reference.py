@@ -191,7 +191,11 @@ def channel_stats(y, stats):
     _add_stats(stats, y)
 
 
-def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True, mbits=None):
+def bn_apply(y, scale, shift, out, *, res=None, res_scale=None, res_shift=None, relu=True, mbits=None, fin=None,
+             res_fin=None):
+    for fn in (fin, res_fin):  # (the kernel finalizes in-launch; here: the finalize first)
+        if fn is not None:
+            fn.run()
     f = y.float() * scale + shift
     if res is not None:
         r = res.float()

@@ -244,3 +244,41 @@ def test_program_consumer_coeff_bit_identical(arch, size, batch, monkeypatch):
         assert torch.equal(b1, b2)
     for bn1, bn2 in zip(t1.prog.bns, t2.prog.bns):
         assert torch.equal(bn1.coeff, bn2.coeff), bn1.name
+
+
+@pytest.mark.parametrize("C,res_mode", [(64, 0), (256, 1), (512, 2), (2048, 2)])
+def test_bn_apply_consumer_finalize_bit_identical(C, res_mode):
+    """bn_apply finalizing its BN(s) in-launch (fin= / res_fin=) == bn_finalize launches + bn_apply:
+    the output, the mask bits, scale / shift / saved moments / running statistics."""
+    torch.manual_seed(C + res_mode)
+    M = 2500
+    y, res = (torch.randn(M, C, device="cuda").bfloat16() for _ in range(2))
+    st1, st2 = K.new_stats(C, "cuda", nshard=4), K.new_stats(C, "cuda", nshard=4)
+    st1.copy_(torch.rand_like(st1) * 100)
+    st2.copy_(torch.rand_like(st2) * 100)
+    res_list = []
+    for consumer in (False, True):
+        torch.manual_seed(3)
+        bns = [_bn_state(C) for _ in range(2)]
+        fins = [K.BnFin(K.BnFin.FWD, st, M, gamma=b["gamma"], beta=b["beta"], eps=1e-5, momentum=0.1,
+                        running_mean=b["rm"], running_var=b["rv"], scale=b["scale"], shift=b["shift"],
+                        mean=b["mean"], invstd=b["invstd"]) for st, b in zip((st1, st2), bns)]
+        out = torch.empty_like(y)
+        bits = torch.zeros(M * C // 8, device="cuda", dtype=torch.uint8)
+        kw = {}
+        if res_mode:
+            kw["res"] = res
+        if res_mode == 2:
+            kw.update(res_scale=bns[1]["scale"], res_shift=bns[1]["shift"])
+        if consumer:
+            K.bn_apply(y, bns[0]["scale"], bns[0]["shift"], out, mbits=bits, fin=fins[0],
+                       res_fin=fins[1] if res_mode == 2 else None, **kw)
+        else:
+            fins[0].run()
+            if res_mode == 2:
+                fins[1].run()
+            K.bn_apply(y, bns[0]["scale"], bns[0]["shift"], out, mbits=bits, **kw)
+        torch.cuda.synchronize()
+        res_list.append([out, bits] + [b[k] for b in bns[:1 + (res_mode == 2)] for k in sorted(b)])
+    for u, v in zip(*res_list):
+        assert torch.equal(u, v)
