@@ -78,10 +78,11 @@ struct IGemmArgs {
   const BnFin* fin1;
   const BnFin* fin2;
   int fin_base, fin_final;
-  // consumer-side forward finalize of the INPUT's BatchNorm (PRO without TAIL; nullable): every
+  // consumer-side forward finalize of the INPUT's BatchNorm (PRO, forward; nullable): every
   // workgroup derives the prologue scale / shift from that BN's statistics shards itself, and
   // workgroup 0 also stores what bn_finalize would (scale, shift, saved mean / invstd, running
-  // stats) -- the separate finalize launch between producer and consumer disappears
+  // stats) -- the separate finalize launch between producer and consumer disappears. TAIL: an array
+  // of two when the shortcut has a BN (res_scale set): [0] the block's last BN, [1] the shortcut's
   const BnFin* fin_in;
 };
 struct WgradArgs {

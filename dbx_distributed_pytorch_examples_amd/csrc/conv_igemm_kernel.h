@@ -413,11 +413,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   int pcb[2] = {0, 0};                    // channel block of the staged set (prologue coefficients)
   if constexpr (PRO && MODE != STEM) {
     for (int c = tid; c < a.IC; c += NT) {
-      if (!TAIL && a.fin_in) {  // wave-uniform: the input BN finalized here (workgroup 0 stores it)
+      if (a.fin_in) {  // wave-uniform: the input BN finalized here (workgroup 0 stores it)
         float sc, sh;
-        bn_fin_consume(*a.fin_in, c, blockIdx.x == 0, sc, sh);
+        bn_fin_consume(a.fin_in[0], c, blockIdx.x == 0, sc, sh);
         sPro[c] = sc;
         sPro[PRO_MAXC + c] = sh;
+        if constexpr (TAIL) {  // forward tail: fin_in[1] is the shortcut's BN when it has one
+          float rs = 1.f, rh = 0.f;
+          if (a.res_scale) bn_fin_consume(a.fin_in[1], c, blockIdx.x == 0, rs, rh);
+          sPro[2 * PRO_MAXC + c] = rs;
+          sPro[3 * PRO_MAXC + c] = rh;
+        }
         continue;
       }
       sPro[c] = a.in_scale[c];

@@ -577,6 +577,10 @@ class ResNetProgram:
                                invstd=bn.invstd)
             bn.fin_b = K.BnFin(K.BnFin.BWD, bn.bstats, cnt, gamma=bn.gamma, mean=bn.mean, invstd=bn.invstd,
                                coeff=bn.coeff, dgamma=bn.dgamma, dbeta=bn.dbeta)
+        for b in self.blocks:  # the tail prologue's [block BN, shortcut BN] descriptor arrays, up front
+            if b.ds_bn is not None and b.bns[-1].fin_f is not None and b.ds_bn.fin_f is not None:
+                if b.bns[-1].fin_f.desc is not None and b.ds_bn.fin_f.desc is not None:
+                    b.bns[-1].fin_f.pair_ptr(b.ds_bn.fin_f)
 
     def _ff(self, bn):
         """The forward finalize descriptor to hand the conv producing ``bn``'s statistics (training)."""
@@ -666,12 +670,12 @@ class ResNetProgram:
             deferred = None  # BN of conv i-1 whose finalize conv i's prologue performs (fin_in)
             for i, cv in enumerate(b.convs):
                 if i == 0 and pending is not None:
-                    pb, res, rsc, rsh = pending
+                    pb, res, rsc, rsh, pfin, prfin = pending
                     K.conv_fwd(pb.ys[-1], cv.w16, b.ys[0], R=cv.R, S=cv.S, stride=cv.stride, pad=cv.pad,
                                stats=b.bns[0].stats if tr else None, in_scale=pb.bns[-1].scale,
                                in_shift=pb.bns[-1].shift, relu_in=True, tail_res=res, tail_res_scale=rsc,
                                tail_res_shift=rsh, tail_out=pb.out, tail_bits=pb.obits if tr else None,
-                               fin=self._ff(b.bns[0]))
+                               fin=self._ff(b.bns[0]), fin_in=pfin, fin_in_res=prfin)
                     pending = None
                 elif i > 0 and b.mat[i - 1]:  # materialised BN output -> plain-operand (eight-wave) conv
                     K.bn_apply(b.ys[i - 1], prev_bn.scale, prev_bn.shift, b.acts[i - 1], relu=True)
@@ -693,8 +697,8 @@ class ResNetProgram:
                     if (tr and self.fin_in and i + 1 < len(b.convs) and not b.mat[i]
                             and b.bns[i].fin_f is not None):
                         deferred = b.bns[i]  # finalized by the next conv's prologue
-                    elif tr and self.fin_in and i + 1 == len(b.convs) and not tail and b.bns[i].fin_f is not None:
-                        out_fin = b.bns[i].fin_f  # finalized by the block-output bn_apply below
+                    elif tr and self.fin_in and i + 1 == len(b.convs) and b.bns[i].fin_f is not None:
+                        out_fin = b.bns[i].fin_f  # finalized by the block-output bn_apply / next conv1 below
                     else:
                         self._bn_fwd(b.bns[i], N * cv.OH * cv.OW)
                 prev_bn = b.bns[i]
@@ -705,15 +709,17 @@ class ResNetProgram:
                 K.conv_fwd(x, dc.w16, b.yd, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad,
                            stats=b.ds_bn.stats if tr else None, fin=self._ff(b.ds_bn))
                 if self._ff(b.ds_bn) is None:
-                    if tr and self.fin_in and not tail and b.ds_bn.fin_f is not None:
-                        res_fin = b.ds_bn.fin_f  # finalized by the block-output bn_apply below
+                    if tr and self.fin_in and b.ds_bn.fin_f is not None:
+                        res_fin = b.ds_bn.fin_f  # finalized by the block-output bn_apply / next conv1 below
                     else:
                         self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
                 res, rsc, rsh = b.yd, b.ds_bn.scale, b.ds_bn.shift
             else:
                 res, rsc, rsh = x, None, None
             if tail:
-                pending = (b, res, rsc, rsh)  # b.out (+ its mask) is written by the next block's conv1
+                # b.out (+ its mask) is written by the next block's conv1 (which also finalizes the
+                # tail BNs deferred above)
+                pending = (b, res, rsc, rsh, out_fin, res_fin)
             else:
                 K.bn_apply(b.ys[-1], last.scale, last.shift, b.out, res=res, res_scale=rsc, res_shift=rsh,
                            relu=True, mbits=b.obits if tr else None, fin=out_fin, res_fin=res_fin)

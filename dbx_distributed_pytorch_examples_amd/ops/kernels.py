@@ -87,6 +87,14 @@ class BnFin:
     def ptr(self) -> int:
         return self.desc.data_ptr() if self.desc is not None else 0
 
+    def pair_ptr(self, other: "BnFin") -> int:
+        """Device address of the two-descriptor array [self, other] (a forward tail prologue with a
+        shortcut BN). Built on first use -- callers that capture graphs build it beforehand (the
+        program's build_fins), so no copy kernel lands in a captured step."""
+        if getattr(self, "_pair", None) is None or self._pair[0] is not other:
+            self._pair = (other, torch.cat([self.desc, other.desc]))
+        return self._pair[1].data_ptr()
+
     def run(self) -> None:
         """The standalone finalize launch (what the fused path replaces)."""
         if self.mode == self.FWD:
@@ -247,7 +255,8 @@ def _use_patch3(tile, mode: str) -> int:
 @_dispatch
 def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None,
              relu_in=True, tile=None, tail_res=None, tail_res_scale=None, tail_res_shift=None, tail_out=None,
-             tail_bits=None, fin: "BnFin" = None, _split=True, _fin=(0, 1), fin_in: "BnFin" = None):
+             tail_bits=None, fin: "BnFin" = None, _split=True, _fin=(0, 1), fin_in: "BnFin" = None,
+             fin_in_res: "BnFin" = None):
     """Y = conv(act(X), W); act = relu(X*in_scale + in_shift) with a BN prologue. "Tail" mode
     (``tail_res`` given; 1x1 stride-1 convs): act = relu(X*in_scale + in_shift + r), r = tail_res or
     tail_res*tail_res_scale + tail_res_shift -- the previous residual block's output computed on the
@@ -308,11 +317,19 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
         return out
     f1 = fin.ptr() if fin is not None and stats is not None else 0
     fi = 0
-    if fin_in is not None:
-        if mode == FWD and in_scale is not None and tail_res is None and dma in (0, 1) and fin_in.desc is not None:
-            fi = fin_in.ptr()  # the implicit-GEMM prologue finalizes it (csrc/bn_fin.h bn_fin_consume)
+    if fin_in is not None or fin_in_res is not None:
+        pair = tail_res is not None and tail_res_scale is not None
+        fins = [f for f in (fin_in, fin_in_res if pair else None) if f is not None]
+        if (mode == FWD and in_scale is not None and dma in (0, 1) and fin_in is not None
+                and all(f.desc is not None for f in fins) and (not pair or fin_in_res is not None)):
+            # the implicit-GEMM prologue finalizes it (csrc/bn_fin.h bn_fin_consume); a forward
+            # tail with a shortcut BN takes both descriptors as one array
+            fi = fin_in.ptr() if not pair else fin_in.pair_ptr(fin_in_res)
         else:
-            fin_in.run()
+            for f in fins:
+                f.run()
+        if fin_in_res is not None and not pair:
+            fin_in_res.run()
     r0, nr = fwd_taps(IH, OH, R, stride, pad)
     s0, ns = fwd_taps(IW, OW, S, stride, pad)
     if nr == 0 or ns == 0:

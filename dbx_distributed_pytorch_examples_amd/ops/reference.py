@@ -47,9 +47,10 @@ def _add_stats(stats, y):
 
 def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_shift=None, relu_in=True, tile=None,
              tail_res=None, tail_res_scale=None, tail_res_shift=None, tail_out=None, tail_bits=None, fin=None,
-             fin_in=None):
-    if fin_in is not None:  # the input BN's finalize, done by the consumer on the GPU
-        fin_in.run()
+             fin_in=None, fin_in_res=None):
+    for f in (fin_in, fin_in_res):  # the input BNs' finalizes, done by the consumer on the GPU
+        if f is not None:
+            f.run()
     OC = w16.shape[0]
     IC = x.shape[-1]
     if tail_res is not None:  # previous block's output relu(bn3(x) + shortcut): bn_apply's semantics

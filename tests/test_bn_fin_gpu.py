@@ -282,3 +282,44 @@ def test_bn_apply_consumer_finalize_bit_identical(C, res_mode):
         res_list.append([out, bits] + [b[k] for b in bns[:1 + (res_mode == 2)] for k in sorted(b)])
     for u, v in zip(*res_list):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("shortcut_bn", [False, True])
+@pytest.mark.parametrize("tile", [(128, 128, 1), (128, 256, 0)])
+def test_tail_prologue_consumer_finalize_bit_identical(shortcut_bn, tile):
+    """The forward tail prologue (relu(bn3(y3) + [bn_ds(yd) | x]) computed inside the next conv1)
+    finalizing bn3 (and the shortcut BN) from their shards == bn_finalize launches first: conv output,
+    statistics, the block output write-back and mask, every finalize output."""
+    torch.manual_seed(7 + shortcut_bn)
+    N, H, C, Kc = 4, 14, 256, 256
+    y3, yd = (torch.randn(N, H, H, C, device="cuda").bfloat16() for _ in range(2))
+    w = (torch.randn(Kc, C, device="cuda") / math.sqrt(C)).bfloat16()
+    sts = [K.new_stats(C, "cuda", nshard=4) for _ in range(2)]
+    for st in sts:
+        st.copy_(torch.rand_like(st) * 200)
+    res = []
+    for consumer in (False, True):
+        torch.manual_seed(3)
+        bns = [_bn_state(C) for _ in range(2)]
+        fins = [K.BnFin(K.BnFin.FWD, st, N * H * H, gamma=b["gamma"], beta=b["beta"], eps=1e-5, momentum=0.1,
+                        running_mean=b["rm"], running_var=b["rv"], scale=b["scale"], shift=b["shift"],
+                        mean=b["mean"], invstd=b["invstd"]) for st, b in zip(sts, bns)]
+        y = torch.empty(N, H, H, Kc, device="cuda", dtype=torch.bfloat16)
+        ost = K.new_stats(Kc, "cuda")
+        out = torch.empty_like(y3)
+        bits = torch.zeros(y3.numel() // 8, device="cuda", dtype=torch.uint8)
+        kw = dict(R=1, S=1, stride=1, pad=0, stats=ost, in_scale=bns[0]["scale"], in_shift=bns[0]["shift"],
+                  tail_res=yd, tail_out=out, tail_bits=bits, tile=tile)
+        if shortcut_bn:
+            kw.update(tail_res_scale=bns[1]["scale"], tail_res_shift=bns[1]["shift"])
+        if consumer:
+            K.conv_fwd(y3, w, y, fin_in=fins[0], fin_in_res=fins[1] if shortcut_bn else None, **kw)
+        else:
+            fins[0].run()
+            if shortcut_bn:
+                fins[1].run()
+            K.conv_fwd(y3, w, y, **kw)
+        torch.cuda.synchronize()
+        res.append([y, ost, out, bits] + [b[k] for b in bns[:1 + shortcut_bn] for k in sorted(b)])
+    for u, v in zip(*res):
+        assert torch.equal(u, v)
