@@ -38,7 +38,7 @@ int dbx_bn_bwd_apply(const bf16*, const bf16*, const bf16*, const float*, const 
 int dbx_bn_bwd_apply2(const bf16*, const bf16*, const float*, bf16*, const bf16*, const float*, bf16*, long long, int,
                       hipStream_t, const dbx::BnFin*, const dbx::BnFin*);
 int dbx_maxpool_fwd(const bf16*, const float*, const float*, bf16*, unsigned char*, bf16*, int, int, int, int, int,
-                    int, int, int, int, int, hipStream_t);
+                    int, int, int, int, int, hipStream_t, const dbx::BnFin*);
 int dbx_maxpool_bwd(const bf16*, const unsigned char*, bf16*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int dbx_pool_bn_bwd(const bf16*, const unsigned char*, const bf16*, const float*, const float*, const float*,
                     const float*, const float*, bf16*, double*, int, int, int, int, int, int, int, int, int, int, int,
@@ -235,9 +235,11 @@ PYBIND11_MODULE(_C, m) {
           "bn_bwd_apply2");
   });
   m.def("maxpool_fwd", [](uintptr_t x, uintptr_t sc, uintptr_t sh, uintptr_t out, uintptr_t arg, uintptr_t ymax, int N,
-                          int H, int W, int C, int Pp, int Q, int K, int stride, int pad, int relu, uintptr_t st) {
+                          int H, int W, int C, int Pp, int Q, int K, int stride, int pad, int relu, uintptr_t st,
+                          uintptr_t fin) {
     check(dbx_maxpool_fwd(P<const bf16*>(x), P<const float*>(sc), P<const float*>(sh), P<bf16*>(out),
-                          P<unsigned char*>(arg), P<bf16*>(ymax), N, H, W, C, Pp, Q, K, stride, pad, relu, S(st)),
+                          P<unsigned char*>(arg), P<bf16*>(ymax), N, H, W, C, Pp, Q, K, stride, pad, relu, S(st),
+                          P<const dbx::BnFin*>(fin)),
           "maxpool_fwd");
   });
   m.def("maxpool_bwd", [](uintptr_t dout, uintptr_t arg, uintptr_t dx, int N, int H, int W, int C, int Pp, int Q, int K,

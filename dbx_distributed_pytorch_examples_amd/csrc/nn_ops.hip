@@ -373,12 +373,16 @@ template <int KF>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ sc,
                                    const float* __restrict__ sh, bf16* __restrict__ out,
                                    unsigned char* __restrict__ arg, bf16* __restrict__ ymax, int N, int H, int W,
-                                   int C, int P, int Q, int K, int stride, int pad, int relu) {
+                                   int C, int P, int Q, int K, int stride, int pad, int relu,
+                                   const BnFin* __restrict__ fin) {
+  __shared__ float sk[2 * 2048];
   const RowMap rm(C);
-  if (rm.r0 >= rm.rpb) return;
   const int c0 = rm.cg * 8;
   float s[8], h[8];
-  if (sc) { load8f(sc + c0, s); load8f(sh + c0, h); }
+  if (fin) fwd_affine8(sc, sh, fin, C, rm.r0 < rm.rpb ? c0 : -1, sk, s, h);  // (the stem BN finalized here)
+  if (rm.r0 >= rm.rpb) return;
+  if (fin) {
+  } else if (sc) { load8f(sc + c0, s); load8f(sh + c0, h); }
   else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) { s[j] = 1.f; h[j] = 0.f; }
@@ -1134,16 +1138,17 @@ extern "C" int dbx_bn_bwd_apply2(const bf16* g, const bf16* y1, const float* c1,
 }
 extern "C" int dbx_maxpool_fwd(const bf16* x, const float* sc, const float* sh, bf16* out, unsigned char* arg,
                                bf16* ymax, int N, int H, int W, int C, int P, int Q, int K, int stride, int pad, int relu,
-                               hipStream_t st) {
+                               hipStream_t st, const BnFin* fin) {
   if (C % 8) return -1;
   if (C / 8 > 256) return -1;
-  const dim3 grid(grid_for((long long)N * P * Q, 256 / (C / 8), 4096));
+  if (fin && !sc) return -2;
+  const dim3 grid(grid_for((long long)N * P * Q, 256 / (C / 8), fin ? 1024 : 4096));
   if (K == 3 && (long long)N * P * Q < (1ll << 31))
     hipLaunchKernelGGL(maxpool_fwd_kernel<3>, grid, dim3(256), 0, st, x, sc, sh, out, arg, ymax, N, H, W, C, P, Q, K,
-                       stride, pad, relu);
+                       stride, pad, relu, fin);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<0>, grid, dim3(256), 0, st, x, sc, sh, out, arg, ymax, N, H, W, C, P, Q, K,
-                       stride, pad, relu);
+                       stride, pad, relu, fin);
   RET_LAST;
 }
 extern "C" int dbx_maxpool_bwd(const bf16* dout, const unsigned char* arg, bf16* dx, int N, int H, int W, int C, int P,

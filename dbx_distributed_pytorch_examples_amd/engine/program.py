@@ -659,9 +659,11 @@ class ResNetProgram:
         st, sbn = self.stem, self.stem_bn
         K.conv_stem_fwd(self.x4, st.w16, self.y0, R=st.R, S=st.S, stride=st.stride, pad=st.pad,
                         stats=sbn.stats if tr else None)
-        self._bn_fwd(sbn, N * st.OH * st.OW)
+        sfin = sbn.fin_f if (tr and self.fin_in and sbn.fin_f is not None) else None  # (finalized by the pool)
+        if sfin is None:
+            self._bn_fwd(sbn, N * st.OH * st.OW)
         K.maxpool_fwd(self.y0, self.p0, self.parg, K=self.pool_k, stride=self.pool_s, pad=self.pool_p,
-                      scale=sbn.scale, shift=sbn.shift, relu=True, ymax=self.pymax if tr else None)
+                      scale=sbn.scale, shift=sbn.shift, relu=True, ymax=self.pymax if tr else None, fin=sfin)
         x = self.p0
         pending = None  # previous block whose output this block's conv1 computes (tail prologue)
         out_fin = None  # the last BN's forward finalize, done by the block-output bn_apply (fin_in)

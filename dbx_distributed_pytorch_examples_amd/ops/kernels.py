@@ -950,9 +950,10 @@ def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2, fin1=None, fin2=None):
 
 
 @_dispatch
-def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True, ymax=None):
+def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True, ymax=None, fin=None):
     """out = max over windows of relu(x*scale + shift), arg = window index of the max; ``ymax``
-    (optional) = the raw x at the argmax (the stem BN backward reduces over pooled positions)."""
+    (optional) = the raw x at the argmax (the stem BN backward reduces over pooled positions).
+    ``fin`` (:class:`BnFin`, mode FWD): the stem BN's forward finalize, done inside this launch."""
     N, H, W, Cc = x.shape
     _, P, Q, _ = out.shape
     _chk(x, torch.bfloat16, "x")
@@ -960,8 +961,11 @@ def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, re
     _chk(arg, torch.uint8, "arg", out.numel())
     if ymax is not None:
         _chk(ymax, torch.bfloat16, "ymax", out.numel())
+    if fin is not None and (fin.desc is None or scale is None):
+        fin.run()
+        fin = None
     C().maxpool_fwd(x.data_ptr(), _p(scale), _p(shift), out.data_ptr(), arg.data_ptr(), _p(ymax), N, H, W, Cc, P, Q,
-                    K, stride, pad, int(relu), stream_ptr())
+                    K, stride, pad, int(relu), stream_ptr(), fin.ptr() if fin else 0)
 
 
 @_dispatch

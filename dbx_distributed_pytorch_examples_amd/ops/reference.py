@@ -265,7 +265,9 @@ def bn_bwd_apply2(g, y1, coeff1, dy1, y2, coeff2, dy2, fin1=None, fin2=None):
     bn_bwd_apply(g, y2, coeff2, dy2, mask_mode=0, fin=fin2)
 
 
-def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True, ymax=None):
+def maxpool_fwd(x, out, arg, *, K=3, stride=2, pad=1, scale=None, shift=None, relu=True, ymax=None, fin=None):
+    if fin is not None:
+        fin.run()
     f = x.float()
     if scale is not None:
         f = f * scale + shift

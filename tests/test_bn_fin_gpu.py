@@ -323,3 +323,31 @@ def test_tail_prologue_consumer_finalize_bit_identical(shortcut_bn, tile):
         res.append([y, ost, out, bits] + [b[k] for b in bns[:1 + shortcut_bn] for k in sorted(b)])
     for u, v in zip(*res):
         assert torch.equal(u, v)
+
+
+def test_maxpool_consumer_finalize_bit_identical():
+    """The stem max-pool finalizing the stem BN in-launch == bn_finalize + max-pool."""
+    torch.manual_seed(4)
+    N, H, C = 8, 32, 64
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    st = K.new_stats(C, "cuda", nshard=4)
+    st.copy_(torch.rand_like(st) * 300)
+    res = []
+    for consumer in (False, True):
+        torch.manual_seed(5)
+        b = _bn_state(C)
+        fin = K.BnFin(K.BnFin.FWD, st, N * H * H, gamma=b["gamma"], beta=b["beta"], eps=1e-5, momentum=0.1,
+                      running_mean=b["rm"], running_var=b["rv"], scale=b["scale"], shift=b["shift"],
+                      mean=b["mean"], invstd=b["invstd"])
+        out = torch.empty(N, H // 2, H // 2, C, device="cuda", dtype=torch.bfloat16)
+        arg = torch.empty(out.numel(), device="cuda", dtype=torch.uint8)
+        ymax = torch.empty_like(out)
+        if consumer:
+            K.maxpool_fwd(x, out, arg, scale=b["scale"], shift=b["shift"], ymax=ymax, fin=fin)
+        else:
+            fin.run()
+            K.maxpool_fwd(x, out, arg, scale=b["scale"], shift=b["shift"], ymax=ymax)
+        torch.cuda.synchronize()
+        res.append([out, arg, ymax] + [b[k] for k in sorted(b)])
+    for u, v in zip(*res):
+        assert torch.equal(u, v)
