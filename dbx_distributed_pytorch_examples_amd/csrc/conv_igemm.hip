@@ -755,6 +755,95 @@ extern "C" int dbx_wgrad_reduce_gather(const float* ws, float* dw, int OC, int R
   return (int)hipGetLastError();
 }
 
+// Batched split-K reductions (the deferred weight-gradient reductions of one side-stream batch): up
+// to kMaxRJobs jobs per launch pair, passed by value. Launch A runs level 1 of every two-level job
+// (the same groups as dbx_wgrad_reduce), launch B every job's final sum -- per element the same adds
+// in the same order as the per-gradient reduce, so the gradients are bit-identical; two launches
+// per batch instead of one or two per weight gradient (the small steps are launch-bound).
+constexpr int kMaxRJobs = 32;
+struct RJob {
+  const float* ws;    // nsplit slabs of n floats (+ the level-1 partials after them)
+  float* dw;
+  int n4, nsplit, G, spg, accumulate;
+  float scale;
+};
+struct RJobs {
+  RJob j[kMaxRJobs];
+  long long pre[kMaxRJobs + 1];  // prefix of the launch's per-job work items
+  int nj;
+};
+__device__ __forceinline__ int rjob_of(const RJobs& J, long long f) {
+  int k = 0;
+  while (k + 1 < J.nj && J.pre[k + 1] <= f) ++k;
+  return k;
+}
+__global__ void wgrad_reduce_multi_l1_kernel(const RJobs J) {  // items: (job, group, i) of two-level jobs
+  for (long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x; f < J.pre[J.nj];
+       f += (long long)gridDim.x * blockDim.x) {
+    const int k = rjob_of(J, f);
+    const RJob& r = J.j[k];
+    const long long loc = f - J.pre[k];
+    const int g = (int)(loc / r.n4), i = (int)(loc - (long long)g * r.n4);
+    const f32x4* w4 = reinterpret_cast<const f32x4*>(r.ws);
+    const int s0 = g * r.spg, s1 = min(r.nsplit, s0 + r.spg);
+    const f32x4 sum = sum_slabs_in_order(f32x4{0.f, 0.f, 0.f, 0.f}, s0, s1,
+                                         [&](int kk) { return w4[(size_t)kk * r.n4 + i]; });
+    reinterpret_cast<f32x4*>(const_cast<float*>(r.ws) + (size_t)r.nsplit * r.n4 * 4)[(size_t)g * r.n4 + i] = sum;
+  }
+}
+__global__ void wgrad_reduce_multi_kernel(const RJobs J) {  // items: (job, i)
+  for (long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x; f < J.pre[J.nj];
+       f += (long long)gridDim.x * blockDim.x) {
+    const int k = rjob_of(J, f);
+    const RJob& r = J.j[k];
+    const int i = (int)(f - J.pre[k]);
+    // two-level jobs sum their G group partials, single-level ones their nsplit slabs
+    const f32x4* w4 = reinterpret_cast<const f32x4*>(r.G > 1 ? r.ws + (size_t)r.nsplit * r.n4 * 4 : r.ws);
+    const int cnt = r.G > 1 ? r.G : r.nsplit;
+    f32x4 sm = sum_slabs_in_order(w4[i], 1, cnt, [&](int kk) { return w4[(size_t)kk * r.n4 + i]; });
+    sm *= r.scale;
+    f32x4* o4 = reinterpret_cast<f32x4*>(r.dw);
+    if (r.accumulate) sm += o4[i];
+    o4[i] = sm;
+  }
+}
+
+// jobs: (ws, dw, n, nsplit, scale, accumulate) each; the level-1 grouping is dbx_wgrad_reduce's.
+extern "C" int dbx_wgrad_reduce_multi(const float* const* ws, float* const* dw, const long long* n, const int* nsplit,
+                                      const float* scale, const int* accumulate, int njobs, hipStream_t st) {
+  for (int b0 = 0; b0 < njobs; b0 += kMaxRJobs) {
+    RJobs A{}, B{};
+    const int nb = njobs - b0 < kMaxRJobs ? njobs - b0 : kMaxRJobs;
+    for (int t = 0; t < nb; ++t) {
+      const int q = b0 + t;
+      if (n[q] % 4) return -1;
+      RJob r{ws[q], dw[q], (int)(n[q] / 4), nsplit[q], 1, 1, accumulate[q], scale[q]};
+      const int gx = (r.n4 + 255) / 256;
+      if (r.nsplit > 8 && (long long)gx * 4 < 1024) {
+        int G = 1024 / gx;
+        if (G > r.nsplit / 4) G = r.nsplit / 4;
+        if (G > 64) G = 64;
+        if (G < 2) G = 2;
+        r.spg = (r.nsplit + G - 1) / G;
+        r.G = (r.nsplit + r.spg - 1) / r.spg;
+        A.j[A.nj] = r;
+        A.pre[A.nj + 1] = A.pre[A.nj] + (long long)r.G * r.n4;
+        ++A.nj;
+      }
+      B.j[B.nj] = r;
+      B.pre[B.nj + 1] = B.pre[B.nj] + r.n4;
+      ++B.nj;
+    }
+    if (A.nj) {
+      const long long g = (A.pre[A.nj] + 255) / 256;
+      hipLaunchKernelGGL(wgrad_reduce_multi_l1_kernel, dim3(g > 4096 ? 4096 : (int)g), dim3(256), 0, st, A);
+    }
+    const long long g = (B.pre[B.nj] + 255) / 256;
+    hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3(g > 4096 ? 4096 : (int)g), dim3(256), 0, st, B);
+  }
+  return (int)hipGetLastError();
+}
+
 extern "C" int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale,
                                 int accumulate, hipStream_t st) {
   if (n % 4) return -1;

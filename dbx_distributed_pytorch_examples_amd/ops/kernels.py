@@ -680,10 +680,39 @@ def wgrad_tiles_max(OC: int, KTOT: int) -> int:
     return (OC // 64) * (KTOT // 64)
 
 
+class ReduceBatch:
+    """Deferred split-K reductions of a batch of weight gradients (the program's side-stream batch
+    of one backward segment): each gradient's slabs go to its own region of ``arena`` and
+    :meth:`flush` finishes them all with two launches (csrc/conv_igemm.hip dbx_wgrad_reduce_multi:
+    level 1 of the two-level reductions, then every final sum) instead of one or two per gradient --
+    bit-identical to ``wgrad_reduce``. A gradient whose slabs do not fit the arena's remainder is
+    reduced at once (``need`` records the size the arena should grow to, outside graph capture)."""
+
+    def __init__(self, arena: torch.Tensor):
+        self.arena, self.off, self.need, self.jobs = arena, 0, 0, []
+
+    def alloc(self, n: int):
+        self.need += n
+        if self.off + n > self.arena.numel():
+            return None
+        r = self.arena[self.off:self.off + n]
+        self.off += n
+        return r
+
+    def add(self, ws, dw, n, nsplit, scale, accumulate):
+        self.jobs.append((ws.data_ptr(), dw.data_ptr(), int(n), int(nsplit), float(scale), int(accumulate)))
+
+    def flush(self):
+        if self.jobs:
+            cols = list(zip(*self.jobs))
+            C().wgrad_reduce_multi(*[list(c) for c in cols], stream_ptr())
+        self.jobs = []
+
+
 @_dispatch
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True,
                scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None, out_krsc=None,
-               rounds=None):
+               rounds=None, defer: "ReduceBatch" = None):
     """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace.
     ``dma``: operand path of the prologue-free kernels -- LDS-DMA ring depth 2 / 3, 0 = register
     staged, -1 = the tune table's choice, else DBX_WGRAD_DMA, else 3 for 256-wide tiles / 2.
@@ -760,11 +789,18 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         _chk(cnt, torch.int32, "cnt")
         if cnt.numel() < (OC // bm) * (KTOT // bn):
             raise ValueError("conv_wgrad: tile counter slice too small")
+    region = None
+    if defer is not None and not fuse:  # slabs (+ level-1 partials) in the batch's arena, reduced at its flush
+        region = defer.alloc((nsplit + (min(64, nsplit) if nsplit > 8 else 0)) * OC * KTOT)
+        if region is not None:
+            ws = region
     C().conv_wgrad(STEM if stem else FWD, bm, bn, dy.data_ptr(), x.data_ptr(), ws.data_ptr(), _p(in_scale),
                    _p(in_shift), int(relu_in), N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, KTOT, nsplit, ms,
                    stream_ptr(), int(lds_pad), int(dma), dw.data_ptr() if fuse else 0,
                    cnt.data_ptr() if fuse and cnt is not None else 0, float(scale), int(accumulate))
-    if not fuse:
+    if region is not None:
+        defer.add(ws, dw, OC * KTOT, nsplit, scale, accumulate)
+    elif not fuse:
         C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsplit, float(scale), int(accumulate), stream_ptr())
     return dw
 
