@@ -230,12 +230,6 @@ class ResNetProgram:
         # at NSHARD = 32 every block of an apply would re-read 64 doubles per channel: profiles/r4_s7/)
         self.coeff_in = (os.environ["DBX_COEFF_IN"] == "1" if "DBX_COEFF_IN" in os.environ
                          else self.fwd_conv_flops() < 5e10 and self.nshard <= 4)
-        # split-K weight-gradient reductions of a side-stream batch deferred to two launches at its end
-        # (K.ReduceBatch; small steps: 19 / 77 reduce launches per CIFAR / TinyImageNet step). Not on the
-        # large steps, where a reduce right behind its weight gradient still finds the slabs in L2.
-        self.defer_reduce = (os.environ["DBX_DEFER_REDUCE"] == "1" if "DBX_DEFER_REDUCE" in os.environ
-                             else self.small_step)
-        self.wred_arena = torch.empty(0, device=device, dtype=torch.float32)
         if not self.overlap_wgrad:
             # without the side stream folding costs no overlap: fold every BN-backward apply it can
             # (unless set explicitly) -- CIFAR b256 193.7k vs 189.5k img/s with overlap (r3s2_knobs)
@@ -794,8 +788,7 @@ class ResNetProgram:
             kw["cnt"] = self._wg_cnt_of.get(args[2].data_ptr())
         if self.wgrad_lds_pad and self.dev.type == "cuda" and self.overlap_wgrad:
             kw["lds_pad"] = self.wgrad_lds_pad  # occupancy cap: leave room for the main stream's kernels
-        # (a queued weight gradient takes the batch's deferred-reduction list when it is launched)
-        self._side(lambda batch=None: K.conv_wgrad(*args, defer=batch, **kw))
+        self._side(lambda: K.conv_wgrad(*args, **kw))
 
     def _flush_side(self):
         """Fork the side stream once from the main stream and launch the queued weight gradients on it."""
@@ -804,19 +797,9 @@ class ResNetProgram:
         if self._wstream is None:
             self._wstream = torch.cuda.Stream(device=self.dev)
         self._wstream.wait_stream(torch.cuda.current_stream(self.dev))
-        batch = K.ReduceBatch(self.wred_arena) if self.defer_reduce else None
         with torch.cuda.stream(self._wstream):
             for fn in self._side_q:
-                if batch is not None and getattr(fn, "__defaults__", None):
-                    fn(batch)  # a weight gradient that can defer its reduction
-                else:
-                    fn()
-            if batch is not None:
-                batch.flush()
-        if batch is not None and batch.need > self.wred_arena.numel() and not torch.cuda.is_current_stream_capturing():
-            # grown for the next batches (the eager warm-up steps size it before any capture)
-            torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
-            self.wred_arena = torch.empty(batch.need, device=self.dev, dtype=torch.float32)
+                fn()
         self._side_q = []
         self._side_pending = True
 

@@ -685,11 +685,16 @@ class ReduceBatch:
     of one backward segment): each gradient's slabs go to its own region of ``arena`` and
     :meth:`flush` finishes them all with two launches (csrc/conv_igemm.hip dbx_wgrad_reduce_multi:
     level 1 of the two-level reductions, then every final sum) instead of one or two per gradient --
-    bit-identical to ``wgrad_reduce``. A gradient whose slabs do not fit the arena's remainder is
-    reduced at once (``need`` records the size the arena should grow to, outside graph capture)."""
+    bit-identical to ``wgrad_reduce`` in eager execution. A gradient whose slabs do not fit the
+    arena's remainder is reduced at once (``need`` records the size the arena should grow to).
 
-    def __init__(self, arena: torch.Tensor):
-        self.arena, self.off, self.need, self.jobs = arena, 0, 0, []
+    NOT used by the program: inside the replayed one-graph step the batched reduce gave
+    run-to-run different gradients at replay steps while the per-gradient reduce over the same arena
+    slabs did not (profiles/r4_s10/README.md) -- root cause open; eager use is covered by
+    tests/test_wgrad_batch_gpu.py."""
+
+    def __init__(self, arena: torch.Tensor, start: int = 0):
+        self.arena, self.off, self.need, self.jobs = arena, start, start, []
 
     def alloc(self, n: int):
         self.need += n
