@@ -759,7 +759,10 @@ extern "C" int dbx_wgrad_reduce_gather(const float* ws, float* dw, int OC, int R
 // to kMaxRJobs jobs per launch pair, passed by value. Launch A runs level 1 of every two-level job
 // (the same groups as dbx_wgrad_reduce), launch B every job's final sum -- per element the same adds
 // in the same order as the per-gradient reduce, so the gradients are bit-identical; two launches
-// per batch instead of one or two per weight gradient (the small steps are launch-bound).
+// per batch instead of one or two per weight gradient (the small steps are launch-bound). Each
+// workgroup serves ONE job (a block range per job): the job is found from blockIdx alone and its
+// fields are read once, uniformly, at the start -- never per lane inside the loop (a per-lane indexed
+// job table gave run-to-run different results inside replayed graphs: profiles/r4_s10/).
 constexpr int kMaxRJobs = 32;
 struct RJob {
   const float* ws;    // nsplit slabs of n floats (+ the level-1 partials after them)
@@ -769,40 +772,40 @@ struct RJob {
 };
 struct RJobs {
   RJob j[kMaxRJobs];
-  long long pre[kMaxRJobs + 1];  // prefix of the launch's per-job work items
+  int bstart[kMaxRJobs + 1];  // first workgroup of each job
   int nj;
 };
-__device__ __forceinline__ int rjob_of(const RJobs& J, long long f) {
+__device__ __forceinline__ int rjob_of_block(const RJobs& J) {
   int k = 0;
-  while (k + 1 < J.nj && J.pre[k + 1] <= f) ++k;
-  return k;
+  while (k + 1 < J.nj && J.bstart[k + 1] <= (int)blockIdx.x) ++k;
+  return __builtin_amdgcn_readfirstlane(k);
 }
-__global__ void wgrad_reduce_multi_l1_kernel(const RJobs J) {  // items: (job, group, i) of two-level jobs
-  for (long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x; f < J.pre[J.nj];
-       f += (long long)gridDim.x * blockDim.x) {
-    const int k = rjob_of(J, f);
-    const RJob& r = J.j[k];
-    const long long loc = f - J.pre[k];
-    const int g = (int)(loc / r.n4), i = (int)(loc - (long long)g * r.n4);
-    const f32x4* w4 = reinterpret_cast<const f32x4*>(r.ws);
+__global__ void wgrad_reduce_multi_l1_kernel(const RJobs J) {  // items of job k: (group g, i) over G x n4
+  const int k = rjob_of_block(J);
+  const RJob r = J.j[k];
+  const int b0 = J.bstart[k], nb = J.bstart[k + 1] - b0;
+  const f32x4* w4 = reinterpret_cast<const f32x4*>(r.ws);
+  f32x4* p4 = reinterpret_cast<f32x4*>(const_cast<float*>(r.ws) + (size_t)r.nsplit * r.n4 * 4);
+  const long long items = (long long)r.G * r.n4;
+  for (long long f = (long long)((int)blockIdx.x - b0) * blockDim.x + threadIdx.x; f < items;
+       f += (long long)nb * blockDim.x) {
+    const int g = (int)(f / r.n4), i = (int)(f - (long long)g * r.n4);
     const int s0 = g * r.spg, s1 = min(r.nsplit, s0 + r.spg);
-    const f32x4 sum = sum_slabs_in_order(f32x4{0.f, 0.f, 0.f, 0.f}, s0, s1,
-                                         [&](int kk) { return w4[(size_t)kk * r.n4 + i]; });
-    reinterpret_cast<f32x4*>(const_cast<float*>(r.ws) + (size_t)r.nsplit * r.n4 * 4)[(size_t)g * r.n4 + i] = sum;
+    p4[(size_t)g * r.n4 + i] = sum_slabs_in_order(f32x4{0.f, 0.f, 0.f, 0.f}, s0, s1,
+                                                  [&](int kk) { return w4[(size_t)kk * r.n4 + i]; });
   }
 }
-__global__ void wgrad_reduce_multi_kernel(const RJobs J) {  // items: (job, i)
-  for (long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x; f < J.pre[J.nj];
-       f += (long long)gridDim.x * blockDim.x) {
-    const int k = rjob_of(J, f);
-    const RJob& r = J.j[k];
-    const int i = (int)(f - J.pre[k]);
-    // two-level jobs sum their G group partials, single-level ones their nsplit slabs
-    const f32x4* w4 = reinterpret_cast<const f32x4*>(r.G > 1 ? r.ws + (size_t)r.nsplit * r.n4 * 4 : r.ws);
-    const int cnt = r.G > 1 ? r.G : r.nsplit;
+__global__ void wgrad_reduce_multi_kernel(const RJobs J) {  // items of job k: i over n4
+  const int k = rjob_of_block(J);
+  const RJob r = J.j[k];
+  const int b0 = J.bstart[k], nb = J.bstart[k + 1] - b0;
+  // two-level jobs sum their G group partials, single-level ones their nsplit slabs
+  const f32x4* w4 = reinterpret_cast<const f32x4*>(r.G > 1 ? r.ws + (size_t)r.nsplit * r.n4 * 4 : r.ws);
+  const int cnt = r.G > 1 ? r.G : r.nsplit;
+  f32x4* o4 = reinterpret_cast<f32x4*>(r.dw);
+  for (int i = ((int)blockIdx.x - b0) * blockDim.x + threadIdx.x; i < r.n4; i += nb * blockDim.x) {
     f32x4 sm = sum_slabs_in_order(w4[i], 1, cnt, [&](int kk) { return w4[(size_t)kk * r.n4 + i]; });
     sm *= r.scale;
-    f32x4* o4 = reinterpret_cast<f32x4*>(r.dw);
     if (r.accumulate) sm += o4[i];
     o4[i] = sm;
   }
@@ -811,6 +814,10 @@ __global__ void wgrad_reduce_multi_kernel(const RJobs J) {  // items: (job, i)
 // jobs: (ws, dw, n, nsplit, scale, accumulate) each; the level-1 grouping is dbx_wgrad_reduce's.
 extern "C" int dbx_wgrad_reduce_multi(const float* const* ws, float* const* dw, const long long* n, const int* nsplit,
                                       const float* scale, const int* accumulate, int njobs, hipStream_t st) {
+  auto blocks_for = [](long long items) {
+    const long long b = (items + 255) / 256;
+    return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+  };
   for (int b0 = 0; b0 < njobs; b0 += kMaxRJobs) {
     RJobs A{}, B{};
     const int nb = njobs - b0 < kMaxRJobs ? njobs - b0 : kMaxRJobs;
@@ -827,19 +834,15 @@ extern "C" int dbx_wgrad_reduce_multi(const float* const* ws, float* const* dw, 
         r.spg = (r.nsplit + G - 1) / G;
         r.G = (r.nsplit + r.spg - 1) / r.spg;
         A.j[A.nj] = r;
-        A.pre[A.nj + 1] = A.pre[A.nj] + (long long)r.G * r.n4;
+        A.bstart[A.nj + 1] = A.bstart[A.nj] + blocks_for((long long)r.G * r.n4);
         ++A.nj;
       }
       B.j[B.nj] = r;
-      B.pre[B.nj + 1] = B.pre[B.nj] + r.n4;
+      B.bstart[B.nj + 1] = B.bstart[B.nj] + blocks_for(r.n4);
       ++B.nj;
     }
-    if (A.nj) {
-      const long long g = (A.pre[A.nj] + 255) / 256;
-      hipLaunchKernelGGL(wgrad_reduce_multi_l1_kernel, dim3(g > 4096 ? 4096 : (int)g), dim3(256), 0, st, A);
-    }
-    const long long g = (B.pre[B.nj] + 255) / 256;
-    hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3(g > 4096 ? 4096 : (int)g), dim3(256), 0, st, B);
+    if (A.nj) hipLaunchKernelGGL(wgrad_reduce_multi_l1_kernel, dim3(A.bstart[A.nj]), dim3(256), 0, st, A);
+    hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3(B.bstart[B.nj]), dim3(256), 0, st, B);
   }
   return (int)hipGetLastError();
 }

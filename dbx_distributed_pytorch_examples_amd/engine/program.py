@@ -230,6 +230,11 @@ class ResNetProgram:
         # at NSHARD = 32 every block of an apply would re-read 64 doubles per channel: profiles/r4_s7/)
         self.coeff_in = (os.environ["DBX_COEFF_IN"] == "1" if "DBX_COEFF_IN" in os.environ
                          else self.fwd_conv_flops() < 5e10 and self.nshard <= 4)
+        # split-K weight-gradient reductions of a side-stream batch deferred to two launches at its end
+        # (K.ReduceBatch: 19 / 77 reduce launches per CIFAR / TinyImageNet step); opt-in (A/B) until measured
+        self.defer_reduce = os.environ.get("DBX_DEFER_REDUCE", "0") == "1"
+        self.wred_arena = torch.empty(0, device=device, dtype=torch.float32)
+        self._wred_off = 0
         if not self.overlap_wgrad:
             # without the side stream folding costs no overlap: fold every BN-backward apply it can
             # (unless set explicitly) -- CIFAR b256 193.7k vs 189.5k img/s with overlap (r3s2_knobs)
@@ -788,7 +793,8 @@ class ResNetProgram:
             kw["cnt"] = self._wg_cnt_of.get(args[2].data_ptr())
         if self.wgrad_lds_pad and self.dev.type == "cuda" and self.overlap_wgrad:
             kw["lds_pad"] = self.wgrad_lds_pad  # occupancy cap: leave room for the main stream's kernels
-        self._side(lambda: K.conv_wgrad(*args, **kw))
+        # (a queued weight gradient takes the batch's deferred-reduction list when it is launched)
+        self._side(lambda batch=None: K.conv_wgrad(*args, defer=batch, **kw))
 
     def _flush_side(self):
         """Fork the side stream once from the main stream and launch the queued weight gradients on it."""
@@ -797,9 +803,22 @@ class ResNetProgram:
         if self._wstream is None:
             self._wstream = torch.cuda.Stream(device=self.dev)
         self._wstream.wait_stream(torch.cuda.current_stream(self.dev))
+        # (each batch of a step takes an arena region of its own)
+        batch = K.ReduceBatch(self.wred_arena, self._wred_off) if self.defer_reduce else None
         with torch.cuda.stream(self._wstream):
             for fn in self._side_q:
-                fn()
+                if batch is not None and getattr(fn, "__defaults__", None):
+                    fn(batch)  # a weight gradient that can defer its reduction
+                else:
+                    fn()
+            if batch is not None:
+                batch.flush()
+        if batch is not None:
+            self._wred_off = batch.off
+            if batch.need > self.wred_arena.numel() and not torch.cuda.is_current_stream_capturing():
+                # grown for the next steps (the eager warm-up steps size it before any capture)
+                torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
+                self.wred_arena = torch.empty(batch.need, device=self.dev, dtype=torch.float32)
         self._side_q = []
         self._side_pending = True
 
@@ -823,6 +842,7 @@ class ResNetProgram:
         if self._side_pending:
             torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
             self._side_pending = False
+        self._wred_off = 0  # (every batch of the step has been joined)
 
     def _bwd_head(self):
         # fc on MFMA (csrc/head_ops.hip): dW = dlogits^T pooled (fp32, straight into the flat gradient),

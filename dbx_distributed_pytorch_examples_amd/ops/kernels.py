@@ -688,10 +688,7 @@ class ReduceBatch:
     bit-identical to ``wgrad_reduce`` in eager execution. A gradient whose slabs do not fit the
     arena's remainder is reduced at once (``need`` records the size the arena should grow to).
 
-    NOT used by the program: inside the replayed one-graph step the batched reduce gave
-    run-to-run different gradients at replay steps while the per-gradient reduce over the same arena
-    slabs did not (profiles/r4_s10/README.md) -- root cause open; eager use is covered by
-    tests/test_wgrad_batch_gpu.py."""
+    The program uses it with DBX_DEFER_REDUCE=1 (engine/program.py ``_flush_side``)."""
 
     def __init__(self, arena: torch.Tensor, start: int = 0):
         self.arena, self.off, self.need, self.jobs = arena, start, start, []

@@ -42,3 +42,31 @@ def test_batched_reduce_matches_per_gradient_reduce():
     dy, x, R, _, _ = ops[1]
     ref = torch.einsum("nhwk,nhwc->kc", dy.float(), x.float()).reshape(-1) * 0.25 + 0.5
     assert (outs[1][1] - ref).abs().max() / ref.abs().max() < 1e-2
+
+
+@pytest.mark.parametrize("arch,size,batch", [("cifar_resnet18", 32, 64), ("resnet50", 64, 32)])
+def test_program_deferred_reduce_bit_identical(arch, size, batch, monkeypatch):
+    """Whole training steps (eager warm-ups, capture, replays) with the batched reduce == without,
+    bit for bit, twice (a run-to-run difference would show in one of the two)."""
+    import copy
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    torch.manual_seed(0)
+    m0 = build_model(arch, num_classes=10)
+    ms = [copy.deepcopy(m0) for _ in range(3)]
+    ts = []
+    for m, flag in zip(ms, ("0", "1", "1")):
+        monkeypatch.setenv("DBX_DEFER_REDUCE", flag)
+        ts.append(NativeTrainer(m, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05)))
+    assert ts[1].prog.defer_reduce and not ts[0].prog.defer_reduce
+    g = torch.Generator().manual_seed(1)
+    for i in range(6):
+        img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).cuda()
+        lab = torch.randint(0, 10, (batch,), generator=g).cuda()
+        for t in ts:
+            t.step(img, lab)
+        m = [t.read_metrics()[0] for t in ts]
+        assert m[0] == m[1] == m[2], (i, m)
+    assert ts[1].prog.wred_arena.numel() > 0  # the warm-up steps sized the arena before the capture
+    for t in ts[1:]:
+        assert torch.equal(ts[0].prog.master, t.prog.master)
