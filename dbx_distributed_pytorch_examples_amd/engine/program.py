@@ -231,8 +231,11 @@ class ResNetProgram:
         self.coeff_in = (os.environ["DBX_COEFF_IN"] == "1" if "DBX_COEFF_IN" in os.environ
                          else self.fwd_conv_flops() < 5e10 and self.nshard <= 4)
         # split-K weight-gradient reductions of a side-stream batch deferred to two launches at its end
-        # (K.ReduceBatch: 19 / 77 reduce launches per CIFAR / TinyImageNet step); opt-in (A/B) until measured
-        self.defer_reduce = os.environ.get("DBX_DEFER_REDUCE", "0") == "1"
+        # (K.ReduceBatch; 19 reduce launches per CIFAR step): on for the smallest steps (< 50 GFLOP),
+        # CIFAR 252.7-253.8k vs 243.7-245.5k img/s; TinyImageNet loses (93.3-93.8k vs 95.4k: its
+        # larger slabs leave L2 before the batch-end reduce), profiles/r4_s12/
+        self.defer_reduce = (os.environ["DBX_DEFER_REDUCE"] == "1" if "DBX_DEFER_REDUCE" in os.environ
+                             else self.fwd_conv_flops() < 5e10)
         self.wred_arena = torch.empty(0, device=device, dtype=torch.float32)
         self._wred_off = 0
         if not self.overlap_wgrad:

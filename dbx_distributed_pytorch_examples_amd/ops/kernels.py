@@ -688,7 +688,7 @@ class ReduceBatch:
     bit-identical to ``wgrad_reduce`` in eager execution. A gradient whose slabs do not fit the
     arena's remainder is reduced at once (``need`` records the size the arena should grow to).
 
-    The program uses it with DBX_DEFER_REDUCE=1 (engine/program.py ``_flush_side``)."""
+    The program uses it for its smallest steps (engine/program.py ``_flush_side``, DBX_DEFER_REDUCE)."""
 
     def __init__(self, arena: torch.Tensor, start: int = 0):
         self.arena, self.off, self.need, self.jobs = arena, start, start, []
