@@ -236,6 +236,9 @@ class ResNetProgram:
         # larger slabs leave L2 before the batch-end reduce), profiles/r4_s12/
         self.defer_reduce = (os.environ["DBX_DEFER_REDUCE"] == "1" if "DBX_DEFER_REDUCE" in os.environ
                              else self.fwd_conv_flops() < 5e10)
+        # (DBX_DEFER_MAX_MB: only gradients with at most this many MB of slabs are deferred; unset: all)
+        mb = os.environ.get("DBX_DEFER_MAX_MB")
+        self.defer_max_bytes = int(float(mb) * (1 << 20)) if mb else None
         self.wred_arena = torch.empty(0, device=device, dtype=torch.float32)
         self._wred_off = 0
         if not self.overlap_wgrad:
@@ -807,7 +810,8 @@ class ResNetProgram:
             self._wstream = torch.cuda.Stream(device=self.dev)
         self._wstream.wait_stream(torch.cuda.current_stream(self.dev))
         # (each batch of a step takes an arena region of its own)
-        batch = K.ReduceBatch(self.wred_arena, self._wred_off) if self.defer_reduce else None
+        batch = (K.ReduceBatch(self.wred_arena, self._wred_off, self.defer_max_bytes) if self.defer_reduce
+                 else None)
         with torch.cuda.stream(self._wstream):
             for fn in self._side_q:
                 if batch is not None and getattr(fn, "__defaults__", None):

@@ -690,8 +690,10 @@ class ReduceBatch:
 
     The program uses it for its smallest steps (engine/program.py ``_flush_side``, DBX_DEFER_REDUCE)."""
 
-    def __init__(self, arena: torch.Tensor, start: int = 0):
+    def __init__(self, arena: torch.Tensor, start: int = 0, max_slab_bytes: Optional[int] = None):
         self.arena, self.off, self.need, self.jobs = arena, start, start, []
+        # gradients whose slabs are larger are reduced at once (their slabs are still in L2 then)
+        self.max_slab_bytes = max_slab_bytes
 
     def alloc(self, n: int):
         self.need += n
@@ -792,7 +794,9 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         if cnt.numel() < (OC // bm) * (KTOT // bn):
             raise ValueError("conv_wgrad: tile counter slice too small")
     region = None
-    if defer is not None and not fuse:  # slabs (+ level-1 partials) in the batch's arena, reduced at its flush
+    if (defer is not None and not fuse and (defer.max_slab_bytes is None
+                                           or 4 * nsplit * OC * KTOT <= defer.max_slab_bytes)):
+        # slabs (+ level-1 partials) in the batch's arena, reduced at its flush
         region = defer.alloc((nsplit + (min(64, nsplit) if nsplit > 8 else 0)) * OC * KTOT)
         if region is not None:
             ws = region
