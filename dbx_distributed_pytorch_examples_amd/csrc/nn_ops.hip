@@ -1054,6 +1054,11 @@ __global__ void cast_bf16_f32_kernel(const bf16* __restrict__ x, float* __restri
 // ======================================================================================
 using namespace dbx;
 
+// grid cap of an elementwise pass whose every block also finalizes all C channels of a BN
+static inline int fin_cap(int C) {
+  const int c = (512 * 256) / (C > 0 ? C : 1);
+  return c < 512 ? 512 : (c > 4096 ? 4096 : c);
+}
 static inline int grid_for(long long n, int block = 256, int cap = 8192) {
   long long g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -1087,7 +1092,7 @@ extern "C" int dbx_bn_apply(const bf16* y, const float* sc, const float* sh, con
   if (rfin && res_mode != 2) return -2;
   const long long M = n / C;
   // (with an in-launch finalize every block derives all C channels' affine: fewer, fatter blocks)
-  const dim3 g(grid_for(M, 256 / (C / 8), (fin || rfin) ? 512 : 4096)), b(256);
+  const dim3 g(grid_for(M, 256 / (C / 8), (fin || rfin) ? fin_cap(C) : 4096)), b(256);
 #define BA(R, A) hipLaunchKernelGGL((bn_apply_kernel<R, A>), g, b, 0, st, y, sc, sh, res, rsc, rsh, out, mbits, M, C, fin, rfin)
   if (res_mode == 0) { if (relu) BA(0, true); else BA(0, false); }
   else if (res_mode == 1) { if (relu) BA(1, true); else BA(1, false); }
@@ -1118,8 +1123,9 @@ extern "C" int dbx_bn_bwd_apply(const bf16* dout, const bf16* mref, const bf16* 
                                 hipStream_t st, const BnFin* fin) {
   if (n % C || C % 8 || C / 8 > 256) return -1;
   const long long M = n / C;
-  // (with the in-launch finalize every block derives all C coefficients: fewer, fatter blocks)
-  const dim3 g(grid_for(M, 256 / (C / 8), fin ? 512 : 4096)), b(256);
+  // (with the in-launch finalize every block derives all C coefficients: fewer, fatter blocks --
+  // as many as keep that work per launch about C x 512 channel-finalizes)
+  const dim3 g(grid_for(M, 256 / (C / 8), fin ? fin_cap(C) : 4096)), b(256);
 #define BB(MK, WG) hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, WG>), g, b, 0, st, dout, mref, y, sc, sh, coeff, dy, gout, M, C, fin)
   if (mask_mode == 0) { if (gout) BB(0, true); else BB(0, false); }
   else if (mask_mode == 1) { if (gout) BB(1, true); else BB(1, false); }
@@ -1132,7 +1138,7 @@ extern "C" int dbx_bn_bwd_apply2(const bf16* g, const bf16* y1, const float* c1,
                                  const BnFin* fin2) {
   if (n % C || C % 8 || C / 8 > 256) return -1;
   const long long M = n / C;
-  hipLaunchKernelGGL(bn_bwd_apply2_kernel, dim3(grid_for(M, 256 / (C / 8), (fin1 || fin2) ? 512 : 4096)), dim3(256), 0, st, g, y1, c1, dy1,
+  hipLaunchKernelGGL(bn_bwd_apply2_kernel, dim3(grid_for(M, 256 / (C / 8), (fin1 || fin2) ? fin_cap(C) : 4096)), dim3(256), 0, st, g, y1, c1, dy1,
                      y2, c2, dy2, M, C, fin1, fin2);
   RET_LAST;
 }
