@@ -18,8 +18,10 @@ int dbx_conv_igemm(int mode, int bm, int bn, const dbx::IGemmArgs* a, int pro, i
                    hipStream_t st, int dma);
 int dbx_conv_wgrad(int mode, int bm, int bn, const dbx::WgradArgs* a, int pro, hipStream_t st, unsigned lds_pad,
                    int dma);
-int dbx_wgrad_reduce_multi(const float* const*, float* const*, const long long*, const int*, const float*, const int*,
-                           int, hipStream_t);
+int dbx_wgrad_reduce_multi_plan(const float* const*, float* const*, const long long*, const int*, const float*,
+                                const int*, int, void*, int*, int*);
+int dbx_wgrad_reduce_multi_run(const void*, int, int, int, hipStream_t);
+int dbx_wgrad_reduce_job_bytes();
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
 int dbx_wgrad_reduce_gather(const float* ws, float* dw, int OC, int R, int S, int IC, int nsplit, float scale,
                             int accumulate, hipStream_t st);
@@ -126,18 +128,25 @@ PYBIND11_MODULE(_C, m) {
     }
     check(dbx_conv_igemm(mode, bm, bn, &a, in_scale != 0, stats != 0, accum, epi, S(st), dma), "conv_igemm");
   });
-  m.def("wgrad_reduce_multi", [](std::vector<uintptr_t> ws, std::vector<uintptr_t> dw, std::vector<long long> n,
-                                  std::vector<int> nsplit, std::vector<float> scale, std::vector<int> acc, uintptr_t st) {
+  m.def("wgrad_reduce_multi_plan", [](std::vector<uintptr_t> ws, std::vector<uintptr_t> dw, std::vector<long long> n,
+                                       std::vector<int> nsplit, std::vector<float> scale, std::vector<int> acc,
+                                       uintptr_t table) {
     const size_t nj = ws.size();
     if (dw.size() != nj || n.size() != nj || nsplit.size() != nj || scale.size() != nj || acc.size() != nj)
-      throw std::invalid_argument("wgrad_reduce_multi: job lists of different lengths");
+      throw std::invalid_argument("wgrad_reduce_multi_plan: job lists of different lengths");
     std::vector<const float*> w(nj);
     std::vector<float*> d(nj);
     for (size_t q = 0; q < nj; ++q) { w[q] = P<const float*>(ws[q]); d[q] = P<float*>(dw[q]); }
-    check(dbx_wgrad_reduce_multi(w.data(), d.data(), n.data(), nsplit.data(), scale.data(), acc.data(), (int)nj,
-                                 S(st)),
-          "wgrad_reduce_multi");
+    int ga = 0, gb = 0;
+    check(dbx_wgrad_reduce_multi_plan(w.data(), d.data(), n.data(), nsplit.data(), scale.data(), acc.data(), (int)nj,
+                                      P<void*>(table), &ga, &gb),
+          "wgrad_reduce_multi_plan");
+    return std::make_pair(ga, gb);
   });
+  m.def("wgrad_reduce_multi_run", [](uintptr_t table_dev, int nj, int ga, int gb, uintptr_t st) {
+    check(dbx_wgrad_reduce_multi_run(P<const void*>(table_dev), nj, ga, gb, S(st)), "wgrad_reduce_multi_run");
+  });
+  m.def("wgrad_reduce_job_bytes", []() { return dbx_wgrad_reduce_job_bytes(); });
   m.def("conv_wgrad", [](int mode, int bm, int bn, uintptr_t dy, uintptr_t x, uintptr_t ws, uintptr_t in_scale,
                          uintptr_t in_shift, int relu_in, int N, int IH, int IW, int IC, int OH, int OW, int OC, int R,
                          int S_, int stride, int pad, int KTOT, int nsplit, int m_per_split, uintptr_t st,

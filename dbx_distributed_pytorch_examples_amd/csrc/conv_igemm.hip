@@ -755,39 +755,41 @@ extern "C" int dbx_wgrad_reduce_gather(const float* ws, float* dw, int OC, int R
   return (int)hipGetLastError();
 }
 
-// Batched split-K reductions (the deferred weight-gradient reductions of one side-stream batch): up
-// to kMaxRJobs jobs per launch pair, passed by value. Launch A runs level 1 of every two-level job
-// (the same groups as dbx_wgrad_reduce), launch B every job's final sum -- per element the same adds
-// in the same order as the per-gradient reduce, so the gradients are bit-identical; two launches
-// per batch instead of one or two per weight gradient (the small steps are launch-bound). Each
-// workgroup serves ONE job (a block range per job): the job is found from blockIdx alone and its
-// fields are read once, uniformly, at the start -- never per lane inside the loop (a per-lane indexed
-// job table gave run-to-run different results inside replayed graphs: profiles/r4_s10/).
-constexpr int kMaxRJobs = 32;
+// Batched split-K reductions (the deferred weight-gradient reductions of one side-stream batch): a
+// device job table, built once per batch shape (ops/kernels.py ReduceBatch), drives two launches --
+// A: level 1 of every two-level job (the same groups as dbx_wgrad_reduce), B: every job's final sum;
+// per element the same adds in the same order as the per-gradient reduce, so the gradients are
+// bit-identical; two launches per batch instead of one or two per weight gradient. Each workgroup
+// serves ONE job (a block range per job): it finds the job from blockIdx alone and reads the job
+// once, uniformly, before its loop. (A per-lane lookup in a by-value job table gave run-to-run
+// different results inside replayed graphs, and big by-value tables in many graph nodes are avoided
+// altogether: profiles/r4_s10/, r4_s12/.)
 struct RJob {
   const float* ws;    // nsplit slabs of n floats (+ the level-1 partials after them)
   float* dw;
   int n4, nsplit, G, spg, accumulate;
   float scale;
+  int bA, bB;         // first workgroup of the job in launch A (two-level jobs, else -1) / launch B
 };
-struct RJobs {
-  RJob j[kMaxRJobs];
-  int bstart[kMaxRJobs + 1];  // first workgroup of each job
-  int nj;
-};
-__device__ __forceinline__ int rjob_of_block(const RJobs& J) {
-  int k = 0;
-  while (k + 1 < J.nj && J.bstart[k + 1] <= (int)blockIdx.x) ++k;
+__device__ __forceinline__ int rjob_find(const RJob* __restrict__ J, int nj, bool levA) {
+  const int b = (int)blockIdx.x;
+  int k = -1;
+  for (int q = 0; q < nj; ++q) {  // (uniform: every lane scans the same table)
+    const int s = levA ? J[q].bA : J[q].bB;
+    if (s >= 0 && s <= b) k = q;
+  }
   return __builtin_amdgcn_readfirstlane(k);
 }
-__global__ void wgrad_reduce_multi_l1_kernel(const RJobs J) {  // items of job k: (group g, i) over G x n4
-  const int k = rjob_of_block(J);
-  const RJob r = J.j[k];
-  const int b0 = J.bstart[k], nb = J.bstart[k + 1] - b0;
+__global__ void wgrad_reduce_multi_l1_kernel(const RJob* __restrict__ J, int nj, int nblocks) {
+  const int k = rjob_find(J, nj, true);
+  const RJob r = J[k];
+  int nb = nblocks - r.bA;  // blocks of this job: up to the next two-level job's first block
+  for (int q = k + 1; q < nj; ++q)
+    if (J[q].bA >= 0) { nb = J[q].bA - r.bA; break; }
   const f32x4* w4 = reinterpret_cast<const f32x4*>(r.ws);
   f32x4* p4 = reinterpret_cast<f32x4*>(const_cast<float*>(r.ws) + (size_t)r.nsplit * r.n4 * 4);
   const long long items = (long long)r.G * r.n4;
-  for (long long f = (long long)((int)blockIdx.x - b0) * blockDim.x + threadIdx.x; f < items;
+  for (long long f = (long long)((int)blockIdx.x - r.bA) * blockDim.x + threadIdx.x; f < items;
        f += (long long)nb * blockDim.x) {
     const int g = (int)(f / r.n4), i = (int)(f - (long long)g * r.n4);
     const int s0 = g * r.spg, s1 = min(r.nsplit, s0 + r.spg);
@@ -795,15 +797,15 @@ __global__ void wgrad_reduce_multi_l1_kernel(const RJobs J) {  // items of job k
                                                   [&](int kk) { return w4[(size_t)kk * r.n4 + i]; });
   }
 }
-__global__ void wgrad_reduce_multi_kernel(const RJobs J) {  // items of job k: i over n4
-  const int k = rjob_of_block(J);
-  const RJob r = J.j[k];
-  const int b0 = J.bstart[k], nb = J.bstart[k + 1] - b0;
+__global__ void wgrad_reduce_multi_kernel(const RJob* __restrict__ J, int nj, int nblocks) {
+  const int k = rjob_find(J, nj, false);
+  const RJob r = J[k];
+  const int nb = (k + 1 < nj ? J[k + 1].bB : nblocks) - r.bB;
   // two-level jobs sum their G group partials, single-level ones their nsplit slabs
   const f32x4* w4 = reinterpret_cast<const f32x4*>(r.G > 1 ? r.ws + (size_t)r.nsplit * r.n4 * 4 : r.ws);
   const int cnt = r.G > 1 ? r.G : r.nsplit;
   f32x4* o4 = reinterpret_cast<f32x4*>(r.dw);
-  for (int i = ((int)blockIdx.x - b0) * blockDim.x + threadIdx.x; i < r.n4; i += nb * blockDim.x) {
+  for (int i = ((int)blockIdx.x - r.bB) * blockDim.x + threadIdx.x; i < r.n4; i += nb * blockDim.x) {
     f32x4 sm = sum_slabs_in_order(w4[i], 1, cnt, [&](int kk) { return w4[(size_t)kk * r.n4 + i]; });
     sm *= r.scale;
     if (r.accumulate) sm += o4[i];
@@ -811,41 +813,45 @@ __global__ void wgrad_reduce_multi_kernel(const RJobs J) {  // items of job k: i
   }
 }
 
-// jobs: (ws, dw, n, nsplit, scale, accumulate) each; the level-1 grouping is dbx_wgrad_reduce's.
-extern "C" int dbx_wgrad_reduce_multi(const float* const* ws, float* const* dw, const long long* n, const int* nsplit,
-                                      const float* scale, const int* accumulate, int njobs, hipStream_t st) {
+// Host side of the job table: fills `table` (host memory, njobs RJob entries) from the job lists and
+// returns the two grid sizes; the caller copies the table to the device once per batch shape.
+extern "C" int dbx_wgrad_reduce_multi_plan(const float* const* ws, float* const* dw, const long long* n,
+                                           const int* nsplit, const float* scale, const int* accumulate, int njobs,
+                                           void* table, int* grid_a, int* grid_b) {
   auto blocks_for = [](long long items) {
     const long long b = (items + 255) / 256;
     return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
   };
-  for (int b0 = 0; b0 < njobs; b0 += kMaxRJobs) {
-    RJobs A{}, B{};
-    const int nb = njobs - b0 < kMaxRJobs ? njobs - b0 : kMaxRJobs;
-    for (int t = 0; t < nb; ++t) {
-      const int q = b0 + t;
-      if (n[q] % 4) return -1;
-      RJob r{ws[q], dw[q], (int)(n[q] / 4), nsplit[q], 1, 1, accumulate[q], scale[q]};
-      const int gx = (r.n4 + 255) / 256;
-      if (r.nsplit > 8 && (long long)gx * 4 < 1024) {
-        int G = 1024 / gx;
-        if (G > r.nsplit / 4) G = r.nsplit / 4;
-        if (G > 64) G = 64;
-        if (G < 2) G = 2;
-        r.spg = (r.nsplit + G - 1) / G;
-        r.G = (r.nsplit + r.spg - 1) / r.spg;
-        A.j[A.nj] = r;
-        A.bstart[A.nj + 1] = A.bstart[A.nj] + blocks_for((long long)r.G * r.n4);
-        ++A.nj;
-      }
-      B.j[B.nj] = r;
-      B.bstart[B.nj + 1] = B.bstart[B.nj] + blocks_for(r.n4);
-      ++B.nj;
+  RJob* T = reinterpret_cast<RJob*>(table);
+  int ga = 0, gb = 0;
+  for (int q = 0; q < njobs; ++q) {
+    if (n[q] % 4) return -1;
+    RJob r{ws[q], dw[q], (int)(n[q] / 4), nsplit[q], 1, 1, accumulate[q], scale[q], -1, gb};
+    const int gx = (r.n4 + 255) / 256;
+    if (r.nsplit > 8 && (long long)gx * 4 < 1024) {
+      int G = 1024 / gx;
+      if (G > r.nsplit / 4) G = r.nsplit / 4;
+      if (G > 64) G = 64;
+      if (G < 2) G = 2;
+      r.spg = (r.nsplit + G - 1) / G;
+      r.G = (r.nsplit + r.spg - 1) / r.spg;
+      r.bA = ga;
+      ga += blocks_for((long long)r.G * r.n4);
     }
-    if (A.nj) hipLaunchKernelGGL(wgrad_reduce_multi_l1_kernel, dim3(A.bstart[A.nj]), dim3(256), 0, st, A);
-    hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3(B.bstart[B.nj]), dim3(256), 0, st, B);
+    gb += blocks_for(r.n4);
+    T[q] = r;
   }
+  *grid_a = ga;
+  *grid_b = gb;
+  return 0;
+}
+extern "C" int dbx_wgrad_reduce_multi_run(const void* table_dev, int njobs, int grid_a, int grid_b, hipStream_t st) {
+  const RJob* J = reinterpret_cast<const RJob*>(table_dev);
+  if (grid_a > 0) hipLaunchKernelGGL(wgrad_reduce_multi_l1_kernel, dim3(grid_a), dim3(256), 0, st, J, njobs, grid_a);
+  hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3(grid_b), dim3(256), 0, st, J, njobs, grid_b);
   return (int)hipGetLastError();
 }
+extern "C" int dbx_wgrad_reduce_job_bytes() { return (int)sizeof(RJob); }
 
 extern "C" int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale,
                                 int accumulate, hipStream_t st) {

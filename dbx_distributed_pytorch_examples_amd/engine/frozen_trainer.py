@@ -40,7 +40,7 @@ from ..parallel.ddp import DistributedDataParallel
 from ..utils import debug as _debug
 from .autograd_trainer import build_torch_optimizer
 from .hyper import DeviceHyper
-from .program import ResNetProgram
+from .program import ResNetProgram, release_dead_graphs
 
 
 def _backbone_proxy(model: FrozenBackboneClassifier) -> nn.Module:
@@ -218,7 +218,7 @@ class FrozenFeatureTrainer:
             if self._warm < 2:  # allocator / library handles settle in eager calls first
                 self._warm += 1
                 return self._run_backbone()
-            torch.cuda.synchronize(self.dev)
+            release_dead_graphs(self.dev)
             s = torch.cuda.Stream(device=self.dev)
             s.wait_stream(torch.cuda.current_stream(self.dev))
             g = torch.cuda.CUDAGraph()
@@ -280,7 +280,7 @@ class FrozenFeatureTrainer:
                         self._head_step(self._backbone_eager(), self.lab)
                     cur.wait_stream(s)
                     return
-                torch.cuda.synchronize(self.dev)
+                release_dead_graphs(self.dev)
                 g = torch.cuda.CUDAGraph()
                 # thread-local whenever a process group (and its watchdog thread) exists, even at world 1
                 mode = "thread_local" if (dist.is_available() and dist.is_initialized()) else "global"

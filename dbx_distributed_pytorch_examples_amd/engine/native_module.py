@@ -45,7 +45,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from .program import ResNetProgram, supports
+from .program import ResNetProgram, supports, release_dead_graphs
 
 
 class _NativeFn(torch.autograd.Function):
@@ -231,7 +231,7 @@ class NativeResNet(nn.Module):
                 self._calls[key] = n + 1
                 fn()
                 return
-            torch.cuda.synchronize(self.prog.dev)
+            release_dead_graphs(self.prog.dev)
             g = torch.cuda.CUDAGraph()
             mode = "thread_local" if (dist.is_available() and dist.is_initialized()) else "global"
             with torch.cuda.graph(g, capture_error_mode=mode):

@@ -31,7 +31,7 @@ from ..parallel.dist import host_sync_for_gloo
 from ..utils import debug as _debug
 from ..utils.profiling import PhaseTimer
 from .hyper import DeviceHyper
-from .program import ResNetProgram
+from .program import ResNetProgram, release_dead_graphs
 
 
 @dataclass
@@ -387,7 +387,7 @@ class NativeTrainer:
 
     def _capture(self):
         """Capture each phase (or the whole step when not segmented) into HIP graphs."""
-        torch.cuda.synchronize(self.dev)
+        release_dead_graphs(self.dev)
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         pool = torch.cuda.graph_pool_handle()

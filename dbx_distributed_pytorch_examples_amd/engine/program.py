@@ -55,9 +55,21 @@ def supports(model: nn.Module) -> bool:
     return True
 
 
+def release_dead_graphs(dev) -> None:
+    """Before a capture: destroy the captured graphs of dead trainers / programs (reference cycles
+    keep them until a GC pass) and drain the device after it. Graph teardown left to the collector
+    inside torch.cuda.graph's own enter (no device sync after it), or to a GC pass while another
+    thread replays, was followed by host crashes in the next graph launch on the GPU box
+    (profiles/r4_final2/README.md)."""
+    import gc
+    gc.collect()
+    torch.cuda.synchronize(dev)
+
+
 # ======================================================================================
 # specs
 # ======================================================================================
+
 @dataclass
 class ConvL:
     name: str

@@ -683,7 +683,7 @@ def wgrad_tiles_max(OC: int, KTOT: int) -> int:
 class ReduceBatch:
     """Deferred split-K reductions of a batch of weight gradients (the program's side-stream batch
     of one backward segment): each gradient's slabs go to its own region of ``arena`` and
-    :meth:`flush` finishes them all with two launches (csrc/conv_igemm.hip dbx_wgrad_reduce_multi:
+    :meth:`flush` finishes them all with two launches (csrc/conv_igemm.hip dbx_wgrad_reduce_multi_run:
     level 1 of the two-level reductions, then every final sum) instead of one or two per gradient --
     bit-identical to ``wgrad_reduce`` in eager execution. A gradient whose slabs do not fit the
     arena's remainder is reduced at once (``need`` records the size the arena should grow to).
@@ -706,11 +706,29 @@ class ReduceBatch:
     def add(self, ws, dw, n, nsplit, scale, accumulate):
         self.jobs.append((ws.data_ptr(), dw.data_ptr(), int(n), int(nsplit), float(scale), int(accumulate)))
 
+    # device job tables by job list: built in eager steps, reused (never freed: captured graphs
+    # read them) when the same batch is captured
+    _tables: dict = {}
+
     def flush(self):
-        if self.jobs:
-            cols = list(zip(*self.jobs))
-            C().wgrad_reduce_multi(*[list(c) for c in cols], stream_ptr())
-        self.jobs = []
+        jobs, self.jobs = tuple(self.jobs), []
+        if not jobs:
+            return
+        ent = ReduceBatch._tables.get(jobs)
+        if ent is None:
+            if torch.cuda.is_current_stream_capturing() or len(ReduceBatch._tables) >= 4096:
+                # no table for this batch (it was never run eagerly): reduce gradient by gradient
+                for ws, dw, n, nsplit, scale, acc in jobs:
+                    C().wgrad_reduce(ws, dw, n, nsplit, scale, acc, stream_ptr())
+                return
+            host = torch.empty(len(jobs) * C().wgrad_reduce_job_bytes(), dtype=torch.uint8)
+            cols = [list(c) for c in zip(*jobs)]
+            ga, gb = C().wgrad_reduce_multi_plan(*cols, host.data_ptr())
+            dev = torch.empty_like(host, device=torch.device("cuda", torch.cuda.current_device()))
+            dev.copy_(host)  # ordered on the current stream, before the launches below
+            ent = ReduceBatch._tables[jobs] = (dev, ga, gb)
+        dev, ga, gb = ent
+        C().wgrad_reduce_multi_run(dev.data_ptr(), len(jobs), ga, gb, stream_ptr())
 
 
 @_dispatch

@@ -25,3 +25,30 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_release(request):
+    """After every GPU test: collect the test's trainers / programs (reference cycles keep them, their
+    captured graphs and the graphs' private memory pools alive until a GC pass) and return the
+    cached memory, so one test's graphs and buffers do not pile up under the next ones.
+    (DBX_TEST_MEMLOG=1 prints the device's free memory before and after each test;
+    DBX_TEST_NO_RELEASE=1 skips this.)"""
+    yield
+    if "gpu" not in request.keywords or os.environ.get("DBX_TEST_NO_RELEASE") == "1":
+        return
+    import gc
+
+    import torch
+    if not torch.cuda.is_available():
+        return
+    log = os.environ.get("DBX_TEST_MEMLOG") == "1"
+    if log:
+        f0, tot = torch.cuda.mem_get_info()
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    if log:
+        f1, _ = torch.cuda.mem_get_info()
+        print(f"\n[memlog] {request.node.nodeid}: free {f0 / 2**30:.1f} -> {f1 / 2**30:.1f} GiB of "
+              f"{tot / 2**30:.1f}", flush=True)
