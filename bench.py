@@ -34,6 +34,7 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import dbx_distributed_pytorch_examples_amd  # noqa: E402,F401  (runtime settings read at HIP init)
 
 # Reference-equivalent stock PyTorch ResNet-50 throughput on ONE MI355X, measured with
 # `python bench.py --impl torch --batch B` (eager nn.Module, channels_last, autocast bf16, MIOpen

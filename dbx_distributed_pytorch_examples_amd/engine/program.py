@@ -833,7 +833,9 @@ class ResNetProgram:
             if batch is not None:
                 batch.flush()
         if batch is not None:
-            self._wred_off = batch.off
+            # (the next batch starts past everything this one asked for, placed or not: a warm-up
+            # step that found the arena too small then sizes it for the whole step at once)
+            self._wred_off = batch.need
             if batch.need > self.wred_arena.numel() and not torch.cuda.is_current_stream_capturing():
                 # grown for the next steps (the eager warm-up steps size it before any capture)
                 torch.cuda.current_stream(self.dev).wait_stream(self._wstream)

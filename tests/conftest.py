@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# (the HIP graph-queue setting the package applies at import, before any test touches the device:
+# dbx_distributed_pytorch_examples_amd/__init__.py)
+os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "2")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
