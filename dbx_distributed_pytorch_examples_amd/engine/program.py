@@ -237,11 +237,17 @@ class ResNetProgram:
             self.fin_in = True
         # consumer-side backward finalize: a BN-backward apply pass computes its coefficients from the
         # moment shards itself (K.bn_bwd_apply fin=) instead of a bn_bwd_coeff launch in front of it
-        # (on by default for the smallest steps, < 50 GFLOP of forward conv work, with 4-shard slabs:
-        # CIFAR 238.2-238.6k vs 233.7k img/s without it; TinyImageNet 96.5k vs 97.1k, so off there;
-        # at NSHARD = 32 every block of an apply would re-read 64 doubles per channel: profiles/r4_s7/)
+        # (on by default for the small steps with 4-shard slabs: CIFAR 238.2-238.6k vs 233.7k img/s
+        # without it; at NSHARD = 32 every block of an apply would re-read 64 doubles per channel:
+        # profiles/r4_s7/); at 50-500 GFLOP (TinyImageNet) only for BNs of <= 512 channels: 95.7-95.9k vs 95.5k img/s
+        # (all widths 94.7k: an apply that finalizes in-launch is capped near C x 512 channel-finalizes,
+        # few blocks at 2048); CIFAR keeps every width (253.1-254.0k vs 251.6-252.5k at <= 256):
+        # profiles/r4_s18/. DBX_COEFF_IN_MAXC overrides the width limit (0: none).
+        fl = self.fwd_conv_flops()
         self.coeff_in = (os.environ["DBX_COEFF_IN"] == "1" if "DBX_COEFF_IN" in os.environ
-                         else self.fwd_conv_flops() < 5e10 and self.nshard <= 4)
+                         else fl < 5e11 and self.nshard <= 4)
+        mc = os.environ.get("DBX_COEFF_IN_MAXC")
+        self.coeff_in_maxc = ((int(mc) or None) if mc else (None if fl < 5e10 else 512))
         # split-K weight-gradient reductions of a side-stream batch deferred to two launches at its end
         # (K.ReduceBatch; 19 reduce launches per CIFAR step): on for the smallest steps (< 50 GFLOP),
         # CIFAR 252.7-253.8k vs 243.7-245.5k img/s; TinyImageNet loses (93.3-93.8k vs 95.4k: its
@@ -879,6 +885,7 @@ class ResNetProgram:
         (DBX_COEFF_IN: no bn_bwd_coeff launch in front of it)?"""
         f = bn.fin_b
         return (self.coeff_in and f is not None and f.desc is not None
+                and (self.coeff_in_maxc is None or bn.C <= self.coeff_in_maxc)
                 and (count is None or float(count) == f.count))
 
     def _coeff(self, bn, count) -> None:
