@@ -268,9 +268,11 @@ def _ds_num(v: Any, auto: Union[int, float]) -> Union[int, float]:
     return float(v) if isinstance(v, str) else v
 
 
-# DeepSpeed's own optimizer defaults (torch.optim.AdamW / Adam / SGD): a key the dict omits takes
-# these, never a TrainConfig default
-_DS_OPT_DEFAULTS = {"adamw": {"weight_decay": 0.01}, "adam": {"weight_decay": 0.0},
+# DeepSpeed's own optimizer defaults: a key the dict omits takes these, never a TrainConfig default.
+# DeepSpeed builds "Adam" / "AdamW" as its FusedAdam (adam_w_mode for "AdamW"), whose weight_decay
+# defaults to 0.0 -- not torch.optim.AdamW's 0.01 (the reference dicts omit the key,
+# `02_deepspeed/deepspeed_config.py:22-32`, so their runs do not decay); SGD: torch's defaults.
+_DS_OPT_DEFAULTS = {"adamw": {"weight_decay": 0.0}, "adam": {"weight_decay": 0.0},
                     "sgd": {"weight_decay": 0.0, "momentum": 0.0}}
 
 
@@ -287,8 +289,8 @@ def from_deepspeed(ds: Dict[str, Any], base: Optional[TrainConfig] = None, world
     * string booleans (``"true"`` / ``"false"``) are parsed, not truth-tested;
     * an explicit ``train_batch_size`` is checked against micro x accumulation x world (as DeepSpeed
       does) or, without a micro batch, defines it;
-    * optimizer keys the dict omits take the optimizer's defaults (AdamW weight decay 0.01), not
-      the TrainConfig's;
+    * optimizer keys the dict omits take DeepSpeed's optimizer defaults (FusedAdam: weight decay 0.0
+      for "Adam" and "AdamW"), not the TrainConfig's;
     * WarmupLR keeps its ``warmup_type`` ("log" when absent, DeepSpeed's default).
     """
     cfg = copy.deepcopy(base) if base is not None else TrainConfig()

@@ -12,6 +12,7 @@
 // /opt/rocm/lib. Nothing links against it at build time: the extension still loads on hosts
 // without RCCL, and every entry point then raises.
 #include <dlfcn.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <rccl/rccl.h>
@@ -21,6 +22,18 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <vector>
+
+#include <pybind11/stl.h>
+
+extern "C" {
+int dbx_dar_launch(float* const*, unsigned* const*, unsigned*, int*, long long, int, int, int, double, hipStream_t);
+int dbx_dar_alloc(int, void**, void**, void**);
+int dbx_dar_free(void*, void*, void*);
+int dbx_dar_max_ranks();
+int dbx_dar_launch_multi(float* const*, unsigned* const*, unsigned* const*, int* const*, long long, int, int, double,
+                         hipStream_t);
+}
 
 namespace py = pybind11;
 
@@ -30,6 +43,7 @@ namespace comm {
 struct Api {
   ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*comm_init_rank_config)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
   ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
   ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
@@ -57,6 +71,7 @@ static Api& api() {
 #define DBX_SYM(field, name) a.field = reinterpret_cast<decltype(a.field)>(dlsym(h, name))
     DBX_SYM(get_unique_id, "ncclGetUniqueId");
     DBX_SYM(comm_init_rank, "ncclCommInitRank");
+    DBX_SYM(comm_init_rank_config, "ncclCommInitRankConfig");
     DBX_SYM(comm_destroy, "ncclCommDestroy");
     DBX_SYM(comm_abort, "ncclCommAbort");
     DBX_SYM(comm_count, "ncclCommCount");
@@ -81,6 +96,10 @@ static Api& need() {
   Api& a = api();
   if (a.origin.empty()) throw std::runtime_error("native comm: librccl could not be loaded");
   return a;
+}
+
+static void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("native comm: ") + what + ": " + hipGetErrorString(e));
 }
 
 static void check(ncclResult_t r, const char* what) {
@@ -118,7 +137,24 @@ static ncclRedOp_t op_of(int code) {
 struct Communicator {
   ncclComm_t comm = nullptr;
   int rank = 0, size = 1, device = 0;
+  bool nonblocking = false;
 };
+
+// A non-blocking communicator may answer any call with ncclInProgress (the operation is accepted
+// and completes asynchronously): wait for its state to settle (bounded), then report it.
+static ncclResult_t settle(Communicator* c, ncclResult_t r) {
+  if (r != ncclInProgress || !c || !c->comm) return r;
+  Api& a = api();
+  if (!a.comm_get_async_error) return ncclSuccess;
+  for (long it = 0; it < 6000000L; ++it) {  // ~10 min at 100 us
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t q = a.comm_get_async_error(c->comm, &st);
+    if (q != ncclSuccess) return q;
+    if (st != ncclInProgress) return st;
+    usleep(100);
+  }
+  return ncclInProgress;
+}
 
 }  // namespace comm
 }  // namespace dbx
@@ -141,8 +177,11 @@ void register_comm(py::module& m) {
     return py::bytes(id.internal, NCCL_UNIQUE_ID_BYTES);
   });
   // returns an opaque handle (pointer as int); the calling thread's current HIP device is the
-  // communicator's device
-  m.def("comm_init", [](py::bytes uid, int nranks, int rank) {
+  // communicator's device. blocking = 0: ncclCommInitRankConfig returns at once and the caller polls
+  // comm_async_error until it leaves ncclInProgress (7) -- so a rank whose peer failed before the
+  // rendezvous can abort instead of hanging inside the init (parallel/comm.py). min_ctas / max_ctas
+  // (> 0): RCCL's channel (CTA) bounds for this communicator (collective_plan.py).
+  m.def("comm_init", [](py::bytes uid, int nranks, int rank, int blocking, int min_ctas, int max_ctas) {
     std::string s = uid;
     if (s.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("native comm: bad unique id");
     if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("native comm: bad rank / size");
@@ -151,18 +190,31 @@ void register_comm(py::module& m) {
     auto* c = new Communicator();
     c->rank = rank;
     c->size = nranks;
+    c->nonblocking = !blocking;
     if (hipGetDevice(&c->device) != hipSuccess) c->device = 0;
+    Api& a = need();
     ncclResult_t r;
     {
-      py::gil_scoped_release nogil;  // init rendezvouses with the other ranks
-      r = need().comm_init_rank(&c->comm, nranks, id, rank);
+      py::gil_scoped_release nogil;  // a blocking init rendezvouses with the other ranks
+      if (a.comm_init_rank_config && (!blocking || min_ctas > 0 || max_ctas > 0)) {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = blocking ? 1 : 0;
+        if (min_ctas > 0) cfg.minCTAs = min_ctas;
+        if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+        r = a.comm_init_rank_config(&c->comm, nranks, id, rank, &cfg);
+        if (!blocking && r == ncclInProgress) r = ncclSuccess;  // completion: comm_async_error
+      } else {
+        r = a.comm_init_rank(&c->comm, nranks, id, rank);
+      }
     }
     if (r != ncclSuccess) {
       delete c;
       check(r, "ncclCommInitRank");
     }
     return reinterpret_cast<uintptr_t>(c);
-  });
+  }, py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("blocking") = 1, py::arg("min_ctas") = 0,
+     py::arg("max_ctas") = 0);
+  m.def("comm_config_supported", []() { return api().comm_init_rank_config != nullptr; });
   m.def("comm_destroy", [](uintptr_t h, bool abort) {
     auto* c = reinterpret_cast<Communicator*>(h);
     if (!c) return;
@@ -203,32 +255,106 @@ void register_comm(py::module& m) {
   m.def("comm_all_reduce", [](uintptr_t h, uintptr_t send, uintptr_t recv, size_t count, int dt, int op,
                               uintptr_t stream) {
     auto* c = reinterpret_cast<Communicator*>(h);
-    check(need().all_reduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count, dtype_of(dt),
-                            op_of(op), c->comm, reinterpret_cast<hipStream_t>(stream)),
+    check(settle(c, need().all_reduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count, dtype_of(dt),
+                            op_of(op), c->comm, reinterpret_cast<hipStream_t>(stream))),
           "ncclAllReduce");
   });
   // recvcount = elements per rank; send holds size * recvcount
   m.def("comm_reduce_scatter", [](uintptr_t h, uintptr_t send, uintptr_t recv, size_t recvcount, int dt, int op,
                                   uintptr_t stream) {
     auto* c = reinterpret_cast<Communicator*>(h);
-    check(need().reduce_scatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), recvcount,
-                                dtype_of(dt), op_of(op), c->comm, reinterpret_cast<hipStream_t>(stream)),
+    check(settle(c, need().reduce_scatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), recvcount,
+                                dtype_of(dt), op_of(op), c->comm, reinterpret_cast<hipStream_t>(stream))),
           "ncclReduceScatter");
   });
   m.def("comm_all_gather", [](uintptr_t h, uintptr_t send, uintptr_t recv, size_t sendcount, int dt,
                               uintptr_t stream) {
     auto* c = reinterpret_cast<Communicator*>(h);
-    check(need().all_gather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), sendcount,
-                            dtype_of(dt), c->comm, reinterpret_cast<hipStream_t>(stream)),
+    check(settle(c, need().all_gather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), sendcount,
+                            dtype_of(dt), c->comm, reinterpret_cast<hipStream_t>(stream))),
           "ncclAllGather");
   });
   m.def("comm_broadcast", [](uintptr_t h, uintptr_t send, uintptr_t recv, size_t count, int dt, int root,
                              uintptr_t stream) {
     auto* c = reinterpret_cast<Communicator*>(h);
-    check(need().broadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count, dtype_of(dt),
-                           root, c->comm, reinterpret_cast<hipStream_t>(stream)),
+    check(settle(c, need().broadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count, dtype_of(dt),
+                           root, c->comm, reinterpret_cast<hipStream_t>(stream))),
           "ncclBroadcast");
   });
   m.def("comm_group_start", []() { check(need().group_start(), "ncclGroupStart"); });
-  m.def("comm_group_end", []() { check(need().group_end(), "ncclGroupEnd"); });
+  m.def("comm_group_end", [](uintptr_t h) {
+    check(settle(reinterpret_cast<Communicator*>(h), need().group_end()), "ncclGroupEnd");
+  }, py::arg("h") = 0);
+
+  // ---- peer-mapped buffers for the direct xGMI all-reduce (csrc/direct_ar.hip) ----------------
+  // handle of the allocation that holds ptr + ptr's offset in it (the caching allocator hands out
+  // sub-blocks of larger segments; the peer maps the segment and adds the offset)
+  m.def("ipc_handle", [](uintptr_t ptr) -> py::tuple {
+    void* base = nullptr;
+    size_t size = 0;
+    hip_check(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(ptr)), "hipMemGetAddressRange");
+    hipIpcMemHandle_t h;
+    hip_check(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
+    return py::make_tuple(py::bytes(reinterpret_cast<const char*>(&h), sizeof(h)),
+                          (long long)(ptr - reinterpret_cast<uintptr_t>(base)));
+  });
+  m.def("ipc_open", [](py::bytes handle) -> uintptr_t {
+    std::string s = handle;
+    if (s.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("ipc_open: bad handle");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, s.data(), sizeof(h));
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("ipc_close", [](uintptr_t p) { (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(p)); });
+  m.def("dar_alloc", [](int grid) -> py::tuple {
+    void *f = nullptr, *g = nullptr, *e = nullptr;
+    const int r = dbx_dar_alloc(grid, &f, &g, &e);
+    if (r != 0) throw std::runtime_error("dar_alloc failed: hip error " + std::to_string(r));
+    return py::make_tuple(reinterpret_cast<uintptr_t>(f), reinterpret_cast<uintptr_t>(g), reinterpret_cast<uintptr_t>(e));
+  });
+  m.def("dar_free", [](uintptr_t f, uintptr_t g, uintptr_t e) {
+    dbx_dar_free(reinterpret_cast<void*>(f), reinterpret_cast<void*>(g), reinterpret_cast<void*>(e));
+  });
+  m.def("dar_max_ranks", []() { return dbx_dar_max_ranks(); });
+  // every rank of one process in one dispatch (tests: co-resident by construction)
+  m.def("dar_launch_multi", [](std::vector<uintptr_t> bufs, std::vector<uintptr_t> flags, std::vector<uintptr_t> gens,
+                               std::vector<uintptr_t> errs, long long n, int grid, double timeout_s, uintptr_t stream) {
+    const int world = (int)bufs.size();
+    if ((int)flags.size() != world || (int)gens.size() != world || (int)errs.size() != world)
+      throw std::invalid_argument("dar_launch_multi: world");
+    std::vector<float*> b(world);
+    std::vector<unsigned*> f(world), g(world);
+    std::vector<int*> e(world);
+    for (int j = 0; j < world; ++j) {
+      b[j] = reinterpret_cast<float*>(bufs[j]);
+      f[j] = reinterpret_cast<unsigned*>(flags[j]);
+      g[j] = reinterpret_cast<unsigned*>(gens[j]);
+      e[j] = reinterpret_cast<int*>(errs[j]);
+    }
+    const int r = dbx_dar_launch_multi(b.data(), f.data(), g.data(), e.data(), n, world, grid, timeout_s,
+                                       reinterpret_cast<hipStream_t>(stream));
+    if (r != 0) throw std::runtime_error("dar_launch_multi failed: code " + std::to_string(r));
+  });
+  // the error word (synchronous copy after a device sync by the caller); reset = clear it
+  m.def("dar_read_err", [](uintptr_t err, bool reset) {
+    int v = 0;
+    hip_check(hipMemcpy(&v, reinterpret_cast<void*>(err), sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy");
+    if (reset && v) hip_check(hipMemset(reinterpret_cast<void*>(err), 0, sizeof(int)), "hipMemset");
+    return v;
+  }, py::arg("err"), py::arg("reset") = false);
+  m.def("dar_launch", [](std::vector<uintptr_t> bufs, std::vector<uintptr_t> flags, uintptr_t gen, uintptr_t err,
+                         long long n, int rank, int world, int grid, double timeout_s, uintptr_t stream) {
+    if ((int)bufs.size() != world || (int)flags.size() != world) throw std::invalid_argument("dar_launch: world");
+    std::vector<float*> b(world);
+    std::vector<unsigned*> f(world);
+    for (int j = 0; j < world; ++j) {
+      b[j] = reinterpret_cast<float*>(bufs[j]);
+      f[j] = reinterpret_cast<unsigned*>(flags[j]);
+    }
+    const int r = dbx_dar_launch(b.data(), f.data(), reinterpret_cast<unsigned*>(gen), reinterpret_cast<int*>(err), n,
+                                 rank, world, grid, timeout_s, reinterpret_cast<hipStream_t>(stream));
+    if (r != 0) throw std::runtime_error("dar_launch failed: code " + std::to_string(r));
+  });
 }

@@ -3,8 +3,9 @@
 ``hfds_download_volume`` (`:8-18`), ``hf_get_num_classes`` (`:20-28`), ``create_torch_image_dataset``
 (`:31-55`) and ``default_image_transforms`` (`:58-81`, in data.transforms). There is no network on
 this image: ``load_dataset`` works from a local HF cache / local files only (``HF_DATASETS_OFFLINE``
-is forced on). ``create_torch_image_dataset`` returns a picklable top-level class (the reference's
-closure class cannot be pickled across processes, which is why `03a…:80-97` re-defines it inline).
+is forced on). ``create_torch_image_dataset`` returns a class the standard pickler handles (registered
+on this module by a name derived from the column names and re-created on demand in a fresh process);
+the reference's closure class cannot be pickled, which is why `03a…:80-97` re-defines it inline.
 """
 from __future__ import annotations
 
@@ -48,12 +49,40 @@ class HFImageDataset(Dataset):
         return image, self.labels[idx]
 
 
+_CLASSES: dict = {}
+_PREFIX = "HFImageDataset__"
+
+
+def _class_name(image_key: str, label_key: str) -> str:
+    # hex of the column names: any names give a valid, dot-free attribute name pickle can resolve
+    return f"{_PREFIX}{image_key.encode().hex()}__{label_key.encode().hex()}"
+
+
 def create_torch_image_dataset(image_key: str, label_key: str):
-    """Returns a dataset *class* bound to the column names (reference signature)."""
-
-    class CustomDataset(HFImageDataset):
+    """Returns a dataset *class* bound to the column names (reference signature,
+    `utils/hf_dataset_utilities.py:31-55`). Unlike the reference's closure class (which is why
+    `03a…:80-97` re-defines it inline), the class is registered on this module under a name derived
+    from the column names, and the module resolves such names on demand (``__getattr__``), so the
+    class and its instances go through the standard pickler -- into spawn-started DataLoader workers
+    and launcher children that never called this function."""
+    name = _class_name(image_key, label_key)
+    cls = _CLASSES.get(name)
+    if cls is None:
         def __init__(self, data, transform=None):
-            super().__init__(data, transform, image_key, label_key)
+            HFImageDataset.__init__(self, data, transform, image_key, label_key)
+        cls = type(name, (HFImageDataset,), {"__init__": __init__, "__module__": __name__, "__qualname__": name,
+                                             "image_key": image_key, "label_key": label_key})
+        _CLASSES[name] = cls
+        globals()[name] = cls
+    return cls
 
-    CustomDataset.__qualname__ = f"HFImageDataset[{image_key},{label_key}]"
-    return CustomDataset
+
+def __getattr__(name: str):
+    """PEP 562: unpickling a dataset class (or instance) in a fresh process recreates the class."""
+    if name.startswith(_PREFIX):
+        try:
+            ih, lh = name[len(_PREFIX):].split("__")
+            return create_torch_image_dataset(bytes.fromhex(ih).decode(), bytes.fromhex(lh).decode())
+        except ValueError:
+            pass
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")

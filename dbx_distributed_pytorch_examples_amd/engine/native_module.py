@@ -86,6 +86,13 @@ class NativeResNet(nn.Module):
         self._sync_queued = False
         if self.world > 1:
             self._init_distributed()
+        # the torch-module path (another batch shape) produces weight gradients in the conv backward's
+        # layout (contiguous); the parameters are channels-last views of the program's KRSC master, so
+        # autograd's accumulation would otherwise break the gradient layout contract (a copy per
+        # gradient, and a .grad that is no longer a view of the flat gradient buffer)
+        for prm in self.model.parameters():
+            if prm.dim() == 4 and prm.requires_grad:
+                prm.register_hook(_grad_to_param_layout(prm))
         if batch:
             self._build(int(batch), tuple(image_hw))
 
@@ -282,6 +289,15 @@ class NativeResNet(nn.Module):
                 prm.grad = gv
             else:
                 prm.grad.add_(gv)
+
+
+def _grad_to_param_layout(prm: torch.Tensor):
+    def hook(g: torch.Tensor) -> torch.Tensor:
+        cl = torch.channels_last
+        if prm.is_contiguous(memory_format=cl) and not prm.is_contiguous() and not g.is_contiguous(memory_format=cl):
+            return g.contiguous(memory_format=cl)
+        return g
+    return hook
 
 
 def native_module(model: nn.Module, batch: Optional[int] = None, image_hw: Optional[Tuple[int, int]] = (224, 224),

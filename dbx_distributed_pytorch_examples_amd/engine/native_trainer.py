@@ -108,6 +108,22 @@ class NativeTrainer:
             from ..parallel.comm import native_comm_requested, open_verified_comm
             if native_comm_requested():
                 self.ncomm = open_verified_comm(process_group, device)
+        # DBX_COMM_LOOPBACK=W (test aid, world 1, DP): the framework communicator's all-reduce scales
+        # by W in place -- the sum of W identical replicas -- and the update divides by W, so an
+        # ordering bug of the one-graph step (a bucket all-reduced before its gradients are final:
+        # invisible at world 1, where the collective is the identity) changes the result
+        self.loopback = 1
+        self.grad_collectives = "c10d"
+        if self.ncomm is not None:
+            self.grad_collectives = "framework RCCL communicator"
+            from ..parallel.collective_plan import direct_enabled
+            # the direct two-shot xGMI path for the ranges the plan prices below the ring (opt-in,
+            # DBX_DIRECT_AR=1: unmeasured at world >= 2 until a multi-GPU node runs it)
+            lb = int(os.environ.get("DBX_COMM_LOOPBACK", "0") or 0)
+            if lb > 1 and self.world == 1 and zero_stage == 0:
+                self.loopback = self.ncomm.loopback = lb
+            if direct_enabled() and zero_stage == 0 and self.world > 1 and self.ncomm.enable_direct(self.prog.grad):
+                self.grad_collectives += " + direct xGMI two-shot (small ranges)"
         # Weight gradients next to the per-segment collectives. In the ONE-graph step (framework
         # communicator) the batched side stream (one fork per backward segment, joined one segment
         # later: DBX_OVERLAP_WGRAD=2, the world-1 default) stays on with LATE posts: segment k's
@@ -251,9 +267,10 @@ class NativeTrainer:
             self.zero.update(hyper=self.hyper)
             return
         gsp = None
+        gdiv = self.world * self.loopback  # the reduced gradient is a sum over gdiv replicas
         if o.grad_clip and o.grad_clip > 0:
             # clip on the averaged gradient: factor computed on device (no host sync)
-            K.global_norm_clip_factor(p.grad, o.grad_clip * self.world, self.clip_work)
+            K.global_norm_clip_factor(p.grad, o.grad_clip * gdiv, self.clip_work)
             gsp = self.clip_work[2:3]
         if self.lars is not None:
             # the clip factor scales the gradient before the trust ratios, as torch's
@@ -261,12 +278,12 @@ class NativeTrainer:
             if gsp is not None:
                 p.grad.mul_(gsp)
             off, ln, adapt, norms, mx = self.lars
-            K.lars_scale(p.master, p.grad, off, ln, adapt, norms, grad_scale=1.0 / self.world,
+            K.lars_scale(p.master, p.grad, off, ln, adapt, norms, grad_scale=1.0 / gdiv,
                          eta=o.trust_coefficient, weight_decay=o.weight_decay, max_len=mx)
             K.sgd_step(p.master, p.grad, self.mom, None, lr=o.lr, momentum=o.momentum, dampening=o.dampening,
                        weight_decay=0.0, nesterov=o.nesterov, first=False, grad_scale=1.0, hyper=self.hyper)
             return
-        gscale = 1.0 / self.world
+        gscale = 1.0 / gdiv
         if o.name == "sgd":
             K.sgd_step(p.master, p.grad, self.mom, None, lr=o.lr, momentum=o.momentum, dampening=o.dampening,
                        weight_decay=o.weight_decay, nesterov=o.nesterov, first=False, grad_scale_ptr=gsp,
@@ -293,17 +310,18 @@ class NativeTrainer:
     def _allreduce_range(self, lo: int, hi: int):
         g = self.prog.grad
         if self.ncomm is not None:  # enqueued on the current (comm) stream; capturable
-            pos = lo
-            while pos < hi:
-                end = min(hi, pos + self.bucket_cap)
-                chunk = g[pos:end]
+            from ..parallel.collective_plan import plan_allreduce
+            esz = torch.tensor([], dtype=self.ar_dtype).element_size()
+            plan = plan_allreduce(hi - lo, esz, self.world, self.bucket_cap,
+                                  allow_direct=self.ncomm.direct is not None and self.ar_dtype == torch.float32)
+            for a, b in plan.buckets:
+                chunk = g[lo + a:lo + b]
                 if self.ar_dtype == torch.float32:
-                    self.ncomm.all_reduce(chunk)
+                    self.ncomm.all_reduce(chunk)  # direct path when the plan picked it (NativeComm.all_reduce)
                 else:
                     buf = chunk.to(self.ar_dtype)
                     self.ncomm.all_reduce(buf)
                     chunk.copy_(buf)
-                pos = end
             return
         host_sync_for_gloo(g, self.pg)
         pos = lo

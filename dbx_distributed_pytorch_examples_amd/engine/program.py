@@ -45,6 +45,13 @@ def _repoint(p: nn.Parameter, view: torch.Tensor) -> None:
     p.data = view
     if p.grad is not None and (p.grad.device != view.device or p.grad.shape != view.shape):
         p.grad = None
+    elif p.grad is not None and p.grad.stride() != view.stride():
+        # a gradient accumulated before compilation (e.g. a first batch on the torch module) keeps
+        # its values in the parameter's NEW layout (KRSC: channels-last), or every later accumulation
+        # into it breaks autograd's gradient layout contract
+        g = torch.empty_strided(view.shape, view.stride(), dtype=p.grad.dtype, device=view.device)
+        g.copy_(p.grad)
+        p.grad = g
 
 
 def supports(model: nn.Module) -> bool:
@@ -62,6 +69,9 @@ def release_dead_graphs(dev) -> None:
     thread replays, was followed by host crashes in the next graph launch on the GPU box
     (profiles/r4_final2/README.md)."""
     import gc
+
+    from .. import check_graph_queues
+    check_graph_queues()
     gc.collect()
     torch.cuda.synchronize(dev)
 

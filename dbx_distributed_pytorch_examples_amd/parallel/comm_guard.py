@@ -66,7 +66,8 @@ class CommWatchdog:
         if comm is not None:
             self.comms.append(comm)
 
-    def step_begin(self, step: int) -> None:
+    def step_begin(self, step) -> None:
+        """``step``: a step number, or a phase label (bench.py brackets "setup" / "warmup" / "timed")."""
         with self._lock:
             self._host_t0 = time.monotonic()
             self._step = step
@@ -83,6 +84,8 @@ class CommWatchdog:
                 self._ev, self._ev_t0 = ev, time.monotonic()
 
     def close(self) -> None:
+        with self._lock:  # nothing in flight any more: a late poll must not fire
+            self._host_t0, self._ev = None, None
         self._stop.set()
         self._th.join(timeout=2 * self.poll + 1)
 
@@ -99,10 +102,11 @@ class CommWatchdog:
         now = time.monotonic()
         with self._lock:
             t0, step, ev, et0 = self._host_t0, self._step, self._ev, self._ev_t0
+        what = f"step {step}" if isinstance(step, int) else f"phase {step!r}"
         if t0 is not None and now - t0 > self.timeout:
-            return f"step {step} has not completed its collectives within {self.timeout:.0f}s (host)"
+            return f"{what} has not completed its collectives within {self.timeout:.0f}s (host)"
         if ev is not None and now - et0 > self.timeout and not ev.query():
-            return f"device work of step {step} has not completed within {self.timeout:.0f}s"
+            return f"device work of {what} has not completed within {self.timeout:.0f}s"
         return None
 
     def _loop(self) -> None:

@@ -47,6 +47,7 @@ def build_torch_step(args, info) -> Tuple[Callable[[], None], Dict]:
         loss.backward()
         opt.step()
 
+    step.model = model  # bench.py replica check
     return step, {"memory_format": "channels_last" if args.channels_last else "nchw",
                   "ddp": "torch DDP 25MiB buckets" if info.world_size > 1 else "none"}
 

@@ -325,121 +325,125 @@ def train(cfg: Optional[TrainConfig] = None, model: Optional[torch.nn.Module] = 
     res = TrainResult(model=model, engine=engine)
     from ..parallel import comm_guard
     watchdog = comm_guard.for_runner(runner, dev)  # a hung / failed peer ends this rank (launcher restarts)
-    # --- resume ----------------------------------------------------------------------------
-    start_epoch, step = 0, 0
-    if cfg.checkpoint_dir and (cfg.resume == "latest" or int(os.environ.get("DBX_RESTART_COUNT", "0")) > 0):
-        path = ckpt.latest_checkpoint(cfg.checkpoint_dir)
-        if path:
-            st = torch.load(path, map_location="cpu", weights_only=True)
+    try:
+        # --- resume ----------------------------------------------------------------------------
+        start_epoch, step = 0, 0
+        if cfg.checkpoint_dir and (cfg.resume == "latest" or int(os.environ.get("DBX_RESTART_COUNT", "0")) > 0):
+            path = ckpt.latest_checkpoint(cfg.checkpoint_dir)
+            if path:
+                st = torch.load(path, map_location="cpu", weights_only=True)
+                model.load_state_dict(st["model"])
+                _params_changed(runner)
+                _restore_trainer_state(runner, st.get("trainer"))
+                start_epoch, step = int(st.get("epoch", 0)), int(st.get("step", 0))
+                _restore_shard_state(runner, cfg.checkpoint_dir, start_epoch)
+                res.history = list(st.get("history", []))
+                res.resumed_epoch = start_epoch
+                _log(f"[train] resumed from {path} (epoch {start_epoch}, step {step})")
+        elif cfg.resume and cfg.resume != "latest":
+            st = torch.load(cfg.resume, map_location="cpu", weights_only=True)
             model.load_state_dict(st["model"])
             _params_changed(runner)
-            _restore_trainer_state(runner, st.get("trainer"))
-            start_epoch, step = int(st.get("epoch", 0)), int(st.get("step", 0))
-            _restore_shard_state(runner, cfg.checkpoint_dir, start_epoch)
-            res.history = list(st.get("history", []))
-            res.resumed_epoch = start_epoch
-            _log(f"[train] resumed from {path} (epoch {start_epoch}, step {step})")
-    elif cfg.resume and cfg.resume != "latest":
-        st = torch.load(cfg.resume, map_location="cpu", weights_only=True)
-        model.load_state_dict(st["model"])
-        _params_changed(runner)
-    # --- mlflow ------------------------------------------------------------------------------
-    is_main = ddist.get_rank() == 0
-    if is_main and log_mlflow:
-        mlflow.set_experiment(cfg.experiment)
-        run = mlflow.start_run(run_name=cfg.run_name or None, nested=mlflow.active_run() is not None)
-        res.run_id = run.info.run_id
-        mlflow.log_params({"batch_size": cfg.batch_size, "epochs": epochs, "learning_rate": cfg.optim.lr,
-                           "model_type": cfg.model, "optimizer": cfg.optim.name, "weight_decay": cfg.optim.weight_decay,
-                           "scheduler": cfg.sched.name, "num_gpus": ddist.get_world_size(), "engine": engine,
-                           "zero_stage": cfg.zero.stage, "trainer": "dbx_amd"})
-    _log(f"[train] engine={engine} world={ddist.get_world_size()} steps/epoch={spe} total_steps={total}")
-    best_val, bad_epochs = -1.0, 0
-    t_start = time.perf_counter()
-    imgs = 0
-    stop = False
-    for epoch in range(start_epoch, epochs):
-        t0 = time.perf_counter()
-        n_local = 0  # samples actually stepped this epoch (early stop / short final batch)
-        t_wait = t_wall = 0.0  # wall_clock_breakdown: host time waiting for batches / per logging window
-        t_mark = time.perf_counter()
-        n_win = 0
-        it = iter(runner.epoch_batches(epoch))
-        while step < total:
-            t_b = time.perf_counter()
-            batch = next(it, None)
-            if batch is None:
-                break
-            t_wait += time.perf_counter() - t_b
-            runner.set_lr(sched(step))
-            fault.heartbeat(step)
-            if fault.maybe_inject(step):
-                raise FloatingPointError(f"injected NaN loss at step {step}")
+        # --- mlflow ------------------------------------------------------------------------------
+        is_main = ddist.get_rank() == 0
+        if is_main and log_mlflow:
+            mlflow.set_experiment(cfg.experiment)
+            run = mlflow.start_run(run_name=cfg.run_name or None, nested=mlflow.active_run() is not None)
+            res.run_id = run.info.run_id
+            mlflow.log_params({"batch_size": cfg.batch_size, "epochs": epochs, "learning_rate": cfg.optim.lr,
+                               "model_type": cfg.model, "optimizer": cfg.optim.name, "weight_decay": cfg.optim.weight_decay,
+                               "scheduler": cfg.sched.name, "num_gpus": ddist.get_world_size(), "engine": engine,
+                               "zero_stage": cfg.zero.stage, "trainer": "dbx_amd"})
+        _log(f"[train] engine={engine} world={ddist.get_world_size()} steps/epoch={spe} total_steps={total}")
+        best_val, bad_epochs = -1.0, 0
+        t_start = time.perf_counter()
+        imgs = 0
+        stop = False
+        for epoch in range(start_epoch, epochs):
+            t0 = time.perf_counter()
+            n_local = 0  # samples actually stepped this epoch (early stop / short final batch)
+            t_wait = t_wall = 0.0  # wall_clock_breakdown: host time waiting for batches / per logging window
+            t_mark = time.perf_counter()
+            n_win = 0
+            it = iter(runner.epoch_batches(epoch))
+            while step < total:
+                t_b = time.perf_counter()
+                batch = next(it, None)
+                if batch is None:
+                    break
+                t_wait += time.perf_counter() - t_b
+                runner.set_lr(sched(step))
+                fault.heartbeat(step)
+                if fault.maybe_inject(step):
+                    raise FloatingPointError(f"injected NaN loss at step {step}")
+                if watchdog is not None:
+                    watchdog.step_begin(step)
+                runner.step(batch)
+                if watchdog is not None:
+                    watchdog.step_end()
+                step += 1
+                n_win += 1
+                n_local += runner.batch_samples(batch)
+                imgs += cfg.batch_size * ddist.get_world_size()
+                if cfg.log_every and step % cfg.log_every == 0:
+                    if cfg.wall_clock_breakdown:  # DeepSpeed's per-window timing (synchronised at the window end)
+                        if dev.type == "cuda":
+                            torch.cuda.synchronize()
+                        t_wall = time.perf_counter() - t_mark
+                        if is_main:
+                            print(f"[wall_clock_breakdown] steps {step - n_win + 1}-{step}: "
+                                  f"{1e3 * t_wall / n_win:.2f} ms/step, data wait {1e3 * t_wait / n_win:.2f} ms/step, "
+                                  f"compute+sync {1e3 * (t_wall - t_wait) / n_win:.2f} ms/step", flush=True)
+                        t_wait, n_win, t_mark = 0.0, 0, time.perf_counter()
+                    if is_main:
+                        print(f"[TRAINING] [RANK {ddist.get_rank()}] step {step}/{total} (epoch {epoch + 1})", flush=True)
             if watchdog is not None:
-                watchdog.step_begin(step)
-            runner.step(batch)
+                watchdog.step_begin(step)  # the epoch-end collectives are bounded too
+            loss_sum, correct = runner.read_metrics()
+            loss_sum, correct, n = ddist.all_reduce_sum([loss_sum, correct, float(n_local)])
             if watchdog is not None:
                 watchdog.step_end()
-            step += 1
-            n_win += 1
-            n_local += runner.batch_samples(batch)
-            imgs += cfg.batch_size * ddist.get_world_size()
-            if cfg.log_every and step % cfg.log_every == 0:
-                if cfg.wall_clock_breakdown:  # DeepSpeed's per-window timing (synchronised at the window end)
-                    if dev.type == "cuda":
-                        torch.cuda.synchronize()
-                    t_wall = time.perf_counter() - t_mark
-                    if is_main:
-                        print(f"[wall_clock_breakdown] steps {step - n_win + 1}-{step}: "
-                              f"{1e3 * t_wall / n_win:.2f} ms/step, data wait {1e3 * t_wait / n_win:.2f} ms/step, "
-                              f"compute+sync {1e3 * (t_wall - t_wait) / n_win:.2f} ms/step", flush=True)
-                    t_wait, n_win, t_mark = 0.0, 0, time.perf_counter()
-                if is_main:
-                    print(f"[TRAINING] [RANK {ddist.get_rank()}] step {step}/{total} (epoch {epoch + 1})", flush=True)
+            if not fault.check_finite(loss_sum):
+                raise FloatingPointError(f"non-finite training loss in epoch {epoch + 1}")
+            rec = {"epoch": epoch + 1, "train_loss": loss_sum / max(1.0, n), "train_accuracy": correct / max(1.0, n),
+                   "learning_rate": sched(max(0, step - 1)), "epoch_time_s": time.perf_counter() - t0}
+            if eval_dataset is not None and cfg.eval_every and (epoch + 1) % cfg.eval_every == 0:
+                rec.update(evaluate(runner, eval_dataset))
+            res.history.append(rec)
+            if is_main:
+                _log(f"Epoch [{epoch + 1}/{epochs}], Loss: {rec['train_loss']:.4f}, Accuracy: {rec['train_accuracy']:.4f}"
+                     + (f", Val Loss: {rec['val_loss']:.4f}, Val Accuracy: {rec['val_accuracy']:.4f}" if "val_loss" in rec else ""))
+                if log_mlflow:
+                    mlflow.log_metrics({k: v for k, v in rec.items() if k != "epoch"}, step=epoch + 1)
+            for cb in callbacks or []:
+                cb(epoch + 1, rec, runner)
+            if cfg.checkpoint_dir and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
+                _sync_master(runner)  # every rank (collective): ZeRO shards -> full fp32 parameters
+                _save_shard_state(runner, cfg.checkpoint_dir, epoch + 1)  # every rank: its ZeRO shard
+            if cfg.checkpoint_dir and is_main and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
+                ckpt.save_checkpoint(cfg.checkpoint_dir, runner.model, None, epoch + 1, step=step,
+                                     trainer=_trainer_state(runner), history=res.history, config=json.dumps(to_dict(cfg)))
+            ddist.barrier()
+            if "val_accuracy" in rec:
+                res.best_val_accuracy = max(res.best_val_accuracy, rec["val_accuracy"])
+                if cfg.patience:
+                    if rec["val_accuracy"] > best_val:
+                        best_val, bad_epochs = rec["val_accuracy"], 0
+                    else:
+                        bad_epochs += 1
+                    stop = bool(ddist.broadcast_object(bad_epochs >= cfg.patience))
+            if stop:
+                _log(f"[train] early stopping after epoch {epoch + 1} (patience {cfg.patience})")
+                break
+            if step >= total:
+                break
+        if torch.cuda.is_available() and dev.type == "cuda":
+            torch.cuda.synchronize()
+    finally:
+        # every exit (an exception out of a step included): a live watchdog would otherwise end the
+        # process DBX_COMM_TIMEOUT seconds later, under a caller that caught the exception
         if watchdog is not None:
-            watchdog.step_begin(step)  # the epoch-end collectives are bounded too
-        loss_sum, correct = runner.read_metrics()
-        loss_sum, correct, n = ddist.all_reduce_sum([loss_sum, correct, float(n_local)])
-        if watchdog is not None:
-            watchdog.step_end()
-        if not fault.check_finite(loss_sum):
-            raise FloatingPointError(f"non-finite training loss in epoch {epoch + 1}")
-        rec = {"epoch": epoch + 1, "train_loss": loss_sum / max(1.0, n), "train_accuracy": correct / max(1.0, n),
-               "learning_rate": sched(max(0, step - 1)), "epoch_time_s": time.perf_counter() - t0}
-        if eval_dataset is not None and cfg.eval_every and (epoch + 1) % cfg.eval_every == 0:
-            rec.update(evaluate(runner, eval_dataset))
-        res.history.append(rec)
-        if is_main:
-            _log(f"Epoch [{epoch + 1}/{epochs}], Loss: {rec['train_loss']:.4f}, Accuracy: {rec['train_accuracy']:.4f}"
-                 + (f", Val Loss: {rec['val_loss']:.4f}, Val Accuracy: {rec['val_accuracy']:.4f}" if "val_loss" in rec else ""))
-            if log_mlflow:
-                mlflow.log_metrics({k: v for k, v in rec.items() if k != "epoch"}, step=epoch + 1)
-        for cb in callbacks or []:
-            cb(epoch + 1, rec, runner)
-        if cfg.checkpoint_dir and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
-            _sync_master(runner)  # every rank (collective): ZeRO shards -> full fp32 parameters
-            _save_shard_state(runner, cfg.checkpoint_dir, epoch + 1)  # every rank: its ZeRO shard
-        if cfg.checkpoint_dir and is_main and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
-            ckpt.save_checkpoint(cfg.checkpoint_dir, runner.model, None, epoch + 1, step=step,
-                                 trainer=_trainer_state(runner), history=res.history, config=json.dumps(to_dict(cfg)))
-        ddist.barrier()
-        if "val_accuracy" in rec:
-            res.best_val_accuracy = max(res.best_val_accuracy, rec["val_accuracy"])
-            if cfg.patience:
-                if rec["val_accuracy"] > best_val:
-                    best_val, bad_epochs = rec["val_accuracy"], 0
-                else:
-                    bad_epochs += 1
-                stop = bool(ddist.broadcast_object(bad_epochs >= cfg.patience))
-        if stop:
-            _log(f"[train] early stopping after epoch {epoch + 1} (patience {cfg.patience})")
-            break
-        if step >= total:
-            break
-    if torch.cuda.is_available() and dev.type == "cuda":
-        torch.cuda.synchronize()
-    if watchdog is not None:
-        watchdog.close()
+            watchdog.close()
     el = time.perf_counter() - t_start
     _sync_master(runner)  # the returned / logged model holds the full parameters on every rank
     res.steps = step

@@ -36,6 +36,7 @@ def build_native_step(args, info):
         def step():
             tr.step()
 
+    step.trainer = tr  # bench.py: replica check, watchdog registration
     if tr.zero is not None:
         extra["zero"] = (f"ZeRO-{tr.zero.stage}: per-segment fp32 reduce-scatter (overlapped with backward), sharded "
                          f"{opt.name} update, bf16 all-gather; {tr.zero.bytes_per_step / 2**20:.1f} MiB sent/rank/step")
@@ -45,6 +46,7 @@ def build_native_step(args, info):
                           f"{str(ar_dtype).split('.')[-1]}, overlapped per backward segment"
                           + (" (framework RCCL communicator, whole step one HIP graph, weight-gradient side stream "
                              "with late posts)" if tr.ncomm is not None else " (c10d between per-segment graphs)"))
+                  + (f"; collectives: {tr.grad_collectives}" if tr.world > 1 else "")
                   if tr.world > 1 or getattr(tr, "segmented", False) else "none",
                   "kernels": "dbx HIP (conv implicit-GEMM MFMA + fused BN/ReLU/pool/CE/SGD)"}
 

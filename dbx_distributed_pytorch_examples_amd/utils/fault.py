@@ -5,7 +5,9 @@
 * :func:`maybe_inject` — deterministic fault injection for tests: ``DBX_FAULT="rank:step:kind"``
   with kind ``exit`` (os._exit(3)), ``raise`` (RuntimeError), ``hang`` (sleep forever),
   ``nan`` (returns True so the caller poisons its loss), ``comm_hang`` (keeps beating but never
-  issues another collective: the peers' ``parallel.comm_guard`` watchdog must end the job). Only fires on attempt
+  issues another collective: the peers' ``parallel.comm_guard`` watchdog must end the job), ``diverge``
+  (consumed by ``bench.py``: the rank perturbs its parameters after warm-up, and the replica check
+  must refuse to report). Only fires on attempt
   ``DBX_FAULT_ATTEMPT`` (default 0) so a restarted job can run clean.
 * :func:`check_finite` — cross-rank divergence / NaN guard (one all-reduce of a flag).
 """
@@ -60,8 +62,8 @@ def maybe_inject(step: int) -> bool:
         while True:  # alive to the heartbeat watchdog, silent to the collectives
             heartbeat(step)
             time.sleep(0.5)
-    if kind == "nan":
-        return True
+    if kind in ("nan", "diverge"):
+        return kind == "nan"
     raise ValueError(f"unknown fault kind {kind!r}")
 
 

@@ -47,3 +47,33 @@ def test_no_gpus_visible_fails_before_spawning():
         pytest.skip("two GPUs visible: --gpus 2 would run")
     r = _run(["--gpus", "2", "--steps", "1"], {"DBX_DIST_BACKEND": ""})
     assert r.returncode == 3 and "GPU(s) visible" in r.stderr
+
+
+def test_two_rank_bench_checks_replicas():
+    """World > 1: bench.py checks after warm-up and after the timed steps that every rank holds
+    bit-identical parameters (the check runs in the gloo rehearsal of the driver's N-GPU command)."""
+    r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "1"],
+             {"DBX_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "replicas in sync after warm-up" in r.stderr and "replicas in sync after the timed steps" in r.stderr
+    _line(r.stdout)
+
+
+def test_diverged_replica_refuses_to_report():
+    r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "1"],
+             {"DBX_DIST_BACKEND": "gloo", "DBX_FAULT": "1:0:diverge"})
+    assert r.returncode == 4 and "diverged" in r.stderr, r.stderr[-2000:]
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
+
+
+def test_stalled_rank_ends_the_bench_within_the_timeout():
+    """A rank that stops in warm-up (DBX_FAULT hang) must not leave the N-GPU bench blocked until the
+    driver's timeout: the watchdog names the phase and the job exits 75 within DBX_BENCH_TIMEOUT."""
+    import time
+    t0 = time.time()
+    r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2"],
+             {"DBX_DIST_BACKEND": "gloo", "DBX_FAULT": "1:1:hang", "DBX_BENCH_TIMEOUT": "10"})
+    assert r.returncode == 75, r.stderr[-2000:]
+    assert "[comm-watchdog]" in r.stderr and "phase 'warmup'" in r.stderr
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
+    assert time.time() - t0 < 120

@@ -120,3 +120,47 @@ def test_open_verified_comm_world1(world1):
     from dbx_distributed_pytorch_examples_amd.parallel.comm import open_verified_comm
     c = open_verified_comm(None, torch.device("cuda"))
     assert c is not None and c.verify()
+
+
+def test_nonblocking_init_and_captured_check(world1):
+    """Non-blocking RCCL init (polled to completion), the eager check collectives and the captured one
+    (all-reduce on a forked side stream inside a HIP graph, joined back; two replays)."""
+    from dbx_distributed_pytorch_examples_amd.parallel.comm import NativeComm
+    c = NativeComm(blocking=False, timeout_s=120)
+    assert c.async_error()[0] == 0
+    assert c.verify(60) and c.verify_captured(60)
+    x = torch.arange(1000, device="cuda", dtype=torch.float32)
+    c.all_reduce(x)
+    torch.cuda.synchronize()
+    assert torch.equal(x, torch.arange(1000, device="cuda", dtype=torch.float32))
+    c.close()
+
+
+@pytest.mark.parametrize("model,hw,batch", [("resnet18", 32, 32), ("resnet50", 64, 16)])
+def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batch):
+    """The one-graph multi-rank step's all-reduce ORDER, checked at world 1: with DBX_COMM_LOOPBACK=2
+    every bucket all-reduce doubles its range in place (the sum of two identical replicas) and the
+    update halves it, so the trajectory equals the plain one bit for bit -- unless a bucket is reduced
+    before its weight gradients are final (late posts, batched side stream), which at world 1 with a
+    real all-reduce (the identity) would go unnoticed."""
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    monkeypatch.setenv("DBX_SEGMENTED_GRAPHS", "1")
+    monkeypatch.setenv("DBX_COMM", "native")
+    torch.manual_seed(0)
+    m1 = build_model(model, num_classes=10)
+    m2 = copy.deepcopy(m1)
+    monkeypatch.setenv("DBX_COMM_LOOPBACK", "2")
+    t1 = NativeTrainer(m1, batch, (hw, hw), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    monkeypatch.delenv("DBX_COMM_LOOPBACK")
+    t2 = NativeTrainer(m2, batch, (hw, hw), torch.device("cuda"), optim=OptimConfig(lr=0.05))
+    assert t1.ncomm is not None and t1.loopback == 2 and t2.loopback == 1 and t1.late_posts
+    g = torch.Generator().manual_seed(1)
+    for i in range(6):
+        img = torch.randint(0, 256, (batch, hw, hw, 3), dtype=torch.uint8, generator=g).cuda()
+        lab = torch.randint(0, 10, (batch,), generator=g).cuda()
+        t1.step(img, lab)
+        t2.step(img, lab)
+        assert t1.read_metrics()[0] == t2.read_metrics()[0], i
+    assert len(t1.graphs) == 1
+    assert torch.equal(t1.prog.master, t2.prog.master)

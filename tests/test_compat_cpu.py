@@ -70,7 +70,7 @@ def test_reference_deepspeed_dicts_load(name):
     assert cfg.zero.stage == stage
     assert cfg.optim.name == "adamw" and cfg.optim.lr == 2e-4 and cfg.optim.betas == (0.9, 0.999)
     assert cfg.optim.eps == 1e-8
-    assert cfg.optim.weight_decay == 0.01  # AdamW's own default: the dict omits it
+    assert cfg.optim.weight_decay == 0.0  # DeepSpeed's FusedAdam default (adam_w_mode): the dict omits it
     assert cfg.optim.grad_clip == 0.3 and cfg.precision == "bf16"
     assert cfg.batch_size == 4 and cfg.grad_accum == 1
     assert cfg.sched.name == "warmup_lr" and cfg.sched.warmup_steps == 100 and cfg.sched.warmup_type == "linear"
@@ -322,3 +322,37 @@ def test_train_func_logs_reference_artifact_names(tmp_path, monkeypatch):
                 names |= set(os.listdir(a))
     assert {"cifar_torch_distributor_resnet", "tiny_imagenet_torch_distributor_resnet"} <= names, names
     assert mlflow.active_run() is None
+
+
+def test_native_module_fallback_grads_follow_param_layout():
+    """native_module's torch-module path (a batch of another shape): the weight gradient of the conv
+    backward arrives in its own layout (contiguous from MIOpen) while the parameters are channels-last
+    views of the program's KRSC master; the wrapper's hooks hand autograd channels-last gradients for
+    channels-last parameters, and leave every other gradient untouched. (On the GPU the Composer test
+    in test_program_gpu.py must run without the layout-contract warning.)"""
+    from dbx_distributed_pytorch_examples_amd.engine.native_module import _grad_to_param_layout, native_module
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    r18 = build_model("resnet18", num_classes=10)
+    native_module(r18, batch=None, device=torch.device("cpu"))
+    assert all(p._backward_hooks for p in r18.parameters() if p.dim() == 4)
+    w_cl = torch.randn(8, 3, 3, 3).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(8, 3, 3, 3)
+    out = _grad_to_param_layout(w_cl)(g)
+    assert out.is_contiguous(memory_format=torch.channels_last) and torch.equal(out, g)
+    w_c = torch.randn(8, 3, 3, 3)
+    assert _grad_to_param_layout(w_c)(g) is g  # contiguous parameter: nothing to do
+    w_1 = torch.randn(8, 1, 1, 1)  # both layouts at once (1x1 / 1-channel): nothing to do
+    assert _grad_to_param_layout(w_1)(g[:, :1, :1, :1]).data_ptr() == g.data_ptr()
+
+
+def test_repoint_keeps_a_precompile_grad_in_the_new_layout():
+    """A gradient that exists before the program is compiled (a first batch through the torch module)
+    is re-laid-out with the parameter (KRSC master view: channels-last), values kept."""
+    from dbx_distributed_pytorch_examples_amd.engine.program import _repoint
+    p = torch.nn.Parameter(torch.randn(8, 4, 3, 3))
+    p.grad = torch.randn(8, 4, 3, 3)
+    g0 = p.grad.clone()
+    master = torch.empty(8 * 3 * 3 * 4)
+    view = master.view(8, 3, 3, 4).permute(0, 3, 1, 2)
+    _repoint(p, view)
+    assert p.grad.stride() == view.stride() and torch.equal(p.grad, g0)

@@ -200,3 +200,24 @@ def test_learnable_synthetic_is_deterministic_and_class_structured():
     d = ((xv.float()[:, None] - means[None]) ** 2).flatten(2).sum(-1)
     acc = (d.argmin(1) == yv).float().mean().item()
     assert acc > 0.3, acc
+
+
+def test_hf_dataset_class_pickles_with_the_standard_pickler():
+    """create_torch_image_dataset's class and instances survive plain pickle, also in a fresh process
+    that never created the class (spawn DataLoader workers, launcher children)."""
+    import pickle
+    import subprocess
+    import sys
+    from dbx_distributed_pytorch_examples_amd.data.hf import create_torch_image_dataset
+    cls = create_torch_image_dataset("img", "fine label")
+    assert create_torch_image_dataset("img", "fine label") is cls
+    ds = cls({"img": [1, 2, 3], "fine label": [0, 1, 1]})
+    blob = pickle.dumps(ds)
+    back = pickle.loads(blob)
+    assert type(back) is cls and back[2] == (3, 1) and back.num_classes == 2
+    assert pickle.loads(pickle.dumps(cls)) is cls
+    code = ("import pickle, sys; ds = pickle.loads(sys.stdin.buffer.read()); "
+            "print(type(ds).image_key, type(ds).label_key, len(ds), ds[1])")
+    r = subprocess.run([sys.executable, "-c", code], input=blob, capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    assert r.stdout.decode().strip() == "img fine label 3 (2, 1)"

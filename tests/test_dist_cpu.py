@@ -511,3 +511,40 @@ def test_open_verified_comm_falls_back_together(tmp_path):
         assert any("c10d" in str(x.message) for x in w)
     finally:
         tdist.destroy_process_group()
+
+
+def test_watchdog_closed_when_a_step_raises(tmp_path):
+    """A step that raises inside train() must not leave the comm watchdog armed: a caller that catches
+    the exception and carries on (a notebook, an in-process retry) would otherwise be killed
+    DBX_COMM_TIMEOUT seconds later by the watchdog's exit."""
+    import subprocess
+    import sys
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import sys, time, torch\n"
+        f"sys.path.insert(0, {os.path.dirname(os.path.abspath(__file__))!r})\n"
+        "from test_dist_cpu import TinyNet, _to_tensor\n"
+        "from dbx_distributed_pytorch_examples_amd.config import TrainConfig\n"
+        "from dbx_distributed_pytorch_examples_amd.data.datasets import SyntheticImages\n"
+        "from dbx_distributed_pytorch_examples_amd.train.engine import train\n"
+        "cfg = TrainConfig(model='tiny', num_classes=5, batch_size=4, epochs=1, log_every=0, engine='autograd')\n"
+        "cfg.data.num_workers = 0\n"
+        "class Boom(TinyNet):\n"
+        "    calls = 0\n"
+        "    def forward(self, x):\n"
+        "        Boom.calls += 1\n"
+        "        if Boom.calls == 2:\n"
+        "            raise RuntimeError('injected fault inside the step')\n"
+        "        return super().forward(x)\n"
+        "try:\n"
+        "    train(cfg, model=Boom(), train_dataset=SyntheticImages(16, 8, 3, 5, seed=1, transform=_to_tensor),\n"
+        "          log_mlflow=False)\n"
+        "except RuntimeError as e:\n"
+        "    print('caught', e, flush=True)\n"
+        "time.sleep(4)\n"
+        "print('alive', flush=True)\n")
+    env = dict(os.environ, DBX_COMM_TIMEOUT="1",
+               PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=300)
+    assert "caught injected fault" in r.stdout, r.stderr[-2000:]
+    assert r.returncode == 0 and "alive" in r.stdout, (r.returncode, r.stderr[-2000:])

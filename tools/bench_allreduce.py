@@ -1,10 +1,21 @@
 #!/usr/bin/env python3
-"""RCCL all-reduce / reduce-scatter / all-gather bandwidth over message sizes (the DDP bucket
-sizing check of SURVEY.md §7.2 step 4): algbw = bytes / time, busbw = algbw * 2(n-1)/n for
-all-reduce ((n-1)/n for reduce-scatter / all-gather), as nccl-tests report them.
+"""Collective bandwidth over message sizes, nccl-tests style: the
+record that calibrates ``parallel/collective_plan.py`` on a multi-GPU node.
 
-  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_allreduce.py
-  (CPU / gloo: DBX_DIST_BACKEND=gloo ... --device cpu)
+For every size and path it prints an nccl-tests-format row
+``size count type redop time(us) algbw(GB/s) busbw(GB/s) #wrong`` (busbw = algbw x 2(n-1)/n for
+all-reduce, (n-1)/n for reduce-scatter / all-gather) and one JSON line per size; at the end one JSON
+summary line with a ``metric`` key (peak all-reduce bus bandwidth) and the model's prediction next
+to every measured point.
+
+Paths (``--path``, comma-separated or ``all``):
+  c10d    torch.distributed on the process group (RCCL under "nccl")
+  native  the framework communicator (parallel/comm.py NativeComm: RCCL driven directly)
+  direct  the direct two-shot xGMI all-reduce (csrc/direct_ar.hip over hipIPC-mapped buffers;
+          all-reduce only, world <= 8)
+
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_allreduce.py --path all
+  (CPU / gloo: DBX_DIST_BACKEND=gloo ... --device cpu --path c10d)
 """
 import argparse
 import json
@@ -16,53 +27,115 @@ import torch
 import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dbx_distributed_pytorch_examples_amd.parallel import collective_plan as cp  # noqa: E402
 from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--sizes-mb", default="1,4,16,25,64,102,256")
+    ap.add_argument("--sizes-mb", default="0.0625,0.25,1,4,16,25,64,102,256")
     ap.add_argument("--dtype", default="float32", choices=["float32", "bfloat16"])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--device", default=None, help="cuda | cpu (default: cuda when available)")
+    ap.add_argument("--path", default="c10d", help="c10d,native,direct or all")
+    ap.add_argument("--ops", default="all_reduce,reduce_scatter,all_gather")
     a = ap.parse_args()
     info = ddist.init_distributed(device=a.device)
     n = info.world_size
     dt = getattr(torch, a.dtype)
     esz = torch.tensor([], dtype=dt).element_size()
-    sync = (lambda: torch.cuda.synchronize()) if info.device.type == "cuda" else (lambda: None)
+    on_gpu = info.device.type == "cuda"
+    sync = (lambda: torch.cuda.synchronize()) if on_gpu else (lambda: None)
+    paths = ["c10d", "native", "direct"] if a.path == "all" else a.path.split(",")
+    nc = None
+    if on_gpu and ("native" in paths or "direct" in paths):
+        from dbx_distributed_pytorch_examples_amd.parallel.comm import open_verified_comm
+        nc = open_verified_comm(None, info.device)
+        if nc is None:
+            paths = [p for p in paths if p == "c10d"]
+    sizes = [float(s) for s in a.sizes_mb.split(",")]
+    maxel = int(max(sizes) * (1 << 20) // esz) // n * n
+    big = torch.ones(maxel, dtype=dt, device=info.device)
+    if "direct" in paths:
+        if dt != torch.float32 or not nc.enable_direct(big):
+            paths = [p for p in paths if p != "direct"]
+    topo = cp.XgmiTopology(n)
     rows = []
-    for mb in [float(s) for s in a.sizes_mb.split(",")]:
+    if info.rank == 0:
+        print(f"# world {n} backend {info.backend} dtype {a.dtype} paths {','.join(paths)}")
+        print(f"# {'path':>7} {'op':>15} {'size':>12} {'count':>11} {'type':>8} {'redop':>5} "
+              f"{'time(us)':>10} {'algbw':>7} {'busbw':>7} {'#wrong':>6} {'model_us':>9}")
+    for mb in sizes:
         numel = int(mb * (1 << 20) // esz) // n * n
-        x = torch.ones(numel, dtype=dt, device=info.device)
+        x = big[:numel]
         shard = torch.empty(numel // n, dtype=dt, device=info.device)
         res = {}
-        for op in ("all_reduce", "reduce_scatter", "all_gather"):
-            def run():
+        for path in paths:
+            for op in a.ops.split(","):
+                if path == "direct" and op != "all_reduce":
+                    continue
+
+                def run():
+                    if path == "c10d":
+                        if op == "all_reduce":
+                            dist.all_reduce(x)
+                        elif op == "reduce_scatter":
+                            dist.reduce_scatter_tensor(shard, x)
+                        else:
+                            dist.all_gather_into_tensor(x, shard)
+                    elif path == "native":
+                        if op == "all_reduce":
+                            nc._c.comm_all_reduce(nc._h, x.data_ptr(), x.data_ptr(), x.numel(), 0 if dt == torch.float32 else 1,
+                                                  0, torch.cuda.current_stream().cuda_stream)
+                        elif op == "reduce_scatter":
+                            nc.reduce_scatter(shard, x)
+                        else:
+                            nc.all_gather(x, shard)
+                    else:
+                        nc.direct.all_reduce(x)
+                # correctness first (the #wrong column): ones summed over n ranks
+                x.fill_(1.0)
+                shard.fill_(1.0)
+                run()
+                sync()
                 if op == "all_reduce":
-                    dist.all_reduce(x)
+                    wrong = int((x != float(n)).sum().item())
                 elif op == "reduce_scatter":
-                    dist.reduce_scatter_tensor(shard, x)
+                    wrong = int((shard != float(n)).sum().item())
                 else:
-                    dist.all_gather_into_tensor(x, shard)
-            for _ in range(3):
-                run()
-            sync()
-            ddist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(a.iters):
-                run()
-            sync()
-            dt_s = ddist.all_reduce_max((time.perf_counter() - t0) / a.iters)
-            nbytes = numel * esz
-            algbw = nbytes / dt_s / 1e9
-            factor = 2 * (n - 1) / n if op == "all_reduce" else (n - 1) / n
-            res[op] = {"us": round(dt_s * 1e6, 1), "algbw_GBps": round(algbw, 1), "busbw_GBps": round(algbw * factor, 1)}
+                    wrong = int((x != 1.0).sum().item())
+                for _ in range(3):
+                    run()
+                sync()
+                ddist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(a.iters):
+                    run()
+                sync()
+                dt_s = ddist.all_reduce_max((time.perf_counter() - t0) / a.iters)
+                nbytes = numel * esz
+                algbw = nbytes / dt_s / 1e9
+                factor = 2 * (n - 1) / n if op == "all_reduce" else (n - 1) / n
+                model = (cp.direct_allreduce_us(nbytes, topo) if path == "direct" else
+                         cp.ring_allreduce_us(nbytes, topo)) if op == "all_reduce" else None
+                r = {"us": round(dt_s * 1e6, 1), "algbw_GBps": round(algbw, 2),
+                     "busbw_GBps": round(algbw * factor, 2), "wrong": wrong,
+                     "model_us": round(model, 1) if model is not None else None}
+                res[f"{path}/{op}"] = r
+                if info.rank == 0:
+                    print(f"  {path:>7} {op:>15} {nbytes:>12} {numel:>11} {a.dtype:>8} {'sum':>5} {r['us']:>10.1f} "
+                          f"{r['algbw_GBps']:>7.2f} {r['busbw_GBps']:>7.2f} {wrong:>6} "
+                          f"{(r['model_us'] if r['model_us'] is not None else float('nan')):>9.1f}", flush=True)
         rows.append({"size_mb": mb, **res})
         if info.rank == 0:
             print(json.dumps({"size_mb": mb, **res}), flush=True)
     if info.rank == 0:
-        print(json.dumps({"world": n, "backend": info.backend, "dtype": a.dtype, "results": rows}))
+        ar = [v["busbw_GBps"] for r in rows for k, v in r.items() if k.endswith("/all_reduce")]
+        print(json.dumps({"metric": "all-reduce bus bandwidth (nccl-tests busbw, peak over sizes)",
+                          "value": max(ar) if ar else None, "unit": "GB/s", "world": n, "backend": info.backend,
+                          "dtype": a.dtype, "paths": paths, "results": rows}))
+    if nc is not None:
+        nc.close()
     ddist.destroy()
 
 
