@@ -335,6 +335,9 @@ static int launch_fast(const IGemmArgs& a, hipStream_t st) {
   const int ntile = (a.OC / BN) * ((a.M + 255) / 256);
   if (pp)
     hipLaunchKernelGGL((pp_igemm_kernel<BN, MODE, STATS, ACCUM, EPI>), dim3(ntile), dim3(512), 0, st, a);
+  else if (deep && BN == 256 && getenv("DBX_FAST_SLOTS") && atoi(getenv("DBX_FAST_SLOTS")) == 5)
+    // A/B: five 32-channel slots (the whole 160 KiB: four stages in flight behind the MFMAs)
+    hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, 5, 32>), dim3(ntile), dim3(512), 0, st, a);
   else if (deep)
     hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, BN == 256 ? 4 : 6, 32>), dim3(ntile), dim3(512),
                        0, st, a);

@@ -380,53 +380,73 @@ __global__ __launch_bounds__(64 * WM * WN, (BM * BN >= 256 * 256) ? 1 : 2) void 
   const int mend = min(a.M, mbeg + a.m_per_split);
   const int nkb = (mend - mbeg + BKM - 1) / BKM;
 
-  // per DMA instruction j: the pixel row inside the block and the source chunk (swizzle inverse)
-  int a_row[DA], a_cc[DA], b_row[DB], b_off[DB], b_th[DB], b_tw[DB];
+  // per DMA instruction j: the pixel row inside the block and the source chunk (swizzle inverse).
+  // A (dy rows): a_base[j] = the row's element offset relative to the block's first pixel.
+  // B (im2col of x): the source position is carried from block to block instead of re-derived --
+  // packed (oh << 16 | ow) of the row's pixel and the element offset of its tap, advanced by the
+  // block's BKM pixels as a mixed-radix add (carries ow -> oh -> n), so the issue path has no
+  // pixel -> (n, oh, ow) divisions (40+ quarter-rate multiplies per block and wave before).
+  int a_row[DA], a_base[DA], b_row[DB], b_off[DB];
+  unsigned b_pos[DB], b_tap[DB];  // (oh << 16) | ow ; (th << 16) | tw
 #pragma unroll
   for (int j = 0; j < DA; ++j) {
     const int p = (j * NW + wid) * 64 + lane;
     a_row[j] = p / NCA;
-    a_cc[j] = tr_swz(a_row[j], p % NCA, NCA);
+    a_base[j] = a_row[j] * a.OC + k0 + tr_swz(a_row[j], p % NCA, NCA) * 8;
   }
+  const int ohw = a.OH * a.OW;
 #pragma unroll
   for (int j = 0; j < DB; ++j) {
     const int p = (j * NW + wid) * 64 + lane;
     b_row[j] = p / NCB;
     const int kk = kk0 + tr_swz(b_row[j], p % NCB, NCB) * 8;
     const int tap = kk / a.IC, ch = kk - (kk / a.IC) * a.IC;
-    b_th[j] = tap / a.S;
-    b_tw[j] = tap - b_th[j] * a.S;
-    b_off[j] = (b_th[j] * a.IW + b_tw[j]) * a.IC + ch;
+    const int th = tap / a.S, tw = tap - (tap / a.S) * a.S;
+    b_tap[j] = ((unsigned)th << 16) | (unsigned)tw;
+    const int mb = mbeg + b_row[j];  // the row's pixel in block 0 (mb < 2^31: any value decomposes)
+    const int n = mdiv(mb, a.mag_ohw);
+    const int pq = mb - n * ohw;
+    const int oh = mdiv(pq, a.mag_ow), ow = pq - oh * a.OW;
+    b_pos[j] = ((unsigned)oh << 16) | (unsigned)ow;
+    b_off[j] = ((n * a.IH + oh * a.stride - a.pad + th) * a.IW + ow * a.stride - a.pad + tw) * a.IC + ch;
   }
+  // one block = BKM pixels = s_n images + s_oh rows + s_ow columns (s_oh < OH, s_ow < OW)
+  const int s_ow = BKM % a.OW, s_oh = (BKM / a.OW) % a.OH, s_n = BKM / ohw;
+  const unsigned pinc = ((unsigned)s_oh << 16) | (unsigned)s_ow;
+  const int d0 = (s_n * a.IH * a.IW + (s_oh * a.IW + s_ow) * a.stride) * a.IC;  // no carry
+  const int d1 = (a.IW - a.OW) * a.stride * a.IC;                               // ow wrapped: next row
+  const int d2 = (a.IH - a.OH * a.stride) * a.IW * a.IC;                        // oh wrapped: next image
   const i32x4 dyr = make_srd(a.dy, 2ull * a.M * a.OC);
   const i32x4 xr = make_srd(a.x, 2ull * a.N * a.IH * a.IW * a.IC);
   const unsigned lbase = lds_addr(lds);
-  const int ohw = a.OH * a.OW;
 
-  // issue block kb into ring slot s (rows past the split / blocks past the end read out of range:
-  // zeros, no traffic). Branch-free: every address is computed, the validity only selects kOOB.
+  // issue block kb (the next block in order: every call advances the B positions by one block) into
+  // ring slot s; rows past the split / blocks past the end read out of range: zeros, no traffic.
+  // Branch-free: every address is computed, the validity only selects kOOB.
   auto issue = [&](int kb, int s) __attribute__((always_inline)) {
     const unsigned sa = lbase + 2u * (unsigned)(s * IMG);
     const unsigned sb = sa + 2u * (unsigned)(BKM * BM);
     const int m0 = mbeg + kb * BKM;
-    const int mlim = kb < nkb ? mend : 0;  // wave-uniform
+    const int rows = (kb < nkb ? mend : 0) - m0;  // wave-uniform: rows of this block inside the split
 #pragma unroll
     for (int j = 0; j < DA; ++j) {
-      const int ma = m0 + a_row[j];
-      const unsigned off = ma < mlim ? 2u * (unsigned)(ma * a.OC + k0 + a_cc[j] * 8) : kOOB;
+      const unsigned off = a_row[j] < rows ? 2u * (unsigned)(m0 * a.OC + a_base[j]) : kOOB;
       lds_dma16(dyr, off, sa + 1024u * (unsigned)(j * NW + wid));
     }
 #pragma unroll
     for (int j = 0; j < DB; ++j) {
-      const int mb = m0 + b_row[j];
-      const int n = mdiv(mb, a.mag_ohw);  // mb < 2^31: any value decomposes (n >= N reads nothing)
-      const int pq = mb - n * ohw;
-      const int oh = mdiv(pq, a.mag_ow), ow = pq - oh * a.OW;
-      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
-      const bool v = mb < mlim && (unsigned)(ih0 + b_th[j]) < (unsigned)a.IH &&
-                     (unsigned)(iw0 + b_tw[j]) < (unsigned)a.IW;
-      const unsigned off = v ? 2u * (unsigned)(((n * a.IH + ih0) * a.IW + iw0) * a.IC + b_off[j]) : kOOB;
-      lds_dma16(xr, off, sb + 1024u * (unsigned)(j * NW + wid));
+      const int ih = __mul24((int)(b_pos[j] >> 16), a.stride) - a.pad + (int)(b_tap[j] >> 16);
+      const int iw = __mul24((int)(b_pos[j] & 0xFFFFu), a.stride) - a.pad + (int)(b_tap[j] & 0xFFFFu);
+      const bool v = b_row[j] < rows && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+      lds_dma16(xr, v ? 2u * (unsigned)b_off[j] : kOOB, sb + 1024u * (unsigned)(j * NW + wid));
+      // advance to the same row of the next block
+      unsigned pos = b_pos[j] + pinc;
+      const bool c1 = (int)(pos & 0xFFFFu) >= a.OW;
+      pos += c1 ? 0x10000u - (unsigned)a.OW : 0u;
+      const bool c2 = (int)(pos >> 16) >= a.OH;
+      pos -= c2 ? (unsigned)a.OH << 16 : 0u;
+      b_pos[j] = pos;
+      b_off[j] += d0 + (c1 ? d1 : 0) + (c2 ? d2 : 0);
     }
   };
 
@@ -664,7 +684,12 @@ static void launch_wgrad_dma_t(const WgradArgs& a, int nblk, hipStream_t st, uns
   constexpr int WM = BIG ? 2 : (BM == 256) ? 4 : 2;
   constexpr int WN = (BN == 256) ? 4 : 2;
   if constexpr (BIG) {
-    if (dma == 4)
+    // DBX_WGRAD_RING5=1 (A/B): the 32-pixel stages in a 5-slot ring (160 KiB: four stages in flight
+    // behind the MFMAs instead of three); only without an occupancy pad (the LDS is full)
+    static const bool ring5 = [] { const char* e = getenv("DBX_WGRAD_RING5"); return e && e[0] == '1'; }();
+    if (ring5 && lds_pad == 0)  // (either operand path of the table)
+      hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 5, 32>), dim3(nblk), dim3(64 * WM * WN), 0, st, a);
+    else if (dma == 4)
       hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 4, 32>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
     else
       hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 2, 64>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
