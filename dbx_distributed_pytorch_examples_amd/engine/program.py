@@ -521,6 +521,26 @@ class ResNetProgram:
             wsmax = max(wsmax, cv.OC * ktot)
         # split-K wgrad workspace: up to 64 splits of the largest layer, >= 64 MiB
         self.ws = torch.empty(max(64 * wsmax, 16 << 20), device=dev, dtype=torch.float32)
+        # The step's exposed end (tools/step_timeline.py): after the last data gradient only the side
+        # stream's last batch (layer1's weight gradients) and the stem weight gradient behind it run.
+        # Small steps (< 0.5 TFLOP of forward conv work) run the stem weight gradient on the main stream
+        # beside that batch (DBX_STEM_WG_MAIN; CIFAR 257.0-257.6k vs 252.1-253.8k, TinyImageNet 96.7-96.8k
+        # vs 96.0-96.1k img/s; the b1024 headline loses 0.3 %: 16.48-16.49k vs 16.53-16.55k), and the
+        # TinyImageNet class (50-500 GFLOP) also moves the batch's last two gradients to the main
+        # stream's end (DBX_TAIL_MAIN, their own workspace of ws's size: the same split depths, the same
+        # bits): 97.5-97.8k img/s; CIFAR loses with it (profiles/r5_tail/)
+        fl = self.fwd_conv_flops()
+        self.stem_wg_main = (os.environ["DBX_STEM_WG_MAIN"] == "1" if "DBX_STEM_WG_MAIN" in os.environ
+                             else fl < 5e11)
+        self.tail_main = int(os.environ["DBX_TAIL_MAIN"] if "DBX_TAIL_MAIN" in os.environ
+                             else (2 if 5e10 <= fl < 5e11 else 0))
+        self._main_tail = []
+        # the stem weight gradient's own slabs when it runs on the main stream (its split count depends
+        # on the grid, not on the workspace capacity)
+        self.ws_stem = (torch.empty(40 << 20, device=dev, dtype=torch.float32)
+                        if dev.type == "cuda" and self.stem_wg_main else self.ws)
+        self.ws_main = (torch.empty_like(self.ws) if (self.tail_main > 0 and dev.type == "cuda"
+                                                       and self.side_batch and self.overlap_wgrad) else self.ws)
         # per-conv tile counters of the in-launch split-K reduction (K.conv_wgrad cnt=): zeroed once,
         # every launch leaves them zero again; keyed by the gradient view's address
         body = [cv for cv in self.convs if not cv.stem]
@@ -798,7 +818,8 @@ class ResNetProgram:
         segs.append(("stem", self._bwd_stem))
         # every segment ends with its weight gradients complete on the main stream (join)
         last = len(segs) - 1
-        self._segments = [(n, (lambda fn=fn, k=k: (fn(), self._join_side(final=k == last))))
+        self._segments = [(n, (lambda fn=fn, k=k: (fn(), self._join_side(final=k == last,
+                                                                         tail_main=k == last - 1))))
                           for k, (n, fn) in enumerate(segs)]
         return self._segments
 
@@ -828,7 +849,9 @@ class ResNetProgram:
         if self.wgrad_lds_pad and self.dev.type == "cuda" and self.overlap_wgrad:
             kw["lds_pad"] = self.wgrad_lds_pad  # occupancy cap: leave room for the main stream's kernels
         # (a queued weight gradient takes the batch's deferred-reduction list when it is launched)
-        self._side(lambda batch=None: K.conv_wgrad(*args, defer=batch, **kw))
+        # (ws: the workspace override of a gradient moved to the main stream's tail, see _join_side)
+        self._side(lambda batch=None, ws=None: K.conv_wgrad(*args[:3], args[3] if ws is None else ws, *args[4:],
+                                                          defer=batch, **kw))
 
     def _flush_side(self):
         """Fork the side stream once from the main stream and launch the queued weight gradients on it."""
@@ -863,14 +886,26 @@ class ResNetProgram:
         if self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
             self._flush_side()  # this block's weight gradients, under the next block's data gradients
 
-    def _join_side(self, final: bool = True):
+    def _join_side(self, final: bool = True, tail_main: bool = False):
         if self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad:
             # batched side stream: the segment's weight gradients fork ONCE, after its data gradients,
             # and run under the NEXT segment's backward; joined one segment later (at most one batch in
             # flight: they share self.ws) and at the end of the backward
+            if final and self._main_tail:
+                # the last batch's tail (moved off the side stream at the previous join) on the main
+                # stream, after the stem's backward, beside the batch's head on the side stream
+                for fn in self._main_tail:
+                    fn(None, self.ws_main)
+                self._main_tail = []
             if self._side_pending:
                 torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
                 self._side_pending = False
+            if tail_main and self.tail_main > 0 and len(self._side_q) > self.tail_main:
+                # the LAST batch (layer1) is exposed at the end of the step: only the stem's short
+                # backward runs beside it. Its last DBX_TAIL_MAIN gradients go to the main stream's
+                # end instead (their own workspace), the rest forks as usual
+                self._main_tail = self._side_q[-self.tail_main:]
+                self._side_q = self._side_q[:-self.tail_main]
             self._flush_side()
             if not final:
                 return
@@ -1116,15 +1151,23 @@ class ResNetProgram:
         else:
             K.maxpool_bwd(dp, self.parg, self.da0, K=self.pool_k, stride=self.pool_s, pad=self.pool_p)
             self._bn_bwd(sbn, self.da0, self.y0, self.dy0, self.N * st.OH * st.OW, K.MASK_Y)
+        # small steps (stem_wg_main, see __init__): with the batched side stream the stem weight gradient
+        # runs on the MAIN stream right here, next to the side stream's last batch (layer1's weight
+        # gradients, forked at layer1's end) instead of queued behind it; its slabs live in ws_stem
+        on_main = self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad and self.stem_wg_main
+
         def stem_wgrad():
             # reduced straight into the flat gradient's (OC, R, S, IC) slice when the stem tile kernel
             # runs (no padded temporary + strided copy)
             g = self.grad[st.off:st.off + st.numel]
-            out = K.conv_wgrad(self.dy0, self.x4, self.stem_grad_tmp, self.ws, R=st.R, S=st.S, stride=st.stride,
-                               pad=st.pad, stem=True, out_krsc=g)
+            out = K.conv_wgrad(self.dy0, self.x4, self.stem_grad_tmp, self.ws_stem if on_main else self.ws, R=st.R,
+                               S=st.S, stride=st.stride, pad=st.pad, stem=True, out_krsc=g)
             if out is not g:
                 g.view(st.OC, st.R, st.S, st.IC).copy_(self.stem_grad_tmp.view(st.OC, 8, 8, 4)[:, :st.R, :st.S, :st.IC])
-        self._side(stem_wgrad)
+        if on_main:
+            stem_wgrad()
+        else:
+            self._side(stem_wgrad)
 
     def backward(self):
         for _, fn in self._segments:

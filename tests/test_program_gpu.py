@@ -456,7 +456,7 @@ def test_composer_trainer_runs_on_native_module():
     assert 0.0 <= hist[-1]["metrics/eval/Accuracy"] <= 1.0
 
 
-@pytest.mark.parametrize("mode", ["2", "3"])
+@pytest.mark.parametrize("mode", ["2", "3", "2+tail2"])
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64)])
 def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch):
     """DBX_OVERLAP_WGRAD=2 (weight gradients forked once per backward segment, joined one segment
@@ -470,11 +470,15 @@ def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch)
     # the same BN-backward fold schedule on both sides (without the side stream it defaults to fold-all)
     monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(1 << 25))
     monkeypatch.setenv("DBX_FOLD_MAX_RATIO", "1")
-    monkeypatch.setenv("DBX_OVERLAP_WGRAD", mode)
+    # "2+tail2": the last batch's two last weight gradients on the main stream's tail (DBX_TAIL_MAIN),
+    # the stem weight gradient on the main stream (the batched default)
+    monkeypatch.setenv("DBX_OVERLAP_WGRAD", mode[0])
+    monkeypatch.setenv("DBX_TAIL_MAIN", "2" if "tail2" in mode else "0")
     t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "0")
     t2 = NativeTrainer(m2, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
-    assert (t1.prog.side_batch if mode == "2" else t1.prog.side_block) and t1.prog.overlap_wgrad
+    assert (t1.prog.side_batch if mode[0] == "2" else t1.prog.side_block) and t1.prog.overlap_wgrad
+    assert t1.prog.tail_main == (2 if "tail2" in mode else 0)
     assert not t2.prog.overlap_wgrad
     g = torch.Generator().manual_seed(3)
     for i in range(5):
