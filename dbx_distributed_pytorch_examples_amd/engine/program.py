@@ -534,12 +534,13 @@ class ResNetProgram:
                              else fl < 5e11)
         self.tail_main = int(os.environ["DBX_TAIL_MAIN"] if "DBX_TAIL_MAIN" in os.environ
                              else (2 if 5e10 <= fl < 5e11 else 0))
+        self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
         self._main_tail = []
         # the stem weight gradient's own slabs when it runs on the main stream (its split count depends
         # on the grid, not on the workspace capacity)
         self.ws_stem = (torch.empty(40 << 20, device=dev, dtype=torch.float32)
                         if dev.type == "cuda" and self.stem_wg_main else self.ws)
-        self.ws_main = (torch.empty_like(self.ws) if (self.tail_main > 0 and dev.type == "cuda"
+        self.ws_main = (torch.empty_like(self.ws) if ((self.tail_main > 0 or self.seg_tail_main > 0) and dev.type == "cuda"
                                                        and self.side_batch and self.overlap_wgrad) else self.ws)
         # per-conv tile counters of the in-launch split-K reduction (K.conv_wgrad cnt=): zeroed once,
         # every launch leaves them zero again; keyed by the gradient view's address
@@ -891,21 +892,23 @@ class ResNetProgram:
             # batched side stream: the segment's weight gradients fork ONCE, after its data gradients,
             # and run under the NEXT segment's backward; joined one segment later (at most one batch in
             # flight: they share self.ws) and at the end of the backward
-            if final and self._main_tail:
-                # the last batch's tail (moved off the side stream at the previous join) on the main
-                # stream, after the stem's backward, beside the batch's head on the side stream
+            if self._main_tail:
+                # the previous batch's tail (moved off the side stream at the previous join) on the main
+                # stream, after this segment's data gradients, beside the batch's head on the side stream
                 for fn in self._main_tail:
                     fn(None, self.ws_main)
                 self._main_tail = []
             if self._side_pending:
                 torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
                 self._side_pending = False
-            if tail_main and self.tail_main > 0 and len(self._side_q) > self.tail_main:
-                # the LAST batch (layer1) is exposed at the end of the step: only the stem's short
-                # backward runs beside it. Its last DBX_TAIL_MAIN gradients go to the main stream's
-                # end instead (their own workspace), the rest forks as usual
-                self._main_tail = self._side_q[-self.tail_main:]
-                self._side_q = self._side_q[:-self.tail_main]
+            # the LAST batch (layer1) is exposed at the end of the step: only the stem's short backward
+            # runs beside it -- its last DBX_TAIL_MAIN gradients go to the main stream's end instead
+            # (their own workspace); DBX_SEG_TAIL_MAIN does the same for the middle batches (a batch the
+            # side stream cannot finish within the next segment makes the main stream wait at the join)
+            n = self.tail_main if tail_main else (0 if final else self.seg_tail_main)
+            if n > 0 and len(self._side_q) > n:
+                self._main_tail = self._side_q[-n:]
+                self._side_q = self._side_q[:-n]
             self._flush_side()
             if not final:
                 return

@@ -456,7 +456,7 @@ def test_composer_trainer_runs_on_native_module():
     assert 0.0 <= hist[-1]["metrics/eval/Accuracy"] <= 1.0
 
 
-@pytest.mark.parametrize("mode", ["2", "3", "2+tail2"])
+@pytest.mark.parametrize("mode", ["2", "3", "2+tail2", "2+tail2+seg3"])
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64)])
 def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch):
     """DBX_OVERLAP_WGRAD=2 (weight gradients forked once per backward segment, joined one segment
@@ -474,6 +474,7 @@ def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch)
     # the stem weight gradient on the main stream (the batched default)
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", mode[0])
     monkeypatch.setenv("DBX_TAIL_MAIN", "2" if "tail2" in mode else "0")
+    monkeypatch.setenv("DBX_SEG_TAIL_MAIN", "3" if "seg3" in mode else "0")
     t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "0")
     t2 = NativeTrainer(m2, batch, (size, size), dev, optim=OptimConfig(lr=0.05))

@@ -19,7 +19,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--tail", type=int, default=15)
+    ap.add_argument("--tail", type=int, default=15, help="last kernels listed (0: none)")
+    ap.add_argument("--gap-us", type=float, default=20.0)
+    ap.add_argument("--top-gaps", type=int, default=12)
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -62,10 +64,18 @@ def main():
         if len(queues) == 2:
             ov = inter(busy[queues[0]], busy[queues[1]])
             print(f"  both queues busy {ov / 1e6:.3f} ms")
-        # the end of the step: the last kernels and which queue runs alone
-        last_main = max(r[1] for r in seg if r[2] == seg[0][2])
+        # idle stretches of each queue inside the step (>= gap_us) and what the other queue ran then
+        for q in queues:
+            iv = busy[q]
+            gaps = [(iv[i][1], iv[i + 1][0]) for i in range(len(iv) - 1) if iv[i + 1][0] - iv[i][1] >= a.gap_us * 1e3]
+            tot = sum(e - s for s, e in gaps)
+            print(f"  queue {q} idle inside the step: {tot / 1e6:.3f} ms in {len(gaps)} stretches >= {a.gap_us} us")
+            for s0, e0 in sorted(gaps, key=lambda g: g[0] - g[1])[:a.top_gaps]:
+                other = [r for r in seg if r[2] != q and r[0] < e0 and r[1] > s0]
+                names = ", ".join(sorted({short(r[3], 40) for r in other}))[:150]
+                print(f"    {(s0 - t0) / 1e6:8.3f} ms +{(e0 - s0) / 1e3:7.1f} us   other queue: {names}")
         print(f"  last {a.tail} kernels (queue, start offset ms, duration us, name):")
-        for r in seg[-a.tail:]:
+        for r in (seg[-a.tail:] if a.tail > 0 else []):
             print(f"    q{r[2]} {(r[0] - t0) / 1e6:8.3f} {(r[1] - r[0]) / 1e3:8.1f}  {short(r[3])}")
     return 0
 
