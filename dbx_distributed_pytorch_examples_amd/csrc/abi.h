@@ -147,6 +147,8 @@ struct GemmArgs {
   unsigned offset, thresh;  // dropout: keep if the Philox draw < thresh
   float inv_keep;
   const unsigned* offset_dev;  // nullable: the Philox offset read from device memory (graph replays)
+  float* ws;             // split-K (splitk > 1): fp32 partials [splitk][M][N], summed in split order
+  int splitk;            // K split over blockIdx.z (1: the tile loop writes C itself)
 };
 
 }  // namespace dbx

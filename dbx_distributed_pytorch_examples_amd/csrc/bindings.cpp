@@ -336,13 +336,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("small_gemm", [](int ta, int tb, int out_f32, int drop, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias_f,
                          uintptr_t bias_h, int M, int N, int K, int lda, int ldb, int ldc, float alpha, int accumulate,
                          unsigned long long seed, unsigned offset, unsigned thresh, float inv_keep, uintptr_t offset_dev,
-                         uintptr_t st) {
-    // classifier-head GEMM (head_ops.hip)
+                         uintptr_t st, uintptr_t ws, int splitk) {
+    // classifier-head GEMM (head_ops.hip); splitk > 1: K split over workgroups, partials in ws
     dbx::GemmArgs g{P<const bf16*>(A), P<const bf16*>(B), P<void*>(C), P<const float*>(bias_f), P<const bf16*>(bias_h),
                     M, N, K, lda, ldb, ldc, alpha, accumulate, seed, offset, thresh, inv_keep,
-                    P<const unsigned*>(offset_dev)};
+                    P<const unsigned*>(offset_dev), P<float*>(ws), splitk};
     check(dbx_small_gemm(ta, tb, out_f32, drop, &g, S(st)), "small_gemm");
-  });
+  }, py::arg("ta"), py::arg("tb"), py::arg("out_f32"), py::arg("drop"), py::arg("A"), py::arg("B"), py::arg("C"),
+     py::arg("bias_f"), py::arg("bias_h"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"),
+     py::arg("ldc"), py::arg("alpha"), py::arg("accumulate"), py::arg("seed"), py::arg("offset"), py::arg("thresh"),
+     py::arg("inv_keep"), py::arg("offset_dev"), py::arg("st"), py::arg("ws") = 0, py::arg("splitk") = 1);
   m.def("mnist_saved_bytes", []() { return dbx_mnist_saved_bytes(); });
   m.def("mnist_fwd", [](uintptr_t x, uintptr_t params, uintptr_t saved, uintptr_t logp, int N, unsigned long long seed,
                         unsigned offset, int train, uintptr_t st) {

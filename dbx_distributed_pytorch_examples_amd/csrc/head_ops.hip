@@ -12,7 +12,9 @@
 // Shapes are arbitrary (masked edges): logits [B, 1000 | 200 | 10] = pooled [B, 2048 | 512] x W^T,
 // dpooled = dlogits x W (reduction over the classes), dW = dlogits^T x h (reduction over the batch).
 // These GEMMs are 0.1-0.3 % of a ResNet-50 step; the point is one native path with the dropout and
-// bias fused, not peak MFMA rate.
+// bias fused, not peak MFMA rate. Long-K shapes with few tiles (the fc forward at batch 512 / 200
+// classes: 32 tiles x 16 k-stages, 35 us on 32 of 256 CUs) split K over blockIdx.z into fp32 partials
+// that split_gemm_reduce sums in split order and finishes (alpha, bias, accumulate, output type).
 //
 // Dropout (DROP = 1: on A, DROP = 2: on B): element at memory index i of that operand is kept with
 // probability keep (scaled 1/keep) by a Philox-4x32-10 draw at counter (i / 4, seed_lo, seed_hi,
@@ -56,6 +58,9 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
   __shared__ __attribute__((aligned(16))) bf16 sB[BN * BK];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid >> 1, wn = wid & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  // split-K: this workgroup's K range (multiples of BK; the last split takes the rest)
+  const int kper = g.splitk > 1 ? ((g.K + g.splitk - 1) / g.splitk + BK - 1) / BK * BK : g.K;
+  const int kbeg = (int)blockIdx.z * kper, kend = min(g.K, kbeg + kper);
   const unsigned doff = (DROP && g.offset_dev) ? *g.offset_dev : g.offset;  // step counter (device)
   f32x4 acc[2][2];
 #pragma unroll
@@ -69,14 +74,14 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
   auto load = [&](const bf16* P, int T, int ld, int rows, int r0, int k0, bool drop, int c) -> bf16x8 {
     const int q = tid + 256 * c, r = r0 + (q >> 4), kk = k0 + (q & 15) * 8;
     bf16x8 v;
-    const bool full = (r < rows) && (kk + 8 <= g.K);
+    const bool full = (r < rows) && (kk + 8 <= kend);
     if (T == 0 && full && ((ld & 7) == 0)) {
       v = *reinterpret_cast<const bf16x8*>(P + (size_t)r * ld + kk);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = kk + j;
-        const bool ok = r < rows && k < g.K;
+        const bool ok = r < rows && k < kend;
         const size_t e = T == 0 ? (size_t)r * ld + k : (size_t)k * ld + r;
         v[j] = ok ? P[e] : (bf16)0.f;
       }
@@ -99,8 +104,8 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
       rb[c] = load(g.B, TB, g.ldb, g.N, n0, k0, DROP == 2, c);
     }
   };
-  fetch(0);
-  for (int k0 = 0; k0 < g.K; k0 += BK) {
+  fetch(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int q = tid + 256 * c, row = q >> 4, ch = q & 15;
@@ -108,7 +113,7 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
       *reinterpret_cast<bf16x8*>(sB + row * BK + swz(row, ch) * 8) = rb[c];
     }
     __syncthreads();
-    if (k0 + BK < g.K) fetch(k0 + BK);  // block-uniform: in flight under this stage's MFMAs
+    if (k0 + BK < kend) fetch(k0 + BK);  // block-uniform: in flight under this stage's MFMAs
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 af[2], bfr[2];
@@ -132,6 +137,22 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
     __syncthreads();
   }
   // epilogue: acc[i][j][q] = C[m = wm*32 + i*16 + (lane & 15)][n = wn*32 + j*16 + 4*(lane >> 4) + q]
+  if (g.splitk > 1) {  // block-uniform: the raw partial of this split; split_gemm_reduce finishes C
+    float* W = g.ws + (size_t)blockIdx.z * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = m0 + wm * 32 + i * 16 + (lane & 15);
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = n0 + wn * 32 + j * 16 + 4 * (lane >> 4) + q;
+          if (n < g.N) W[(size_t)m * g.N + n] = acc[i][j][q];
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = m0 + wm * 32 + i * 16 + (lane & 15);
@@ -154,6 +175,29 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const GemmArgs g) {
           C[e] = (bf16)(g.accumulate ? (float)C[e] + v : v);
         }
       }
+  }
+}
+
+// split-K finish: C = alpha * (partial_0 + partial_1 + ... in split order) (+ bias) (+ C) -- the same
+// fixed order for every element and every run (deterministic)
+template <bool OUT_F32>
+__global__ __launch_bounds__(256) void split_gemm_reduce_kernel(const GemmArgs g) {
+  const long long total = (long long)g.M * g.N;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    float s = g.ws[e];
+    for (int k = 1; k < g.splitk; ++k) s += g.ws[(size_t)k * total + e];
+    const int m = (int)(e / g.N), n = (int)(e - (long long)m * g.N);
+    float v = g.alpha * s;
+    if (g.bias_f) v += g.bias_f[n];
+    if (g.bias_h) v += (float)g.bias_h[n];
+    const size_t c = (size_t)m * g.ldc + n;
+    if constexpr (OUT_F32) {
+      float* C = reinterpret_cast<float*>(g.C);
+      C[c] = g.accumulate ? C[c] + v : v;
+    } else {
+      bf16* C = reinterpret_cast<bf16*>(g.C);
+      C[c] = (bf16)(g.accumulate ? (float)C[c] + v : v);
+    }
   }
 }
 
@@ -191,8 +235,14 @@ using namespace dbx;
 
 template <int TA, int TB, bool F32, int DROP>
 static int launch_gemm(const GemmArgs& g, hipStream_t st) {
-  const dim3 grid((g.N + 63) / 64, (g.M + 63) / 64);
+  const int sk = g.splitk > 1 ? g.splitk : 1;
+  const dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, sk);
   hipLaunchKernelGGL((small_gemm_kernel<TA, TB, F32, DROP>), grid, dim3(256), 0, st, g);
+  if (sk > 1) {
+    const long long total = (long long)g.M * g.N;
+    const int blocks = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
+    hipLaunchKernelGGL((split_gemm_reduce_kernel<F32>), dim3(blocks), dim3(256), 0, st, g);
+  }
   return (int)hipGetLastError();
 }
 
@@ -200,6 +250,7 @@ static int launch_gemm(const GemmArgs& g, hipStream_t st) {
 extern "C" int dbx_small_gemm(int ta, int tb, int out_f32, int drop, const dbx::GemmArgs* args, hipStream_t st) {
   const GemmArgs& g = *args;
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return -50;
+  if (g.splitk > 1 && (g.ws == nullptr || g.splitk > 64)) return -52;
 #define DBX_G(TA, TB)                                                                                   \
   if (ta == TA && tb == TB) {                                                                           \
     if (out_f32) return drop == 1 ? launch_gemm<TA, TB, true, 1>(g, st)                                 \

@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..parallel.ddp import DistributedDataParallel, unwrap
+from ..parallel.ddp import DistributedDataParallel, flat_view, unwrap
 
 
 class LARS(torch.optim.Optimizer):
@@ -125,7 +125,7 @@ class AutogradTrainer:
             # ZeRO over the DDP flat gradient buffer: master = flat copy of params in the same order
             self._zero_master = torch.zeros_like(self.ddp.flat.buffer)
             for p, off in zip(self.ddp._params, self.ddp.flat.offsets):
-                self._zero_master[off:off + p.numel()].copy_(p.detach().reshape(-1))
+                flat_view(self._zero_master, off, p).copy_(p.detach())  # the gradients' memory order
             self.zero = ZeroShardedOptimizer(self._zero_master, self.ddp.flat.buffer, optim, stage=zero_stage,
                                              grad_scale=1.0)  # DDP already averaged
             self.opt = None
@@ -186,7 +186,7 @@ class AutogradTrainer:
             self.zero.step(grads_already_reduced=True)
             with torch.no_grad():
                 for p, off in zip(self.ddp._params, self.ddp.flat.offsets):
-                    p.copy_(self._zero_master[off:off + p.numel()].view_as(p))
+                    p.copy_(flat_view(self._zero_master, off, p))
         elif self.opt is not None:
             self.opt.step()
         self.ddp.zero_grad()

@@ -566,6 +566,9 @@ class ResNetProgram:
         self.dpooled = E(N, self.feat_c)
         self.logits = E(N, self.num_classes)
         self.dlogits = E(N, self.num_classes)
+        # split-K partials of the head GEMMs (K.head_splitk: the few-tile, long-K fc shapes)
+        self.head_ws = (torch.empty(8 * max(N * self.num_classes, self.num_classes * self.feat_c), device=dev,
+                                    dtype=torch.float32) if dev.type == "cuda" else None)
         self.labels = torch.zeros(N, device=dev, dtype=torch.int64)
         sh, sw = self.src_hw
         self.img_u8 = torch.zeros(N, sh, sw, 3 if self.in_ch != 1 else 1, device=dev, dtype=torch.uint8)
@@ -791,7 +794,7 @@ class ResNetProgram:
         if features_only:
             return self.pooled
         F, Cn = self.feat_c, self.num_classes
-        K.small_gemm(self.pooled, self.fc_w16, self.logits, M=N, N=Cn, K=F, bias=self.fc_b16)
+        K.small_gemm(self.pooled, self.fc_w16, self.logits, M=N, N=Cn, K=F, bias=self.fc_b16, ws=self.head_ws)
         mix = self.cutmix and self.training
         K.softmax_ce(self.logits, self.labels, self.dlogits if compute_grad else None, None,
                      self.metrics if metrics else None, smoothing=smoothing, grad_scale=grad_scale,
@@ -923,9 +926,9 @@ class ResNetProgram:
         # fc on MFMA (csrc/head_ops.hip): dW = dlogits^T pooled (fp32, straight into the flat gradient),
         # db = column sums of dlogits, dpooled = dlogits W
         N, F, Cn = self.N, self.feat_c, self.num_classes
-        K.small_gemm(self.dlogits, self.pooled, self.fc_w_grad, ta=True, tb=True, M=Cn, N=F, K=N)
+        K.small_gemm(self.dlogits, self.pooled, self.fc_w_grad, ta=True, tb=True, M=Cn, N=F, K=N, ws=self.head_ws)
         K.colsum(self.dlogits, self.fc_b_grad)
-        K.small_gemm(self.dlogits, self.fc_w16, self.dpooled, ta=False, tb=True, M=N, N=F, K=Cn)
+        K.small_gemm(self.dlogits, self.fc_w16, self.dpooled, ta=False, tb=True, M=N, N=F, K=Cn, ws=self.head_ws)
         K.avgpool_bwd(self.dpooled, self.dlast)
 
     def _cin(self, bn, count=None) -> bool:

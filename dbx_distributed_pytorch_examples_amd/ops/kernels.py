@@ -12,6 +12,7 @@ calls are captured by ``torch.cuda.graph``), and never synchronises. Layout conv
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -1157,13 +1158,24 @@ def dropout_threshold(p_drop: float) -> Tuple[int, float]:
     return min(0xFFFFFFFF, int(round(keep * 4294967296.0))), 1.0 / keep
 
 
+def head_splitk(M: int, N: int, K: int, ws_elems: int) -> int:
+    """Split-K depth of a head GEMM: long-K shapes with few 64 x 64 tiles (< 192: the fc forward at
+    TinyImageNet's batch 512 / 200 classes has 32) split K so ~256 workgroups run, >= 2 k-stages each."""
+    tiles = -(-M // 64) * -(-N // 64)
+    kst = -(-K // 128)
+    if os.environ.get("DBX_HEAD_SPLITK", "1") == "0" or tiles >= 192 or kst < 4 or ws_elems < 2 * M * N:
+        return 1
+    return max(1, min(kst // 2, max(2, 256 // tiles), 64, ws_elems // (M * N)))
+
+
 @_dispatch
 def small_gemm(A, B, out, *, ta=False, tb=False, M, N, K, alpha=1.0, bias=None, accumulate=False,
-               dropout=None):
+               dropout=None, ws=None):
     """out[M, N] (fp32 / bf16) = alpha * A(m, k) B(k, n) (+ bias[n]) (+ out) on MFMA (csrc/head_ops.hip).
     A: ``ta`` False -> [M, K], True -> [K, M]; B: ``tb`` False -> [N, K], True -> [K, N] (bf16, contiguous).
     ``dropout``: (operand "A" | "B", p, seed, offset) -- Philox mask on that operand's elements; ``offset``
-    an int or an int32[1] device tensor (read by the kernel: a replayed graph draws a new mask each step)."""
+    an int or an int32[1] device tensor (read by the kernel: a replayed graph draws a new mask each step).
+    ``ws``: fp32 workspace enabling split-K for long-K / few-tile shapes (:func:`head_splitk`)."""
     _chk(A, torch.bfloat16, "A", M * K)
     _chk(B, torch.bfloat16, "B", N * K)
     if out.dtype not in (torch.float32, torch.bfloat16) or out.numel() != M * N or not out.is_contiguous():
@@ -1183,9 +1195,13 @@ def small_gemm(A, B, out, *, ta=False, tb=False, M, N, K, alpha=1.0, bias=None, 
             off, offd = 0, off
     lda = M if ta else K
     ldb = N if tb else K
+    sk = 1
+    if ws is not None:
+        _chk(ws, torch.float32, "ws")
+        sk = head_splitk(M, N, K, ws.numel())
     C().small_gemm(int(ta), int(tb), int(out.dtype == torch.float32), drop, A.data_ptr(), B.data_ptr(), out.data_ptr(),
                    _p(bf), _p(bh), M, N, K, lda, ldb, N, float(alpha), int(accumulate), int(seed) & ((1 << 64) - 1),
-                   int(off) & 0xFFFFFFFF, thr, float(inv), _p(offd), stream_ptr())
+                   int(off) & 0xFFFFFFFF, thr, float(inv), _p(offd), stream_ptr(), ws.data_ptr() if sk > 1 else 0, sk)
     return out
 
 

@@ -556,7 +556,8 @@ def dropout_mask(numel: int, p: float, seed: int, offset: int, device=None) -> t
     return torch.from_numpy((u < np.uint64(thr)).astype(np.float32) / keep).to(device)
 
 
-def small_gemm(A, B, out, *, ta=False, tb=False, M, N, K, alpha=1.0, bias=None, accumulate=False, dropout=None):
+def small_gemm(A, B, out, *, ta=False, tb=False, M, N, K, alpha=1.0, bias=None, accumulate=False, dropout=None,
+               ws=None):
     a = A.float().reshape(K, M).t() if ta else A.float().reshape(M, K)
     b = B.float().reshape(K, N) if tb else B.float().reshape(N, K).t()
     if dropout is not None:

@@ -29,6 +29,15 @@ import torch.nn as nn
 from .dist import host_sync_for_gloo
 
 
+def flat_view(buf: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
+    """``buf[off:off + p.numel()]`` viewed with ``p``'s shape AND strides when ``p`` is densely packed
+    in another memory format (channels-last conv weights): the gradient then obeys autograd's layout
+    contract (accumulated in place, no per-step re-layout copy)."""
+    if p.is_contiguous() or p.dim() != 4 or not p.is_contiguous(memory_format=torch.channels_last):
+        return buf[off:off + p.numel()].view_as(p)
+    return buf.as_strided(p.shape, p.stride(), buf.storage_offset() + off)
+
+
 class FlatGradBuffer:
     """Contiguous gradient storage with params' ``.grad`` as views (reverse order)."""
 
@@ -46,7 +55,7 @@ class FlatGradBuffer:
 
     def attach(self):
         for p, o in zip(self.params, self.offsets):
-            p.grad = self.buffer[o:o + p.numel()].view_as(p)
+            p.grad = flat_view(self.buffer, o, p)
 
     def zero_(self):
         self.buffer.zero_()

@@ -131,3 +131,35 @@ def test_native_trainer_cutmix_trains():
         if i % 10 == 9:
             losses.append(tr.read_metrics()[0] / (10 * 64))
     assert all(l == l for l in losses) and losses[-1] < losses[0], losses
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (False, False)])
+@pytest.mark.parametrize("M,N,Kd", [(512, 200, 2048), (32, 1000, 2048), (200, 2048, 512), (37, 70, 1111)])
+def test_small_gemm_split_k_matches_single_pass(ta, tb, M, N, Kd):
+    """Split-K (few output tiles, long K: the TinyImageNet / small-batch fc shapes) sums the
+    partials in split order after one pass: same result as the fp32 reference; fp32 + bias + alpha,
+    bf16 out + accumulate, and the dropout operand all go through the reduce epilogue."""
+    torch.manual_seed(M * 7 + N + Kd)
+    A = _bf(Kd, M) if ta else _bf(M, Kd)
+    B = _bf(Kd, N) if tb else _bf(N, Kd)
+    bias = torch.randn(N, device="cuda")
+    ws = torch.empty(8 * max(M * N, 1), device="cuda")
+    sk = K.head_splitk(M, N, Kd, ws.numel())
+    out = torch.empty(M, N, device="cuda")
+    K.small_gemm(A, B, out, ta=ta, tb=tb, M=M, N=N, K=Kd, bias=bias, alpha=0.5, ws=ws)
+    a = A.float().t() if ta else A.float()
+    b = B.float() if tb else B.float().t()
+    ref = 0.5 * (a @ b) + bias
+    torch.cuda.synchronize()
+    err = (out - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, (sk, err)
+    o16 = _bf(M, N)
+    base = o16.float().clone()
+    K.small_gemm(A, B, o16, ta=ta, tb=tb, M=M, N=N, K=Kd, accumulate=True, ws=ws)
+    assert torch.allclose(o16.float(), base + a @ b, atol=0.25, rtol=1e-2), sk
+    if not ta and tb:
+        spec = ("A", 0.5, 99, 7)
+        K.small_gemm(A, B, out, tb=True, M=M, N=N, K=Kd, dropout=spec, ws=ws)
+        one = torch.empty_like(out)
+        K.small_gemm(A, B, one, tb=True, M=M, N=N, K=Kd, dropout=spec)
+        assert torch.allclose(out, one, atol=1e-4, rtol=1e-4), sk
