@@ -324,7 +324,8 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x4 (&acc)[
 // staged (it carries the BN prologue); 2 / 3 = both operands by LDS-DMA, a 2- / 3-slot ring (no
 // prologue). A DMA wave-instruction fills 8 tile rows x 128 B; the XOR swizzle moves to the
 // source side (LDS position (row, slot) receives chunk slot ^ ((row >> 1) & 7) of that row), so
-// the fragment reads are unchanged. The DMA variants run one tile per workgroup (no persistence).
+// the fragment reads are unchanged. The ring variants (DMA >= 2) run one tile per workgroup; DMA 1
+// (weights only) is persistent like the register-staged path.
 // DMA 4: both operands by LDS-DMA in 32-channel stages through a 4-slot ring -- the LDS of the
 // 2-slot 64-channel ring (two workgroups per CU stay resident) with three stages instead of one in
 // flight behind the MFMAs of the current stage.
@@ -701,6 +702,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     load_a(0);
     load_b(0);
     advance();
+  } else if constexpr (DMA == 1) {
+    load_a(0);  // (B by DMA at the top of the tile loop)
+    advance();
   }
   for (;;) {  // persistent tile loop (exit: every wave of the workgroup leaves after the same tile)
   if constexpr (DMA == 0) {
@@ -728,15 +732,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     // after the MFMAs of the current block). The vector-memory ops a wave has in flight at the
     // end of step kb, oldest first: B(kb+1) DMA, A(kb+2) loads, the tail write-back stores of
     // A(kb+1): the counted wait retires B(kb+1) and leaves the rest in flight.
+    // (A(0) is already in flight: issued before the loop, or before the previous tile's epilogue)
     constexpr int TAIL_ST = TAIL ? (MODE == DGRAD ? A_CH : 2 * A_CH) : 0;
     dma_b(0);
-    load_a(0);
-    advance();
     load_a(1);
     advance();
     pro_a(0);
     store_a(0, 0);
-    dma_wait<A_CH + TAIL_ST>();  // B(0) (older than the A(1) loads and the tail stores)
+    dma_wait<A_CH + TAIL_ST>();  // A(0), B(0) (older than the A(1) loads and the tail stores)
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -794,19 +797,28 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // keep a staged block alive across them, so those stage the next tile after the epilogue)
   // Only those run persistent (PF); the rest leave the loop after one tile (the host launches
   // one workgroup per tile for them), which compiles to the straight-line single-tile kernel.
-  constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64) && DMA == 0;  // (+: register room)
+  // DMA 1 (weights by LDS-DMA): A(0) of the next tile is staged in registers the same way, its
+  // weights are DMA-ed at the top of the next iteration (they land in the LDS the epilogue stages
+  // C through, so only after the barrier below)
+  constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64) && DMA <= 1;  // (+: register room)
   const int m0 = lm0, n0 = ln0, tm = ltm;
   tcur += gridDim.x;
   const bool more = PF && tcur < ntile;  // workgroup-uniform
   if (more) {  // A (activations, HBM latency) now; B (weights, L2-resident) after the epilogue
     set_tile(tcur);
     load_a(0);
+    if constexpr (DMA == 1) {
+      advance();
+      bk = bcb = bts = btr = 0;
+    }
   }
 
   igemm_epilogue<BM, BN, WM, WN, MODE, STATS, ACCUM, EPI>(a, acc, lds, m0, n0, tm, blockIdx.x);
   if (!more) break;
-  load_b(0);
-  advance();
+  if constexpr (DMA == 0) {
+    load_b(0);
+    advance();
+  }
   __syncthreads();  // the epilogue's LDS reads are done before the next tile's staging writes
   }
 }
@@ -836,8 +848,13 @@ static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
     if ((e && e[0] == '0') || per_cu <= 0 || cus <= 0) return 1 << 30;
     return (per_cu * cus) & ~7;
   }();
-  constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64) && DMA == 0;  // persistent (see the kernel)
-  const int nwg = (!PF || ntile <= cap) ? ntile : cap;
+  constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64) && DMA <= 1;  // persistent (see the kernel)
+  // the weights-by-DMA variants walk tiles only when each workgroup gets at least
+  // DBX_PERSIST_DMA1 (default 8) of them: headline ResNet-50 b1024 +0.8 %, the TinyImageNet step
+  // (~4 tiles per workgroup) -0.3 % when they always do (profiles/r5_persist_dma1/); 0 = never
+  static const int pf_dma1 = [] { const char* e = getenv("DBX_PERSIST_DMA1"); return e ? atoi(e) : 8; }();
+  const bool one_per_wg = DMA == 1 && (pf_dma1 <= 0 || ntile < (long long)pf_dma1 * cap);
+  const int nwg = (!PF || ntile <= cap || one_per_wg) ? ntile : cap;
   hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI, TAIL, DMA>), dim3(nwg), dim3(64 * WM * WN), 0, st, a);
   return (int)hipGetLastError();
 }

@@ -700,11 +700,14 @@ def test_dgrad_bwd_apply_prologue(variant, tile, cc):
         assert ((a - b).abs() / (b.abs() + N * H * W * 0.01)).max().item() < 2e-2
 
 
+@pytest.mark.parametrize("dma", [0, 1])
 @pytest.mark.parametrize("tile", [(128, 128), (128, 256), (256, 128), (128, 64), (64, 64)])
 @pytest.mark.parametrize("R", [1, 3])
-def test_conv_fwd_persistent_many_tiles(tile, R):
+def test_conv_fwd_persistent_many_tiles(tile, R, dma):
     """Far more tiles than resident workgroups (each workgroup walks several tiles, staging the
-    next tile's first block during the epilogue): output and BN statistics vs fp32 torch."""
+    next tile's first block during the epilogue; dma 1: weights by LDS-DMA, DMA-ed after the
+    epilogue): output and BN statistics vs fp32 torch."""
+    tile = tuple(tile) + (dma,)
     k = K()
     N, H, W, IC, OC = 24, 56, 56, 64, 256
     torch.manual_seed(41)

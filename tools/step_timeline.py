@@ -3,7 +3,7 @@
 time each hardware queue is busy, the time both are (overlap), and the step's phases in order --
 where the main chain waits on the side stream and what runs alone at the end of the step.
 
-  python tools/step_timeline.py run_kernel_trace.csv [--steps 2] [--tail 12]
+  python tools/step_timeline.py run_kernel_trace.csv|run_results.db [--steps 2] [--tail 12]
 A step starts at each augment_u8 (input normalisation) kernel."""
 import argparse
 import csv
@@ -24,9 +24,15 @@ def main():
     ap.add_argument("--top-gaps", type=int, default=12)
     a = ap.parse_args()
     rows = []
-    with open(a.trace) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Queue_Id"]), r["Kernel_Name"]))
+    if a.trace.endswith(".db"):  # rocprofv3's default rocpd (SQLite) output
+        import sqlite3
+        with sqlite3.connect(a.trace) as c:
+            rows = [(int(s), int(e), int(q), n) for s, e, q, n in
+                    c.execute("select start, end, queue_id, name from kernels")]
+    else:
+        with open(a.trace) as f:
+            for r in csv.DictReader(f):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Queue_Id"]), r["Kernel_Name"]))
     rows.sort()
     starts = [i for i, r in enumerate(rows) if "augment_u8" in r[3]]
     for si in range(max(0, len(starts) - 1 - a.steps), len(starts) - 1):
@@ -64,6 +70,12 @@ def main():
         if len(queues) == 2:
             ov = inter(busy[queues[0]], busy[queues[1]])
             print(f"  both queues busy {ov / 1e6:.3f} ms")
+        # no queue busy at all: dispatch gaps between dependent kernels (by size)
+        anyb = union([(r[0], r[1]) for r in seg])
+        holes = [anyb[i + 1][0] - anyb[i][1] for i in range(len(anyb) - 1)] + [t1 - anyb[-1][1]]
+        hist = {lim: sum(1 for h in holes if h < lim * 1e3) for lim in (2, 5, 20)}
+        print(f"  GPU idle (no queue busy): {sum(holes) / 1e6:.3f} ms in {len(holes)} holes "
+              f"(< 2 us: {hist[2]}, < 5 us: {hist[5]}, < 20 us: {hist[20]}; mean {sum(holes) / max(1, len(holes)) / 1e3:.2f} us)")
         # idle stretches of each queue inside the step (>= gap_us) and what the other queue ran then
         for q in queues:
             iv = busy[q]
