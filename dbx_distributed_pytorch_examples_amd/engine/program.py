@@ -536,6 +536,13 @@ class ResNetProgram:
                              else (2 if 5e10 <= fl < 5e11 else 0))
         self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
         self._main_tail = []
+        # layer1 (the last batch, exposed at the end of the step) forks its weight gradients per block
+        # instead of once at the segment's end, so they start under layer1's own remaining data
+        # gradients; the join at layer1's end then waits only for layer2's batch (an event recorded
+        # behind it), the final join for everything (DBX_LAST_SEG_BLOCKS)
+        self.last_seg_blocks = os.environ.get("DBX_LAST_SEG_BLOCKS", "0") == "1"
+        self._join_evt = None
+        self._after_evt = False
         # the stem weight gradient's own slabs when it runs on the main stream (its split count depends
         # on the grid, not on the workspace capacity)
         self.ws_stem = (torch.empty(40 << 20, device=dev, dtype=torch.float32)
@@ -818,7 +825,10 @@ class ResNetProgram:
         segs.append(("head", self._bwd_head))
         for li in (4, 3, 2, 1):
             idx = list(reversed(stages[li]))
-            segs.append((f"layer{li}", (lambda idx=idx: [(self._bwd_block(i), self._block_flush()) for i in idx])))
+            per_block = li == 1 and self.last_seg_blocks
+            segs.append((f"layer{li}", (lambda idx=idx, pb=per_block: [
+                (self._bwd_block(i), self._block_flush(), self._seg_block_flush(pb and j < len(idx) - 1))
+                for j, i in enumerate(idx)])))
         segs.append(("stem", self._bwd_stem))
         # every segment ends with its weight gradients complete on the main stream (join)
         last = len(segs) - 1
@@ -890,6 +900,11 @@ class ResNetProgram:
         if self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
             self._flush_side()  # this block's weight gradients, under the next block's data gradients
 
+    def _seg_block_flush(self, on: bool):
+        if on and self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad:
+            self._flush_side()  # (DBX_LAST_SEG_BLOCKS: this block's weight gradients now, behind the batch)
+            self._after_evt = True
+
     def _join_side(self, final: bool = True, tail_main: bool = False):
         if self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad:
             # batched side stream: the segment's weight gradients fork ONCE, after its data gradients,
@@ -902,8 +917,13 @@ class ResNetProgram:
                     fn(None, self.ws_main)
                 self._main_tail = []
             if self._side_pending:
-                torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
-                self._side_pending = False
+                if self._join_evt is not None:  # the previous batch only, not the blocks flushed since
+                    torch.cuda.current_stream(self.dev).wait_event(self._join_evt)
+                    self._side_pending = self._after_evt
+                else:
+                    torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
+                    self._side_pending = False
+            self._join_evt = None
             # the LAST batch (layer1) is exposed at the end of the step: only the stem's short backward
             # runs beside it -- its last DBX_TAIL_MAIN gradients go to the main stream's end instead
             # (their own workspace); DBX_SEG_TAIL_MAIN does the same for the middle batches (a batch the
@@ -913,6 +933,10 @@ class ResNetProgram:
                 self._main_tail = self._side_q[-n:]
                 self._side_q = self._side_q[:-n]
             self._flush_side()
+            if self.last_seg_blocks and not final and self._side_pending:
+                self._join_evt = torch.cuda.Event()
+                self._join_evt.record(self._wstream)
+                self._after_evt = False
             if not final:
                 return
         elif self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
