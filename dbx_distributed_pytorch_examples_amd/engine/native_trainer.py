@@ -143,6 +143,18 @@ class NativeTrainer:
             # per-segment collectives right after their own phase need each segment's weight gradients
             # final at its end: no batched side stream (it joins a segment late)
             self.prog.side_batch = False
+        # DBX_COMM_SIDE (default 1): in the one-graph step the collectives run on the weight-gradient
+        # side stream itself (behind the batch that finished their range) instead of a third stream.
+        # Under DEBUG_HIP_FORCE_GRAPH_QUEUES=2 a separate comm branch took the graph's second hardware
+        # queue and pushed the weight-gradient branch onto the main chain's queue: with a real
+        # collective in the graph (world-1 DBX_COMM_LOOPBACK=2) TinyImageNet fell from 97.9k to 85.5k
+        # img/s and the headline by 1.2 % (profiles/r5_comm_queue/). The joins then wait on an event
+        # behind each batch, not on the collectives queued after it.
+        self.comm_side = bool(self.ncomm is not None and self.late_posts and device.type == "cuda"
+                              and os.environ.get("DBX_COMM_SIDE", "1") == "1")
+        if self.comm_side:
+            self.comm_stream = self.prog.side_stream()
+            self.prog.event_joins = True
         self.flip = None
         self.seg_ranges = self._segment_ranges()
         self.zero = None

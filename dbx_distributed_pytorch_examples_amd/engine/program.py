@@ -543,6 +543,10 @@ class ResNetProgram:
         self.last_seg_blocks = os.environ.get("DBX_LAST_SEG_BLOCKS", "0") == "1"
         self._join_evt = None
         self._after_evt = False
+        # set by the multi-rank trainer when its collectives share the side stream (DBX_COMM_SIDE):
+        # every segment join then waits for the event behind the segment's batch, not for the
+        # collectives queued behind it on the same stream (the final join waits for everything)
+        self.event_joins = False
         # the stem weight gradient's own slabs when it runs on the main stream (its split count depends
         # on the grid, not on the workspace capacity)
         self.ws_stem = (torch.empty(40 << 20, device=dev, dtype=torch.float32)
@@ -900,6 +904,12 @@ class ResNetProgram:
         if self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
             self._flush_side()  # this block's weight gradients, under the next block's data gradients
 
+    def side_stream(self):
+        """The weight-gradient side stream (created on first use)."""
+        if self._wstream is None:
+            self._wstream = torch.cuda.Stream(device=self.dev)
+        return self._wstream
+
     def _seg_block_flush(self, on: bool):
         if on and self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad:
             self._flush_side()  # (DBX_LAST_SEG_BLOCKS: this block's weight gradients now, behind the batch)
@@ -919,7 +929,7 @@ class ResNetProgram:
             if self._side_pending:
                 if self._join_evt is not None:  # the previous batch only, not the blocks flushed since
                     torch.cuda.current_stream(self.dev).wait_event(self._join_evt)
-                    self._side_pending = self._after_evt
+                    self._side_pending = self._after_evt or self.event_joins  # (collectives behind it)
                 else:
                     torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
                     self._side_pending = False
@@ -933,7 +943,7 @@ class ResNetProgram:
                 self._main_tail = self._side_q[-n:]
                 self._side_q = self._side_q[:-n]
             self._flush_side()
-            if self.last_seg_blocks and not final and self._side_pending:
+            if (self.last_seg_blocks or self.event_joins) and not final and self._side_pending:
                 self._join_evt = torch.cuda.Event()
                 self._join_evt.record(self._wstream)
                 self._after_evt = False
