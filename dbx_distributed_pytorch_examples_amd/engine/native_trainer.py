@@ -155,6 +155,8 @@ class NativeTrainer:
         if self.comm_side:
             self.comm_stream = self.prog.side_stream()
             self.prog.event_joins = True
+            if os.environ.get("DBX_SIDE_DEFER") is None:
+                self.prog.side_defer = True  # (the side branch then keeps its own hardware queue)
         self.flip = None
         self.seg_ranges = self._segment_ranges()
         self.zero = None
@@ -401,6 +403,7 @@ class NativeTrainer:
         cur = torch.cuda.current_stream(self.dev)
         for i, (name, fn, post) in enumerate(self.phases):
             if self._waits_comm(i, name):
+                self.prog.launch_pending()
                 cur.wait_stream(self.comm_stream)
             if self.phase_timer is not None:
                 with self.phase_timer.phase(name):
@@ -408,9 +411,12 @@ class NativeTrainer:
             else:
                 fn()
             if post is not None and self.segmented:
-                self.comm_stream.wait_stream(cur)
-                with torch.cuda.stream(self.comm_stream):
-                    self._post(post)
+                # (DBX_COMM_SIDE with a deferred side batch: the collective goes in behind the batch,
+                # under the batch's fork event -- the main stream's state at this phase's end)
+                if not (self.comm_side and self.prog.defer_on_side(lambda post=post: self._post(post))):
+                    self.comm_stream.wait_stream(cur)
+                    with torch.cuda.stream(self.comm_stream):
+                        self._post(post)
 
     def _graph_phases(self):
         return self.phases
@@ -434,6 +440,7 @@ class NativeTrainer:
                 try:
                     with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode=mode):
                         self._run_phases_eager()
+                        self.prog.launch_pending()
                         torch.cuda.current_stream(self.dev).wait_stream(self.comm_stream)
                 finally:
                     self._capturing_one = False

@@ -547,6 +547,13 @@ class ResNetProgram:
         # every segment join then waits for the event behind the segment's batch, not for the
         # collectives queued behind it on the same stream (the final join waits for everything)
         self.event_joins = False
+        # DBX_SIDE_DEFER: launch each side batch after the main stream's next kernel (see _flush_side).
+        # Default: on for the small steps (< 0.5 TFLOP of forward conv work: CIFAR +0.7 %, TinyImageNet
+        # neutral), off for the b1024 headline (-0.4 %); the multi-rank one-graph step turns it on
+        # (its collectives ride the side stream: TinyImageNet +2.7 %, CIFAR +5 %, profiles/r5_side_defer/)
+        self.side_defer = (os.environ["DBX_SIDE_DEFER"] == "1" if "DBX_SIDE_DEFER" in os.environ
+                           else self.fwd_conv_flops() < 5e11)
+        self._pending_side = []
         # the stem weight gradient's own slabs when it runs on the main stream (its split count depends
         # on the grid, not on the workspace capacity)
         self.ws_stem = (torch.empty(40 << 20, device=dev, dtype=torch.float32)
@@ -871,34 +878,81 @@ class ResNetProgram:
         self._side(lambda batch=None, ws=None: K.conv_wgrad(*args[:3], args[3] if ws is None else ws, *args[4:],
                                                           defer=batch, **kw))
 
-    def _flush_side(self):
-        """Fork the side stream once from the main stream and launch the queued weight gradients on it."""
+    def _flush_side(self, join_evt: Optional[torch.cuda.Event] = None) -> bool:
+        """Fork the side stream once from the main stream and launch the queued weight gradients on it
+        (``join_evt``: recorded on the side stream right behind them). With ``side_defer`` the fork point
+        is an event recorded on the main stream now and the launch waits for the main stream's next
+        kernel launch (kernels.set_post_launch): in the captured graph the fork node's FIRST edge then
+        continues the main chain, so the runtime's depth-first split of the graph into per-queue lists
+        keeps the main chain in one list and chains the side batches into another."""
         if not self._side_q:
-            return
+            return False
+        self.launch_pending()  # (at most one deferred batch)
         if self._wstream is None:
             self._wstream = torch.cuda.Stream(device=self.dev)
-        self._wstream.wait_stream(torch.cuda.current_stream(self.dev))
-        # (each batch of a step takes an arena region of its own)
-        batch = (K.ReduceBatch(self.wred_arena, self._wred_off, self.defer_max_bytes) if self.defer_reduce
-                 else None)
-        with torch.cuda.stream(self._wstream):
-            for fn in self._side_q:
-                if batch is not None and getattr(fn, "__defaults__", None):
-                    fn(batch)  # a weight gradient that can defer its reduction
-                else:
-                    fn()
-            if batch is not None:
-                batch.flush()
-        if batch is not None:
-            # (the next batch starts past everything this one asked for, placed or not: a warm-up
-            # step that found the arena too small then sizes it for the whole step at once)
-            self._wred_off = batch.need
-            if batch.need > self.wred_arena.numel() and not torch.cuda.is_current_stream_capturing():
-                # grown for the next steps (the eager warm-up steps size it before any capture)
-                torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
-                self.wred_arena = torch.empty(batch.need, device=self.dev, dtype=torch.float32)
+        q = self._side_q
         self._side_q = []
         self._side_pending = True
+        main = torch.cuda.current_stream(self.dev)
+        fork = None
+        if self.side_defer:
+            fork = torch.cuda.Event()
+            fork.record(main)
+        else:
+            self._wstream.wait_stream(main)
+
+        def launch():
+            if fork is not None:
+                self._wstream.wait_event(fork)
+            # (each batch of a step takes an arena region of its own)
+            batch = (K.ReduceBatch(self.wred_arena, self._wred_off, self.defer_max_bytes) if self.defer_reduce
+                     else None)
+            with torch.cuda.stream(self._wstream):
+                for fn in q:
+                    if batch is not None and getattr(fn, "__defaults__", None):
+                        fn(batch)  # a weight gradient that can defer its reduction
+                    else:
+                        fn()
+                if batch is not None:
+                    batch.flush()
+            if join_evt is not None:
+                join_evt.record(self._wstream)
+            if batch is not None:
+                # (the next batch starts past everything this one asked for, placed or not: a warm-up
+                # step that found the arena too small then sizes it for the whole step at once)
+                self._wred_off = batch.need
+                if batch.need > self.wred_arena.numel() and not torch.cuda.is_current_stream_capturing():
+                    # grown for the next steps (the eager warm-up steps size it before any capture)
+                    torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
+                    self.wred_arena = torch.empty(batch.need, device=self.dev, dtype=torch.float32)
+
+        if fork is None:
+            launch()
+        else:
+            self._pending_side = [launch]
+            K.set_post_launch(self.launch_pending)
+        return True
+
+    def defer_on_side(self, fn) -> bool:
+        """Queue ``fn`` (run under the side stream) behind the deferred batch; False: nothing deferred."""
+        if not self._pending_side:
+            return False
+
+        def run():
+            with torch.cuda.stream(self._wstream):
+                fn()
+        self._pending_side.append(run)
+        return True
+
+    def launch_pending(self) -> None:
+        """Launch the deferred side batch (and what was queued behind it) now."""
+        if not self._pending_side:
+            return
+        items = self._pending_side
+        self._pending_side = []
+        K.set_post_launch(None)
+        for f in items:
+            f()
 
     def _block_flush(self):
         if self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
@@ -926,6 +980,7 @@ class ResNetProgram:
                 for fn in self._main_tail:
                     fn(None, self.ws_main)
                 self._main_tail = []
+            self.launch_pending()
             if self._side_pending:
                 if self._join_evt is not None:  # the previous batch only, not the blocks flushed since
                     torch.cuda.current_stream(self.dev).wait_event(self._join_evt)
@@ -942,15 +997,19 @@ class ResNetProgram:
             if n > 0 and len(self._side_q) > n:
                 self._main_tail = self._side_q[-n:]
                 self._side_q = self._side_q[:-n]
-            self._flush_side()
-            if (self.last_seg_blocks or self.event_joins) and not final and self._side_pending:
+            want = (self.last_seg_blocks or self.event_joins) and not final
+            evt = torch.cuda.Event() if want else None
+            if self._flush_side(join_evt=evt):
+                self._join_evt = evt
+            elif want and self._side_pending:
                 self._join_evt = torch.cuda.Event()
                 self._join_evt.record(self._wstream)
-                self._after_evt = False
+            self._after_evt = False
             if not final:
                 return
         elif self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
             self._flush_side()  # (the stem / head segments queue theirs here), joined below
+        self.launch_pending()
         if self._side_pending:
             torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
             self._side_pending = False

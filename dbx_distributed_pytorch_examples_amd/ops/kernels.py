@@ -27,6 +27,16 @@ _NO_EPI = (0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
 MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
 
 
+_POST_LAUNCH = None
+
+
+def set_post_launch(cb) -> None:
+    """Run ``cb`` once, right after the next native kernel launch (None: cancel). The program's
+    deferred side-stream batches use it to enter the captured graph after the main chain's next node."""
+    global _POST_LAUNCH
+    _POST_LAUNCH = cb
+
+
 def _dispatch(fn):
     """Run the HIP kernel for GPU tensors, the PyTorch reference (ops/reference.py) otherwise.
     With ``DBX_DEBUG=1`` every native launch is followed by a sync + output check (utils/debug.py)."""
@@ -34,12 +44,15 @@ def _dispatch(fn):
     checked = _debug.checked_op(fn)
 
     def wrapper(*args, **kw):
+        global _POST_LAUNCH
         t = args[0]
         if isinstance(t, torch.Tensor) and not use_native(t):
             return ref(*args, **kw)
-        if _debug.enabled():
-            return checked(*args, **kw)
-        return fn(*args, **kw)
+        r = checked(*args, **kw) if _debug.enabled() else fn(*args, **kw)
+        if _POST_LAUNCH is not None:
+            cb, _POST_LAUNCH = _POST_LAUNCH, None
+            cb()
+        return r
 
     wrapper.__name__ = fn.__name__
     wrapper.__doc__ = fn.__doc__

@@ -136,7 +136,7 @@ def test_nonblocking_init_and_captured_check(world1):
     c.close()
 
 
-@pytest.mark.parametrize("comm_side", ["1", "0"])
+@pytest.mark.parametrize("comm_side", ["1", "0", "1+defer"])
 @pytest.mark.parametrize("model,hw,batch", [("resnet18", 32, 32), ("resnet50", 64, 16)])
 def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batch, comm_side):
     """The one-graph multi-rank step's all-reduce ORDER, checked at world 1: with DBX_COMM_LOOPBACK=2
@@ -149,7 +149,8 @@ def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batc
     from dbx_distributed_pytorch_examples_amd.models import build_model
     monkeypatch.setenv("DBX_SEGMENTED_GRAPHS", "1")
     monkeypatch.setenv("DBX_COMM", "native")
-    monkeypatch.setenv("DBX_COMM_SIDE", comm_side)
+    monkeypatch.setenv("DBX_COMM_SIDE", comm_side[0])
+    monkeypatch.setenv("DBX_SIDE_DEFER", "1" if "defer" in comm_side else "0")
     torch.manual_seed(0)
     m1 = build_model(model, num_classes=10)
     m2 = copy.deepcopy(m1)
@@ -158,7 +159,8 @@ def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batc
     monkeypatch.delenv("DBX_COMM_LOOPBACK")
     t2 = NativeTrainer(m2, batch, (hw, hw), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     assert t1.ncomm is not None and t1.loopback == 2 and t2.loopback == 1 and t1.late_posts
-    assert t1.comm_side == (comm_side == "1") and t1.prog.event_joins == t1.comm_side
+    assert t1.comm_side == (comm_side[0] == "1") and t1.prog.event_joins == t1.comm_side
+    assert t1.prog.side_defer == ("defer" in comm_side)
     g = torch.Generator().manual_seed(1)
     for i in range(6):
         img = torch.randint(0, 256, (batch, hw, hw, 3), dtype=torch.uint8, generator=g).cuda()

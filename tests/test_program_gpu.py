@@ -456,7 +456,8 @@ def test_composer_trainer_runs_on_native_module():
     assert 0.0 <= hist[-1]["metrics/eval/Accuracy"] <= 1.0
 
 
-@pytest.mark.parametrize("mode", ["2", "3", "2+tail2", "2+tail2+seg3", "2+l1blocks", "2+tail2+l1blocks"])
+@pytest.mark.parametrize("mode", ["2", "3", "2+tail2", "2+tail2+seg3", "2+l1blocks", "2+tail2+l1blocks", "2+defer",
+                                  "2+tail2+defer"])
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64)])
 def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch):
     """DBX_OVERLAP_WGRAD=2 (weight gradients forked once per backward segment, joined one segment
@@ -477,12 +478,15 @@ def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch)
     monkeypatch.setenv("DBX_SEG_TAIL_MAIN", "3" if "seg3" in mode else "0")
     # "l1blocks": layer1's weight gradients forked per block (DBX_LAST_SEG_BLOCKS)
     monkeypatch.setenv("DBX_LAST_SEG_BLOCKS", "1" if "l1blocks" in mode else "0")
+    # "defer": each side batch launched after the main stream's next kernel (DBX_SIDE_DEFER)
+    monkeypatch.setenv("DBX_SIDE_DEFER", "1" if "defer" in mode else "0")
     t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "0")
     t2 = NativeTrainer(m2, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     assert (t1.prog.side_batch if mode[0] == "2" else t1.prog.side_block) and t1.prog.overlap_wgrad
     assert t1.prog.tail_main == (2 if "tail2" in mode else 0)
     assert t1.prog.last_seg_blocks == ("l1blocks" in mode)
+    assert t1.prog.side_defer == ("defer" in mode)
     assert not t2.prog.overlap_wgrad
     g = torch.Generator().manual_seed(3)
     for i in range(5):
