@@ -530,10 +530,17 @@ class ResNetProgram:
         # stream's end (DBX_TAIL_MAIN, their own workspace of ws's size: the same split depths, the same
         # bits): 97.5-97.8k img/s; CIFAR loses with it (profiles/r5_tail/)
         fl = self.fwd_conv_flops()
+        # DBX_SIDE_DEFER: launch each side batch after the main stream's next kernel (see _flush_side).
+        # Default: on for the small steps (< 0.5 TFLOP of forward conv work: CIFAR +0.7 %, TinyImageNet
+        # neutral), off for the b1024 headline (-0.4 % / neutral); the multi-rank one-graph step turns it
+        # on (its collectives ride the side stream: TinyImageNet +2.8 %, CIFAR +5 %, profiles/r5_side_defer/)
+        self.side_defer = (os.environ["DBX_SIDE_DEFER"] == "1" if "DBX_SIDE_DEFER" in os.environ
+                           else fl < 5e11)
         self.stem_wg_main = (os.environ["DBX_STEM_WG_MAIN"] == "1" if "DBX_STEM_WG_MAIN" in os.environ
                              else fl < 5e11)
+        # (with the deferred launch the TinyImageNet class moves three: 99.7-100.4k vs 99.0-99.6k img/s)
         self.tail_main = int(os.environ["DBX_TAIL_MAIN"] if "DBX_TAIL_MAIN" in os.environ
-                             else (2 if 5e10 <= fl < 5e11 else 0))
+                             else ((3 if self.side_defer else 2) if 5e10 <= fl < 5e11 else 0))
         self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
         self._main_tail = []
         # layer1 (the last batch, exposed at the end of the step) forks its weight gradients per block
@@ -547,12 +554,6 @@ class ResNetProgram:
         # every segment join then waits for the event behind the segment's batch, not for the
         # collectives queued behind it on the same stream (the final join waits for everything)
         self.event_joins = False
-        # DBX_SIDE_DEFER: launch each side batch after the main stream's next kernel (see _flush_side).
-        # Default: on for the small steps (< 0.5 TFLOP of forward conv work: CIFAR +0.7 %, TinyImageNet
-        # neutral), off for the b1024 headline (-0.4 %); the multi-rank one-graph step turns it on
-        # (its collectives ride the side stream: TinyImageNet +2.7 %, CIFAR +5 %, profiles/r5_side_defer/)
-        self.side_defer = (os.environ["DBX_SIDE_DEFER"] == "1" if "DBX_SIDE_DEFER" in os.environ
-                           else self.fwd_conv_flops() < 5e11)
         self._pending_side = []
         # the stem weight gradient's own slabs when it runs on the main stream (its split count depends
         # on the grid, not on the workspace capacity)
