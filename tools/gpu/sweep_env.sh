@@ -8,7 +8,7 @@ for p in $PRESETS; do
   for st in "$@"; do
     envs=""; [ "$st" != base ] && envs="${st//+/ }"
     args="--steps 30 --warmup 10"; [ $p = headline ] && args="--steps 15 --warmup 5" || args="$args --preset $p"
-    f=$O/${p}_${st//[=+]/_}.log
+    f=$O/${p}_$(echo "$st" | tr "=+/" "___").log
     env $envs timeout -k 10 300 python bench.py $args > $f 2>&1 || { tail -20 $f; exit 1; }
     echo "$p $st: $(grep -o '"value": [0-9.]*' $f)"
   done
