@@ -139,6 +139,68 @@ def _replica_tensors(step):
     return [p.detach() for p in getattr(step, "model").parameters()]
 
 
+def _measure(args, info, wd, build_step, ddist, fault):
+    """Build the step, warm up, check the replicas, time ``args.steps`` steps, check again.
+    Returns (rc, elapsed seconds (max over ranks), meta); rc 4 = replicas diverged."""
+    step, meta = build_step(args, info)
+    tr = getattr(step, "trainer", None)
+    meta["_native_comm"] = getattr(tr, "ncomm", None) is not None
+    if wd is not None:
+        wd.register(getattr(tr, "ncomm", None))
+        wd.step_end()
+
+    def sync():
+        if info.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    def release():  # a rebuilt step must not hold the first one's buffers / graphs / communicator
+        nonlocal step, tr
+        if tr is not None and getattr(tr, "ncomm", None) is not None:
+            if wd is not None:
+                wd.unregister(tr.ncomm)  # (the watchdog polls registered communicators)
+            tr.ncomm.close()
+        step = tr = None
+        import gc
+        gc.collect()
+        if info.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+    inject = fault.parse_fault() is not None  # DBX_FAULT=rank:step:kind (warm-up steps only)
+    if wd is not None:
+        wd.step_begin("warmup")
+    for i in range(args.warmup):
+        if inject:
+            fault.maybe_inject(i)
+        step()
+    sync()
+    ddist.barrier()
+    sync()
+    if wd is not None:
+        wd.step_end()
+    spec = fault.parse_fault()
+    if spec is not None and spec[2] == "diverge" and spec[0] == info.rank:
+        _replica_tensors(step)[0].view(-1)[:1].add_(1.0)  # injected divergence (tests the replica check)
+    if not replicas_in_sync(step, info, "warm-up", wd):
+        release()
+        return 4, 0.0, meta
+    if wd is not None:
+        wd.step_begin("timed")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    ddist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    elapsed = ddist.all_reduce_max(elapsed)
+    if wd is not None:
+        wd.step_end()
+    if not replicas_in_sync(step, info, "the timed steps", wd):
+        release()
+        return 4, 0.0, meta
+    return 0, elapsed, meta
+
+
 def main(argv=None) -> int:
     raw = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(raw)
@@ -163,48 +225,24 @@ def main(argv=None) -> int:
     if info.world_size > 1:
         from dbx_distributed_pytorch_examples_amd.parallel.comm_guard import CommWatchdog
         wd = CommWatchdog(timeout_s=float(os.environ.get("DBX_BENCH_TIMEOUT", "300")), device=info.device)
-        wd.step_begin("setup")
-    step, meta = build_step(args, info)
-    if wd is not None:
-        wd.register(getattr(getattr(step, "trainer", None), "ncomm", None))
-        wd.step_end()
-
-    def sync():
-        if info.device.type == "cuda":
-            torch.cuda.synchronize()
-
     from dbx_distributed_pytorch_examples_amd.utils import fault
-    inject = fault.parse_fault() is not None  # DBX_FAULT=rank:step:kind (warm-up steps only)
-    if wd is not None:
-        wd.step_begin("warmup")
-    for i in range(args.warmup):
-        if inject:
-            fault.maybe_inject(i)
-        step()
-    sync()
-    ddist.barrier()
-    sync()
-    if wd is not None:
-        wd.step_end()
-    spec = fault.parse_fault()
-    if spec is not None and spec[2] == "diverge" and spec[0] == info.rank:
-        _replica_tensors(step)[0].view(-1)[:1].add_(1.0)  # injected divergence (tests the replica check)
-    if not replicas_in_sync(step, info, "warm-up", wd):
-        return 4
-    if wd is not None:
-        wd.step_begin("timed")
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync()
-    ddist.barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-    elapsed = ddist.all_reduce_max(elapsed)
-    if wd is not None:
-        wd.step_end()
-    if not replicas_in_sync(step, info, "the timed steps", wd):
-        return 4
+    for attempt in (0, 1):
+        if wd is not None:
+            wd.step_begin("setup")
+        rc, elapsed, meta = _measure(args, info, wd, build_step, ddist, fault)
+        # the one-graph multi-rank step (framework RCCL communicator) is checked here against its own
+        # replicas: if they diverged, every rank saw it (the check gathers all checksums) and all of them
+        # rebuild the step on the c10d path (DBX_COMM=torch) and measure again instead of failing
+        if rc == 4 and attempt == 0 and meta.get("_native_comm"):
+            if info.rank == 0:
+                print("[bench] warning: the one-graph step's replicas diverged; re-measuring on the c10d "
+                      "collectives (DBX_COMM=torch)", file=sys.stderr, flush=True)
+            os.environ["DBX_COMM"] = "torch"
+            continue
+        break
+    if rc != 0:
+        return rc
+    meta.pop("_native_comm", None)
     if wd is not None:
         wd.close()
 

@@ -64,7 +64,13 @@ class CommWatchdog:
 
     def register(self, comm) -> None:
         if comm is not None:
-            self.comms.append(comm)
+            with self._lock:
+                self.comms = self.comms + [comm]
+
+    def unregister(self, comm) -> None:
+        """Stop polling ``comm`` (before it is closed: bench.py's rebuild on the c10d path)."""
+        with self._lock:
+            self.comms = [c for c in self.comms if c is not comm]
 
     def step_begin(self, step) -> None:
         """``step``: a step number, or a phase label (bench.py brackets "setup" / "warmup" / "timed")."""
@@ -92,7 +98,9 @@ class CommWatchdog:
     # ------------------------------------------------------------------------------------------
     def check(self) -> Optional[str]:
         """The failure to act on now, if any (also usable without the thread, e.g. in tests)."""
-        for c in self.comms:
+        with self._lock:
+            comms = self.comms  # (replaced, never mutated in place: a snapshot)
+        for c in comms:
             try:
                 code, msg = c.async_error()
             except Exception as e:  # noqa: BLE001 - an unreachable communicator is a failure too

@@ -77,3 +77,28 @@ def test_stalled_rank_ends_the_bench_within_the_timeout():
     assert "[comm-watchdog]" in r.stderr and "phase 'warmup'" in r.stderr
     assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
     assert time.time() - t0 < 120
+
+
+def test_diverged_one_graph_step_is_remeasured_on_c10d(monkeypatch, capsys):
+    """The one-graph multi-rank step failing its replica check (on every rank: the check gathers all
+    checksums) is rebuilt on the c10d collectives (DBX_COMM=torch) and measured again; a divergence
+    on the c10d path (or without the framework communicator) still ends the run with 4."""
+    sys.path.insert(0, ROOT)
+    import bench
+    calls = []
+
+    def fake(args, info, wd, build_step, ddist, fault):
+        calls.append(os.environ.get("DBX_COMM"))
+        if len(calls) == 1:
+            return 4, 0.0, {"_native_comm": True}
+        return 0, 1.0, {"grad_collectives": "c10d"}
+
+    monkeypatch.delenv("DBX_COMM", raising=False)
+    monkeypatch.setattr(bench, "_measure", fake)
+    assert bench.main(["--steps", "1", "--warmup", "0", "--preset", "resnet18_cifar10"]) == 0
+    assert calls == [None, "torch"]
+    d = _line(capsys.readouterr().out)
+    assert d["config"]["grad_collectives"] == "c10d" and "_native_comm" not in d["config"]
+    calls.clear()
+    monkeypatch.setattr(bench, "_measure", lambda *a: (calls.append(1), (4, 0.0, {"_native_comm": False}))[1])
+    assert bench.main(["--steps", "1", "--warmup", "0", "--preset", "resnet18_cifar10"]) == 4 and calls == [1]
