@@ -495,7 +495,11 @@ class NativeTrainer:
         if self.cutmix_alpha > 0:
             self._sample_cutmix()
         self._set_hyper()
-        self._step_inner()
+        try:
+            self._step_inner()
+        except BaseException:
+            p.drop_pending()  # a side batch deferred by the failed step must not launch later
+            raise
         if self.zero is not None:
             # a replayed graph does not run zero.step() in Python: keep its counter (saved in
             # ZeRO checkpoints) on the trainer's

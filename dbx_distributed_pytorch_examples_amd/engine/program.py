@@ -951,9 +951,14 @@ class ResNetProgram:
             return
         items = self._pending_side
         self._pending_side = []
-        K.set_post_launch(None)
+        K.set_post_launch(None, owner=self.launch_pending)
         for f in items:
             f()
+
+    def drop_pending(self) -> None:
+        """Forget a deferred side batch (the step that queued it failed)."""
+        self._pending_side = []
+        K.set_post_launch(None, owner=self.launch_pending)
 
     def _block_flush(self):
         if self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:

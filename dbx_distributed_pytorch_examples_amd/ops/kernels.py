@@ -30,10 +30,14 @@ MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
 _POST_LAUNCH = None
 
 
-def set_post_launch(cb) -> None:
-    """Run ``cb`` once, right after the next native kernel launch (None: cancel). The program's
-    deferred side-stream batches use it to enter the captured graph after the main chain's next node."""
+def set_post_launch(cb, owner=None) -> None:
+    """Run ``cb`` once, right after the next native kernel launch. ``cb=None`` cancels -- with
+    ``owner`` given, only if the pending callback is ``owner`` (one program never cancels another's).
+    The program's deferred side-stream batches use it to enter the captured graph after the main
+    chain's next node."""
     global _POST_LAUNCH
+    if cb is None and owner is not None and _POST_LAUNCH is not None and _POST_LAUNCH != owner:
+        return
     _POST_LAUNCH = cb
 
 

@@ -46,3 +46,24 @@ def test_device_hyper_copies_only_changes():
     t.fill_(0.0)
     h.set([0.2, 0.5, 0.25, 0.0])
     assert t.tolist() == pytest.approx([0.2, 0.5, 0.25, 0.0])
+
+
+def test_post_launch_hook_owner_scoped_cancel():
+    """ops.kernels.set_post_launch: a program cancels only its own pending deferred side launch."""
+    from dbx_distributed_pytorch_examples_amd.ops import kernels as K
+
+    class P:
+        def launch(self):
+            pass
+    a, b = P(), P()
+    try:
+        K.set_post_launch(a.launch)
+        K.set_post_launch(None, owner=b.launch)   # another program's cancel: kept
+        assert K._POST_LAUNCH == a.launch
+        K.set_post_launch(None, owner=a.launch)   # its own: cancelled
+        assert K._POST_LAUNCH is None
+        K.set_post_launch(b.launch)
+        K.set_post_launch(None)                   # unconditional cancel
+        assert K._POST_LAUNCH is None
+    finally:
+        K.set_post_launch(None)
