@@ -143,6 +143,8 @@ class NativeTrainer:
             # per-segment collectives right after their own phase need each segment's weight gradients
             # final at its end: no batched side stream (it joins a segment late)
             self.prog.side_batch = False
+        if self.segmented and os.environ.get("DBX_COMM_SIDE", "1") != "1":
+            self.prog.lazy_join = False  # (a separate comm stream orders after the main stream's joins)
         # DBX_COMM_SIDE (default 1): in the one-graph step the collectives run on the weight-gradient
         # side stream itself (behind the batch that finished their range) instead of a third stream.
         # Under DEBUG_HIP_FORCE_GRAPH_QUEUES=2 a separate comm branch took the graph's second hardware

@@ -554,6 +554,14 @@ class ResNetProgram:
         # every segment join then waits for the event behind the segment's batch, not for the
         # collectives queued behind it on the same stream (the final join waits for everything)
         self.event_joins = False
+        # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
+        # its own segment's per-block buffers (never reused within a step) and the workspaces of the main
+        # stream's weight gradients are separate, so only the final join (before the optimizer) orders
+        # the two; not with collectives on their own stream (they wait on the main stream at the joins)
+        # (default: the CIFAR class, < 50 GFLOP of forward conv work, +1.2 %; TinyImageNet -0.3 %, the
+        # headline -0.5 %: profiles/r5_side_defer/lazy_join.txt)
+        self.lazy_join = (os.environ["DBX_LAZY_JOIN"] == "1" if "DBX_LAZY_JOIN" in os.environ
+                          else self.fwd_conv_flops() < 5e10)
         self._pending_side = []
         # the stem weight gradient's own slabs when it runs on the main stream (its split count depends
         # on the grid, not on the workspace capacity)
@@ -987,7 +995,9 @@ class ResNetProgram:
                     fn(None, self.ws_main)
                 self._main_tail = []
             self.launch_pending()
-            if self._side_pending:
+            if self._side_pending and self.lazy_join and not final:
+                pass  # (DBX_LAZY_JOIN: the final join below waits for everything)
+            elif self._side_pending:
                 if self._join_evt is not None:  # the previous batch only, not the blocks flushed since
                     torch.cuda.current_stream(self.dev).wait_event(self._join_evt)
                     self._side_pending = self._after_evt or self.event_joins  # (collectives behind it)

@@ -136,7 +136,7 @@ def test_nonblocking_init_and_captured_check(world1):
     c.close()
 
 
-@pytest.mark.parametrize("comm_side", ["1", "0", "1+defer"])
+@pytest.mark.parametrize("comm_side", ["1", "0", "1+defer", "1+defer+lazy"])
 @pytest.mark.parametrize("model,hw,batch", [("resnet18", 32, 32), ("resnet50", 64, 16)])
 def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batch, comm_side):
     """The one-graph multi-rank step's all-reduce ORDER, checked at world 1: with DBX_COMM_LOOPBACK=2
@@ -151,6 +151,7 @@ def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batc
     monkeypatch.setenv("DBX_COMM", "native")
     monkeypatch.setenv("DBX_COMM_SIDE", comm_side[0])
     monkeypatch.setenv("DBX_SIDE_DEFER", "1" if "defer" in comm_side else "0")
+    monkeypatch.setenv("DBX_LAZY_JOIN", "1" if "lazy" in comm_side else "0")
     torch.manual_seed(0)
     m1 = build_model(model, num_classes=10)
     m2 = copy.deepcopy(m1)
