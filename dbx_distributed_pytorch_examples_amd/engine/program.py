@@ -183,6 +183,7 @@ class ResNetProgram:
         # BN finalize / backward coefficients computed by the producing conv's last tiles (K.BnFin)
         self.fuse_fin = os.environ.get("DBX_FUSE_BN_FIN", "0") == "1"
         self.wgrad_lds_pad = int(os.environ.get("DBX_WGRAD_LDS_PAD", "0"))
+
         # store block-internal BN outputs from the MASK_Y dgrad epilogue for the wgrads (A/B switch)
         self.act_writeback = os.environ.get("DBX_ACT_WRITEBACK", "1") == "1"
         # compute block outputs inside the next block's conv1 prologue instead of a bn_apply pass
@@ -536,6 +537,12 @@ class ResNetProgram:
         # on (its collectives ride the side stream: TinyImageNet +2.8 %, CIFAR +5 %, profiles/r5_side_defer/)
         self.side_defer = (os.environ["DBX_SIDE_DEFER"] == "1" if "DBX_SIDE_DEFER" in os.environ
                            else fl < 5e11)
+        # DBX_SIDE_CU_RESERVE: side-stream weight gradients sized to one round over all but N CUs, so
+        # the main chain's small kernels find a CU (the BN-backward coefficient launches took 4.9 us alone
+        # and 26.5 us beside the weight gradients); default 64 from the TinyImageNet class up (headline
+        # +0.8 %, TinyImageNet +0.6-0.9 %), 0 for the CIFAR class (-0.4 %): profiles/r5_cu_reserve/
+        self.side_cu_reserve = int(os.environ["DBX_SIDE_CU_RESERVE"] if "DBX_SIDE_CU_RESERVE" in os.environ
+                                   else (64 if fl >= 5e10 else 0))
         self.stem_wg_main = (os.environ["DBX_STEM_WG_MAIN"] == "1" if "DBX_STEM_WG_MAIN" in os.environ
                              else fl < 5e11)
         # (with the deferred launch the TinyImageNet class moves three: 99.7-100.4k vs 99.0-99.6k img/s)
@@ -882,6 +889,8 @@ class ResNetProgram:
             kw["cnt"] = self._wg_cnt_of.get(args[2].data_ptr())
         if self.wgrad_lds_pad and self.dev.type == "cuda" and self.overlap_wgrad:
             kw["lds_pad"] = self.wgrad_lds_pad  # occupancy cap: leave room for the main stream's kernels
+        if self.side_cu_reserve and self.dev.type == "cuda" and self.overlap_wgrad:
+            kw["cu_reserve"] = self.side_cu_reserve  # one round over all but N CUs (DBX_SIDE_CU_RESERVE)
         # (a queued weight gradient takes the batch's deferred-reduction list when it is launched)
         # (ws: the workspace override of a gradient moved to the main stream's tail, see _join_side)
         self._side(lambda batch=None, ws=None: K.conv_wgrad(*args[:3], args[3] if ws is None else ws, *args[4:],

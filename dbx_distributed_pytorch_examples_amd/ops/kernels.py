@@ -655,7 +655,7 @@ def _stem_wgrad_tile() -> bool:
 
 
 def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int,
-                 rounds: Optional[float] = None) -> Tuple[int, int]:
+                 rounds: Optional[float] = None, cus: Optional[int] = None) -> Tuple[int, int]:
     """Split the pixel reduction so that ``rounds`` rounds of workgroups stream over the CUs (>= 8
     K-blocks each); the workspace holds nsplit slabs + up to 64 level-1 partial slabs of the
     reduction. ``rounds``: the tune table's per-shape value, else DBX_WGRAD_ROUNDS (2); 0 = no split
@@ -670,7 +670,8 @@ def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int
     tiles = (OC // bm) * (KTOT // bn)
     # r rounds of workgroups over the CUs (8-wave (256-wide) tiles run one per CU, 4-wave two):
     # fewer rounds = longer workgroups and proportionally smaller fp32 partial slabs
-    target = max(1, int(r * (num_cus() if max(bm, bn) >= 256 else 2 * num_cus())) // tiles)
+    ncu = num_cus() if cus is None else cus  # (cus: a side-stream launch sized to leave CUs free)
+    target = max(1, int(r * (ncu if max(bm, bn) >= 256 else 2 * ncu)) // tiles)
     ms = max(512, ((M + target - 1) // target + 63) // 64 * 64)
     nsplit = (M + ms - 1) // ms
     while (nsplit + min(64, nsplit)) * OC * KTOT > max_ws_elems and nsplit > 1:
@@ -752,7 +753,7 @@ class ReduceBatch:
 @_dispatch
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True,
                scale=1.0, accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None, out_krsc=None,
-               rounds=None, defer: "ReduceBatch" = None):
+               rounds=None, defer: "ReduceBatch" = None, cu_reserve: int = 0):
     """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace.
     ``dma``: operand path of the prologue-free kernels -- LDS-DMA ring depth 2 / 3, 0 = register
     staged, -1 = the tune table's choice, else DBX_WGRAD_DMA, else 3 for 256-wide tiles / 2.
@@ -820,7 +821,10 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         _chk(in_scale, torch.float32, "in_scale", IC)
         _chk(in_shift, torch.float32, "in_shift", IC)
     M = N * OH * OW
-    nsplit, ms = wgrad_splits(M, OC, KTOT, bm, bn, ws.numel(), rounds)
+    if cu_reserve > 0:  # one round over all but cu_reserve CUs (the main stream's small kernels keep a place)
+        rounds = min(1.0, 1.0 if rounds is None or rounds <= 0 else float(rounds))
+    nsplit, ms = wgrad_splits(M, OC, KTOT, bm, bn, ws.numel(), rounds,
+                              cus=num_cus() - cu_reserve if cu_reserve > 0 else None)
     if (nsplit + (min(64, nsplit) if nsplit > 8 else 0)) * OC * KTOT > ws.numel():
         raise ValueError("wgrad workspace too small")
     # one split: the kernel writes the finished gradient itself (no slab, no reduce launch)

@@ -126,7 +126,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
 
 def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None, relu_in=True, scale=1.0,
                accumulate=False, stem=False, tile=None, lds_pad=0, dma=-1, cnt=None, out_krsc=None, rounds=None,
-               defer=None):
+               defer=None, cu_reserve=0):
     N, OH, OW, OC = dy.shape
     IC = x.shape[-1]
     xf = _act_in(x, in_scale, in_shift, relu_in)
