@@ -25,7 +25,7 @@ int dbx_wgrad_reduce_job_bytes();
 int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float scale, int accumulate, hipStream_t st);
 int dbx_wgrad_reduce_gather(const float* ws, float* dw, int OC, int R, int S, int IC, int nsplit, float scale,
                             int accumulate, hipStream_t st);
-int dbx_wgrad_patch3(const dbx::WgradArgs* a, long long ws_cap, hipStream_t st);
+int dbx_wgrad_patch3(const dbx::WgradArgs* a, long long ws_cap, hipStream_t st, int max_wg);
 int dbx_conv_dwfused(const dbx::DwFusedArgs* a, long long ws_cap, hipStream_t st);
 int dbx_stem_bwd(dbx::StemBwdArgs* a, long long ws_cap, int fused, hipStream_t st);
 int dbx_bn_finalize(const double*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
@@ -162,11 +162,11 @@ PYBIND11_MODULE(_C, m) {
     check(dbx_conv_wgrad(mode, bm, bn, &a, in_scale != 0, S(st), lds_pad, dma), "conv_wgrad");
   });
   m.def("wgrad_patch3", [](uintptr_t dy, uintptr_t x, uintptr_t ws, long long ws_cap, int N, int IH, int IW, int IC,
-                           int OH, int OW, int OC, int R, int S_, int stride, int pad, uintptr_t st) {
+                           int OH, int OW, int OC, int R, int S_, int stride, int pad, uintptr_t st, int max_wg) {
     // 3x3 patch weight gradient (conv_patch3.hip): one fp32 slab per workgroup; returns the count
     dbx::WgradArgs a{P<const bf16*>(dy), P<const bf16*>(x), P<float*>(ws), nullptr, nullptr, N, IH, IW, IC, OH, OW,
                      OC, R, S_, stride, pad, N * OH * OW, R * S_ * IC, 0, 0, 0, 0ull, 0ull};
-    const int n = dbx_wgrad_patch3(&a, ws_cap, S(st));
+    const int n = dbx_wgrad_patch3(&a, ws_cap, S(st), max_wg);
     if (n <= 0) check(n ? n : -1, "wgrad_patch3");
     return n;
   });

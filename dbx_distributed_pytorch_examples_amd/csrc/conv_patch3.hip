@@ -648,7 +648,8 @@ extern "C" int dbx_stem_patch(const IGemmArgs* args, int stats, hipStream_t st) 
 
 // Weight gradient of the 64 -> 64 3x3 stride-1 convs at width 56: the patch kernel above writes
 // one fp32 slab per workgroup into ws; returns the slab count (the caller reduces), < 0 on error.
-extern "C" int dbx_wgrad_patch3(const WgradArgs* args, long long ws_cap, hipStream_t st) {
+// max_wg > 0: at most that many persistent workgroups (a side-stream launch leaving CUs free)
+extern "C" int dbx_wgrad_patch3(const WgradArgs* args, long long ws_cap, hipStream_t st, int max_wg) {
   const WgradArgs& a = *args;
   if (a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1 || a.IC != 64 || a.OC != 64) return -40;
   if (a.OW != 56 || a.IW != 56 || a.OH != a.IH || a.OH % 4 != 0) return -41;
@@ -659,7 +660,8 @@ extern "C" int dbx_wgrad_patch3(const WgradArgs* args, long long ws_cap, hipStre
     (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return n > 0 ? n : 256;
   }();
-  const int nwg = ntile < cus ? ntile : cus;
+  const int cap = (max_wg > 0 && max_wg < cus) ? max_wg : cus;
+  const int nwg = ntile < cap ? ntile : cap;
   // one slab per workgroup + the caller's two-level reduction partials (<= 64 slabs)
   if ((long long)(nwg + (nwg < 64 ? nwg : 64)) * a.OC * a.R * a.S * a.IC > ws_cap) return -42;
   hipLaunchKernelGGL((wgrad_patch3_kernel<4, 56>), dim3(nwg), dim3(256), 0, st, a);

@@ -654,6 +654,13 @@ def _stem_wgrad_tile() -> bool:
     return _STEM_WGRAD
 
 
+def _patch3_reserve() -> bool:
+    """DBX_PATCH3_RESERVE (default 0): the persistent 3x3 patch weight gradient honours cu_reserve too
+    (headline 16,601-16,639 with vs 16,620-16,653 img/s without: profiles/r5_cu_reserve/)."""
+    import os
+    return os.environ.get("DBX_PATCH3_RESERVE", "0") == "1"
+
+
 def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int,
                  rounds: Optional[float] = None, cus: Optional[int] = None) -> Tuple[int, int]:
     """Split the pixel reduction so that ``rounds`` rounds of workgroups stream over the CUs (>= 8
@@ -779,7 +786,8 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         if (num_cus() + 64) * OC * R * S * IC > ws.numel():  # one slab per CU + the reduction's partials
             raise ValueError("wgrad workspace too small for the patch kernel")
         nsl = C().wgrad_patch3(dy.data_ptr(), x.data_ptr(), ws.data_ptr(), ws.numel(), N, IH, IW, IC, OH, OW, OC, R,
-                               S, stride, pad, stream_ptr())
+                               S, stride, pad, stream_ptr(),
+                               num_cus() - cu_reserve if cu_reserve > 0 and _patch3_reserve() else 0)
         C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsl, float(scale), int(accumulate), stream_ptr())
         return dw
     if isinstance(tile, str):
