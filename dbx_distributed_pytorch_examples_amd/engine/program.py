@@ -1034,6 +1034,8 @@ class ResNetProgram:
                 return
         elif self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
             self._flush_side()  # (the stem / head segments queue theirs here), joined below
+            if self.lazy_join and not final:
+                return  # (DBX_LAZY_JOIN: per-block batches too, joined only at the end)
         self.launch_pending()
         if self._side_pending:
             torch.cuda.current_stream(self.dev).wait_stream(self._wstream)

@@ -457,7 +457,7 @@ def test_composer_trainer_runs_on_native_module():
 
 
 @pytest.mark.parametrize("mode", ["2", "3", "2+tail2", "2+tail2+seg3", "2+l1blocks", "2+tail2+l1blocks", "2+defer",
-                                  "2+tail2+defer", "2+lazy", "2+tail2+defer+lazy"])
+                                  "2+tail2+defer", "2+lazy", "2+tail2+defer+lazy", "3+defer+lazy"])
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64)])
 def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch):
     """DBX_OVERLAP_WGRAD=2 (weight gradients forked once per backward segment, joined one segment
