@@ -118,7 +118,7 @@ class NativeResNet(nn.Module):
                 # next to the comm stream the wgrad side stream costs more than it overlaps
                 # (NativeTrainer, profiles/r2s2_multirank/): weight gradients run on the main stream
                 p.overlap_wgrad = False
-                p.side_batch = False
+                p.side_batch = p.side_block = False
 
     # ------------------------------------------------------------------------------
     def _init_distributed(self):

@@ -134,6 +134,13 @@ class NativeTrainer:
         # gradients in order on the main stream, every range posted right after its own phase
         # (per-gradient forks next to the comm stream cost more than they overlapped:
         # profiles/r2s2_multirank/).
+        if self.segmented and getattr(self.prog, "side_block_default", False):
+            # the per-block default of the larger single-GPU steps posts nothing per segment: the
+            # multi-rank step keeps the batched side stream and its late posts (the validated layout)
+            p = self.prog
+            p.side_block, p.side_batch = False, True
+            p.side_defer = os.environ.get("DBX_SIDE_DEFER", "1" if p.fwd_flops < 5e11 else "0") == "1"
+            p.lazy_join = os.environ.get("DBX_LAZY_JOIN", "1" if p.fwd_flops < 5e10 else "0") == "1"
         seg_side = os.environ.get("DBX_SEG_SIDE", "1") == "1" and (self.ncomm is not None or not self.use_graphs)
         if self.segmented and os.environ.get("DBX_OVERLAP_WGRAD") is None and not seg_side:
             self.prog.overlap_wgrad = False
@@ -159,6 +166,10 @@ class NativeTrainer:
             self.prog.event_joins = True
             if os.environ.get("DBX_SIDE_DEFER") is None:
                 self.prog.side_defer = True  # (the side branch then keeps its own hardware queue)
+        if self.segmented and (self.prog.side_block or not self.comm_side):
+            # collectives posted per segment need that segment's weight gradients joined at its end
+            # (lazy joins only where the collectives ride the side stream behind the batches)
+            self.prog.lazy_join = False
         self.flip = None
         self.seg_ranges = self._segment_ranges()
         self.zero = None

@@ -255,6 +255,17 @@ class ResNetProgram:
         # few blocks at 2048); CIFAR keeps every width (253.1-254.0k vs 251.6-252.5k at <= 256):
         # profiles/r4_s18/. DBX_COEFF_IN_MAXC overrides the width limit (0: none).
         fl = self.fwd_conv_flops()
+        self.fwd_flops = fl
+        # from 50 GFLOP of forward conv work up (TinyImageNet, ImageNet) the default side stream forks
+        # once per residual BLOCK (DBX_OVERLAP_WGRAD=3) -- with the deferred launch and lazy joins below
+        # that fills the windows where the batched side stream waited for its next fork: headline
+        # 16,755-16,865 vs 16,709-16,731, TinyImageNet 100.4-100.8k vs 99.4k img/s; the CIFAR class
+        # keeps one fork per segment (neutral there): profiles/r5_side_defer/mode3.txt. The multi-rank
+        # trainer puts the batched layout back (its collectives are posted per segment).
+        self.side_block_default = ("DBX_OVERLAP_WGRAD" not in os.environ and fl >= 5e10 and not self.fuse_stem_bwd
+                                   and self.overlap_wgrad)
+        if self.side_block_default:
+            self.side_block, self.side_batch = True, False
         self.coeff_in = (os.environ["DBX_COEFF_IN"] == "1" if "DBX_COEFF_IN" in os.environ
                          else fl < 5e11 and self.nshard <= 4)
         mc = os.environ.get("DBX_COEFF_IN_MAXC")
@@ -536,7 +547,7 @@ class ResNetProgram:
         # neutral), off for the b1024 headline (-0.4 % / neutral); the multi-rank one-graph step turns it
         # on (its collectives ride the side stream: TinyImageNet +2.8 %, CIFAR +5 %, profiles/r5_side_defer/)
         self.side_defer = (os.environ["DBX_SIDE_DEFER"] == "1" if "DBX_SIDE_DEFER" in os.environ
-                           else fl < 5e11)
+                           else fl < 5e11 or self.side_block)
         # DBX_SIDE_CU_RESERVE: side-stream weight gradients sized to one round over all but N CUs, so
         # the main chain's small kernels find a CU (the BN-backward coefficient launches took 4.9 us alone
         # and 26.5 us beside the weight gradients); default 64 from the TinyImageNet class up (headline
@@ -568,14 +579,15 @@ class ResNetProgram:
         # (default: the CIFAR class, < 50 GFLOP of forward conv work, +1.2 %; TinyImageNet -0.3 %, the
         # headline -0.5 %: profiles/r5_side_defer/lazy_join.txt)
         self.lazy_join = (os.environ["DBX_LAZY_JOIN"] == "1" if "DBX_LAZY_JOIN" in os.environ
-                          else self.fwd_conv_flops() < 5e10)
+                          else self.fwd_conv_flops() < 5e10 or self.side_block)
         self._pending_side = []
         # the stem weight gradient's own slabs when it runs on the main stream (its split count depends
         # on the grid, not on the workspace capacity)
         self.ws_stem = (torch.empty(40 << 20, device=dev, dtype=torch.float32)
                         if dev.type == "cuda" and self.stem_wg_main else self.ws)
+        # (not tied to the batched layout: the multi-rank trainer may switch a per-block default back to it)
         self.ws_main = (torch.empty_like(self.ws) if ((self.tail_main > 0 or self.seg_tail_main > 0) and dev.type == "cuda"
-                                                       and self.side_batch and self.overlap_wgrad) else self.ws)
+                                                       and self.overlap_wgrad) else self.ws)
         # per-conv tile counters of the in-launch split-K reduction (K.conv_wgrad cnt=): zeroed once,
         # every launch leaves them zero again; keyed by the gradient view's address
         body = [cv for cv in self.convs if not cv.stem]

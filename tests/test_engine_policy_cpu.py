@@ -67,3 +67,22 @@ def test_post_launch_hook_owner_scoped_cancel():
         assert K._POST_LAUNCH is None
     finally:
         K.set_post_launch(None)
+
+
+def test_side_stream_defaults_by_step_size(monkeypatch):
+    """From 50 GFLOP of forward conv work up the default side stream forks per residual block with the
+    deferred launch and lazy joins; below, one fork per segment with lazy joins; an explicit
+    DBX_OVERLAP_WGRAD wins. (The step size is patched: the real ones need GPU-sized buffers.)"""
+    for var in ("DBX_OVERLAP_WGRAD", "DBX_SIDE_DEFER", "DBX_LAZY_JOIN", "DBX_SIDE_CU_RESERVE"):
+        monkeypatch.delenv(var, raising=False)
+    m = build_model("resnet18", num_classes=10)
+    monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e11)
+    p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
+    assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (True, False, True, True, 64)
+    monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e10)
+    p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
+    assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (False, True, True, True, 0)
+    monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e12)
+    monkeypatch.setenv("DBX_OVERLAP_WGRAD", "2")
+    p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
+    assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join) == (False, True, False, False)
