@@ -572,6 +572,8 @@ class ResNetProgram:
         # every segment join then waits for the event behind the segment's batch, not for the
         # collectives queued behind it on the same stream (the final join waits for everything)
         self.event_joins = False
+        self.ds_branch = os.environ.get("DBX_DS_BRANCH", "0") == "1"
+        self._ds_stream = None
         # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
         # its own segment's per-block buffers (never reused within a step) and the workspaces of the main
         # stream's weight gradients are separate, so only the final join (before the optimizer) orders
@@ -1157,6 +1159,22 @@ class ResNetProgram:
             else:
                 K.bn_bwd_apply(g, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_NONE, fin=fin_of(lbn))
         assert not todo, "a tail BN's backward finalize was left pending"
+        # DBX_DS_BRANCH: the downsample conv's data gradient depends only on the block-output gradient
+        # (and its BN-backward apply): run it on a branch stream beside the inner convs' data gradients,
+        # joined right before conv1's dgrad consumes it as the shortcut gradient
+        ds_evt = None
+        if b.ds_conv is not None and self.ds_branch and self.dev.type == "cuda":
+            if self._ds_stream is None:
+                self._ds_stream = torch.cuda.Stream(device=self.dev)
+            dc = b.ds_conv
+            self._ds_stream.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(self._ds_stream):
+                if ds_fold is None:
+                    K.conv_dgrad(b.dyd, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0)
+                else:
+                    K.conv_dgrad(g, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0, **ds_fold)
+            ds_evt = torch.cuda.Event()
+            ds_evt.record(self._ds_stream)
         # inner convs, last to second: dgrad epilogue masks with the previous BN's ReLU and
         # accumulates that BN's backward statistics
         for j in range(nconv - 1, 0, -1):
@@ -1208,7 +1226,10 @@ class ResNetProgram:
             self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
         if b.ds_conv is not None:
             dc = b.ds_conv
-            if ds_fold is None:
+            if ds_evt is not None:  # (dgrad on the branch stream above: join it; the wgrad follows)
+                torch.cuda.current_stream(self.dev).wait_event(ds_evt)
+                self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
+            elif ds_fold is None:
                 self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
                 # 1x1 strided downsample: its dgrad is a dense GEMM onto the stride-subsampled pixels
                 K.conv_dgrad(b.dyd, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0)
@@ -1292,7 +1313,8 @@ class ResNetProgram:
         # small steps (stem_wg_main, see __init__): with the batched side stream the stem weight gradient
         # runs on the MAIN stream right here, next to the side stream's last batch (layer1's weight
         # gradients, forked at layer1's end) instead of queued behind it; its slabs live in ws_stem
-        on_main = self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad and self.stem_wg_main
+        on_main = ((self.side_batch or self.side_block) and self.dev.type == "cuda" and self.overlap_wgrad
+                   and self.stem_wg_main)
 
         def stem_wgrad():
             # reduced straight into the flat gradient's (OC, R, S, IC) slice when the stem tile kernel
