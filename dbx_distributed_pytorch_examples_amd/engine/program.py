@@ -572,7 +572,7 @@ class ResNetProgram:
         # every segment join then waits for the event behind the segment's batch, not for the
         # collectives queued behind it on the same stream (the final join waits for everything)
         self.event_joins = False
-        self.ds_branch = os.environ.get("DBX_DS_BRANCH", "0") == "1"
+        self.ds_branch = int(os.environ.get("DBX_DS_BRANCH", "0"))
         self._ds_stream = None
         # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
         # its own segment's per-block buffers (never reused within a step) and the workspaces of the main
@@ -1162,19 +1162,42 @@ class ResNetProgram:
         # DBX_DS_BRANCH: the downsample conv's data gradient depends only on the block-output gradient
         # (and its BN-backward apply): run it on a branch stream beside the inner convs' data gradients,
         # joined right before conv1's dgrad consumes it as the shortcut gradient
+        # (1: its own stream -- a third graph branch, which the runtime's queue mapping handles badly;
+        # 2: the weight-gradient side stream, launched like a deferred side batch after the main
+        # stream's next kernel)
         ds_evt = None
-        if b.ds_conv is not None and self.ds_branch and self.dev.type == "cuda":
-            if self._ds_stream is None:
-                self._ds_stream = torch.cuda.Stream(device=self.dev)
+        if b.ds_conv is not None and self.ds_branch and self.dev.type == "cuda" and self.overlap_wgrad:
             dc = b.ds_conv
-            self._ds_stream.wait_stream(torch.cuda.current_stream(self.dev))
-            with torch.cuda.stream(self._ds_stream):
+
+            def ds_dgrad():
                 if ds_fold is None:
                     K.conv_dgrad(b.dyd, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0)
                 else:
                     K.conv_dgrad(g, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0, **ds_fold)
             ds_evt = torch.cuda.Event()
-            ds_evt.record(self._ds_stream)
+            if self.ds_branch == 1:
+                if self._ds_stream is None:
+                    self._ds_stream = torch.cuda.Stream(device=self.dev)
+                self._ds_stream.wait_stream(torch.cuda.current_stream(self.dev))
+                with torch.cuda.stream(self._ds_stream):
+                    ds_dgrad()
+                ds_evt.record(self._ds_stream)
+            else:
+                side = self.side_stream()
+                fork = torch.cuda.Event()
+                fork.record(torch.cuda.current_stream(self.dev))
+
+                def launch_ds():
+                    side.wait_event(fork)
+                    with torch.cuda.stream(side):
+                        ds_dgrad()
+                    ds_evt.record(side)
+                self._side_pending = True
+                if self._pending_side:
+                    self._pending_side.append(launch_ds)
+                else:
+                    self._pending_side = [launch_ds]
+                    K.set_post_launch(self.launch_pending)
         # inner convs, last to second: dgrad epilogue masks with the previous BN's ReLU and
         # accumulates that BN's backward statistics
         for j in range(nconv - 1, 0, -1):
@@ -1227,6 +1250,7 @@ class ResNetProgram:
         if b.ds_conv is not None:
             dc = b.ds_conv
             if ds_evt is not None:  # (dgrad on the branch stream above: join it; the wgrad follows)
+                self.launch_pending()
                 torch.cuda.current_stream(self.dev).wait_event(ds_evt)
                 self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
             elif ds_fold is None:
