@@ -573,6 +573,7 @@ class ResNetProgram:
         # collectives queued behind it on the same stream (the final join waits for everything)
         self.event_joins = False
         self.ds_branch = int(os.environ.get("DBX_DS_BRANCH", "0"))
+        self.ds_fwd_side = os.environ.get("DBX_DS_FWD_SIDE", "0") == "1"
         self._ds_stream = None
         # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
         # its own segment's per-block buffers (never reused within a step) and the workspaces of the main
@@ -776,6 +777,10 @@ class ResNetProgram:
         K.maxpool_fwd(self.y0, self.p0, self.parg, K=self.pool_k, stride=self.pool_s, pad=self.pool_p,
                       scale=sbn.scale, shift=sbn.shift, relu=True, ymax=self.pymax if tr else None, fin=sfin)
         x = self.p0
+        # DBX_DS_FWD_SIDE: a downsample conv reads only the block input (written by the block's conv1
+        # tail prologue): it runs on the side stream beside conv2 / conv3, launched like a deferred side
+        # batch after the main stream's next kernel, joined at the block's end
+        ds_launch = {} if (self.ds_fwd_side and tr and self.dev.type == "cuda" and self.overlap_wgrad) else None
         pending = None  # previous block whose output this block's conv1 computes (tail prologue)
         out_fin = None  # the last BN's forward finalize, done by the block-output bn_apply (fin_in)
         for bi, b in enumerate(self.blocks):
@@ -802,6 +807,8 @@ class ResNetProgram:
                                in_shift=prev_bn.shift if prev_bn else None, relu_in=True,
                                fin=self._ff(b.bns[i]), fin_in=deferred.fin_f if deferred is not None else None)
                 deferred = None
+                if i == 0 and ds_launch is not None and b.ds_conv is not None:
+                    ds_launch[bi] = self._ds_fwd_on_side(b, x, N)
                 nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
                 c1 = nxt.convs[0] if nxt is not None else None
                 tail = (self.fuse_tail and c1 is not None
@@ -819,13 +826,18 @@ class ResNetProgram:
             res_fin = None
             if b.ds_conv is not None:
                 dc = b.ds_conv
-                K.conv_fwd(x, dc.w16, b.yd, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad,
-                           stats=b.ds_bn.stats if tr else None, fin=self._ff(b.ds_bn))
+                side_ds = ds_launch.get(bi) if ds_launch else None
+                if side_ds is None:
+                    K.conv_fwd(x, dc.w16, b.yd, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad,
+                               stats=b.ds_bn.stats if tr else None, fin=self._ff(b.ds_bn))
                 if self._ff(b.ds_bn) is None:
                     if tr and self.fin_in and b.ds_bn.fin_f is not None:
                         res_fin = b.ds_bn.fin_f  # finalized by the block-output bn_apply / next conv1 below
-                    else:
+                    elif side_ds is None:
                         self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
+                if side_ds is not None:  # (launched on the side stream after conv1: join it here)
+                    self.launch_pending()
+                    torch.cuda.current_stream(self.dev).wait_event(side_ds)
                 res, rsc, rsh = b.yd, b.ds_bn.scale, b.ds_bn.shift
             else:
                 res, rsc, rsh = x, None, None
@@ -848,6 +860,28 @@ class ResNetProgram:
                      self.metrics if metrics else None, smoothing=smoothing, grad_scale=grad_scale,
                      labels2=self.labels2 if mix else None, lam=self.mix_lam if mix else None)
         return self.logits
+
+    def _ds_fwd_on_side(self, b, x, N):
+        """Queue block b's downsample conv (+ its BN finalize unless a consumer does it) for the side
+        stream, forked from the main stream's current point; returns the event that ends it."""
+        dc, side = b.ds_conv, self.side_stream()
+        fork, done = torch.cuda.Event(), torch.cuda.Event()
+        fork.record(torch.cuda.current_stream(self.dev))
+
+        def launch():
+            side.wait_event(fork)
+            with torch.cuda.stream(side):
+                K.conv_fwd(x, dc.w16, b.yd, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad, stats=b.ds_bn.stats,
+                           fin=self._ff(b.ds_bn))
+                if self._ff(b.ds_bn) is None and not (self.fin_in and b.ds_bn.fin_f is not None):
+                    self._bn_fwd(b.ds_bn, N * dc.OH * dc.OW)
+            done.record(side)
+        if self._pending_side:  # (joined by its event at the block's end: no _side_pending)
+            self._pending_side.append(launch)
+        else:
+            self._pending_side = [launch]
+            K.set_post_launch(self.launch_pending)
+        return done
 
     def backward_segments(self):
         """Yield closures, one per backward segment; after segment k all params whose

@@ -457,7 +457,8 @@ def test_composer_trainer_runs_on_native_module():
 
 
 @pytest.mark.parametrize("mode", ["2", "3", "2+tail2", "2+tail2+seg3", "2+l1blocks", "2+tail2+l1blocks", "2+defer",
-                                  "2+tail2+defer", "2+lazy", "2+tail2+defer+lazy", "3+defer+lazy", "3+defer+lazy+ds", "3+defer+lazy+ds2"])
+                                  "2+tail2+defer", "2+lazy", "2+tail2+defer+lazy", "3+defer+lazy", "3+defer+lazy+ds", "3+defer+lazy+ds2",
+                                  "3+defer+lazy+dsf"])
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64)])
 def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch):
     """DBX_OVERLAP_WGRAD=2 (weight gradients forked once per backward segment, joined one segment
@@ -483,7 +484,10 @@ def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch)
     # "lazy": no intermediate joins of the side stream (DBX_LAZY_JOIN)
     monkeypatch.setenv("DBX_LAZY_JOIN", "1" if "lazy" in mode else "0")
     # "ds": the downsample conv's data gradient on a branch stream (DBX_DS_BRANCH)
-    monkeypatch.setenv("DBX_DS_BRANCH", "2" if "+ds2" in mode else ("1" if "+ds" in mode else "0"))
+    opts = mode.split("+")
+    monkeypatch.setenv("DBX_DS_BRANCH", "2" if "ds2" in opts else ("1" if "ds" in opts else "0"))
+    # "dsf": the downsample conv's forward on the side stream beside conv2 / conv3 (DBX_DS_FWD_SIDE)
+    monkeypatch.setenv("DBX_DS_FWD_SIDE", "1" if "dsf" in opts else "0")
     t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "0")
     t2 = NativeTrainer(m2, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
