@@ -573,7 +573,10 @@ class ResNetProgram:
         # collectives queued behind it on the same stream (the final join waits for everything)
         self.event_joins = False
         self.ds_branch = int(os.environ.get("DBX_DS_BRANCH", "0"))
-        self.ds_fwd_side = os.environ.get("DBX_DS_FWD_SIDE", "0") == "1"
+        # the downsample conv's forward beside conv2 / conv3 on the side stream: +0.24 % on the headline
+        # over five interleaved rounds, neutral on TinyImageNet (profiles/r5_side_defer/ds_fwd.txt)
+        self.ds_fwd_side = (os.environ["DBX_DS_FWD_SIDE"] == "1" if "DBX_DS_FWD_SIDE" in os.environ
+                            else fl >= 5e11)
         self._ds_stream = None
         # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
         # its own segment's per-block buffers (never reused within a step) and the workspaces of the main
