@@ -217,7 +217,10 @@ class ResNetProgram:
         # block's acts buffer, which backward needs anyway) and runs the conv without a prologue
         self.fast_mat = os.environ.get("DBX_FAST_MAT", "1") == "1"
         # ... also the 1x1 conv3 of a bottleneck (short-K C -> 4C forward) where its plain shape has one
-        self.fast_mat1 = os.environ.get("DBX_FAST_MAT1", "0") == "1"
+        # (DBX_FAST_MAT1=1: every stage; a value > 1: only maps of at most that size, e.g. 14)
+        _m1 = int(os.environ.get("DBX_FAST_MAT1", "0"))
+        self.fast_mat1 = _m1 > 0
+        self.fast_mat1_max_hw = _m1 if _m1 > 1 else 1 << 30
         self._wstream = None
         self._side_pending = False
         # DBX_OVERLAP_WGRAD unset / 2: the side stream forks once per backward segment (batched) instead
@@ -1324,7 +1327,8 @@ class ResNetProgram:
     def _materialize(self, cv: ConvL) -> bool:
         """Does conv ``cv`` (a block-internal 3x3, or with DBX_FAST_MAT1 a bottleneck conv3) take a
         materialised BN output on the eight-wave kernel?"""
-        if not (self.fast_mat and self.dev.type == "cuda" and cv.stride == 1 and (cv.R == 3 or (cv.R == 1 and self.fast_mat1))):
+        if not (self.fast_mat and self.dev.type == "cuda" and cv.stride == 1
+                and (cv.R == 3 or (cv.R == 1 and self.fast_mat1 and cv.OH <= self.fast_mat1_max_hw))):
             return False
         t = K.pick_tile(self.N * cv.OH * cv.OW, cv.OC, "fwd0", cv.IC, cv.R, cv.stride)
         return len(t) > 2 and t[2] in (4, 5)
