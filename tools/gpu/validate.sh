@@ -1,6 +1,6 @@
 #!/bin/bash
 # Validation of the tree on one GPU: the full GPU suite, smoke, every bench line (headline twice, ZeRO-1,
-# presets, the world-1 RCCL one-graph step), then the headline kernel profile.
+# presets, the world-1 RCCL one-graph step, two gloo ranks on the device), then the headline kernel profile.
 set -o pipefail
 O=${1:-gpurun_out/validate}
 mkdir -p $O
@@ -20,4 +20,9 @@ DBX_FORCE_PG=1 DBX_SEGMENTED_GRAPHS=1 timeout -k 10 300 python -m torch.distribu
   || { tail -20 $O/bench_rccl_world1.log; exit 1; }
 grep '"metric"' $O/bench_rccl_world1.log >> $O/bench_lines.txt
 echo "headline world-1 RCCL one-graph: $(grep -o '"value": [0-9.]*' $O/bench_rccl_world1.log)"
+# two ranks on the one device over gloo (the c10d segmented step, replica checks at world 2)
+DBX_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --preset resnet18_cifar10 --steps 10 --warmup 3 \
+  > $O/bench_gloo2.log 2>&1 || { tail -20 $O/bench_gloo2.log; exit 1; }
+grep '"metric"' $O/bench_gloo2.log >> $O/bench_lines.txt
+grep "replicas in sync" $O/bench_gloo2.log
 bash tools/gpu/profile_headline.sh $O/prof
