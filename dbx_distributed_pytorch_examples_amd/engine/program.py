@@ -563,6 +563,8 @@ class ResNetProgram:
         self.tail_main = int(os.environ["DBX_TAIL_MAIN"] if "DBX_TAIL_MAIN" in os.environ
                              else ((3 if self.side_defer else 2) if 5e10 <= fl < 5e11 else 0))
         self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
+        # the same for the per-block side forks (DBX_OVERLAP_WGRAD=3): the last block's last N
+        self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN", "0"))
         self._main_tail = []
         # layer1 (the last batch, exposed at the end of the step) forks its weight gradients per block
         # instead of once at the segment's end, so they start under layer1's own remaining data
@@ -595,7 +597,8 @@ class ResNetProgram:
         self.ws_stem = (torch.empty(40 << 20, device=dev, dtype=torch.float32)
                         if dev.type == "cuda" and self.stem_wg_main else self.ws)
         # (not tied to the batched layout: the multi-rank trainer may switch a per-block default back to it)
-        self.ws_main = (torch.empty_like(self.ws) if ((self.tail_main > 0 or self.seg_tail_main > 0) and dev.type == "cuda"
+        self.ws_main = (torch.empty_like(self.ws) if ((self.tail_main > 0 or self.seg_tail_main > 0
+                                                      or self.block_tail_main > 0) and dev.type == "cuda"
                                                        and self.overlap_wgrad) else self.ws)
         # per-conv tile counters of the in-launch split-K reduction (K.conv_wgrad cnt=): zeroed once,
         # every launch leaves them zero again; keyed by the gradient view's address
@@ -907,8 +910,9 @@ class ResNetProgram:
         for li in (4, 3, 2, 1):
             idx = list(reversed(stages[li]))
             per_block = li == 1 and self.last_seg_blocks
-            segs.append((f"layer{li}", (lambda idx=idx, pb=per_block: [
-                (self._bwd_block(i), self._block_flush(), self._seg_block_flush(pb and j < len(idx) - 1))
+            segs.append((f"layer{li}", (lambda idx=idx, pb=per_block, li=li: [
+                (self._bwd_block(i), self._block_flush(li == 1 and j == len(idx) - 1),
+                 self._seg_block_flush(pb and j < len(idx) - 1))
                 for j, i in enumerate(idx)])))
         segs.append(("stem", self._bwd_stem))
         # every segment ends with its weight gradients complete on the main stream (join)
@@ -1031,8 +1035,14 @@ class ResNetProgram:
         self._pending_side = []
         K.set_post_launch(None, owner=self.launch_pending)
 
-    def _block_flush(self):
+    def _block_flush(self, last: bool = False):
         if self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
+            # the step's last block: its last DBX_TAIL_MAIN weight gradients run on the main stream after
+            # the stem's backward (their own workspace) instead of behind the rest on the side stream
+            n = self.block_tail_main if last else 0
+            if n > 0 and len(self._side_q) > n:
+                self._main_tail = self._side_q[-n:]
+                self._side_q = self._side_q[:-n]
             self._flush_side()  # this block's weight gradients, under the next block's data gradients
 
     def side_stream(self):
@@ -1090,6 +1100,10 @@ class ResNetProgram:
             self._flush_side()  # (the stem / head segments queue theirs here), joined below
             if self.lazy_join and not final:
                 return  # (DBX_LAZY_JOIN: per-block batches too, joined only at the end)
+            if final and self._main_tail:
+                for fn in self._main_tail:  # (see _block_flush)
+                    fn(None, self.ws_main)
+                self._main_tail = []
         self.launch_pending()
         if self._side_pending:
             torch.cuda.current_stream(self.dev).wait_stream(self._wstream)

@@ -458,7 +458,7 @@ def test_composer_trainer_runs_on_native_module():
 
 @pytest.mark.parametrize("mode", ["2", "3", "2+tail2", "2+tail2+seg3", "2+l1blocks", "2+tail2+l1blocks", "2+defer",
                                   "2+tail2+defer", "2+lazy", "2+tail2+defer+lazy", "3+defer+lazy", "3+defer+lazy+ds", "3+defer+lazy+ds2",
-                                  "3+defer+lazy+dsf"])
+                                  "3+defer+lazy+dsf", "3+btail2+defer+lazy"])
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64)])
 def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch):
     """DBX_OVERLAP_WGRAD=2 (weight gradients forked once per backward segment, joined one segment
@@ -475,7 +475,7 @@ def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch)
     # "2+tail2": the last batch's two last weight gradients on the main stream's tail (DBX_TAIL_MAIN),
     # the stem weight gradient on the main stream (the batched default)
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", mode[0])
-    monkeypatch.setenv("DBX_TAIL_MAIN", "2" if "tail2" in mode else "0")
+    monkeypatch.setenv("DBX_TAIL_MAIN", "2" if "tail2" in mode.split("+") else "0")
     monkeypatch.setenv("DBX_SEG_TAIL_MAIN", "3" if "seg3" in mode else "0")
     # "l1blocks": layer1's weight gradients forked per block (DBX_LAST_SEG_BLOCKS)
     monkeypatch.setenv("DBX_LAST_SEG_BLOCKS", "1" if "l1blocks" in mode else "0")
@@ -486,13 +486,15 @@ def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch)
     # "ds": the downsample conv's data gradient on a branch stream (DBX_DS_BRANCH)
     opts = mode.split("+")
     monkeypatch.setenv("DBX_DS_BRANCH", "2" if "ds2" in opts else ("1" if "ds" in opts else "0"))
+    # "btail2": per-block forks, the last block's last two weight gradients on the main stream (DBX_BLOCK_TAIL_MAIN)
+    monkeypatch.setenv("DBX_BLOCK_TAIL_MAIN", "2" if "btail2" in opts else "0")
     # "dsf": the downsample conv's forward on the side stream beside conv2 / conv3 (DBX_DS_FWD_SIDE)
     monkeypatch.setenv("DBX_DS_FWD_SIDE", "1" if "dsf" in opts else "0")
     t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "0")
     t2 = NativeTrainer(m2, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     assert (t1.prog.side_batch if mode[0] == "2" else t1.prog.side_block) and t1.prog.overlap_wgrad
-    assert t1.prog.tail_main == (2 if "tail2" in mode else 0)
+    assert t1.prog.tail_main == (2 if "tail2" in mode.split("+") else 0)
     assert t1.prog.last_seg_blocks == ("l1blocks" in mode)
     assert t1.prog.side_defer == ("defer" in mode)
     assert not t2.prog.overlap_wgrad
