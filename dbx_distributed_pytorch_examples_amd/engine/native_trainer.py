@@ -141,6 +141,7 @@ class NativeTrainer:
             p.side_block, p.side_batch = False, True
             p.side_defer = os.environ.get("DBX_SIDE_DEFER", "1" if p.fwd_flops < 5e11 else "0") == "1"
             p.lazy_join = os.environ.get("DBX_LAZY_JOIN", "1" if p.fwd_flops < 5e10 else "0") == "1"
+            p.stem_wg_main = os.environ.get("DBX_STEM_WG_MAIN", "1" if p.fwd_flops < 5e11 else "0") == "1"
         seg_side = os.environ.get("DBX_SEG_SIDE", "1") == "1" and (self.ncomm is not None or not self.use_graphs)
         if self.segmented and os.environ.get("DBX_OVERLAP_WGRAD") is None and not seg_side:
             self.prog.overlap_wgrad = False

@@ -557,14 +557,16 @@ class ResNetProgram:
         # +0.8 %, TinyImageNet +0.6-0.9 %), 0 for the CIFAR class (-0.4 %): profiles/r5_cu_reserve/
         self.side_cu_reserve = int(os.environ["DBX_SIDE_CU_RESERVE"] if "DBX_SIDE_CU_RESERVE" in os.environ
                                    else (64 if fl >= 5e10 else 0))
+        # (with the per-block forks from 500 GFLOP up, together with two of the last block's weight
+        # gradients: headline +0.38 % over five interleaved rounds, profiles/r5_side_defer/block_tail.txt)
         self.stem_wg_main = (os.environ["DBX_STEM_WG_MAIN"] == "1" if "DBX_STEM_WG_MAIN" in os.environ
-                             else fl < 5e11)
+                             else fl < 5e11 or self.side_block)
         # (with the deferred launch the TinyImageNet class moves three: 99.7-100.4k vs 99.0-99.6k img/s)
         self.tail_main = int(os.environ["DBX_TAIL_MAIN"] if "DBX_TAIL_MAIN" in os.environ
                              else ((3 if self.side_defer else 2) if 5e10 <= fl < 5e11 else 0))
         self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
         # the same for the per-block side forks (DBX_OVERLAP_WGRAD=3): the last block's last N
-        self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN", "0"))
+        self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN", "2" if fl >= 5e11 else "0"))
         self._main_tail = []
         # layer1 (the last batch, exposed at the end of the step) forks its weight gradients per block
         # instead of once at the segment's end, so they start under layer1's own remaining data

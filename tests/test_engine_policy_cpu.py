@@ -73,18 +73,21 @@ def test_side_stream_defaults_by_step_size(monkeypatch):
     """From 50 GFLOP of forward conv work up the default side stream forks per residual block with the
     deferred launch and lazy joins; below, one fork per segment with lazy joins; an explicit
     DBX_OVERLAP_WGRAD wins. (The step size is patched: the real ones need GPU-sized buffers.)"""
-    for var in ("DBX_OVERLAP_WGRAD", "DBX_SIDE_DEFER", "DBX_LAZY_JOIN", "DBX_SIDE_CU_RESERVE", "DBX_DS_FWD_SIDE"):
+    for var in ("DBX_OVERLAP_WGRAD", "DBX_SIDE_DEFER", "DBX_LAZY_JOIN", "DBX_SIDE_CU_RESERVE", "DBX_DS_FWD_SIDE",
+                "DBX_BLOCK_TAIL_MAIN", "DBX_STEM_WG_MAIN"):
         monkeypatch.delenv(var, raising=False)
     m = build_model("resnet18", num_classes=10)
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e11)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (True, False, True, True, 64)
     assert not p.ds_fwd_side  # (the downsample forward on the side stream: from 500 GFLOP up)
+    assert (p.block_tail_main, p.stem_wg_main) == (0, True)
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e10)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (False, True, True, True, 0)
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e12)
-    assert ResNetProgram(m, 2, (32, 32), torch.device("cpu")).ds_fwd_side
+    p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
+    assert p.ds_fwd_side and (p.block_tail_main, p.stem_wg_main) == (2, True)
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "2")
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
-    assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join) == (False, True, False, False)
+    assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.stem_wg_main) == (False, True, False, False, False)
