@@ -566,7 +566,8 @@ class ResNetProgram:
                              else ((3 if self.side_defer else 2) if 5e10 <= fl < 5e11 else 0))
         self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
         # the same for the per-block side forks (DBX_OVERLAP_WGRAD=3): the last block's last N
-        self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN", "2" if fl >= 5e11 else "0"))
+        self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN",
+                                                  "2" if fl >= 5e11 else ("1" if fl >= 5e10 else "0")))
         self._main_tail = []
         # layer1 (the last batch, exposed at the end of the step) forks its weight gradients per block
         # instead of once at the segment's end, so they start under layer1's own remaining data
@@ -581,9 +582,10 @@ class ResNetProgram:
         self.event_joins = False
         self.ds_branch = int(os.environ.get("DBX_DS_BRANCH", "0"))
         # the downsample conv's forward beside conv2 / conv3 on the side stream: +0.24 % on the headline
-        # over five interleaved rounds, neutral on TinyImageNet (profiles/r5_side_defer/ds_fwd.txt)
+        # over five interleaved rounds, TinyImageNet neutral alone and +0.67 % with its block tail of one
+        # (profiles/r5_side_defer/ds_fwd.txt, block_tail.txt)
         self.ds_fwd_side = (os.environ["DBX_DS_FWD_SIDE"] == "1" if "DBX_DS_FWD_SIDE" in os.environ
-                            else fl >= 5e11)
+                            else fl >= 5e10)
         self._ds_stream = None
         # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
         # its own segment's per-block buffers (never reused within a step) and the workspaces of the main

@@ -136,7 +136,7 @@ def test_nonblocking_init_and_captured_check(world1):
     c.close()
 
 
-@pytest.mark.parametrize("comm_side", ["1", "0", "1+defer", "1+defer+lazy"])
+@pytest.mark.parametrize("comm_side", ["1", "0", "1+defer", "1+defer+lazy", "1+defer+dsf"])
 @pytest.mark.parametrize("model,hw,batch", [("resnet18", 32, 32), ("resnet50", 64, 16)])
 def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batch, comm_side):
     """The one-graph multi-rank step's all-reduce ORDER, checked at world 1: with DBX_COMM_LOOPBACK=2
@@ -152,6 +152,8 @@ def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batc
     monkeypatch.setenv("DBX_COMM_SIDE", comm_side[0])
     monkeypatch.setenv("DBX_SIDE_DEFER", "1" if "defer" in comm_side else "0")
     monkeypatch.setenv("DBX_LAZY_JOIN", "1" if "lazy" in comm_side else "0")
+    # "dsf": the downsample forwards on the same side stream as the collectives (DBX_DS_FWD_SIDE)
+    monkeypatch.setenv("DBX_DS_FWD_SIDE", "1" if "dsf" in comm_side else "0")
     torch.manual_seed(0)
     m1 = build_model(model, num_classes=10)
     m2 = copy.deepcopy(m1)
@@ -161,7 +163,7 @@ def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batc
     t2 = NativeTrainer(m2, batch, (hw, hw), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     assert t1.ncomm is not None and t1.loopback == 2 and t2.loopback == 1 and t1.late_posts
     assert t1.comm_side == (comm_side[0] == "1") and t1.prog.event_joins == t1.comm_side
-    assert t1.prog.side_defer == ("defer" in comm_side)
+    assert t1.prog.side_defer == ("defer" in comm_side) and t1.prog.ds_fwd_side == ("dsf" in comm_side)
     g = torch.Generator().manual_seed(1)
     for i in range(6):
         img = torch.randint(0, 256, (batch, hw, hw, 3), dtype=torch.uint8, generator=g).cuda()

@@ -80,10 +80,11 @@ def test_side_stream_defaults_by_step_size(monkeypatch):
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e11)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (True, False, True, True, 64)
-    assert not p.ds_fwd_side  # (the downsample forward on the side stream: from 500 GFLOP up)
-    assert (p.block_tail_main, p.stem_wg_main) == (0, True)
+    assert p.ds_fwd_side  # (the downsample forward on the side stream: from 50 GFLOP up)
+    assert (p.block_tail_main, p.stem_wg_main) == (1, True)
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e10)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
+    assert not p.ds_fwd_side and p.block_tail_main == 0
     assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (False, True, True, True, 0)
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e12)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
