@@ -553,10 +553,12 @@ class ResNetProgram:
                            else fl < 5e11 or self.side_block)
         # DBX_SIDE_CU_RESERVE: side-stream weight gradients sized to one round over all but N CUs, so
         # the main chain's small kernels find a CU (the BN-backward coefficient launches took 4.9 us alone
-        # and 26.5 us beside the weight gradients); default 64 from the TinyImageNet class up (headline
-        # +0.8 %, TinyImageNet +0.6-0.9 %), 0 for the CIFAR class (-0.4 %): profiles/r5_cu_reserve/
+        # and 26.5 us beside the weight gradients); default 128 from the TinyImageNet class up (64: headline
+        # +0.8 %, TinyImageNet +0.6-0.9 %; re-swept with the per-block forks and main-stream tails, 128 over
+        # 64: TinyImageNet +1.8 %, headline +0.4 %; 160+ loses), 0 for the CIFAR class (64: -0.4 %, 128:
+        # -1 %): profiles/r5_cu_reserve/
         self.side_cu_reserve = int(os.environ["DBX_SIDE_CU_RESERVE"] if "DBX_SIDE_CU_RESERVE" in os.environ
-                                   else (64 if fl >= 5e10 else 0))
+                                   else (128 if fl >= 5e10 else 0))
         # (with the per-block forks from 500 GFLOP up, together with two of the last block's weight
         # gradients: headline +0.38 % over five interleaved rounds, profiles/r5_side_defer/block_tail.txt)
         self.stem_wg_main = (os.environ["DBX_STEM_WG_MAIN"] == "1" if "DBX_STEM_WG_MAIN" in os.environ
