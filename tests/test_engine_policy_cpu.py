@@ -81,7 +81,7 @@ def test_side_stream_defaults_by_step_size(monkeypatch):
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (True, False, True, True, 128)
     assert p.ds_fwd_side  # (the downsample forward on the side stream: from 50 GFLOP up)
-    assert (p.block_tail_main, p.stem_wg_main) == (1, True)
+    assert (p.block_tail_main, p.stem_wg_main) == (2, True)
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e10)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert not p.ds_fwd_side and p.block_tail_main == 0
