@@ -889,12 +889,14 @@ def dwfused_grid(C: int, K: int) -> int:
 
 def dwfused_preferred(C: int, K: int, M: int) -> bool:
     """Schedule policy: the fused conv3 backward only when every resident workgroup walks >=
-    DBX_FUSE_DW_MIN_TILES (default 8) tiles -- with fewer, the per-workgroup weight load and slab write
+    DBX_FUSE_DW_MIN_TILES (default 4) tiles -- with fewer, the per-workgroup weight load and slab write
     and the lost wgrad side-stream overlap outweigh the saved traffic (TinyImageNet b512 fused at 2-4
-    tiles per workgroup: 86.5k vs 87.2k img/s, profiles/r2s4_dwfused/)."""
+    tiles per workgroup: 86.5k vs 87.2k img/s in round 2, profiles/r2s4_dwfused/; with the round-5
+    per-block side forks and the 128-CU reservation its 4-tile layer1 conv3 gains: 104.3k vs 103.7k,
+    2 tiles still loses: profiles/r5_side_defer/tiny_knobs_late.txt)."""
     import os
     grid = dwfused_grid(C, K)
-    return dwfused_supported(C, K, M) and M >= int(os.environ.get("DBX_FUSE_DW_MIN_TILES", "8")) * grid * 64
+    return dwfused_supported(C, K, M) and M >= int(os.environ.get("DBX_FUSE_DW_MIN_TILES", "4")) * grid * 64
 
 
 @_dispatch
