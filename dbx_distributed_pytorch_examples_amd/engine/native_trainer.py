@@ -142,6 +142,11 @@ class NativeTrainer:
             p.side_defer = os.environ.get("DBX_SIDE_DEFER", "1" if p.fwd_flops < 5e11 else "0") == "1"
             p.lazy_join = os.environ.get("DBX_LAZY_JOIN", "1" if p.fwd_flops < 5e10 else "0") == "1"
             p.stem_wg_main = os.environ.get("DBX_STEM_WG_MAIN", "1" if p.fwd_flops < 5e11 else "0") == "1"
+            # (with its collectives on the side stream the batched layout keeps the 64-CU reservation:
+            # world-1 RCCL one-graph step with a real collective kernel, headline +0.5-1.1 % over 128,
+            # TinyImageNet +0.1 %, profiles/r5_cu_reserve/sweep_late.txt)
+            if "DBX_SIDE_CU_RESERVE" not in os.environ:
+                p.side_cu_reserve = 64 if p.fwd_flops >= 5e10 else 0
         seg_side = os.environ.get("DBX_SEG_SIDE", "1") == "1" and (self.ncomm is not None or not self.use_graphs)
         if self.segmented and os.environ.get("DBX_OVERLAP_WGRAD") is None and not seg_side:
             self.prog.overlap_wgrad = False

@@ -259,13 +259,16 @@ class ResNetProgram:
         # profiles/r4_s18/. DBX_COEFF_IN_MAXC overrides the width limit (0: none).
         fl = self.fwd_conv_flops()
         self.fwd_flops = fl
-        # from 50 GFLOP of forward conv work up (TinyImageNet, ImageNet) the default side stream forks
-        # once per residual BLOCK (DBX_OVERLAP_WGRAD=3) -- with the deferred launch and lazy joins below
+        # by default the side stream forks once per residual BLOCK (DBX_OVERLAP_WGRAD=3; first from 50
+        # GFLOP of forward conv work up, TinyImageNet and ImageNet) -- with the deferred launch and lazy joins below
         # that fills the windows where the batched side stream waited for its next fork: headline
         # 16,755-16,865 vs 16,709-16,731, TinyImageNet 100.4-100.8k vs 99.4k img/s; the CIFAR class
         # keeps one fork per segment (neutral there): profiles/r5_side_defer/mode3.txt. The multi-rank
         # trainer puts the batched layout back (its collectives are posted per segment).
-        self.side_block_default = ("DBX_OVERLAP_WGRAD" not in os.environ and fl >= 5e10 and not self.fuse_stem_bwd
+        # (late in round 5, with the block tails on the main stream and the downsample forward on the side
+        # stream, the CIFAR class gains too: 267.4-267.8k vs 262.3-263.0k img/s, profiles/r5_side_defer/
+        # cifar_late.txt -- the per-block default now covers every step size)
+        self.side_block_default = ("DBX_OVERLAP_WGRAD" not in os.environ and not self.fuse_stem_bwd
                                    and self.overlap_wgrad)
         if self.side_block_default:
             self.side_block, self.side_batch = True, False
@@ -569,7 +572,7 @@ class ResNetProgram:
         self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
         # the same for the per-block side forks (DBX_OVERLAP_WGRAD=3): the last block's last N
         # (TinyImageNet at the 128-CU reservation: 2 over 1 +0.4 % in five of five interleaved rounds)
-        self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN", "2" if fl >= 5e10 else "0"))
+        self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN", "2"))
         self._main_tail = []
         # layer1 (the last batch, exposed at the end of the step) forks its weight gradients per block
         # instead of once at the segment's end, so they start under layer1's own remaining data
@@ -584,10 +587,9 @@ class ResNetProgram:
         self.event_joins = False
         self.ds_branch = int(os.environ.get("DBX_DS_BRANCH", "0"))
         # the downsample conv's forward beside conv2 / conv3 on the side stream: +0.24 % on the headline
-        # over five interleaved rounds, TinyImageNet neutral alone and +0.67 % with its block tail of one
-        # (profiles/r5_side_defer/ds_fwd.txt, block_tail.txt)
-        self.ds_fwd_side = (os.environ["DBX_DS_FWD_SIDE"] == "1" if "DBX_DS_FWD_SIDE" in os.environ
-                            else fl >= 5e10)
+        # over five interleaved rounds, TinyImageNet neutral alone and +0.67 % with its block tail of one,
+        # CIFAR +0.6 % (profiles/r5_side_defer/ds_fwd.txt, block_tail.txt, cifar_late.txt)
+        self.ds_fwd_side = os.environ.get("DBX_DS_FWD_SIDE", "1") == "1"
         self._ds_stream = None
         # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
         # its own segment's per-block buffers (never reused within a step) and the workspaces of the main

@@ -22,14 +22,16 @@ def test_fwd_conv_flops():
 
 
 def test_side_stream_defaults(monkeypatch):
-    """Default: the batched side stream (one fork per backward segment); 1 = per-gradient forks; 0 = off."""
-    for env, overlap, batch in ((None, True, True), ("2", True, True), ("1", True, False), ("0", False, False)):
+    """Default: one side fork per residual block; 2 = the batched side stream (one fork per backward
+    segment); 1 = per-gradient forks; 0 = off."""
+    for env, overlap, batch, block in ((None, True, False, True), ("2", True, True, False), ("1", True, False, False),
+                                       ("0", False, False, False)):
         if env is None:
             monkeypatch.delenv("DBX_OVERLAP_WGRAD", raising=False)
         else:
             monkeypatch.setenv("DBX_OVERLAP_WGRAD", env)
         p = ResNetProgram(build_model("resnet18", num_classes=10), 2, (32, 32), torch.device("cpu"))
-        assert (p.overlap_wgrad, p.side_batch) == (overlap, batch), env
+        assert (p.overlap_wgrad, p.side_batch, p.side_block) == (overlap, batch, block), env
 
 
 def test_device_hyper_copies_only_changes():
@@ -70,8 +72,9 @@ def test_post_launch_hook_owner_scoped_cancel():
 
 
 def test_side_stream_defaults_by_step_size(monkeypatch):
-    """From 50 GFLOP of forward conv work up the default side stream forks per residual block with the
-    deferred launch and lazy joins; below, one fork per segment with lazy joins; an explicit
+    """The default side stream forks per residual block with the deferred launch and lazy joins, the
+    last block's tail and the stem weight gradient on the main stream, the downsample forwards on the
+    side stream; the CU reservation from 50 GFLOP of forward conv work up; an explicit
     DBX_OVERLAP_WGRAD wins. (The step size is patched: the real ones need GPU-sized buffers.)"""
     for var in ("DBX_OVERLAP_WGRAD", "DBX_SIDE_DEFER", "DBX_LAZY_JOIN", "DBX_SIDE_CU_RESERVE", "DBX_DS_FWD_SIDE",
                 "DBX_BLOCK_TAIL_MAIN", "DBX_STEM_WG_MAIN"):
@@ -80,12 +83,12 @@ def test_side_stream_defaults_by_step_size(monkeypatch):
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e11)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (True, False, True, True, 128)
-    assert p.ds_fwd_side  # (the downsample forward on the side stream: from 50 GFLOP up)
+    assert p.ds_fwd_side
     assert (p.block_tail_main, p.stem_wg_main) == (2, True)
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e10)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
-    assert not p.ds_fwd_side and p.block_tail_main == 0
-    assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (False, True, True, True, 0)
+    assert p.ds_fwd_side and p.block_tail_main == 2
+    assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.side_cu_reserve) == (True, False, True, True, 0)
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e12)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert p.ds_fwd_side and (p.block_tail_main, p.stem_wg_main) == (2, True)
