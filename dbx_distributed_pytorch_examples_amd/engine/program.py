@@ -590,6 +590,8 @@ class ResNetProgram:
         # over five interleaved rounds, TinyImageNet neutral alone and +0.67 % with its block tail of one,
         # CIFAR +0.6 % (profiles/r5_side_defer/ds_fwd.txt, block_tail.txt, cifar_late.txt)
         self.ds_fwd_side = os.environ.get("DBX_DS_FWD_SIDE", "1") == "1"
+        # (... only for downsample outputs of at most this size: DBX_DS_FWD_SIDE_MAX_HW)
+        self.ds_fwd_side_max_hw = int(os.environ.get("DBX_DS_FWD_SIDE_MAX_HW", str(1 << 30)))
         self._ds_stream = None
         # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
         # its own segment's per-block buffers (never reused within a step) and the workspaces of the main
@@ -824,7 +826,8 @@ class ResNetProgram:
                                in_shift=prev_bn.shift if prev_bn else None, relu_in=True,
                                fin=self._ff(b.bns[i]), fin_in=deferred.fin_f if deferred is not None else None)
                 deferred = None
-                if i == 0 and ds_launch is not None and b.ds_conv is not None:
+                if (i == 0 and ds_launch is not None and b.ds_conv is not None
+                        and b.ds_conv.OH <= self.ds_fwd_side_max_hw):
                     ds_launch[bi] = self._ds_fwd_on_side(b, x, N)
                 nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
                 c1 = nxt.convs[0] if nxt is not None else None
