@@ -661,6 +661,13 @@ def _patch3_reserve() -> bool:
     return os.environ.get("DBX_PATCH3_RESERVE", "0") == "1"
 
 
+def _reserve_max_rounds() -> float:
+    """DBX_RESERVE_MAX_ROUNDS (default 1): workgroup rounds over the unreserved CUs of a weight
+    gradient launched with cu_reserve."""
+    import os
+    return float(os.environ.get("DBX_RESERVE_MAX_ROUNDS", "1"))
+
+
 def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int,
                  rounds: Optional[float] = None, cus: Optional[int] = None) -> Tuple[int, int]:
     """Split the pixel reduction so that ``rounds`` rounds of workgroups stream over the CUs (>= 8
@@ -830,7 +837,8 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         _chk(in_shift, torch.float32, "in_shift", IC)
     M = N * OH * OW
     if cu_reserve > 0:  # one round over all but cu_reserve CUs (the main stream's small kernels keep a place)
-        rounds = min(1.0, 1.0 if rounds is None or rounds <= 0 else float(rounds))
+        cap = _reserve_max_rounds()
+        rounds = min(cap, cap if rounds is None or rounds <= 0 else float(rounds))
     nsplit, ms = wgrad_splits(M, OC, KTOT, bm, bn, ws.numel(), rounds,
                               cus=num_cus() - cu_reserve if cu_reserve > 0 else None)
     if (nsplit + (min(64, nsplit) if nsplit > 8 else 0)) * OC * KTOT > ws.numel():
