@@ -26,7 +26,7 @@ int dbx_wgrad_reduce(const float* ws, float* dw, long long n, int nsplit, float 
 int dbx_wgrad_reduce_gather(const float* ws, float* dw, int OC, int R, int S, int IC, int nsplit, float scale,
                             int accumulate, hipStream_t st);
 int dbx_wgrad_patch3(const dbx::WgradArgs* a, long long ws_cap, hipStream_t st, int max_wg);
-int dbx_conv_dwfused(const dbx::DwFusedArgs* a, long long ws_cap, hipStream_t st);
+int dbx_conv_dwfused(const dbx::DwFusedArgs* a, long long ws_cap, hipStream_t st, int max_cus);
 int dbx_stem_bwd(dbx::StemBwdArgs* a, long long ws_cap, int fused, hipStream_t st);
 int dbx_bn_finalize(const double*, int, int, float, const float*, const float*, float, float, float*, float*, float*,
                     float*, float*, float*, hipStream_t);
@@ -172,13 +172,13 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_dwfused", [](uintptr_t g, uintptr_t y3, uintptr_t coeff, uintptr_t wt, uintptr_t y2, uintptr_t bsc,
                            uintptr_t bsh, uintptr_t mean2, uintptr_t inv2, uintptr_t da, uintptr_t bstats, uintptr_t ws,
-                           long long ws_cap, int M, int K, int C, int nshard, uintptr_t st) {
+                           long long ws_cap, int M, int K, int C, int nshard, uintptr_t st, int max_cus) {
     // fused bottleneck-conv3 backward (conv_dwfused.hip): returns the number of dW partial slabs
     dbx::DwFusedArgs a{P<const bf16*>(g), P<const bf16*>(y3), P<const float*>(coeff), P<const bf16*>(wt),
                        P<const bf16*>(y2), P<const float*>(bsc), P<const float*>(bsh), P<const float*>(mean2),
                        P<const float*>(inv2), P<bf16*>(da), P<double*>(bstats), P<float*>(ws), M, K, C,
                        nshard > 0 ? nshard : 1};
-    const int n = dbx_conv_dwfused(&a, ws_cap, S(st));
+    const int n = dbx_conv_dwfused(&a, ws_cap, S(st), max_cus);
     if (n <= 0) check(n ? n : -1, "conv_dwfused");
     return n;
   });

@@ -320,16 +320,21 @@ using namespace dbx;
 
 // Returns the number of partial slabs written (= workgroups), or a negative error.
 template <int C, int NKB, int BM, int NS, int NT, int WN, int OCC, bool Y2N>
-static int launch_dwfused(const DwFusedArgs& a, long long ws_cap, hipStream_t st) {
+static int launch_dwfused(const DwFusedArgs& a, long long ws_cap, hipStream_t st, int max_cus) {
   if (a.M % BM != 0 || a.M <= 0) return -31;
-  static const int cap = [] {
+  struct Occ { int per_cu, cus; };
+  static const Occ occ = [] {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, reinterpret_cast<const void*>(&dwfused_kernel<C, NKB, BM, NS, NT, WN, OCC, Y2N>), NT, 0);
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return (per_cu > 0 && cus > 0) ? per_cu * cus : 256;
+    return Occ{per_cu, cus};
   }();
+  // max_cus > 0: the persistent grid spans only that many CUs (a multiple of 8: XCD round-robin), the
+  // rest stay with a concurrent side stream
+  const int cus = (max_cus > 0 && max_cus < occ.cus) ? (max_cus & ~7) : occ.cus;
+  const int cap = (occ.per_cu > 0 && cus > 0) ? occ.per_cu * cus : 256;
   const int ntile = a.M / BM;
   const int grid = ntile < cap ? ntile : cap;
   if ((long long)(grid + (grid < 64 ? grid : 64)) * a.K * a.C > ws_cap) return -33;
@@ -338,9 +343,10 @@ static int launch_dwfused(const DwFusedArgs& a, long long ws_cap, hipStream_t st
   return e == hipSuccess ? grid : -(int)e - 1000;
 }
 
-// ws_cap: floats available at a.ws (the slabs plus wgrad_reduce's level-1 partials).
+// ws_cap: floats available at a.ws (the slabs plus wgrad_reduce's level-1 partials); max_cus: see
+// launch_dwfused (0: all CUs).
 // Returns the number of partial slabs written (= workgroups), or a negative error.
-extern "C" int dbx_conv_dwfused(const DwFusedArgs* args, long long ws_cap, hipStream_t st) {
+extern "C" int dbx_conv_dwfused(const DwFusedArgs* args, long long ws_cap, hipStream_t st, int max_cus) {
   const DwFusedArgs& a = *args;
   if (2ull * a.M * a.K >= (unsigned long long)kOOB) return -32;  // 32-bit buffer offsets
   // 56x56 stage: two workgroups per CU (32 KB resident weights), 64-pixel tiles, two register sets
@@ -348,7 +354,7 @@ extern "C" int dbx_conv_dwfused(const DwFusedArgs* args, long long ws_cap, hipSt
 #ifndef DBX_DWF64
 #define DBX_DWF64 64, 2, 256, 2, 2, false
 #endif
-  if (a.C == 64 && a.K == 256) return launch_dwfused<64, 4, DBX_DWF64>(a, ws_cap, st);
+  if (a.C == 64 && a.K == 256) return launch_dwfused<64, 4, DBX_DWF64>(a, ws_cap, st, max_cus);
   // 28x28 stage: 128 KB resident weights -> one workgroup per CU; 4 waves (2 x 2) whose lanes hold
   // the 256 weight-gradient accumulators in AGPRs, 64-pixel tiles, two register sets in flight.
   // Measured at b1024 (tools/bench_dwfused.py, profiles/r2s4_dwfused/): 0.631 ms vs 0.875 ms with
@@ -357,6 +363,6 @@ extern "C" int dbx_conv_dwfused(const DwFusedArgs* args, long long ws_cap, hipSt
 #ifndef DBX_DWF128
 #define DBX_DWF128 64, 2, 256, 2, 1, false
 #endif
-  if (a.C == 128 && a.K == 512) return launch_dwfused<128, 8, DBX_DWF128>(a, ws_cap, st);
+  if (a.C == 128 && a.K == 512) return launch_dwfused<128, 8, DBX_DWF128>(a, ws_cap, st, max_cus);
   return -30;
 }

@@ -571,6 +571,10 @@ class ResNetProgram:
                              else ((3 if self.side_defer else 2) if 5e10 <= fl < 5e11 else 0))
         self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
         # the same for the per-block side forks (DBX_OVERLAP_WGRAD=3): the last block's last N
+        # the fused conv3 backward's persistent grid spans only this many CUs, so the side stream's weight
+        # gradients keep theirs (DBX_DWF_CUS; 0 = all): TinyImageNet class 128 (+0.4-0.8 %), the headline
+        # loses with any span (-0.9 % at 192), profiles/r5_side_defer/tiny_knobs_late.txt
+        self.dwf_cus = int(os.environ.get("DBX_DWF_CUS", "128" if 5e10 <= fl < 5e11 else "0"))
         # (TinyImageNet at the 128-CU reservation: 2 over 1 +0.4 % in five of five interleaved rounds)
         self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN", "2"))
         self._main_tail = []
@@ -1275,7 +1279,8 @@ class ResNetProgram:
             if fuse3 and j == nconv - 1:
                 # one pass: dy3 = BN3-bwd apply(g, y3) -> da2 (+ BN2 moments) and dW3 = dy3^T relu(bn2(y2))
                 K.conv_dwfused(src, kw["bwd_y"], kw["bwd_coeff"], cv.wt16, b.ys[j - 1], pbn.scale, pbn.shift,
-                               pbn.mean, pbn.invstd, pbn.bstats, b.das[j - 1], cv.grad, self.ws_dw)
+                               pbn.mean, pbn.invstd, pbn.bstats, b.das[j - 1], cv.grad, self.ws_dw,
+                               cus=self.dwf_cus if self.overlap_wgrad else 0)
                 act, kw = None, None
             pre = act is None and kw == {}  # wgrad re-applies BN+ReLU to its staged input tiles (BN prologue)
             if pre:

@@ -908,12 +908,13 @@ def dwfused_preferred(C: int, K: int, M: int) -> bool:
 
 
 @_dispatch
-def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2, da, dw, ws):
+def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2, da, dw, ws, cus: int = 0):
     """Backward of a bottleneck conv3 (1x1 stride 1, C -> K) in one pass (csrc/conv_dwfused.hip):
     dy3 = k1*g + k2*y3 + k3 (BN3-backward apply, ``coeff`` [3, K]) -> data gradient
     ``da`` = [a2 > 0] * conv_transpose(dy3) with the BN2-backward moments into ``bstats2`` (the MASK_Y
     epilogue, a2 = relu(y2*scale2 + shift2)), and weight gradient ``dw`` [K, C] = dy3^T a2 (fp32,
-    per-workgroup slabs in ``ws`` + the deterministic split reduction). dy3 and a2 never reach HBM."""
+    per-workgroup slabs in ``ws`` + the deterministic split reduction). dy3 and a2 never reach HBM.
+    ``cus`` > 0: the persistent grid spans only that many CUs (0: all)."""
     N, H, W, Kc = g.shape
     Cc = y2.shape[-1]
     M = N * H * W
@@ -932,7 +933,7 @@ def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2
         raise ValueError(f"conv_dwfused: unsupported geometry C={Cc} K={Kc} M={M}")
     n = C().conv_dwfused(g.data_ptr(), y3.data_ptr(), coeff.data_ptr(), wt16.data_ptr(), y2.data_ptr(),
                          scale2.data_ptr(), shift2.data_ptr(), mean2.data_ptr(), invstd2.data_ptr(), da.data_ptr(),
-                         bstats2.data_ptr(), ws.data_ptr(), ws.numel(), M, Kc, Cc, nsh2, stream_ptr())
+                         bstats2.data_ptr(), ws.data_ptr(), ws.numel(), M, Kc, Cc, nsh2, stream_ptr(), int(cus))
     C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), Kc * Cc, n, 1.0, 0, stream_ptr())
     return da
 

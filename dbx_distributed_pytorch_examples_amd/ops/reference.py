@@ -147,7 +147,7 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
     return dw
 
 
-def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2, da, dw, ws):
+def conv_dwfused(g, y3, coeff, wt16, y2, scale2, shift2, mean2, invstd2, bstats2, da, dw, ws, cus=0):
     """Fused bottleneck-conv3 backward = BN3-backward apply -> MASK_Y dgrad + weight gradient."""
     from types import SimpleNamespace
     dy = torch.empty_like(g)

@@ -32,7 +32,7 @@ def _inputs(N, H, W, seed=7, Cc=64, Kc=256):
     return g, y3, coeff, wt, y2, sc, sh, mean, inv
 
 
-def _run_fused(g, y3, coeff, wt, y2, sc, sh, mean, inv):
+def _run_fused(g, y3, coeff, wt, y2, sc, sh, mean, inv, cus=0):
     k = K()
     N, H, W, Kc = g.shape
     Cc = y2.shape[-1]
@@ -40,7 +40,7 @@ def _run_fused(g, y3, coeff, wt, y2, sc, sh, mean, inv):
     dw = torch.full((Kc, Cc), float("nan"), device=dev)
     st = k.new_stats(Cc, dev)
     ws = torch.empty((1024 + 64) * Kc * Cc, device=dev)
-    k.conv_dwfused(g, y3, coeff, wt, y2, sc, sh, mean, inv, st, da, dw, ws)
+    k.conv_dwfused(g, y3, coeff, wt, y2, sc, sh, mean, inv, st, da, dw, ws, cus=cus)
     torch.cuda.synchronize()
     return da, dw, st.view(-1, 2, Cc).sum(0)
 
@@ -103,6 +103,18 @@ def test_dwfused_deterministic(nhw, ck):
     b = _run_fused(*args)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("nhw,ck", [((16, 56, 56), (64, 256)), ((16, 28, 28), (128, 512))])
+def test_dwfused_cu_span(nhw, ck):
+    """``cus`` (the persistent grid spans only 128 CUs): the same data gradient bit for bit (it does not
+    depend on the tile -> workgroup assignment), the weight gradient summed over fewer slabs."""
+    args = _inputs(*nhw, seed=5, Cc=ck[0], Kc=ck[1])
+    da, dw, st = _run_fused(*args)
+    da2, dw2, st2 = _run_fused(*args, cus=128)
+    assert torch.equal(da, da2)
+    assert relerr(dw2, dw) < 1e-5
+    assert ((st2 - st).abs() / (st.abs() + 1.0)).max().item() < 1e-6
 
 
 def test_native_step_fused_vs_unfused(monkeypatch):
