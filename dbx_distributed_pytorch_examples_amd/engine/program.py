@@ -590,6 +590,8 @@ class ResNetProgram:
         # collectives queued behind it on the same stream (the final join waits for everything)
         self.event_joins = False
         self.ds_branch = int(os.environ.get("DBX_DS_BRANCH", "0"))
+        # DBX_SIDE_REV=1: each side batch's weight gradients in reverse queue order
+        self.side_rev = os.environ.get("DBX_SIDE_REV", "0") == "1"
         # the downsample conv's forward beside conv2 / conv3 on the side stream: +0.24 % on the headline
         # over five interleaved rounds, TinyImageNet neutral alone and +0.67 % with its block tail of one,
         # CIFAR +0.6 % (profiles/r5_side_defer/ds_fwd.txt, block_tail.txt, cifar_late.txt)
@@ -981,7 +983,7 @@ class ResNetProgram:
         self.launch_pending()  # (at most one deferred batch)
         if self._wstream is None:
             self._wstream = torch.cuda.Stream(device=self.dev)
-        q = self._side_q
+        q = self._side_q[::-1] if self.side_rev else self._side_q
         self._side_q = []
         self._side_pending = True
         main = torch.cuda.current_stream(self.dev)
