@@ -262,9 +262,9 @@ class ResNetProgram:
         # by default the side stream forks once per residual BLOCK (DBX_OVERLAP_WGRAD=3; first from 50
         # GFLOP of forward conv work up, TinyImageNet and ImageNet) -- with the deferred launch and lazy joins below
         # that fills the windows where the batched side stream waited for its next fork: headline
-        # 16,755-16,865 vs 16,709-16,731, TinyImageNet 100.4-100.8k vs 99.4k img/s; the CIFAR class
-        # keeps one fork per segment (neutral there): profiles/r5_side_defer/mode3.txt. The multi-rank
-        # trainer puts the batched layout back (its collectives are posted per segment).
+        # 16,755-16,865 vs 16,709-16,731, TinyImageNet 100.4-100.8k vs 99.4k img/s (CIFAR neutral at
+        # first): profiles/r5_side_defer/mode3.txt. The multi-rank trainer puts the batched layout back
+        # (its collectives are posted per segment).
         # (late in round 5, with the block tails on the main stream and the downsample forward on the side
         # stream, the CIFAR class gains too: 267.4-267.8k vs 262.3-263.0k img/s, profiles/r5_side_defer/
         # cifar_late.txt -- the per-block default now covers every step size)
@@ -570,12 +570,13 @@ class ResNetProgram:
         self.tail_main = int(os.environ["DBX_TAIL_MAIN"] if "DBX_TAIL_MAIN" in os.environ
                              else ((3 if self.side_defer else 2) if 5e10 <= fl < 5e11 else 0))
         self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
-        # the same for the per-block side forks (DBX_OVERLAP_WGRAD=3): the last block's last N
         # the fused conv3 backward's persistent grid spans only this many CUs, so the side stream's weight
-        # gradients keep theirs (DBX_DWF_CUS; 0 = all): TinyImageNet class 128 (+0.4-0.8 %), the headline
+        # gradients keep theirs (DBX_DWF_CUS; 0 = all): TinyImageNet class 128 (+0.3 %), the headline
         # loses with any span (-0.9 % at 192), profiles/r5_side_defer/tiny_knobs_late.txt
         self.dwf_cus = int(os.environ.get("DBX_DWF_CUS", "128" if 5e10 <= fl < 5e11 else "0"))
-        # (TinyImageNet at the 128-CU reservation: 2 over 1 +0.4 % in five of five interleaved rounds)
+        # the same as DBX_TAIL_MAIN for the per-block side forks (DBX_OVERLAP_WGRAD=3): the last block's
+        # last N weight gradients (TinyImageNet at the 128-CU reservation: 2 over 1 +0.4 % in five of five
+        # interleaved rounds; headline +0.38 % with the stem's, profiles/r5_side_defer/block_tail.txt)
         self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN", "2"))
         self._main_tail = []
         # layer1 (the last batch, exposed at the end of the step) forks its weight gradients per block
@@ -1054,7 +1055,7 @@ class ResNetProgram:
 
     def _block_flush(self, last: bool = False):
         if self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
-            # the step's last block: its last DBX_TAIL_MAIN weight gradients run on the main stream after
+            # the step's last block: its last DBX_BLOCK_TAIL_MAIN weight gradients run on the main stream after
             # the stem's backward (their own workspace) instead of behind the rest on the side stream
             n = self.block_tail_main if last else 0
             if n > 0 and len(self._side_q) > n:
