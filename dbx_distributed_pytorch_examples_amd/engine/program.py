@@ -599,6 +599,8 @@ class ResNetProgram:
         self.ds_fwd_side = os.environ.get("DBX_DS_FWD_SIDE", "1") == "1"
         # (... only for downsample outputs of at most this size: DBX_DS_FWD_SIDE_MAX_HW)
         self.ds_fwd_side_max_hw = int(os.environ.get("DBX_DS_FWD_SIDE_MAX_HW", str(1 << 30)))
+        # (DBX_DS_FWD_EARLY: fork it before conv1 when the block input is already in memory)
+        self.ds_fwd_early = os.environ.get("DBX_DS_FWD_EARLY", "0") == "1"
         self._ds_stream = None
         # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
         # its own segment's per-block buffers (never reused within a step) and the workspaces of the main
@@ -812,6 +814,12 @@ class ResNetProgram:
         for bi, b in enumerate(self.blocks):
             prev_bn = None
             deferred = None  # BN of conv i-1 whose finalize conv i's prologue performs (fin_in)
+            # (a block input already in memory -- the stem's pooled output -- forks its downsample conv
+            # before conv1; otherwise conv1's tail prologue writes it and the fork follows conv1)
+            early_ds = (self.ds_fwd_early and pending is None and ds_launch is not None and b.ds_conv is not None
+                        and b.ds_conv.OH <= self.ds_fwd_side_max_hw)
+            if early_ds:
+                ds_launch[bi] = self._ds_fwd_on_side(b, x, N)
             for i, cv in enumerate(b.convs):
                 if i == 0 and pending is not None:
                     pb, res, rsc, rsh, pfin, prfin = pending
@@ -833,7 +841,7 @@ class ResNetProgram:
                                in_shift=prev_bn.shift if prev_bn else None, relu_in=True,
                                fin=self._ff(b.bns[i]), fin_in=deferred.fin_f if deferred is not None else None)
                 deferred = None
-                if (i == 0 and ds_launch is not None and b.ds_conv is not None
+                if (i == 0 and not early_ds and ds_launch is not None and b.ds_conv is not None
                         and b.ds_conv.OH <= self.ds_fwd_side_max_hw):
                     ds_launch[bi] = self._ds_fwd_on_side(b, x, N)
                 nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None

@@ -458,7 +458,7 @@ def test_composer_trainer_runs_on_native_module():
 
 @pytest.mark.parametrize("mode", ["2", "3", "2+tail2", "2+tail2+seg3", "2+l1blocks", "2+tail2+l1blocks", "2+defer",
                                   "2+tail2+defer", "2+lazy", "2+tail2+defer+lazy", "3+defer+lazy", "3+defer+lazy+ds", "3+defer+lazy+ds2",
-                                  "3+defer+lazy+dsf", "3+btail2+defer+lazy"])
+                                  "3+defer+lazy+dsf", "3+btail2+defer+lazy", "3+defer+lazy+dsf+early"])
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64)])
 def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch):
     """DBX_OVERLAP_WGRAD=2 (weight gradients forked once per backward segment, joined one segment
@@ -490,6 +490,7 @@ def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch)
     monkeypatch.setenv("DBX_BLOCK_TAIL_MAIN", "2" if "btail2" in opts else "0")
     # "dsf": the downsample conv's forward on the side stream beside conv2 / conv3 (DBX_DS_FWD_SIDE)
     monkeypatch.setenv("DBX_DS_FWD_SIDE", "1" if "dsf" in opts else "0")
+    monkeypatch.setenv("DBX_DS_FWD_EARLY", "1" if "early" in opts else "0")
     t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     monkeypatch.setenv("DBX_OVERLAP_WGRAD", "0")
     t2 = NativeTrainer(m2, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
