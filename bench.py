@@ -104,8 +104,94 @@ def self_launch(args, argv) -> int:
         print(f"[bench] error: --gpus {args.gpus} but {ndev} GPU(s) visible (RCCL needs one GPU per rank; "
               f"DBX_DIST_BACKEND=gloo rehearses several ranks on one device)", file=sys.stderr)
         return 3
-    from dbx_distributed_pytorch_examples_amd.launch import run_subprocess_ranks
-    return run_subprocess_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + list(argv))
+    from dbx_distributed_pytorch_examples_amd.launch import describe_exit, run_subprocess_ranks
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(argv)
+    rc = run_subprocess_ranks(args.gpus, cmd)
+    if rc == 0 or not _may_fall_back(args) or not _retryable(rc):
+        return rc
+    # the ranks failed on the default (framework-RCCL one-graph) step -- e.g. a hung collective ended by
+    # the watchdog (75): this parent never touched the GPU, so it starts FRESH ranks once on the c10d step
+    reason = f"attempt 1 failed: worst rank {describe_exit(rc)}"
+    print(f"[bench] {reason}; re-running {args.gpus} fresh ranks with DBX_COMM=torch", file=sys.stderr, flush=True)
+    return run_subprocess_ranks(args.gpus, cmd, env={**fallback_env(reason), "DBX_RESTART_COUNT": "1"})
+
+
+def _may_fall_back(args) -> bool:
+    """A failed multi-rank native run is re-measured once on fresh ranks (c10d collectives) unless it
+    already is that re-measurement, runs on c10d anyway, or DBX_BENCH_FALLBACK=0."""
+    return (args.impl == "native" and os.environ.get("DBX_BENCH_FALLBACK", "1") != "0"
+            and not os.environ.get("DBX_COMM_FALLBACK_REASON") and os.environ.get("DBX_COMM", "") != "torch")
+
+
+def _retryable(rc: int) -> bool:
+    # 2 = usage error, 3 = world / --gpus mismatch, 4 = replicas diverged on the c10d path too: a re-run
+    # would repeat them. Anything else (watchdog 75, abort, segfault, a raised error) may be the one-graph
+    # RCCL step's own failure.
+    return rc not in (0, 2, 3, 4)
+
+
+def fallback_env(reason: str) -> dict:
+    return {"DBX_COMM": "torch", "DBX_COMM_FALLBACK_REASON": reason}
+
+
+def supervise(args, argv) -> int:
+    """Under torchrun (the driver's N-GPU command): this rank process becomes a GPU-free supervisor of a
+    child that does the work, so a failed one-graph attempt can be re-run on fresh ranks
+    (``launch.supervise_rank``)."""
+    from dbx_distributed_pytorch_examples_amd.launch import supervise_rank
+    return supervise_rank([sys.executable, os.path.abspath(__file__)] + list(argv), fallback_env, _retryable)
+
+
+def _rccl_log_setup(info_world: int) -> str:
+    """World > 1 on RCCL: route RCCL's INFO log (rings, channels, version) to a per-process file unless the
+    user set NCCL_DEBUG (then it passes through untouched). Returns the file path ('' = none)."""
+    if info_world <= 1 or os.environ.get("DBX_DIST_BACKEND") == "gloo" or os.environ.get("DBX_RCCL_SUMMARY") == "0":
+        return ""
+    if "NCCL_DEBUG" in os.environ:
+        return os.environ.get("NCCL_DEBUG_FILE", "")
+    import tempfile
+    path = os.path.join(tempfile.gettempdir(), f"dbx_rccl_{os.getpid()}.log")
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_FILE"] = path
+    return path
+
+
+def rccl_summary(path: str) -> dict:
+    """Version, channel count and the first ring(s) from an RCCL INFO log."""
+    import re
+    import socket
+    if not path:
+        return {}
+    path = path.replace("%h", socket.gethostname()).replace("%p", str(os.getpid()))
+    try:
+        with open(path, errors="replace") as f:
+            lines = f.read().splitlines()
+    except OSError:
+        return {}
+    out: dict = {}
+    rings, nch = [], 0
+    for ln in lines:
+        m = re.search(r"(RCCL|NCCL) version\s*(\S+)", ln)
+        if m and "version" not in out:
+            out["version"] = m.group(2)
+        m = re.search(r"Channel (\d+)/(\d+) :((?:\s+\d+)+)\s*$", ln)
+        if m:
+            nch = max(nch, int(m.group(2)))
+            if len(rings) < 2:
+                rings.append(" ".join(m.group(3).split()))
+        m = re.search(r"(\d+) coll channels", ln)
+        if m:
+            out["coll_channels"] = int(m.group(1))
+    if nch:
+        out["channels"] = nch
+        out["rings"] = rings
+    out["log_lines"] = len(lines)
+    if os.environ.get("NCCL_DEBUG_FILE", "").startswith(os.path.join(os.path.dirname(path), "dbx_rccl_")):
+        try:
+            os.remove(path)
+        except OSError:
+            pass
+    return out
 
 
 def replicas_in_sync(step, info, when: str, wd=None) -> bool:
@@ -206,6 +292,10 @@ def main(argv=None) -> int:
     args = parse_args(raw)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return self_launch(args, raw)
+    if (args.gpus > 1 and not os.environ.get("DBX_SUPERVISED_CHILD") and _may_fall_back(args)
+            and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"):
+        return supervise(args, raw)
+    rccl_log = _rccl_log_setup(int(os.environ.get("WORLD_SIZE", "1")))
     from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
     from dbx_distributed_pytorch_examples_amd.train.bench_steps import build_step
 
@@ -226,6 +316,7 @@ def main(argv=None) -> int:
         from dbx_distributed_pytorch_examples_amd.parallel.comm_guard import CommWatchdog
         wd = CommWatchdog(timeout_s=float(os.environ.get("DBX_BENCH_TIMEOUT", "300")), device=info.device)
     from dbx_distributed_pytorch_examples_amd.utils import fault
+    comm_fallback = os.environ.get("DBX_COMM_FALLBACK_REASON") or None
     for attempt in (0, 1):
         if wd is not None:
             wd.step_begin("setup")
@@ -238,6 +329,7 @@ def main(argv=None) -> int:
                 print("[bench] warning: the one-graph step's replicas diverged; re-measuring on the c10d "
                       "collectives (DBX_COMM=torch)", file=sys.stderr, flush=True)
             os.environ["DBX_COMM"] = "torch"
+            comm_fallback = "replicas_diverged on the one-graph step; re-measured in-process with DBX_COMM=torch"
             continue
         break
     if rc != 0:
@@ -272,6 +364,7 @@ def main(argv=None) -> int:
         "scaling": "weak",
         "vs_baseline": (round(value / (base * n), 4) if base else None),
         "dtype": "bf16",
+        **({"comm_fallback": comm_fallback} if n > 1 else {}),
         "data": (f"synthetic (uint8 NHWC {args.image_size}x{args.image_size} images + random labels, on-device; "
                  "random-init weights)") if args.data == "synthetic" else (
             f"synthetic images of the config's shape streamed from zstd MDS shards ({meta.get('mds', '')}); "
@@ -292,6 +385,10 @@ def main(argv=None) -> int:
             **meta,
         },
     }
+    if n > 1:
+        rs = rccl_summary(rccl_log) if info.rank == 0 else {}
+        if rs:
+            out["config"]["rccl"] = rs
     if info.rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

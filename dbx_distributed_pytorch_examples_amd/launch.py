@@ -317,6 +317,128 @@ def run_subprocess_ranks(nproc: int, cmd: List[str], nnodes: int = 1, node_rank:
     return code if code else 1
 
 
+def describe_exit(code: Optional[int]) -> str:
+    """A rank's exit code in words (75 is ``parallel.comm_guard.EXIT_COMM_FAILURE``)."""
+    import signal
+    if code is None:
+        return "no exit code"
+    if code < 0:
+        try:
+            return f"killed by {signal.Signals(-code).name}"
+        except ValueError:
+            return f"killed by signal {-code}"
+    return {75: "exit 75 (comm watchdog: a hung collective or rank)", 124: "exit 124 (time limit)",
+            134: "exit 134 (abort)", 137: "exit 137 (SIGKILL)", 139: "exit 139 (segfault)"}.get(code, f"exit {code}")
+
+
+def agent_store(timeout_s: float = 60.0):
+    """A client of torchrun's agent TCPStore (``TORCHELASTIC_USE_AGENT_STORE=True``: the static and c10d
+    rendezvous host it at MASTER_ADDR:MASTER_PORT for the workers' lifetime), or None. Opening it touches
+    no GPU."""
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") != "True" or "MASTER_PORT" not in os.environ:
+        return None
+    import datetime
+
+    import torch.distributed as tdist
+    try:
+        return tdist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]),
+                              is_master=False, timeout=datetime.timedelta(seconds=timeout_s))
+    except Exception as e:  # noqa: BLE001 - no store: the caller runs unsupervised
+        print(f"[supervise] no agent store ({type(e).__name__}: {e})", file=sys.stderr, flush=True)
+        return None
+
+
+def _kill_tree(p: "subprocess.Popen", grace_s: float = 10.0) -> None:
+    import signal
+    for sig, wait in ((signal.SIGTERM, grace_s), (signal.SIGKILL, 30.0)):
+        try:
+            os.killpg(p.pid, sig)
+        except (ProcessLookupError, PermissionError):
+            pass
+        try:
+            p.wait(wait)
+            return
+        except subprocess.TimeoutExpired:
+            continue
+
+
+def supervise_rank(cmd: List[str], fallback_env: Callable[[str], Dict[str, str]],
+                   retryable: Callable[[int], bool], peer_grace_s: float = 30.0,
+                   agree_timeout_s: float = 900.0, tag: str = "dbx_supervise") -> int:
+    """Run this torchrun rank's work in a CHILD process and, if the attempt fails on any rank, run it
+    once more in fresh child processes with ``fallback_env(reason)`` added -- the torchrun form of
+    ``run_subprocess_ranks(max_restarts=1)`` for a job that must produce a number (``bench.py`` under the
+    driver's ``torch.distributed.run``, whose own ranks cannot be replaced).
+
+    The supervisor never touches the GPU: the child is the process that initialises HIP, so its
+    failure (a hung collective ended by the comm watchdog with exit 75, an abort, a segfault) leaves
+    the supervisor free to start another. All ranks' supervisors agree through torchrun's agent
+    store: each posts its child's exit code; a child still running when a peer has failed gets
+    ``peer_grace_s`` to end by itself (its watchdog) before its process group is killed. The retry
+    runs only if rank 0's first child did not succeed and some failure is ``retryable``; the retry
+    children rendezvous on a fresh port that rank 0 publishes (their own TCPStore, hosted by the
+    rank-0 child), so no key of the failed attempt is read again. Returns the last child's exit code.
+    """
+    import datetime
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    store = agent_store()
+    base = dict(os.environ, DBX_SUPERVISED_CHILD="1")
+    if store is None:
+        return subprocess.run(list(cmd), env=base).returncode
+
+    def key(attempt, what):
+        return f"{tag}/{attempt}/{what}"
+
+    def peer_failed(attempt):
+        for r in range(world):
+            k = key(attempt, f"rc/{r}")
+            if r != rank and store.check([k]) and int(store.get(k)) != 0:
+                return r
+        return None
+
+    def run(attempt, env):
+        p = subprocess.Popen(list(cmd), env=env, start_new_session=True)
+        t_peer = None
+        while True:
+            try:
+                return p.wait(1.0)
+            except subprocess.TimeoutExpired:
+                pass
+            if t_peer is None and peer_failed(attempt) is not None:
+                t_peer = time.time()
+            if t_peer is not None and time.time() - t_peer > peer_grace_s:
+                print(f"[supervise] rank {rank}: a peer failed and this rank's child did not end within "
+                      f"{peer_grace_s:.0f}s; killing it", file=sys.stderr, flush=True)
+                _kill_tree(p)
+                return p.returncode if p.returncode is not None else -9
+
+    rc = run(0, base)
+    store.set(key(0, f"rc/{rank}"), str(rc))
+    keys = [key(0, f"rc/{r}") for r in range(world)]
+    try:
+        store.wait(keys, datetime.timedelta(seconds=agree_timeout_s))
+    except Exception as e:  # noqa: BLE001 - a supervisor that never reported: decide on what is known
+        print(f"[supervise] rank {rank}: not every rank reported ({type(e).__name__}); deciding on the "
+              f"codes that arrived", file=sys.stderr, flush=True)
+    codes = {r: int(store.get(k)) for r, k in enumerate(keys) if store.check([k])}
+    bad = {r: c for r, c in sorted(codes.items()) if c != 0}
+    if codes.get(0) == 0 or not bad or not any(retryable(c) for c in bad.values()) \
+            or any(c in (2, 3) for c in bad.values()):
+        return rc
+    reason = "attempt 1 failed: " + "; ".join(f"rank {r} {describe_exit(c)}" for r, c in bad.items())
+    if rank == 0:
+        store.set(key(1, "port"), str(_free_port()))
+    port = store.get(key(1, "port")).decode()
+    if rank == 0:
+        print(f"[supervise] {reason}; re-running every rank once in fresh processes", file=sys.stderr, flush=True)
+    env = dict(base, MASTER_PORT=port, TORCHELASTIC_USE_AGENT_STORE="False",
+               DBX_RESTART_COUNT=str(int(os.environ.get("DBX_RESTART_COUNT", "0")) + 1))
+    env.update(fallback_env(reason))
+    rc = run(1, env)
+    store.set(key(1, f"rc/{rank}"), str(rc))
+    return rc
+
+
 def main(argv=None) -> int:
     """``python -m dbx_distributed_pytorch_examples_amd.launch --nproc-per-node 8 train.py args...``
     or ``... --nproc-per-node 8 -m package.module args...`` (like torchrun / python -m)."""

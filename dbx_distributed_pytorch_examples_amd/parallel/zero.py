@@ -250,8 +250,19 @@ class SegmentedZero:
                 if a < b:
                     self._bn_own.append((bo + a - lo, a, b - a))
             bo += hi - lo
-        self.bytes_per_step = int(sum((hi - lo) * (W - 1) / W * (4 + 2) for (lo, hi, *_ ) in self.parts) + 8 * nbn) \
-            if W > 1 else 0
+        self.nbn = nbn
+        self.bytes_per_step = self.planned_bytes(W)
+
+    def planned_bytes(self, world: int) -> int:
+        """Bytes one rank sends per step at ``world`` ranks on a ring: the fp32 reduce-scatter and the
+        bf16 all-gather of every segment, plus the fp32 all-reduce of the BN affine blocks (0 at world 1).
+        The bench label reports it for the configured world AND for 8 ranks, so a world-1 run still
+        states what the exchange will cost."""
+        if world <= 1:
+            return 0
+        n = sum(hi - lo for (lo, hi, *_) in self.parts)
+        f = (world - 1) / world
+        return int(n * f * (4 + 2) + 2 * f * 4 * self.nbn)
 
     # ---- helpers ------------------------------------------------------------------------
     def _gpart(self, part):

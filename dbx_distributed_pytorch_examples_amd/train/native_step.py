@@ -39,7 +39,7 @@ def build_native_step(args, info):
     step.trainer = tr  # bench.py: replica check, watchdog registration
     if tr.zero is not None:
         extra["zero"] = (f"ZeRO-{tr.zero.stage}: per-segment fp32 reduce-scatter (overlapped with backward), sharded "
-                         f"{opt.name} update, bf16 all-gather; {tr.zero.bytes_per_step / 2**20:.1f} MiB sent/rank/step")
+                         f"{opt.name} update, bf16 all-gather; " + zero_bytes_label(tr.zero))
     return step, {**extra, "memory_format": "nhwc", "graphs": use_graphs,
                   "ddp": (f"flat-bucket {'RCCL' if info.backend == 'nccl' else info.backend} all-reduce, "
                           f"{tr.bucket_cap * 4 >> 20} MiB chunks, "
@@ -49,6 +49,15 @@ def build_native_step(args, info):
                   + (f"; collectives: {tr.grad_collectives}" if tr.world > 1 else "")
                   if tr.world > 1 or getattr(tr, "segmented", False) else "none",
                   "kernels": "dbx HIP (conv implicit-GEMM MFMA + fused BN/ReLU/pool/CE/SGD)"}
+
+
+def zero_bytes_label(z) -> str:
+    """Ring bytes per rank and step of the ZeRO exchange: at the run's world, and planned at 8 ranks (the
+    north-star node) when the run is smaller, so a one-GPU run does not print a bare 0."""
+    here = f"{z.bytes_per_step / 2**20:.1f} MiB sent/rank/step at world {z.world}"
+    if z.world >= 8:
+        return here
+    return here + f" (planned at 8 ranks: {z.planned_bytes(8) / 2**20:.1f} MiB sent/rank/step)"
 
 
 def _mds_step(args, info, tr):

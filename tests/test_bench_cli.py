@@ -68,15 +68,62 @@ def test_diverged_replica_refuses_to_report():
 
 def test_stalled_rank_ends_the_bench_within_the_timeout():
     """A rank that stops in warm-up (DBX_FAULT hang) must not leave the N-GPU bench blocked until the
-    driver's timeout: the watchdog names the phase and the job exits 75 within DBX_BENCH_TIMEOUT."""
+    driver's timeout: the watchdog names the phase and the job exits 75 within DBX_BENCH_TIMEOUT
+    (with the fresh-rank re-run switched off, DBX_BENCH_FALLBACK=0)."""
     import time
     t0 = time.time()
     r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2"],
-             {"DBX_DIST_BACKEND": "gloo", "DBX_FAULT": "1:1:hang", "DBX_BENCH_TIMEOUT": "10"})
+             {"DBX_DIST_BACKEND": "gloo", "DBX_FAULT": "1:1:hang", "DBX_BENCH_TIMEOUT": "10",
+              "DBX_BENCH_FALLBACK": "0"})
     assert r.returncode == 75, r.stderr[-2000:]
     assert "[comm-watchdog]" in r.stderr and "phase 'warmup'" in r.stderr
     assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
     assert time.time() - t0 < 120
+
+
+def test_hung_self_launched_ranks_are_remeasured_on_fresh_ranks():
+    """bench.py --gpus N (self-launched): a collective hang in warm-up ends the ranks with exit 75; the
+    GPU-free parent starts fresh ranks once on the c10d step (DBX_COMM=torch; the injected fault only
+    fires on attempt 0) and the JSON line carries the reason in ``comm_fallback``."""
+    r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2"],
+             {"DBX_DIST_BACKEND": "gloo", "DBX_FAULT": "1:1:comm_hang", "DBX_BENCH_TIMEOUT": "10"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "[comm-watchdog]" in r.stderr and "re-running 2 fresh ranks" in r.stderr
+    d = _line(r.stdout)
+    assert "exit 75" in d["comm_fallback"] and d["n_gpus"] == 2
+
+
+def test_hung_torchrun_ranks_are_remeasured_on_fresh_ranks():
+    """The driver's form, ``torch.distributed.run ... bench.py --gpus N``: each torchrun rank supervises a
+    child (GPU-free supervisor); a hang in warm-up ends the children (75), the supervisors agree through
+    torchrun's agent store and re-run every rank once on a fresh rendezvous with DBX_COMM=torch."""
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    env = dict(os.environ, DBX_DIST_BACKEND="gloo", DBX_FAULT="1:1:comm_hang", DBX_BENCH_TIMEOUT="10")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2"],
+                       cwd="/tmp", env=env, capture_output=True, text=True, timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "[comm-watchdog]" in r.stderr and "[supervise]" in r.stderr
+    d = _line(r.stdout)
+    assert "exit 75" in d["comm_fallback"] and d["config"]["world_size_seen"] == 2
+
+
+def test_rccl_summary_parses_the_ring_log(tmp_path):
+    sys.path.insert(0, ROOT)
+    import bench
+    log = tmp_path / "r.log"
+    log.write_text("host:1:1 [0] NCCL INFO RCCL version 2.26.6-develop:abc\n"
+                   "host:1:1 [0] NCCL INFO Channel 00/16 :    0   1   2   3   4   5   6   7\n"
+                   "host:1:1 [0] NCCL INFO Channel 01/16 :    0   7   6   5   4   3   2   1\n"
+                   "host:1:1 [0] NCCL INFO 16 coll channels, 16 collnet channels, 0 nvls channels\n")
+    d = bench.rccl_summary(str(log))
+    assert d["version"].startswith("2.26.6") and d["channels"] == 16 and d["coll_channels"] == 16
+    assert d["rings"][0] == "0 1 2 3 4 5 6 7" and len(d["rings"]) == 2
 
 
 def test_diverged_one_graph_step_is_remeasured_on_c10d(monkeypatch, capsys):

@@ -392,6 +392,7 @@ def _native_zero_vs_dp(optim, clip):
     from dbx_distributed_pytorch_examples_amd.models import build_model
     from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
     info = ddist.init_distributed(device="cpu")
+    from dbx_distributed_pytorch_examples_amd.train.native_step import zero_bytes_label
     out, nbytes, shard = {}, 0, 0
     for z in (0, 1):
         torch.manual_seed(0)
@@ -407,6 +408,10 @@ def _native_zero_vs_dp(optim, clip):
         out[z] = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
         if z:
             nbytes, shard, coll = tr.zero.bytes_per_step, tr.zero.m.numel(), tr.zero.coll
+            label = zero_bytes_label(tr.zero)
+            assert f"at world {info.world_size}" in label
+            if info.world_size < 8:  # a small world still states the 8-rank exchange it plans
+                assert "planned at 8 ranks" in label and tr.zero.planned_bytes(8) > 0
     ddist.destroy()
     rel = ((out[0] - out[1]).norm() / out[0].norm()).item()
     return torch.equal(out[0], out[1]), rel, nbytes, shard, out[0].numel(), coll
