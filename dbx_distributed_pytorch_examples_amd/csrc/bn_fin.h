@@ -139,7 +139,7 @@ __device__ __forceinline__ void bn_fin_consume(const BnFin& f, int c, bool store
 // release fence -- a buffer_wbl2 per tile would write back the tile's just-stored outputs, which
 // measured 1.6x slower steps), one lane per 64-channel group takes a ticket; the tile that completes
 // a group's count (all ceil(M / BM) M-tiles of the producer, over all its launches) finalizes those
-// 64 channels from sc1 loads of the shards (MI355X_MICROARCH.md "Valid forms", row 1: the last
+// 64 channels from sc1 loads of the shards (/opt/skills/guides/MI355X_MICROARCH.md, the image's CDNA4 guide, "Valid forms", row 1: the last
 // adder loads after its add returned, the other waves after a barrier), then resets the counter.
 // The finalizing block reads 2 x nshard x 64 doubles. n0: first output channel of the tile.
 template <int BM, int BN>

@@ -21,7 +21,7 @@ namespace dbx {
 // stores in the accumulators' own lane order -- tile region ((split * ntile + tile) * BM * BN) -- so
 // no release fence (a buffer_wbl2 per block) is needed; each wave drains its stores, then one lane
 // takes a relaxed agent-scope ticket from cnt[tile]; the block drawing nsplit-1 loads the nsplit
-// partials of the tile with sc1 loads at the same lane positions (MI355X_MICROARCH.md "Valid forms",
+// partials of the tile with sc1 loads at the same lane positions (/opt/skills/guides/MI355X_MICROARCH.md, the image's CDNA4 guide, "Valid forms",
 // row 1) and sums them in split order -- the same fp32 order per element as wgrad_reduce_kernel, so
 // the result is bit-identical to the two-kernel path when that sums in one level -- and writes dw;
 // then resets the counter. The host enables it only when a tile's partials are small (the reducer

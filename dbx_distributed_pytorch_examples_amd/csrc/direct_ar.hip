@@ -22,7 +22,10 @@
 // their own slots and acquire at system scope before any peer data is read. Generations live in
 // device memory (one counter per workgroup), so a launch captured into a HIP graph replays
 // correctly. Every poll is bounded by a wall-clock deadline (s_memrealtime, 100 MHz): a missing
-// peer ends the wait with an error bit instead of a wave that never finishes.
+// peer ends the wait with an error bit instead of a wave that never finishes. A workgroup whose
+// barrier timed out skips the rest of the protocol (no further waits) and writes NaN over every
+// element it owns in the result, so a partial sum can never pass as a gradient; the error bit also
+// lands in a pinned host word that the comm watchdog polls without a device sync.
 #include "common.h"
 
 namespace dbx {
@@ -35,6 +38,7 @@ struct DarArgs {
   unsigned* flags[DAR_MAX_RANKS];   // every rank's flag array: [3 phases][grid][DAR_MAX_RANKS] (uncached)
   unsigned* gen;                    // this rank's per-workgroup generation counters [grid]
   int* err;                         // this rank's error word (bit 0: a barrier timed out)
+  int* err_host;                    // device view of a pinned host word mirroring err (may be null)
   long long n;                      // elements
   long long seg;                    // elements per segment (multiple of 4)
   unsigned long long timeout_ticks; // per barrier, in s_memrealtime ticks (100 MHz)
@@ -47,7 +51,7 @@ __device__ __forceinline__ unsigned* dar_slot(unsigned* f, int phase, int b, int
 
 // the kernel body of rank `rank`'s workgroup b of G (rank / gen / err given apart from the shared args)
 __device__ __forceinline__ void dar_body(const DarArgs& a, const int rank, unsigned* const gen, int* const err,
-                                         const int b, const int G) {
+                                         int* const err_host, const int b, const int G) {
   const int tid = threadIdx.x;
   __shared__ unsigned s_gen;
   __shared__ int s_bad;
@@ -90,7 +94,28 @@ __device__ __forceinline__ void dar_body(const DarArgs& a, const int rank, unsig
   auto seg_hi = [&](int r) __attribute__((always_inline)) { const long long hi = (long long)(r + 1) * S; return hi < n ? hi : n; };
   const long long stride = (long long)G * DAR_THREADS;
 
+  // a timed-out barrier: poison every element this workgroup owns in the result (its stripe of every
+  // segment) and leave without waiting again
+  auto poison = [&]() __attribute__((always_inline)) {
+    const float qnan = __builtin_nanf("");
+    for (int j = 0; j < a.world; ++j) {
+      const long long lo = seg_lo(j), hi = seg_hi(j);
+      for (long long i = lo + (long long)b * DAR_THREADS + tid; i < hi; i += stride) a.buf[rank][i] = qnan;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      gen[b] = g;
+      atomicOr(err, 1);
+      if (err_host) __hip_atomic_store(err_host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  };
+
   barrier(0);  // entry: every rank's producers of this range have finished
+  if (s_bad) {
+    poison();
+    return;
+  }
   {
     // reduce-scatter: my segment, summed over ranks in rank order (the same order on every rank:
     // each segment is reduced by exactly one rank, so all ranks end with identical bits)
@@ -116,6 +141,10 @@ __device__ __forceinline__ void dar_body(const DarArgs& a, const int rank, unsig
     }
   }
   barrier(1);  // every rank's reduce-scatter reads of my buffer are done; every reduced segment is published
+  if (s_bad) {
+    poison();
+    return;
+  }
   for (int jj = 1; jj < a.world; ++jj) {
     // all-gather: segment j from rank j (start at my right neighbour: the ranks spread their reads)
     const int j = (rank + jj) % a.world;
@@ -129,12 +158,16 @@ __device__ __forceinline__ void dar_body(const DarArgs& a, const int rank, unsig
   barrier(2);  // exit: every rank's all-gather reads of my buffer are done
   if (tid == 0) {
     gen[b] = g;
-    if (s_bad) atomicOr(err, 1);
+    // the data is complete here; a late peer only delays its own exit, but the bit still ends the job
+    if (s_bad) {
+      atomicOr(err, 1);
+      if (err_host) __hip_atomic_store(err_host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
 __global__ __launch_bounds__(DAR_THREADS) void dar_kernel(const DarArgs a) {
-  dar_body(a, a.rank, a.gen, a.err, blockIdx.x, gridDim.x);
+  dar_body(a, a.rank, a.gen, a.err, a.err_host, blockIdx.x, gridDim.x);
 }
 
 // Test form: every rank of one process in ONE dispatch (workgroup = rank * G + b), so the ranks are
@@ -149,7 +182,7 @@ struct DarMultiArgs {
 
 __global__ __launch_bounds__(DAR_THREADS) void dar_multi_kernel(const DarMultiArgs m) {
   const int r = blockIdx.x / m.grid, b = blockIdx.x - r * m.grid;
-  dar_body(m.base, r, m.gen[r], m.err[r], b, m.grid);
+  dar_body(m.base, r, m.gen[r], m.err[r], nullptr, b, m.grid);
 }
 
 }  // namespace dbx
@@ -158,8 +191,8 @@ using namespace dbx;
 
 // peers / flags: world device pointers each (rank order). Returns a hipError_t code, or -70.. for
 // argument errors (checked again on the Python side).
-extern "C" int dbx_dar_launch(float* const* bufs, unsigned* const* flags, unsigned* gen, int* err, long long n,
-                              int rank, int world, int grid, double timeout_s, hipStream_t st) {
+extern "C" int dbx_dar_launch(float* const* bufs, unsigned* const* flags, unsigned* gen, int* err, int* err_host,
+                              long long n, int rank, int world, int grid, double timeout_s, hipStream_t st) {
   if (world < 1 || world > DAR_MAX_RANKS || rank < 0 || rank >= world) return -70;
   if (grid < 1 || n < 0) return -71;
   DarArgs a{};
@@ -170,6 +203,7 @@ extern "C" int dbx_dar_launch(float* const* bufs, unsigned* const* flags, unsign
   }
   a.gen = gen;
   a.err = err;
+  a.err_host = err_host;
   a.n = n;
   a.seg = ((n + world - 1) / world + 3) & ~3LL;
   a.timeout_ticks = (unsigned long long)(timeout_s * 1e8);
@@ -180,8 +214,9 @@ extern "C" int dbx_dar_launch(float* const* bufs, unsigned* const* flags, unsign
 }
 
 // flags of one rank: 3 phases x grid x DAR_MAX_RANKS words in uncached device memory (peer stores
-// land in memory, local polls read memory), zeroed; gen / err in ordinary device memory, zeroed
-extern "C" int dbx_dar_alloc(int grid, void** flags, void** gen, void** err) {
+// land in memory, local polls read memory), zeroed; gen / err in ordinary device memory, zeroed;
+// err_host: a zeroed pinned host word, mapped for the device (its device address in *err_host_dev)
+extern "C" int dbx_dar_alloc(int grid, void** flags, void** gen, void** err, void** err_host, void** err_host_dev) {
   const size_t fb = sizeof(unsigned) * 3 * (size_t)grid * DAR_MAX_RANKS;
   HIP_CHECK_RET(hipExtMallocWithFlags(flags, fb, hipDeviceMallocUncached));
   HIP_CHECK_RET(hipMemset(*flags, 0, fb));
@@ -189,13 +224,17 @@ extern "C" int dbx_dar_alloc(int grid, void** flags, void** gen, void** err) {
   HIP_CHECK_RET(hipMemset(*gen, 0, sizeof(unsigned) * grid));
   HIP_CHECK_RET(hipMalloc(err, sizeof(int)));
   HIP_CHECK_RET(hipMemset(*err, 0, sizeof(int)));
+  HIP_CHECK_RET(hipHostMalloc(err_host, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  *reinterpret_cast<volatile int*>(*err_host) = 0;
+  HIP_CHECK_RET(hipHostGetDevicePointer(err_host_dev, *err_host, 0));
   return (int)hipDeviceSynchronize();
 }
 
-extern "C" int dbx_dar_free(void* flags, void* gen, void* err) {
+extern "C" int dbx_dar_free(void* flags, void* gen, void* err, void* err_host) {
   if (flags) (void)hipFree(flags);
   if (gen) (void)hipFree(gen);
   if (err) (void)hipFree(err);
+  if (err_host) (void)hipHostFree(err_host);
   return 0;
 }
 

@@ -11,6 +11,7 @@
 // exactly one RCCL instance and one set of xGMI channels per process), falling back to
 // /opt/rocm/lib. Nothing links against it at build time: the extension still loads on hosts
 // without RCCL, and every entry point then raises.
+#include <chrono>
 #include <dlfcn.h>
 #include <unistd.h>
 #include <hip/hip_runtime.h>
@@ -27,9 +28,9 @@
 #include <pybind11/stl.h>
 
 extern "C" {
-int dbx_dar_launch(float* const*, unsigned* const*, unsigned*, int*, long long, int, int, int, double, hipStream_t);
-int dbx_dar_alloc(int, void**, void**, void**);
-int dbx_dar_free(void*, void*, void*);
+int dbx_dar_launch(float* const*, unsigned* const*, unsigned*, int*, int*, long long, int, int, int, double, hipStream_t);
+int dbx_dar_alloc(int, void**, void**, void**, void**, void**);
+int dbx_dar_free(void*, void*, void*, void*);
 int dbx_dar_max_ranks();
 int dbx_dar_launch_multi(float* const*, unsigned* const*, unsigned* const*, int* const*, long long, int, int, double,
                          hipStream_t);
@@ -135,25 +136,35 @@ static ncclRedOp_t op_of(int code) {
 }
 
 struct Communicator {
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;  // read / cleared with __atomic builtins where the watchdog thread may abort
   int rank = 0, size = 1, device = 0;
   bool nonblocking = false;
+  double timeout_s = 1800.0;  // bound of settle(): the process's collective timeout (comm_set_timeout)
 };
 
+static ncclComm_t live(Communicator* c) { return __atomic_load_n(&c->comm, __ATOMIC_ACQUIRE); }
+
 // A non-blocking communicator may answer any call with ncclInProgress (the operation is accepted
-// and completes asynchronously): wait for its state to settle (bounded), then report it.
+// and completes asynchronously): wait for its state to settle, bounded by the communicator's timeout,
+// then report it. The wait releases the GIL so the comm watchdog (a Python thread,
+// parallel/comm_guard.py) keeps polling and can abort the communicator; an abort ends the wait.
 static ncclResult_t settle(Communicator* c, ncclResult_t r) {
-  if (r != ncclInProgress || !c || !c->comm) return r;
+  if (r != ncclInProgress || !c || !live(c)) return r;
   Api& a = api();
   if (!a.comm_get_async_error) return ncclSuccess;
-  for (long it = 0; it < 6000000L; ++it) {  // ~10 min at 100 us
+  py::gil_scoped_release nogil;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    ncclComm_t comm = live(c);
+    if (!comm) return ncclInvalidUsage;  // aborted meanwhile
     ncclResult_t st = ncclSuccess;
-    const ncclResult_t q = a.comm_get_async_error(c->comm, &st);
+    const ncclResult_t q = a.comm_get_async_error(comm, &st);
     if (q != ncclSuccess) return q;
     if (st != ncclInProgress) return st;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s)
+      return ncclInProgress;
     usleep(100);
   }
-  return ncclInProgress;
 }
 
 }  // namespace comm
@@ -245,10 +256,14 @@ void register_comm(py::module& m) {
     auto* c = reinterpret_cast<Communicator*>(h);
     Api& a = need();
     if (!c || !c->comm || !a.comm_abort) return;
-    ncclComm_t comm = c->comm;
-    c->comm = nullptr;
+    ncclComm_t comm = __atomic_exchange_n(&c->comm, (ncclComm_t) nullptr, __ATOMIC_ACQ_REL);
+    if (!comm) return;
     py::gil_scoped_release nogil;
     a.comm_abort(comm);
+  });
+  m.def("comm_set_timeout", [](uintptr_t h, double s) {
+    auto* c = reinterpret_cast<Communicator*>(h);
+    if (c && s > 0) c->timeout_s = s;
   });
   m.def("comm_rank", [](uintptr_t h) { return reinterpret_cast<Communicator*>(h)->rank; });
   m.def("comm_size", [](uintptr_t h) { return reinterpret_cast<Communicator*>(h)->size; });
@@ -308,14 +323,21 @@ void register_comm(py::module& m) {
     return reinterpret_cast<uintptr_t>(p);
   });
   m.def("ipc_close", [](uintptr_t p) { (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(p)); });
+  // (flags, gen, err, err_host, err_host_dev): err_host is a pinned host word the kernel mirrors its
+  // error bit into, read by dar_host_err without any device sync (the comm watchdog's poll)
   m.def("dar_alloc", [](int grid) -> py::tuple {
-    void *f = nullptr, *g = nullptr, *e = nullptr;
-    const int r = dbx_dar_alloc(grid, &f, &g, &e);
+    void *f = nullptr, *g = nullptr, *e = nullptr, *eh = nullptr, *ehd = nullptr;
+    const int r = dbx_dar_alloc(grid, &f, &g, &e, &eh, &ehd);
     if (r != 0) throw std::runtime_error("dar_alloc failed: hip error " + std::to_string(r));
-    return py::make_tuple(reinterpret_cast<uintptr_t>(f), reinterpret_cast<uintptr_t>(g), reinterpret_cast<uintptr_t>(e));
+    return py::make_tuple(reinterpret_cast<uintptr_t>(f), reinterpret_cast<uintptr_t>(g), reinterpret_cast<uintptr_t>(e),
+                          reinterpret_cast<uintptr_t>(eh), reinterpret_cast<uintptr_t>(ehd));
   });
-  m.def("dar_free", [](uintptr_t f, uintptr_t g, uintptr_t e) {
-    dbx_dar_free(reinterpret_cast<void*>(f), reinterpret_cast<void*>(g), reinterpret_cast<void*>(e));
+  m.def("dar_free", [](uintptr_t f, uintptr_t g, uintptr_t e, uintptr_t eh) {
+    dbx_dar_free(reinterpret_cast<void*>(f), reinterpret_cast<void*>(g), reinterpret_cast<void*>(e),
+                 reinterpret_cast<void*>(eh));
+  }, py::arg("flags"), py::arg("gen"), py::arg("err"), py::arg("err_host") = 0);
+  m.def("dar_host_err", [](uintptr_t eh) {
+    return eh ? static_cast<int>(*reinterpret_cast<volatile int*>(eh)) : 0;
   });
   m.def("dar_max_ranks", []() { return dbx_dar_max_ranks(); });
   // every rank of one process in one dispatch (tests: co-resident by construction)
@@ -345,7 +367,8 @@ void register_comm(py::module& m) {
     return v;
   }, py::arg("err"), py::arg("reset") = false);
   m.def("dar_launch", [](std::vector<uintptr_t> bufs, std::vector<uintptr_t> flags, uintptr_t gen, uintptr_t err,
-                         long long n, int rank, int world, int grid, double timeout_s, uintptr_t stream) {
+                         long long n, int rank, int world, int grid, double timeout_s, uintptr_t stream,
+                         uintptr_t err_host_dev) {
     if ((int)bufs.size() != world || (int)flags.size() != world) throw std::invalid_argument("dar_launch: world");
     std::vector<float*> b(world);
     std::vector<unsigned*> f(world);
@@ -353,8 +376,9 @@ void register_comm(py::module& m) {
       b[j] = reinterpret_cast<float*>(bufs[j]);
       f[j] = reinterpret_cast<unsigned*>(flags[j]);
     }
-    const int r = dbx_dar_launch(b.data(), f.data(), reinterpret_cast<unsigned*>(gen), reinterpret_cast<int*>(err), n,
-                                 rank, world, grid, timeout_s, reinterpret_cast<hipStream_t>(stream));
+    const int r = dbx_dar_launch(b.data(), f.data(), reinterpret_cast<unsigned*>(gen), reinterpret_cast<int*>(err),
+                                 reinterpret_cast<int*>(err_host_dev), n, rank, world, grid, timeout_s,
+                                 reinterpret_cast<hipStream_t>(stream));
     if (r != 0) throw std::runtime_error("dar_launch failed: code " + std::to_string(r));
   });
 }

@@ -17,7 +17,8 @@ direction), so
 :func:`plan_allreduce` prices both with the model below and returns the plan for one buffer: path
 (``rccl`` | ``direct``), the chunking of the buffer into buckets, and the RCCL channel bounds of the
 framework communicator. The model's constants are ASSUMPTIONS (link rate from the platform spec,
-latencies from the one-GPU measurements of flag hand-offs in MI355X_MICROARCH.md); the world >= 2
+latencies from the one-GPU flag hand-off measurements in the image's CDNA4 guide,
+/opt/skills/guides/MI355X_MICROARCH.md -- outside this repository); the world >= 2
 measurement that would calibrate them needs a multi-GPU node (``tools/bench_allreduce.py --path
 all`` prints the nccl-tests lines to do so). Until then the direct path is opt-in
 (``DBX_DIRECT_AR=1``) and the defaults keep RCCL for everything.

@@ -183,6 +183,8 @@ class NativeComm:
         with torch.cuda.device(self.device):
             self._h = c.comm_init(obj[0], self.size, self.rank, 0 if nonblocking else 1, lo, hi)
         self._c = c
+        from .comm_guard import comm_timeout_s
+        c.comm_set_timeout(self._h, comm_timeout_s())  # bounds the wait on a collective's ncclInProgress
         if nonblocking:
             self._settle_init(comm_init_timeout() if timeout_s is None else float(timeout_s), abort_if)
 
@@ -326,7 +328,9 @@ class NativeComm:
         ag = _Agreement(self.pg)
         d, err = None, ""
         try:
-            d = DirectAllReduce(self, buf, grid=grid)
+            # barrier deadlines well inside the verify wait: a missing peer ends the kernel (error bit,
+            # poisoned range) before verify gives up, and the RCCL communicator is never aborted here
+            d = DirectAllReduce(self, buf, grid=grid, barrier_timeout_s=max(0.05, timeout / 4), setup_timeout_s=timeout)
             ok = d.verify(timeout)
             err = "" if ok else "check all-reduce returned wrong values"
         except Exception as e:  # noqa: BLE001
@@ -344,6 +348,9 @@ class NativeComm:
         code 0 = healthy, 7 (``ncclInProgress``) = still initialising, -1 = aborted, else a failure."""
         if not getattr(self, "_h", 0):
             return -1, "communicator closed"
+        d = getattr(self, "direct", None)
+        if d is not None and d.pending_error():
+            return -2, "direct xGMI all-reduce: a flag barrier timed out (a peer is missing); the range is NaN"
         code, msg = self._c.comm_async_error(self._h)
         return int(code), str(msg)
 
@@ -383,7 +390,8 @@ class DirectAllReduce:
     rank) that the plan sends down this path; :meth:`all_reduce` launches the kernel on the stream
     (capturable: the kernel's barrier generations live in device memory)."""
 
-    def __init__(self, comm: "NativeComm", buf: torch.Tensor, grid: int = 64, barrier_timeout_s: float = 120.0):
+    def __init__(self, comm: "NativeComm", buf: torch.Tensor, grid: int = 64, barrier_timeout_s: float = 120.0,
+                 setup_timeout_s: Optional[float] = None):
         from .collective_plan import DAR_MAX_RANKS
         if buf.dtype != torch.float32 or not buf.is_cuda or not buf.is_contiguous():
             raise ValueError("DirectAllReduce: a contiguous fp32 device buffer")
@@ -393,11 +401,22 @@ class DirectAllReduce:
         self._c, self.comm, self.grid = c, comm, int(grid)
         self.buf, self.timeout = buf, float(barrier_timeout_s)
         self.rank, self.size = comm.rank, comm.size
-        self._flags, self._gen, self._err = c.dar_alloc(self.grid)
+        self._flags = self._gen = self._err = self._err_host = self._err_host_dev = 0
         self._opened = []
-        h, off = c.ipc_handle(buf.data_ptr())
-        fh, foff = c.ipc_handle(self._flags)
-        mine = (h, off, fh, foff, buf.numel(), self.grid)
+        # local setup (allocation, handle export) is voted on BEFORE the collective handle exchange, so
+        # a rank that fails here cannot leave its peers blocked in all_gather_object
+        mine, err = None, ""
+        try:
+            self._flags, self._gen, self._err, self._err_host, self._err_host_dev = c.dar_alloc(self.grid)
+            h, off = c.ipc_handle(buf.data_ptr())
+            fh, foff = c.ipc_handle(self._flags)
+            mine = (h, off, fh, foff, buf.numel(), self.grid)
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        setup_timeout = comm_init_timeout() if setup_timeout_s is None else float(setup_timeout_s)
+        if not _Agreement(comm.pg).all_true(mine is not None, "direct_setup", setup_timeout, comm.device):
+            self.close()
+            raise RuntimeError(f"DirectAllReduce: local setup failed on a rank ({err or 'a peer'})")
         allinfo = [None] * self.size
         dist.all_gather_object(allinfo, mine, group=comm.pg)
         self.peer_buf, self.peer_flags = [], []
@@ -429,21 +448,35 @@ class DirectAllReduce:
     def all_reduce(self, t: torch.Tensor, stream=None) -> None:
         off = t.data_ptr() - self.buf.data_ptr()
         self._c.dar_launch([b + off for b in self.peer_buf], list(self.peer_flags), self._gen, self._err,
-                           t.numel(), self.rank, self.size, self.grid, self.timeout, _stream_ptr(stream))
+                           t.numel(), self.rank, self.size, self.grid, self.timeout, _stream_ptr(stream),
+                           self._err_host_dev)
 
     def errors(self) -> int:
         """The error word (bit 0: a flag barrier timed out); reading it synchronises the device."""
         torch.cuda.synchronize(self.comm.device)
         return int(self._c.dar_read_err(self._err, False))
 
+    def pending_error(self) -> int:
+        """The kernel's pinned host mirror of the error word, read WITHOUT a device sync (the comm
+        watchdog's poll, through :meth:`NativeComm.async_error`): non-zero once any launch timed out."""
+        return int(self._c.dar_host_err(self._err_host)) if self._err_host else 0
+
     def verify(self, timeout_s: float) -> bool:
-        """A direct all-reduce of a buffer range holding rank + 1 must give the exact sum (bounded wait)."""
+        """A direct all-reduce of a buffer range holding rank + 1 must give the exact sum. The wait is on
+        an event of this launch only: the kernel's own barrier deadlines (3 x ``self.timeout``, set
+        below ``timeout_s`` by :meth:`NativeComm.enable_direct`) end it, so nothing is aborted here --
+        in particular not the shared RCCL communicator the buckets fall back to."""
         n = min(self.buf.numel(), 1 << 16)
         saved = self.buf[:n].clone()
         self.buf[:n].fill_(float(self.rank + 1))
         self.all_reduce(self.buf[:n])
-        if not self.comm._wait_device(timeout_s):
-            return False
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.comm.device))
+        t0 = time.monotonic()
+        while not ev.query():
+            if time.monotonic() - t0 > timeout_s:
+                return False
+            time.sleep(0.0005)
         ok = bool((self.buf[:n] == float(self.size * (self.size + 1) // 2)).all().item()) and self.errors() == 0
         self.buf[:n].copy_(saved)
         return ok
@@ -456,8 +489,8 @@ class DirectAllReduce:
                 pass
         self._opened = []
         if getattr(self, "_flags", 0):
-            self._c.dar_free(self._flags, self._gen, self._err)
-            self._flags = self._gen = self._err = 0
+            self._c.dar_free(self._flags, self._gen, self._err, self._err_host)
+            self._flags = self._gen = self._err = self._err_host = self._err_host_dev = 0
 
 
 def bus_bandwidth(op: str, nbytes: int, seconds: float, world: int) -> float:

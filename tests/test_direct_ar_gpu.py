@@ -21,7 +21,7 @@ def _launch(c, bufs, fl, n, grid, timeout, streams, ranks=None):
     world = len(bufs)
     for r in (range(world) if ranks is None else ranks):
         c.dar_launch([b.data_ptr() for b in bufs], [f[0] for f in fl], fl[r][1], fl[r][2], n, r, world, grid,
-                     timeout, streams[r].cuda_stream)
+                     timeout, streams[r].cuda_stream, fl[r][4])
 
 
 def _ref(src):
@@ -52,7 +52,7 @@ def test_direct_two_shot_protocol(world, n):
                 assert torch.equal(b, ref)
     finally:
         for f in fl:
-            c.dar_free(*f)
+            c.dar_free(*f[:4])
 
 
 def test_direct_per_rank_launches_on_two_queues():
@@ -77,7 +77,7 @@ def test_direct_per_rank_launches_on_two_queues():
                 assert torch.equal(b, ref)
     finally:
         for f in fl:
-            c.dar_free(*f)
+            c.dar_free(*f[:4])
 
 
 def test_direct_two_shot_graph_replay():
@@ -108,7 +108,7 @@ def test_direct_two_shot_graph_replay():
         del g
         torch.cuda.synchronize()
         for f in fl:
-            c.dar_free(*f)
+            c.dar_free(*f[:4])
 
 
 def test_direct_missing_peer_times_out_with_error_bit():
@@ -118,13 +118,17 @@ def test_direct_missing_peer_times_out_with_error_bit():
     fl = [c.dar_alloc(grid) for _ in range(world)]
     streams = [torch.cuda.Stream() for _ in range(world)]
     try:
-        _launch(c, bufs, fl, n, grid, 0.2, streams, ranks=[0])  # rank 1 never arrives (3 x 0.2 s)
-        torch.cuda.synchronize()  # bounded: every barrier gives up at its deadline
+        assert c.dar_host_err(fl[0][3]) == 0
+        _launch(c, bufs, fl, n, grid, 0.2, streams, ranks=[0])  # rank 1 never arrives
+        torch.cuda.synchronize()  # bounded: the first barrier gives up at its deadline, no later waits
+        assert c.dar_host_err(fl[0][3]) == 1  # the pinned mirror the comm watchdog polls (no device sync)
         assert c.dar_read_err(fl[0][2], True) == 1
         assert c.dar_read_err(fl[0][2]) == 0  # reset
+        # the timed-out rank's result is poisoned, never a partial sum passed off as a gradient
+        assert torch.isnan(bufs[0]).all() and torch.equal(bufs[1], torch.ones(n, device="cuda"))
     finally:
         for f in fl:
-            c.dar_free(*f)
+            c.dar_free(*f[:4])
 
 
 def test_direct_allreduce_class_world1(tmp_path):
