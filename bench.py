@@ -85,6 +85,12 @@ def parse_args(argv=None):
     p.add_argument("--mds-samples", type=int, default=0, help="samples per rank written for --data mds "
                    "(default: enough for warmup + steps, at least 8 batches)")
     p.add_argument("--json-out", default=None)
+    p.add_argument("--phase-timeout", type=float, default=300.0,
+                   help="world > 1: watchdog bound (s) on every phase (setup / warm-up / timed / checks); exit 75")
+    p.add_argument("--comm-fallback", type=int, default=1, choices=[0, 1],
+                   help="world > 1: re-run failed ranks once, fresh, on the c10d step (comm=torch)")
+    p.add_argument("--rccl-summary", type=int, default=1, choices=[0, 1],
+                   help="world > 1 on RCCL: log RCCL's rings / channels to a file and summarise them in the JSON")
     a = p.parse_args(argv)
     given = {t.split("=", 1)[0] for t in (sys.argv[1:] if argv is None else argv) if t.startswith("--")}
     for k, v in PRESETS.get(a.preset, {}).items():
@@ -112,15 +118,20 @@ def self_launch(args, argv) -> int:
     # the ranks failed on the default (framework-RCCL one-graph) step -- e.g. a hung collective ended by
     # the watchdog (75): this parent never touched the GPU, so it starts FRESH ranks once on the c10d step
     reason = f"attempt 1 failed: worst rank {describe_exit(rc)}"
-    print(f"[bench] {reason}; re-running {args.gpus} fresh ranks with DBX_COMM=torch", file=sys.stderr, flush=True)
+    print(f"[bench] {reason}; re-running {args.gpus} fresh ranks with comm=torch", file=sys.stderr, flush=True)
     return run_subprocess_ranks(args.gpus, cmd, env={**fallback_env(reason), "DBX_RESTART_COUNT": "1"})
+
+
+def _engine():
+    from dbx_distributed_pytorch_examples_amd.engine_config import EngineConfig
+    return EngineConfig.current()
 
 
 def _may_fall_back(args) -> bool:
     """A failed multi-rank native run is re-measured once on fresh ranks (c10d collectives) unless it
-    already is that re-measurement, runs on c10d anyway, or DBX_BENCH_FALLBACK=0."""
-    return (args.impl == "native" and os.environ.get("DBX_BENCH_FALLBACK", "1") != "0"
-            and not os.environ.get("DBX_COMM_FALLBACK_REASON") and os.environ.get("DBX_COMM", "") != "torch")
+    already is that re-measurement, runs on c10d anyway, or --comm-fallback 0."""
+    return (args.impl == "native" and args.comm_fallback == 1 and not os.environ.get("DBX_BENCH_RETRY")
+            and _engine().comm != "torch")
 
 
 def _retryable(rc: int) -> bool:
@@ -131,7 +142,8 @@ def _retryable(rc: int) -> bool:
 
 
 def fallback_env(reason: str) -> dict:
-    return {"DBX_COMM": "torch", "DBX_COMM_FALLBACK_REASON": reason}
+    from dbx_distributed_pytorch_examples_amd.engine_config import engine_env
+    return {"DBX_ENGINE": engine_env(comm="torch"), "DBX_BENCH_RETRY": reason}
 
 
 def supervise(args, argv) -> int:
@@ -142,10 +154,10 @@ def supervise(args, argv) -> int:
     return supervise_rank([sys.executable, os.path.abspath(__file__)] + list(argv), fallback_env, _retryable)
 
 
-def _rccl_log_setup(info_world: int) -> str:
+def _rccl_log_setup(info_world: int, on: bool = True) -> str:
     """World > 1 on RCCL: route RCCL's INFO log (rings, channels, version) to a per-process file unless the
     user set NCCL_DEBUG (then it passes through untouched). Returns the file path ('' = none)."""
-    if info_world <= 1 or os.environ.get("DBX_DIST_BACKEND") == "gloo" or os.environ.get("DBX_RCCL_SUMMARY") == "0":
+    if info_world <= 1 or os.environ.get("DBX_DIST_BACKEND") == "gloo" or not on:
         return ""
     if "NCCL_DEBUG" in os.environ:
         return os.environ.get("NCCL_DEBUG_FILE", "")
@@ -295,7 +307,7 @@ def main(argv=None) -> int:
     if (args.gpus > 1 and not os.environ.get("DBX_SUPERVISED_CHILD") and _may_fall_back(args)
             and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"):
         return supervise(args, raw)
-    rccl_log = _rccl_log_setup(int(os.environ.get("WORLD_SIZE", "1")))
+    rccl_log = _rccl_log_setup(int(os.environ.get("WORLD_SIZE", "1")), args.rccl_summary == 1)
     from dbx_distributed_pytorch_examples_amd.parallel import dist as ddist
     from dbx_distributed_pytorch_examples_amd.train.bench_steps import build_step
 
@@ -314,22 +326,23 @@ def main(argv=None) -> int:
     wd = None
     if info.world_size > 1:
         from dbx_distributed_pytorch_examples_amd.parallel.comm_guard import CommWatchdog
-        wd = CommWatchdog(timeout_s=float(os.environ.get("DBX_BENCH_TIMEOUT", "300")), device=info.device)
+        wd = CommWatchdog(timeout_s=args.phase_timeout, device=info.device)
     from dbx_distributed_pytorch_examples_amd.utils import fault
-    comm_fallback = os.environ.get("DBX_COMM_FALLBACK_REASON") or None
+    comm_fallback = os.environ.get("DBX_BENCH_RETRY") or None
     for attempt in (0, 1):
         if wd is not None:
             wd.step_begin("setup")
         rc, elapsed, meta = _measure(args, info, wd, build_step, ddist, fault)
         # the one-graph multi-rank step (framework RCCL communicator) is checked here against its own
         # replicas: if they diverged, every rank saw it (the check gathers all checksums) and all of them
-        # rebuild the step on the c10d path (DBX_COMM=torch) and measure again instead of failing
+        # rebuild the step on the c10d path (comm=torch) and measure again instead of failing
         if rc == 4 and attempt == 0 and meta.get("_native_comm"):
             if info.rank == 0:
                 print("[bench] warning: the one-graph step's replicas diverged; re-measuring on the c10d "
-                      "collectives (DBX_COMM=torch)", file=sys.stderr, flush=True)
-            os.environ["DBX_COMM"] = "torch"
-            comm_fallback = "replicas_diverged on the one-graph step; re-measured in-process with DBX_COMM=torch"
+                      "collectives (comm=torch)", file=sys.stderr, flush=True)
+            from dbx_distributed_pytorch_examples_amd.engine_config import engine_env
+            os.environ["DBX_ENGINE"] = engine_env(comm="torch")
+            comm_fallback = "replicas_diverged on the one-graph step; re-measured in-process with comm=torch"
             continue
         break
     if rc != 0:

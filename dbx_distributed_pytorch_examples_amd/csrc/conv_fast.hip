@@ -164,186 +164,18 @@ __global__ __launch_bounds__(512, 1) void fast_igemm_kernel(const IGemmArgs a) {
   igemm_epilogue<BM, BN, WM, WN, MODE, STATS, ACCUM, EPI>(a, acc, lds, m0, n0, tm, blockIdx.x);
 }
 
-// Ping-pong variant of the eight-wave kernel (DBX_FAST_PP=1). The two wave groups (waves 0-3 own
-// tile rows 0-127, waves 4-7 rows 128-255; wave w runs on SIMD w % 4, so every SIMD holds one wave
-// of each) run half a phase apart: group 1 passes one extra barrier first, so while one group issues
-// its MFMA burst the other issues its fragment reads and its share of the LDS-DMA ring, and the
-// matrix pipe of each SIMD is fed by one wave or the other on every barrier interval
-// (cdna_hip_programming.md §5, the staggered wave groups of the 256^2 8-phase template).
-//
-// Stages: 32 channels of one tap (A 256 x 32, B BN x 32), NS = D + 2 ring slots, D stages prefetched.
-// Each group DMAs its own 128 A rows and half of the B rows. Barrier event e separates interval e
-// from e + 1; group 0 runs READ(t) in interval 2t and MFMA(t) in 2t + 1, group 1 READ(t) in 2t + 1
-// and MFMA(t) in 2t + 2. Orders (all by counted vmcnt / lgkmcnt + the next barrier event):
-//   RAW: group 0 retires its part of stage t + 1 at the end of MFMA(t), group 1 at the end of READ(t)
-//        -- both before event 2t + 1; the first read of stage t + 1 is in interval 2t + 2;
-//   WAR: stage t's last reads (group 1, interval 2t + 1) retire at the lgkmcnt(0) of its MFMA(t),
-//        published by event 2t + 2; slot t % NS is refilled (stage t + NS) in interval
-//        2(t + NS - D) >= 2t + 4.
-template <int BN, int MODE, bool STATS, bool ACCUM, int EPI>
-__global__ __launch_bounds__(512, 1) void pp_igemm_kernel(const IGemmArgs a) {
-  constexpr int BM = 256, NT = 512, NW = 8, BK = 32;
-  constexpr int WM = BN == 256 ? 2 : 4, WN = NW / WM;
-  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
-  constexpr int CPR = BK / 8;                    // 16-B chunks per stage row
-  constexpr int GT = NT / 2;                     // threads per group
-  constexpr int RPP = GT / CPR;                  // rows per group DMA pass (64)
-  constexpr int A_CH = (BM / 2) / RPP, B_CH = (BN / 2) / RPP;
-  constexpr int ND = A_CH + B_CH;                // DMA instructions per wave and stage
-  constexpr int STG = (BM + BN) * BK;            // bf16 per stage
-  constexpr int NS = BN == 256 ? 5 : 6, D = NS - 2;
-  constexpr int LDS_AB = NS * STG;
-  constexpr int LDS_EP = BM * (BN + 8) + 2 * (3 * NW * BN);
-  constexpr int LDS_MAIN = LDS_AB > LDS_EP ? LDS_AB : LDS_EP;
-  static_assert(2 * LDS_MAIN <= 163840, "LDS");
-  static_assert(RPP % 16 == 0 && A_CH >= 1 && B_CH >= 1, "DMA geometry");
-  static_assert(MODE == FWD || MODE == DGRAD, "fast kernel: forward / data gradient");
-  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_MAIN];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
-  // wave-uniform in an SGPR: the group branches around s_barrier must be scalar branches (an
-  // exec-masked block would still execute its s_barrier)
-  const int grp = __builtin_amdgcn_readfirstlane(wid >> 2), gt = tid & (GT - 1), gw = (wid & 3);
-  const int ntn = a.OC / BN, ntm = (a.M + BM - 1) / BM, ntile = ntn * ntm;
-  const int bid = xcd_remap(blockIdx.x, ntile);
-  const int tm = bid / ntn, tn = bid - tm * ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  // ---- this thread's DMA rows: A rows grp*128 + gt/CPR + RPP*i, B rows grp*BN/2 + gt/CPR + RPP*i
-  const int ach = gt & (CPR - 1);
-  const int lch = ach ^ fswz<BK>(gt / CPR);
-  int ahb[A_CH], awb[A_CH];
-  unsigned apix[A_CH];
-#pragma unroll
-  for (int i = 0; i < A_CH; ++i) {
-    const int m = m0 + grp * (BM / 2) + gt / CPR + RPP * i;
-    const int ohw = a.OH * a.OW;
-    int n = mdiv_or(m, a.mag_ohw, ohw);
-    const int pq = m - n * ohw;
-    const int oh = mdiv_or(pq, a.mag_ow, a.OW), ow = pq - oh * a.OW;
-    if (m >= a.M) n = 0;
-    if (MODE == DGRAD) { ahb[i] = oh + a.dh0; awb[i] = ow + a.dw0; }
-    else { ahb[i] = oh * a.stride - a.pad; awb[i] = ow * a.stride - a.pad; }
-    apix[i] = 2u * (unsigned)(((n * a.IH + ahb[i]) * a.IW + awb[i]) * a.IC + lch * 8);
-    if (m >= a.M) ahb[i] = -(1 << 28);
-  }
-  const int KTOT = a.R * a.S * a.IC;
-  const int cpt = a.IC / BK;
-  const int KS = a.nr * a.ns * cpt;  // stages
-  const i32x4 xsrd = make_srd(a.x, 2ull * a.N * a.IH * a.IW * a.IC);
-  const i32x4 wsrd = make_srd(a.w, 2ull * a.OC * KTOT);
-  const unsigned lds0 = lds_addr(lds);
-  int lk = 0, lcb = 0, lts = 0, ltr = 0;  // loader position (stage lk = (tap row, tap column, channel block))
-  int lslot = 0;
-  auto issue = [&]() __attribute__((always_inline)) {
-    const bool live = lk < KS;  // past the last stage: out-of-range offsets (zeros into a slot no one reads)
-    const int cb = lcb * BK;
-    const int r = a.r0 + a.tstep * ltr, s = a.s0 + a.tstep * lts;
-    const int dh = (MODE == DGRAD) ? -ltr : r, dw = (MODE == DGRAD) ? -lts : s;
-    const unsigned toff = 2u * (unsigned)((dh * a.IW + dw) * a.IC + cb);
-    const unsigned sbase = lds0 + 2u * (unsigned)(lslot * STG);
-    const unsigned da = sbase + 2u * (unsigned)(grp * (BM / 2) * BK) + 1024u * (unsigned)gw;
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const bool v = live && (unsigned)(ahb[i] + dh) < (unsigned)a.IH && (unsigned)(awb[i] + dw) < (unsigned)a.IW;
-      lds_dma16(xsrd, v ? apix[i] + toff : kOOB, da + 1024u * (unsigned)(4 * i));
-    }
-    const int koff = (r * a.S + s) * a.IC + cb + lch * 8;
-    const unsigned db = sbase + 2u * (unsigned)((BM + grp * (BN / 2)) * BK) + 1024u * (unsigned)gw;
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int n = n0 + grp * (BN / 2) + gt / CPR + RPP * i;
-      lds_dma16(wsrd, live ? 2u * (unsigned)(n * KTOT + koff) : kOOB, db + 1024u * (unsigned)(4 * i));
-    }
-    ++lk;
-    lslot = lslot + 1 == NS ? 0 : lslot + 1;
-    if (++lcb == cpt) { lcb = 0; if (++lts == a.ns) { lts = 0; ++ltr; } }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[TM], fb[TN];
-  auto read_frags = [&](int slot) __attribute__((always_inline)) {
-    const bf16* cA = lds + slot * STG;
-    const bf16* cB = cA + BM * BK;
-    const int ch = lane >> 4;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int row = wn * (BN / WN) + j * 16 + (lane & 15);
-      fb[j] = *reinterpret_cast<const bf16x8*>(cB + row * BK + ((ch ^ fswz<BK>(row)) << 3));
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = wm * (BM / WM) + i * 16 + (lane & 15);
-      fa[i] = *reinterpret_cast<const bf16x8*>(cA + row * BK + ((ch ^ fswz<BK>(row)) << 3));
-    }
-  };
-
-  // prologue: D stages in flight, stage 0 published; group 1 then falls one barrier behind
-#pragma unroll
-  for (int t = 0; t < D; ++t) issue();
-  dma_wait<(D - 1) * ND>();
-  __builtin_amdgcn_s_barrier();
-  if (grp == 1) __builtin_amdgcn_s_barrier();
-  int rslot = 0;
-  for (int t = 0; t < KS; ++t) {
-    // READ(t): refill (stage t + D), fragments of stage t
-    __builtin_amdgcn_sched_barrier(0);
-    issue();
-    read_frags(rslot);
-    if (grp == 1) dma_wait<(D - 1) * ND>();  // my part of stage t + 1 (group 1: before event 2t + 1)
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    // MFMA(t)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)  // C^T = W X^T: a lane's 4 accumulators = 4 channels of one pixel
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (grp == 0) dma_wait<(D - 1) * ND>();  // my part of stage t + 1 (group 0: before event 2t + 1)
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    rslot = rslot + 1 == NS ? 0 : rslot + 1;
-  }
-  if (grp == 0) __builtin_amdgcn_s_barrier();  // realign the two groups' barrier counts
-  dma_wait<0>();  // the past-the-end ring issues have landed before the epilogue reuses the LDS
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  igemm_epilogue<BM, BN, WM, WN, MODE, STATS, ACCUM, EPI>(a, acc, lds, m0, n0, tm, blockIdx.x);
-}
-
 }  // namespace dbx
 
 using namespace dbx;
 
-// DBX_FAST_STAGE=32: the deep ring of 32-channel stages (4 slots at BN 256, 6 at BN 128) instead of
-// 64-channel stages (2 / 3 slots); A/B switch, read at each launch (graph capture records the choice)
-// DBX_FAST_PP=1: the ping-pong variant (pp_igemm_kernel); also read at each launch
+// 64-channel stages in a 2- (BN 256) / 3-slot (BN 128) ring. (Measured and removed in round 6: the deep
+// ring of 32-channel stages (4 / 5 slots) and a ping-pong variant with staggered wave groups, neither
+// faster in the step: profiles/r5_ring/, profiles/r4_s5/.)
 template <int BN, int MODE, bool STATS, bool ACCUM, int EPI>
 static int launch_fast(const IGemmArgs& a, hipStream_t st) {
-  const char* e = getenv("DBX_FAST_STAGE");
-  const bool deep = e && atoi(e) == 32;
-  const char* p = getenv("DBX_FAST_PP");
-  const bool pp = p && atoi(p) == 1;
   const int ntile = (a.OC / BN) * ((a.M + 255) / 256);
-  if (pp)
-    hipLaunchKernelGGL((pp_igemm_kernel<BN, MODE, STATS, ACCUM, EPI>), dim3(ntile), dim3(512), 0, st, a);
-  else if (deep && BN == 256 && getenv("DBX_FAST_SLOTS") && atoi(getenv("DBX_FAST_SLOTS")) == 5)
-    // A/B: five 32-channel slots (the whole 160 KiB: four stages in flight behind the MFMAs)
-    hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, 5, 32>), dim3(ntile), dim3(512), 0, st, a);
-  else if (deep)
-    hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, BN == 256 ? 4 : 6, 32>), dim3(ntile), dim3(512),
-                       0, st, a);
-  else
-    hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, BN == 256 ? 2 : 3, 64>), dim3(ntile),
-                       dim3(512), 0, st, a);
+  hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, BN == 256 ? 2 : 3, 64>), dim3(ntile),
+                     dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -619,7 +619,6 @@ static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, int dma, hipSt
 
 
 extern "C" int dbx_conv_fast(int mode, int bn, const IGemmArgs* args, int stats, int accum, int epi, hipStream_t st);
-extern "C" int dbx_conv_rowtile(int mode, const IGemmArgs* args, int stats, int accum, int epi, hipStream_t st);
 
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
                               int accum, int epi, hipStream_t st, int dma) {
@@ -627,10 +626,6 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
   if (dma == 4) {  // eight-wave 256-row kernel (conv_fast.hip): plain operands, stride-1 data gradients
     if (bm != 256 || pro || mode == STEM || (mode == DGRAD && (a.osub != 1 || a.add_sub > 1))) return -65;
     return dbx_conv_fast(mode, bn, args, stats, accum, epi, st);
-  }
-  if (dma == 7) {  // row-tile kernel (conv_rowtile.hip): 1x1 stride-1 BN-prologue forwards / folded dgrads
-    if (mode != FWD && mode != DGRAD) return -70;
-    return dbx_conv_rowtile(mode, args, stats, accum, epi, st);
   }
   if (mode == FWD_PATCH || mode == DGRAD_PATCH) {  // 3x3 weights-stationary patch kernel (conv_patch3.hip)
     if (pro && !a.relu_in) return -7;
@@ -684,12 +679,8 @@ static void launch_wgrad_dma_t(const WgradArgs& a, int nblk, hipStream_t st, uns
   constexpr int WM = BIG ? 2 : (BM == 256) ? 4 : 2;
   constexpr int WN = (BN == 256) ? 4 : 2;
   if constexpr (BIG) {
-    // DBX_WGRAD_RING5=1 (A/B): the 32-pixel stages in a 5-slot ring (160 KiB: four stages in flight
-    // behind the MFMAs instead of three); only without an occupancy pad (the LDS is full)
-    static const bool ring5 = [] { const char* e = getenv("DBX_WGRAD_RING5"); return e && e[0] == '1'; }();
-    if (ring5 && lds_pad == 0)  // (either operand path of the table)
-      hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 5, 32>), dim3(nblk), dim3(64 * WM * WN), 0, st, a);
-    else if (dma == 4)
+    // (a 5-slot ring of 32-pixel stages measured not faster: profiles/r5_ring/)
+    if (dma == 4)
       hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 4, 32>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
     else
       hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, 2, 64>), dim3(nblk), dim3(64 * WM * WN), lds_pad, st, a);
@@ -716,15 +707,9 @@ extern "C" int dbx_conv_wgrad(int mode, int bm, int bn, const WgradArgs* args, i
   }
   if (a.IC % bn != 0) return -4;  // a column tile must stay inside one tap
   // LDS-DMA operand path for the prologue-free weight gradients: ring depth 2 or 3, 0 = the
-  // register-staged wgrad_kernel; dma_req < 0 = DBX_WGRAD_DMA, unset = auto: 3 slots for the
-  // 8-wave 256-wide tiles (one workgroup per CU either way), 2 for the 4-wave tiles (keeps two
-  // workgroups per CU)
-  static const int dma_env = [] {
-    const char* e = getenv("DBX_WGRAD_DMA");
-    return e ? atoi(e) : -1;
-  }();
-  const int dreq = dma_req >= 0 ? dma_req : dma_env >= 0 ? dma_env : (bm == 256 && bn == 256) ? 4
-                   : ((bm == 256 || bn == 256) ? 3 : 2);
+  // register-staged wgrad_kernel; dma_req < 0 = auto: 3 slots for the 8-wave 256-wide tiles (one
+  // workgroup per CU either way), 2 for the 4-wave tiles (keeps two workgroups per CU)
+  const int dreq = dma_req >= 0 ? dma_req : (bm == 256 && bn == 256) ? 4 : ((bm == 256 || bn == 256) ? 3 : 2);
   int dma = (dreq == 2 || dreq == 3 || dreq == 4) ? dreq : 0;
   if (bm == 256 && bn == 256) {
     if (pro) return -3;      // the 256 x 256 tile is LDS-DMA only (no register-staged prologue variant)

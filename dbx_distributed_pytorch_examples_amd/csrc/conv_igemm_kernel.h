@@ -844,16 +844,15 @@ static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
         64 * WM * WN, 0);
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const char* e = getenv("DBX_PERSIST");
-    if ((e && e[0] == '0') || per_cu <= 0 || cus <= 0) return 1 << 30;
+    if (per_cu <= 0 || cus <= 0) return 1 << 30;
     return (per_cu * cus) & ~7;
   }();
   constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64) && DMA <= 1;  // persistent (see the kernel)
-  // the weights-by-DMA variants walk tiles only when each workgroup gets at least
-  // DBX_PERSIST_DMA1 (default 8) of them: headline ResNet-50 b1024 +0.8 %, the TinyImageNet step
-  // (~4 tiles per workgroup) -0.3 % when they always do (profiles/r5_persist_dma1/); 0 = never
-  static const int pf_dma1 = [] { const char* e = getenv("DBX_PERSIST_DMA1"); return e ? atoi(e) : 8; }();
-  const bool one_per_wg = DMA == 1 && (pf_dma1 <= 0 || ntile < (long long)pf_dma1 * cap);
+  // the weights-by-DMA variants walk tiles only when each workgroup gets at least 8 of them: headline
+  // ResNet-50 b1024 +0.8 %, the TinyImageNet step (~4 tiles per workgroup) -0.3 % when they always do
+  // (profiles/r5_persist_dma1/)
+  constexpr int kPersistDma1 = 8;
+  const bool one_per_wg = DMA == 1 && ntile < (long long)kPersistDma1 * cap;
   const int nwg = (!PF || ntile <= cap || one_per_wg) ? ntile : cap;
   hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI, TAIL, DMA>), dim3(nwg), dim3(64 * WM * WN), 0, st, a);
   return (int)hipGetLastError();

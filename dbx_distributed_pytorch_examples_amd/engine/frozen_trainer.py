@@ -10,7 +10,7 @@ for backward) up to the pooled features, and only the head — dropout + linear,
 is trained, by :class:`NativeHead` on the HIP kernels: the fc GEMMs on MFMA with the bias and a
 Philox dropout mask fused into the operand loads (the weight gradient regenerates the forward's
 mask from (seed, step) instead of storing it), the fused softmax-CE, the bias-gradient column sum
-and the fused Adam / SGD over the head's flat fp32 master (``DBX_FROZEN_NATIVE_HEAD=0``: the
+and the fused Adam / SGD over the head's flat fp32 master (engine field ``frozen_native_head=0``: the
 autograd head with the flat-bucket DDP). At world > 1 the head's flat gradient is all-reduced once.
 
 The backbone forward (~150 kernels for ResNet-50; launch-bound at the reference's small batches,
@@ -41,6 +41,7 @@ from ..utils import debug as _debug
 from .autograd_trainer import build_torch_optimizer
 from .hyper import DeviceHyper
 from .program import ResNetProgram, release_dead_graphs
+from ..engine_config import EngineConfig
 
 
 def _backbone_proxy(model: FrozenBackboneClassifier) -> nn.Module:
@@ -160,7 +161,8 @@ class FrozenFeatureTrainer:
         self.head = model.resnet.fc.to(device)
         self.smoothing = label_smoothing
         self.nhead = None
-        if os.environ.get("DBX_FROZEN_NATIVE_HEAD", "1") != "0" and optim.name in ("sgd", "adam", "adamw"):
+        eng = EngineConfig.current()
+        if eng.frozen_native_head and optim.name in ("sgd", "adam", "adamw"):
             try:
                 self.nhead = NativeHead(self.head, batch, device, optim, label_smoothing)
             except TypeError:
@@ -173,7 +175,7 @@ class FrozenFeatureTrainer:
         self.metrics = torch.zeros(2, device=device)  # loss sum, correct (device-side, no host sync)
         self.metrics64 = torch.zeros(2, device=device, dtype=torch.float64)  # the same, from the native CE
         self.use_graphs = (use_graphs and device.type == "cuda" and not _debug.enabled()
-                           and os.environ.get("DBX_FROZEN_GRAPHS", "1") != "0")
+                           and eng.frozen_graphs)
         self._graph = None
         self._feats = None
         self._warm = 0
@@ -181,8 +183,8 @@ class FrozenFeatureTrainer:
         # whole-step graph: pays off where the step is launch-bound (measured on one MI355X,
         # profiles/r2s5_frozen/: ResNet-18 CIFAR b256 530k vs 455k img/s with the backbone-only graph);
         # for larger inputs the capturable optimizer costs a little more than the head launches it
-        # hides (ResNet-50 64x64 / 224x224: -2..-3 %). DBX_FROZEN_FULL_GRAPH=1 / 0 forces it.
-        mode = os.environ.get("DBX_FROZEN_FULL_GRAPH", "auto")
+        # hides (ResNet-50 64x64 / 224x224: -2..-3 %). frozen_full_graph=1 / 0 forces it.
+        mode = eng.frozen_full_graph
         small = batch * image_hw[0] * image_hw[1] <= 256 * 32 * 32
         world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
         if self.nhead is not None:  # native head: no autograd / capturable-optimizer cost in the graph

@@ -74,7 +74,8 @@ class NativeResNet(nn.Module):
         self.dev = device
         self.pg = process_group
         self.prog = None
-        self.use_graphs = device.type == "cuda" and os.environ.get("DBX_NATIVE_MODULE_GRAPHS", "1") != "0"
+        from ..engine_config import EngineConfig
+        self.use_graphs = device.type == "cuda" and EngineConfig.current().native_module_graphs
         self._graphs = {}  # "fwd_train" / "fwd_eval" / "bwd*" -> CUDAGraph
         self._calls = {}
         # autograd needs one leaf that requires grad to route the loss back into _NativeFn

@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..engine_config import EngineConfig
 from ..ops import kernels as K
 from ..parallel.dist import host_sync_for_gloo
 from ..utils import debug as _debug
@@ -53,8 +54,10 @@ class NativeTrainer:
                  optim: Optional[OptimConfig] = None, label_smoothing: float = 0.0, use_graphs: bool = True,
                  bucket_cap_mb: float = 64.0, allreduce_dtype: torch.dtype = torch.float32,
                  process_group=None, src_hw: Optional[Tuple[int, int]] = None, mean=None, std=None,
-                 zero_stage: int = 0, cutmix_alpha: float = 0.0, seed: int = 0):
+                 zero_stage: int = 0, cutmix_alpha: float = 0.0, seed: int = 0,
+                 engine: Optional[EngineConfig] = None):
         self.dev = device
+        self.cfg = cfg = engine if engine is not None else EngineConfig.current()
         optim = optim or OptimConfig()
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
@@ -63,7 +66,8 @@ class NativeTrainer:
         # ZeRO: segment groups aligned to 16 x world elements (equal per-rank parts) and a flat bf16
         # parameter copy (the all-gather target the weight preparation reads)
         self.prog = ResNetProgram(model, batch, image_hw, device, src_hw=src_hw, mean=mean, std=std,
-                                  param_align=16 * self.world if zero_stage else 16, param16=bool(zero_stage))
+                                  param_align=16 * self.world if zero_stage else 16, param16=bool(zero_stage),
+                                  engine=cfg)
         self.prog.build_backward()
         self.opt = optim
         self.smoothing = label_smoothing
@@ -83,21 +87,20 @@ class NativeTrainer:
         self.clip_work = torch.zeros(4, device=device)
         self.step_count = 0
         # debug mode synchronizes after every kernel, which graph capture forbids; per-phase
-        # profiling (DBX_PROFILE_PHASES=1: hipEvent timers + roctx ranges) needs eager phases too
-        self.phase_timer = PhaseTimer() if os.environ.get("DBX_PROFILE_PHASES", "0") == "1" else None
+        # profiling (DBX_PROFILE=phases: hipEvent timers + roctx ranges) needs eager phases too
+        self.phase_timer = PhaseTimer() if "phases" in os.environ.get("DBX_PROFILE", "").split(",") else None
         self.use_graphs = (use_graphs and device.type == "cuda" and not _debug.enabled()
                            and self.phase_timer is None)
         self.graphs: List[Optional[torch.cuda.CUDAGraph]] = []
         self.bucket_cap = int(bucket_cap_mb * (1 << 20) // 4)
         self.ar_dtype = allreduce_dtype
         # segmented = per-segment graphs + side-stream bucket all-reduces. Always on for world > 1;
-        # DBX_SEGMENTED_GRAPHS=1 forces it at world 1 (with an initialised process group) so the
+        # segmented_graphs forces it at world 1 (with an initialised process group) so the
         # RCCL + capture interplay can be rehearsed on a one-GPU box.
-        self.segmented = self.world > 1 or (os.environ.get("DBX_SEGMENTED_GRAPHS", "0") == "1"
-                                            and dist.is_available() and dist.is_initialized())
+        self.segmented = self.world > 1 or (cfg.segmented_graphs and dist.is_available() and dist.is_initialized())
         self.comm_stream = (torch.cuda.Stream(device=device, priority=-1)
                             if self.segmented and device.type == "cuda" else None)
-        # DBX_COMM=native: the DP bucket all-reduces go through the framework's own RCCL communicator
+        # comm "native": the DP bucket all-reduces go through the framework's own RCCL communicator
         # (parallel/comm.py) on the comm stream, and the whole step -- backward segments, forked
         # all-reduces, join, optimizer -- is captured as ONE graph instead of per-segment graphs
         # with eager c10d collectives between replays (ZeRO's reduce-scatter / all-gather included)
@@ -106,9 +109,9 @@ class NativeTrainer:
         self.ncomm = None
         if self.segmented and device.type == "cuda" and (self.world == 1 or dist.get_backend(process_group) == "nccl"):
             from ..parallel.comm import native_comm_requested, open_verified_comm
-            if native_comm_requested():
+            if native_comm_requested(cfg):
                 self.ncomm = open_verified_comm(process_group, device)
-        # DBX_COMM_LOOPBACK=W (test aid, world 1, DP): the framework communicator's all-reduce scales
+        # comm_loopback W (test aid, world 1, DP): the framework communicator's all-reduce scales
         # by W in place -- the sum of W identical replicas -- and the update divides by W, so an
         # ordering bug of the one-graph step (a bucket all-reduced before its gradients are final:
         # invisible at world 1, where the collective is the identity) changes the result
@@ -118,37 +121,37 @@ class NativeTrainer:
             self.grad_collectives = "framework RCCL communicator"
             from ..parallel.collective_plan import direct_enabled
             # the direct two-shot xGMI path for the ranges the plan prices below the ring (opt-in,
-            # DBX_DIRECT_AR=1: unmeasured at world >= 2 until a multi-GPU node runs it)
-            lb = int(os.environ.get("DBX_COMM_LOOPBACK", "0") or 0)
+            # direct_ar: unmeasured at world >= 2 until a multi-GPU node runs it)
+            lb = cfg.comm_loopback
             if lb > 1 and self.world == 1 and zero_stage == 0:
                 self.loopback = self.ncomm.loopback = lb
-            if direct_enabled() and zero_stage == 0 and self.world > 1 and self.ncomm.enable_direct(self.prog.grad):
+            if direct_enabled(cfg) and zero_stage == 0 and self.world > 1 and self.ncomm.enable_direct(self.prog.grad):
                 self.grad_collectives += " + direct xGMI two-shot (small ranges)"
         # Weight gradients next to the per-segment collectives. In the ONE-graph step (framework
         # communicator) the batched side stream (one fork per backward segment, joined one segment
-        # later: DBX_OVERLAP_WGRAD=2, the world-1 default) stays on with LATE posts: segment k's
+        # later: overlap_wgrad 2) stays on with LATE posts: segment k's
         # gradient range is final only after segment k+1 joins it, so its all-reduce / reduce-scatter
         # is issued after phase k+1 (the last phase posts the last two ranges). Per-segment graphs
         # (c10d collectives between replays) cannot carry a fork across a graph boundary (a capture
-        # must end joined), so there -- and with DBX_SEG_SIDE=0 -- the round-3 layout stays: weight
+        # must end joined), so there -- and with seg_side off -- the round-3 layout stays: weight
         # gradients in order on the main stream, every range posted right after its own phase
         # (per-gradient forks next to the comm stream cost more than they overlapped:
         # profiles/r2s2_multirank/).
         if self.segmented and getattr(self.prog, "side_block_default", False):
             # the per-block default of the larger single-GPU steps posts nothing per segment: the
             # multi-rank step keeps the batched side stream and its late posts (the validated layout)
-            p = self.prog
+            p, pol = self.prog, cfg.policy
             p.side_block, p.side_batch = False, True
-            p.side_defer = os.environ.get("DBX_SIDE_DEFER", "1" if p.fwd_flops < 5e11 else "0") == "1"
-            p.lazy_join = os.environ.get("DBX_LAZY_JOIN", "1" if p.fwd_flops < 5e10 else "0") == "1"
-            p.stem_wg_main = os.environ.get("DBX_STEM_WG_MAIN", "1" if p.fwd_flops < 5e11 else "0") == "1"
+            p.side_defer = cfg.side_defer if cfg.side_defer is not None else pol.small(p.fwd_flops)
+            p.lazy_join = cfg.lazy_join if cfg.lazy_join is not None else pol.tiny(p.fwd_flops)
+            p.stem_wg_main = cfg.stem_wg_main if cfg.stem_wg_main is not None else pol.small(p.fwd_flops)
             # (with its collectives on the side stream the batched layout keeps the 64-CU reservation:
             # world-1 RCCL one-graph step with a real collective kernel, headline +0.5-1.1 % over 128,
             # TinyImageNet +0.1 %, profiles/r5_cu_reserve/sweep_late.txt)
-            if "DBX_SIDE_CU_RESERVE" not in os.environ:
-                p.side_cu_reserve = 64 if p.fwd_flops >= 5e10 else 0
-        seg_side = os.environ.get("DBX_SEG_SIDE", "1") == "1" and (self.ncomm is not None or not self.use_graphs)
-        if self.segmented and os.environ.get("DBX_OVERLAP_WGRAD") is None and not seg_side:
+            if cfg.side_cu_reserve is None:
+                p.side_cu_reserve = 0 if pol.tiny(p.fwd_flops) else 64
+        seg_side = cfg.seg_side and (self.ncomm is not None or not self.use_graphs)
+        if self.segmented and cfg.overlap_wgrad is None and not seg_side:
             self.prog.overlap_wgrad = False
         self.late_posts = bool(self.segmented and device.type == "cuda" and seg_side and self.prog.overlap_wgrad
                                and self.prog.side_batch)
@@ -156,21 +159,20 @@ class NativeTrainer:
             # per-segment collectives right after their own phase need each segment's weight gradients
             # final at its end: no batched side stream (it joins a segment late)
             self.prog.side_batch = False
-        if self.segmented and os.environ.get("DBX_COMM_SIDE", "1") != "1":
+        if self.segmented and not cfg.comm_side:
             self.prog.lazy_join = False  # (a separate comm stream orders after the main stream's joins)
-        # DBX_COMM_SIDE (default 1): in the one-graph step the collectives run on the weight-gradient
+        # comm_side (default on): in the one-graph step the collectives run on the weight-gradient
         # side stream itself (behind the batch that finished their range) instead of a third stream.
         # Under DEBUG_HIP_FORCE_GRAPH_QUEUES=2 a separate comm branch took the graph's second hardware
         # queue and pushed the weight-gradient branch onto the main chain's queue: with a real
-        # collective in the graph (world-1 DBX_COMM_LOOPBACK=2) TinyImageNet fell from 97.9k to 85.5k
+        # collective in the graph (world-1 comm_loopback=2) TinyImageNet fell from 97.9k to 85.5k
         # img/s and the headline by 1.2 % (profiles/r5_comm_queue/). The joins then wait on an event
         # behind each batch, not on the collectives queued after it.
-        self.comm_side = bool(self.ncomm is not None and self.late_posts and device.type == "cuda"
-                              and os.environ.get("DBX_COMM_SIDE", "1") == "1")
+        self.comm_side = bool(self.ncomm is not None and self.late_posts and device.type == "cuda" and cfg.comm_side)
         if self.comm_side:
             self.comm_stream = self.prog.side_stream()
             self.prog.event_joins = True
-            if os.environ.get("DBX_SIDE_DEFER") is None:
+            if cfg.side_defer is None:
                 self.prog.side_defer = True  # (the side branch then keeps its own hardware queue)
         if self.segmented and (self.prog.side_block or not self.comm_side):
             # collectives posted per segment need that segment's weight gradients joined at its end
@@ -246,22 +248,22 @@ class NativeTrainer:
         self.phases = phases
 
     def _merge_phases(self, phases):
-        """Optional coarser graph segmentation of the multi-rank path: DBX_SEG_GROUPS="3,3" merges
+        """Optional coarser graph segmentation of the multi-rank path: seg_groups "3:3" merges
         the six backward segments into two graphs (one all-reduce cut after layer3). Default: one
         graph per backward segment. Measured over RCCL on one MI355X (world-1 process group with
-        DBX_SEGMENTED_GRAPHS=1, ResNet-50 b1024, wgrad side stream on): 6 segments 13.98k / 14.03k
+        segmented_graphs=1, ResNet-50 b1024, wgrad side stream on): 6 segments 13.98k / 14.03k
         img/s, 2 segments 14.05k / 14.07k, one backward graph 13.99k / 14.00k, plain single graph
         14.45k / 14.43k (profiles/r2s2_multirank/step_layout_ab.txt) -- boundaries are not what
         the segmented path cost: the wgrad side stream next to the comm streams was (now off in
         this mode, see __init__). The finer split (more overlap, smallest exposed tail) stays.
         Groups merge only when their gradient ranges are disjoint and in order."""
-        spec = os.environ.get("DBX_SEG_GROUPS", "")
+        spec = self.cfg.seg_groups
         if not spec:
             return phases
-        sizes = [int(x) for x in spec.split(",") if x.strip()]
+        sizes = [int(x) for x in spec.split(":") if x.strip()]
         sizes = [x for x in sizes if x > 0]
         if sum(sizes) != len(phases):
-            raise ValueError(f"DBX_SEG_GROUPS={spec!r} does not cover {len(phases)} backward segments")
+            raise ValueError(f"seg_groups={spec!r} does not cover {len(phases)} backward segments")
         merged, pos = [], 0
         for sz in sizes:
             grp = phases[pos:pos + sz]
@@ -430,7 +432,7 @@ class NativeTrainer:
             else:
                 fn()
             if post is not None and self.segmented:
-                # (DBX_COMM_SIDE with a deferred side batch: the collective goes in behind the batch,
+                # (comm_side with a deferred side batch: the collective goes in behind the batch,
                 # under the batch's fork event -- the main stream's state at this phase's end)
                 if not (self.comm_side and self.prog.defer_on_side(lambda post=post: self._post(post))):
                     self.comm_stream.wait_stream(cur)

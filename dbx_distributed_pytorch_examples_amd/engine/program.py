@@ -32,6 +32,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 import torch.nn as nn
 
+from ..engine_config import EngineConfig
 from ..models.resnet import BasicBlock, Bottleneck, CifarBlock, CifarResNet18, ResNet
 from ..ops import kernels as K
 
@@ -154,13 +155,15 @@ class ResNetProgram:
 
     def __init__(self, model: nn.Module, batch: int, image_hw: Tuple[int, int], device: torch.device,
                  src_hw: Optional[Tuple[int, int]] = None, mean=None, std=None, param_align: int = 16,
-                 param16: bool = False):
+                 param16: bool = False, engine: Optional[EngineConfig] = None):
         """``image_hw``: network input size; ``src_hw``: size of the uint8 images handed in
         (crop/resize to image_hw happens on the GPU, ``augment_u8``); default = image_hw.
         ``param_align``: every backward segment's parameter group starts on a multiple of this many
         elements (ZeRO: 16 x world, so a segment splits into equal per-rank parts); ``param16``:
         keep a flat bf16 copy of the parameters (``self.param16``, ZeRO's all-gather target) and
-        derive the compute weights from it instead of from the fp32 master."""
+        derive the compute weights from it instead of from the fp32 master. ``engine``: the schedule /
+        fusion switches (default ``EngineConfig.current()``; its ``None`` fields are resolved here by
+        the step-size policy)."""
         if not supports(model):
             raise TypeError(f"ResNetProgram does not support {type(model).__name__}")
         self.model = model
@@ -171,83 +174,82 @@ class ResNetProgram:
         self.norm_std = tuple(std) if std else None
         self.dev = device
         self.in_ch = model.conv1.in_channels
-        # weight gradients on a side stream (DBX_OVERLAP_WGRAD unset / "2": batched, one fork per backward
+        self.cfg = cfg = engine if engine is not None else EngineConfig.current()
+        pol = cfg.policy
+        ow = cfg.overlap_wgrad
+        # weight gradients on a side stream (overlap_wgrad None / 2: batched, one fork per backward
         # segment -- see self.side_batch; "1": one fork per weight gradient; "0": in order on the main
         # stream). Per-gradient forks cost more than they overlap on launch-bound steps (ResNet-18 CIFAR
         # b256 189k img/s vs 222k in order) while one fork per segment wins at every size: CIFAR
         # 229-230k, TinyImageNet 95.3-95.5k vs 90.6-91.5k, headline 16.07-16.15k vs 15.94-15.99k
         # (profiles/r3s2_batched/)
-        self.overlap_wgrad = os.environ.get("DBX_OVERLAP_WGRAD", "2") != "0"
-        # split-K weight-gradient reduction inside the wgrad launch where a tile's slabs are small
-        self.fuse_wgrad_reduce = os.environ.get("DBX_FUSE_WGRAD_REDUCE", "0") == "1"
-        # BN finalize / backward coefficients computed by the producing conv's last tiles (K.BnFin)
-        self.fuse_fin = os.environ.get("DBX_FUSE_BN_FIN", "0") == "1"
-        self.wgrad_lds_pad = int(os.environ.get("DBX_WGRAD_LDS_PAD", "0"))
+        self.overlap_wgrad = ow != 0
+        # (the in-launch split-K reduce and the producer-side BN finalize (K.BnFin) measured slower than
+        # the launches they remove on all three presets and were removed in round 6: profiles/r3s2_fuse_ab/)
+        self.fuse_fin = False
 
-        # store block-internal BN outputs from the MASK_Y dgrad epilogue for the wgrads (A/B switch)
-        self.act_writeback = os.environ.get("DBX_ACT_WRITEBACK", "1") == "1"
+        # store block-internal BN outputs from the MASK_Y dgrad epilogue for the wgrads
+        self.act_writeback = cfg.act_writeback
         # compute block outputs inside the next block's conv1 prologue instead of a bn_apply pass
-        self.fuse_tail = os.environ.get("DBX_FUSE_TAIL", "1") == "1"
-        self.pool_reduce = os.environ.get("DBX_POOL_REDUCE", "1") == "1"
+        self.fuse_tail = cfg.fuse_tail
+        self.pool_reduce = cfg.pool_reduce
         # BN-backward apply of a 1x1 conv's output BN computed in that conv's dgrad prologue
-        self.fuse_bwd_apply = os.environ.get("DBX_FUSE_BWD_APPLY", "1") == "1"
+        self.fuse_bwd_apply = cfg.fuse_bwd_apply
         # ... only for large operands: folding orders the wgrad after the dgrad (no overlap), which
         # costs more than the saved pass when the kernels are too small to fill the GPU
-        self.fold_min = int(os.environ.get("DBX_FOLD_MIN_ELEMS", str(1 << 25)))
+        self.fold_min = cfg.fold_min_elems if cfg.fold_min_elems is not None else 1 << 25
         # ... and only where the dgrad's output channels (N) are at most this multiple of its
         # reduction channels: every N tile of a folded dgrad re-reads and re-applies the operand
         # (default 1: the bottleneck conv1 dgrads, N = 4K, stay unfolded -- 14.39-14.41k vs
         # 14.22-14.27k img/s folded, ResNet-50 b1024, profiles/r2s3_fold/fold_ratio_ab.txt)
-        self.fold_max_ratio = float(os.environ.get("DBX_FOLD_MAX_RATIO", "1"))
+        self.fold_max_ratio = cfg.fold_max_ratio if cfg.fold_max_ratio is not None else 1.0
         # ... except at feature maps >= this size (the ratio limit is about the N-tile repeats of
         # the operand prologue: at 56x56 the conv1 dgrads have only 1-2 N tiles; 15.19k / 15.21k vs
         # 15.17k / 15.13k img/s with the limit everywhere, profiles/r2s3_fold/fold_ratio_ab.txt)
-        self.fold_ratio_min_hw = int(os.environ.get("DBX_FOLD_RATIO_MIN_HW", "56"))
+        self.fold_ratio_min_hw = cfg.fold_ratio_min_hw
         # bottleneck conv3 backward as ONE kernel (BN3-backward apply + dgrad + MASK_Y epilogue +
         # weight gradient, K.conv_dwfused): dy3 and the BN2 output a2 never reach HBM
-        self.fuse_dw = os.environ.get("DBX_FUSE_DW", "1") == "1"
+        self.fuse_dw = cfg.fuse_dw
         # stem backward as ONE kernel (max-pool backward + BN-backward apply + stem weight gradient,
         # K.stem_bwd_fused): the full-resolution stem gradient never reaches HBM. Off by default: it
         # saves the 3.3 GB dy0 round trip at b1024 but runs 1.97 ms against 0.91 + 0.92 ms for the
         # streaming pool/BN pass + the stem wgrad (the 4-window argmax routing per element is VALU work
         # that the two-workgroups-per-CU MFMA kernel cannot hide; profiles/r2s4_stem/)
-        self.fuse_stem_bwd = os.environ.get("DBX_FUSE_STEM_BWD", "0") == "1"
+        self.fuse_stem_bwd = cfg.fuse_stem_bwd
         # 3x3 convs whose plain-operand shape has an eight-wave kernel entry (ops/tune_table.json "fwd0",
         # csrc/conv_fast.hip): the forward materialises the input BN output relu(bn(y)) once (the
         # block's acts buffer, which backward needs anyway) and runs the conv without a prologue
-        self.fast_mat = os.environ.get("DBX_FAST_MAT", "1") == "1"
-        # ... also the 1x1 conv3 of a bottleneck (short-K C -> 4C forward) where its plain shape has one
-        # (DBX_FAST_MAT1=1: every stage; a value > 1: only maps of at most that size, e.g. 14)
-        _m1 = int(os.environ.get("DBX_FAST_MAT1", "0"))
-        self.fast_mat1 = _m1 > 0
-        self.fast_mat1_max_hw = _m1 if _m1 > 1 else 1 << 30
+        # (the same for the bottleneck's 1x1 conv3 measured -0.3 %: profiles/r3s2_hipenv/fast_mat1_ab.txt)
+        self.fast_mat = cfg.fast_mat
         self._wstream = None
         self._side_pending = False
-        # DBX_OVERLAP_WGRAD unset / 2: the side stream forks once per backward segment (batched) instead
+        # overlap_wgrad 2: the side stream forks once per backward segment (batched) instead
         # of once per weight gradient. Callers that need every segment's gradients final at its end
         # (per-segment all-reduces: NativeTrainer / native_module at world > 1) turn it off.
-        self.side_batch = os.environ.get("DBX_OVERLAP_WGRAD", "2") == "2" and not self.fuse_stem_bwd  # (shares self.ws)
-        # "3": one fork per residual block (after its data gradients), every segment joined at its end:
+        self.side_batch = ow in (None, 2) and not self.fuse_stem_bwd  # (shares self.ws)
+        # 3: one fork per residual block (after its data gradients), every segment joined at its end:
         # overlap that keeps segment-final gradients (the per-segment all-reduces at world > 1)
-        self.side_block = os.environ.get("DBX_OVERLAP_WGRAD") == "3" and not self.fuse_stem_bwd
+        self.side_block = ow == 3 and not self.fuse_stem_bwd
         self._side_q = []
         self.param_align = max(16, int(param_align))
         self._want_param16 = param16
         self._build_layers()
-        # consumer-side forward BN finalize (K.conv_fwd fin_in, DBX_FIN_IN=1): each workgroup of the
+        # consumer-side forward BN finalize (K.conv_fwd fin_in): each workgroup of the
         # consuming conv re-reads the statistics shards (2 x NSHARD x C doubles). Off: measured slower
         # than the finalize launch it removes even on the launch-bound CIFAR step (212-214k vs 222k
         # img/s; TinyImageNet 87.6k vs 89.5-89.9k, profiles/r3s2_finin/)
-        self.fin_in = os.environ.get("DBX_FIN_IN", "0") == "1"
+        fl = self.fwd_conv_flops()
+        self.fwd_flops = fl
+        self.fin_in = bool(cfg.fin_in)
         # Launch-bound small steps (< 0.5 TFLOP of forward conv work: the CIFAR / TinyImageNet presets)
         # keep 4 statistics shards per BN instead of NSHARD, which makes the consumer-side forward
         # finalize cheap enough to replace the bn_finalize launches: CIFAR 233.7-236.6k vs 229.1-231.0k,
         # TinyImageNet 96.9-97.1k vs 95.4-96.0k img/s; the b1024 headline keeps NSHARD and standalone
-        # finalizes (16.14k with them vs 16.38-16.40k; profiles/r4_s6/, r4_s7/). DBX_NSHARD / DBX_FIN_IN
-        # set explicitly win.
-        self.small_step = self.fwd_conv_flops() < 5e11
-        self.nshard = 4 if (self.small_step and "DBX_NSHARD" not in os.environ) else K.NSHARD
-        if self.small_step and "DBX_FIN_IN" not in os.environ:
+        # finalizes (16.14k with them vs 16.38-16.40k; profiles/r4_s6/, r4_s7/). nshard / fin_in set
+        # explicitly win.
+        self.small_step = pol.small(fl)
+        self.nshard = cfg.nshard if cfg.nshard is not None else (4 if self.small_step else K.NSHARD)
+        if self.small_step and cfg.fin_in is None:
             self.fin_in = True
         # consumer-side backward finalize: a BN-backward apply pass computes its coefficients from the
         # moment shards itself (K.bn_bwd_apply fin=) instead of a bn_bwd_coeff launch in front of it
@@ -256,10 +258,8 @@ class ResNetProgram:
         # profiles/r4_s7/); at 50-500 GFLOP (TinyImageNet) only for BNs of <= 512 channels: 95.7-95.9k vs 95.5k img/s
         # (all widths 94.7k: an apply that finalizes in-launch is capped near C x 512 channel-finalizes,
         # few blocks at 2048); CIFAR keeps every width (253.1-254.0k vs 251.6-252.5k at <= 256):
-        # profiles/r4_s18/. DBX_COEFF_IN_MAXC overrides the width limit (0: none).
-        fl = self.fwd_conv_flops()
-        self.fwd_flops = fl
-        # by default the side stream forks once per residual BLOCK (DBX_OVERLAP_WGRAD=3; first from 50
+        # profiles/r4_s18/. coeff_in_maxc overrides the width limit (0: none).
+        # by default the side stream forks once per residual BLOCK (overlap_wgrad 3; first from 50
         # GFLOP of forward conv work up, TinyImageNet and ImageNet) -- with the deferred launch and lazy joins below
         # that fills the windows where the batched side stream waited for its next fork: headline
         # 16,755-16,865 vs 16,709-16,731, TinyImageNet 100.4-100.8k vs 99.4k img/s (CIFAR neutral at
@@ -268,31 +268,25 @@ class ResNetProgram:
         # (late in round 5, with the block tails on the main stream and the downsample forward on the side
         # stream, the CIFAR class gains too: 267.4-267.8k vs 262.3-263.0k img/s, profiles/r5_side_defer/
         # cifar_late.txt -- the per-block default now covers every step size)
-        self.side_block_default = ("DBX_OVERLAP_WGRAD" not in os.environ and not self.fuse_stem_bwd
-                                   and self.overlap_wgrad)
+        self.side_block_default = ow is None and not self.fuse_stem_bwd and self.overlap_wgrad
         if self.side_block_default:
             self.side_block, self.side_batch = True, False
-        self.coeff_in = (os.environ["DBX_COEFF_IN"] == "1" if "DBX_COEFF_IN" in os.environ
-                         else fl < 5e11 and self.nshard <= 4)
-        mc = os.environ.get("DBX_COEFF_IN_MAXC")
-        self.coeff_in_maxc = ((int(mc) or None) if mc else (None if fl < 5e10 else 512))
+        self.coeff_in = cfg.coeff_in if cfg.coeff_in is not None else (pol.small(fl) and self.nshard <= 4)
+        mc = cfg.coeff_in_maxc
+        self.coeff_in_maxc = (mc or None) if mc is not None else (None if pol.tiny(fl) else 512)
         # split-K weight-gradient reductions of a side-stream batch deferred to two launches at its end
         # (K.ReduceBatch; 19 reduce launches per CIFAR step): on for the smallest steps (< 50 GFLOP),
         # CIFAR 252.7-253.8k vs 243.7-245.5k img/s; TinyImageNet loses (93.3-93.8k vs 95.4k: its
         # larger slabs leave L2 before the batch-end reduce), profiles/r4_s12/
-        self.defer_reduce = (os.environ["DBX_DEFER_REDUCE"] == "1" if "DBX_DEFER_REDUCE" in os.environ
-                             else self.fwd_conv_flops() < 5e10)
-        # (DBX_DEFER_MAX_MB: only gradients with at most this many MB of slabs are deferred; unset: all)
-        mb = os.environ.get("DBX_DEFER_MAX_MB")
-        self.defer_max_bytes = int(float(mb) * (1 << 20)) if mb else None
+        self.defer_reduce = cfg.defer_reduce if cfg.defer_reduce is not None else pol.tiny(fl)
         self.wred_arena = torch.empty(0, device=device, dtype=torch.float32)
         self._wred_off = 0
         if not self.overlap_wgrad:
             # without the side stream folding costs no overlap: fold every BN-backward apply it can
             # (unless set explicitly) -- CIFAR b256 193.7k vs 189.5k img/s with overlap (r3s2_knobs)
-            if "DBX_FOLD_MIN_ELEMS" not in os.environ:
+            if cfg.fold_min_elems is None:
                 self.fold_min = 0
-            if "DBX_FOLD_MAX_RATIO" not in os.environ:
+            if cfg.fold_max_ratio is None:
                 self.fold_max_ratio = 8.0
         self._alloc_params()
         self._alloc_activations()
@@ -542,92 +536,66 @@ class ResNetProgram:
         # The step's exposed end (tools/step_timeline.py): after the last data gradient only the side
         # stream's last batch (layer1's weight gradients) and the stem weight gradient behind it run.
         # Small steps (< 0.5 TFLOP of forward conv work) run the stem weight gradient on the main stream
-        # beside that batch (DBX_STEM_WG_MAIN; CIFAR 257.0-257.6k vs 252.1-253.8k, TinyImageNet 96.7-96.8k
+        # beside that batch (stem_wg_main; CIFAR 257.0-257.6k vs 252.1-253.8k, TinyImageNet 96.7-96.8k
         # vs 96.0-96.1k img/s; the b1024 headline loses 0.3 %: 16.48-16.49k vs 16.53-16.55k), and the
         # TinyImageNet class (50-500 GFLOP) also moves the batch's last two gradients to the main
-        # stream's end (DBX_TAIL_MAIN, their own workspace of ws's size: the same split depths, the same
+        # stream's end (tail_main, their own workspace of ws's size: the same split depths, the same
         # bits): 97.5-97.8k img/s; CIFAR loses with it (profiles/r5_tail/)
-        fl = self.fwd_conv_flops()
-        # DBX_SIDE_DEFER: launch each side batch after the main stream's next kernel (see _flush_side).
+        fl = self.fwd_flops
+        cfg, pol = self.cfg, self.cfg.policy
+        # side_defer: launch each side batch after the main stream's next kernel (see _flush_side).
         # Default: on for the small steps (< 0.5 TFLOP of forward conv work: CIFAR +0.7 %, TinyImageNet
         # neutral), off for the b1024 headline (-0.4 % / neutral); the multi-rank one-graph step turns it
         # on (its collectives ride the side stream: TinyImageNet +2.8 %, CIFAR +5 %, profiles/r5_side_defer/)
-        self.side_defer = (os.environ["DBX_SIDE_DEFER"] == "1" if "DBX_SIDE_DEFER" in os.environ
-                           else fl < 5e11 or self.side_block)
-        # DBX_SIDE_CU_RESERVE: side-stream weight gradients sized to one round over all but N CUs, so
+        self.side_defer = cfg.side_defer if cfg.side_defer is not None else (pol.small(fl) or self.side_block)
+        # side_cu_reserve: side-stream weight gradients sized to one round over all but N CUs, so
         # the main chain's small kernels find a CU (the BN-backward coefficient launches took 4.9 us alone
         # and 26.5 us beside the weight gradients); default 128 from the TinyImageNet class up (64: headline
         # +0.8 %, TinyImageNet +0.6-0.9 %; re-swept with the per-block forks and main-stream tails, 128 over
         # 64: TinyImageNet +1.8 %, headline +0.4 %; 160+ loses), 0 for the CIFAR class (64: -0.4 %, 128:
         # -1 %): profiles/r5_cu_reserve/
-        self.side_cu_reserve = int(os.environ["DBX_SIDE_CU_RESERVE"] if "DBX_SIDE_CU_RESERVE" in os.environ
-                                   else (128 if fl >= 5e10 else 0))
+        self.side_cu_reserve = (cfg.side_cu_reserve if cfg.side_cu_reserve is not None
+                                else (0 if pol.tiny(fl) else 128))
         # (with the per-block forks from 500 GFLOP up, together with two of the last block's weight
         # gradients: headline +0.38 % over five interleaved rounds, profiles/r5_side_defer/block_tail.txt)
-        self.stem_wg_main = (os.environ["DBX_STEM_WG_MAIN"] == "1" if "DBX_STEM_WG_MAIN" in os.environ
-                             else fl < 5e11 or self.side_block)
+        self.stem_wg_main = cfg.stem_wg_main if cfg.stem_wg_main is not None else (pol.small(fl) or self.side_block)
         # (with the deferred launch the TinyImageNet class moves three: 99.7-100.4k vs 99.0-99.6k img/s)
-        self.tail_main = int(os.environ["DBX_TAIL_MAIN"] if "DBX_TAIL_MAIN" in os.environ
-                             else ((3 if self.side_defer else 2) if 5e10 <= fl < 5e11 else 0))
-        self.seg_tail_main = int(os.environ.get("DBX_SEG_TAIL_MAIN", "0"))
+        self.tail_main = (cfg.tail_main if cfg.tail_main is not None
+                          else ((3 if self.side_defer else 2) if pol.mid(fl) else 0))
         # the fused conv3 backward's persistent grid spans only this many CUs, so the side stream's weight
-        # gradients keep theirs (DBX_DWF_CUS; 0 = all): TinyImageNet class 128 (+0.3 %), the headline
+        # gradients keep theirs (dwf_cus; 0 = all): TinyImageNet class 128 (+0.3 %), the headline
         # loses with any span (-0.9 % at 192), profiles/r5_side_defer/tiny_knobs_late.txt
-        self.dwf_cus = int(os.environ.get("DBX_DWF_CUS", "128" if 5e10 <= fl < 5e11 else "0"))
-        # the same as DBX_TAIL_MAIN for the per-block side forks (DBX_OVERLAP_WGRAD=3): the last block's
+        self.dwf_cus = cfg.dwf_cus if cfg.dwf_cus is not None else (128 if pol.mid(fl) else 0)
+        # the same as tail_main for the per-block side forks (overlap_wgrad 3): the last block's
         # last N weight gradients (TinyImageNet at the 128-CU reservation: 2 over 1 +0.4 % in five of five
         # interleaved rounds; headline +0.38 % with the stem's, profiles/r5_side_defer/block_tail.txt)
-        self.block_tail_main = int(os.environ.get("DBX_BLOCK_TAIL_MAIN", "2"))
+        self.block_tail_main = cfg.block_tail_main
         self._main_tail = []
-        # layer1 (the last batch, exposed at the end of the step) forks its weight gradients per block
-        # instead of once at the segment's end, so they start under layer1's own remaining data
-        # gradients; the join at layer1's end then waits only for layer2's batch (an event recorded
-        # behind it), the final join for everything (DBX_LAST_SEG_BLOCKS)
-        self.last_seg_blocks = os.environ.get("DBX_LAST_SEG_BLOCKS", "0") == "1"
         self._join_evt = None
-        self._after_evt = False
-        # set by the multi-rank trainer when its collectives share the side stream (DBX_COMM_SIDE):
+        # set by the multi-rank trainer when its collectives share the side stream (comm_side):
         # every segment join then waits for the event behind the segment's batch, not for the
         # collectives queued behind it on the same stream (the final join waits for everything)
         self.event_joins = False
-        self.ds_branch = int(os.environ.get("DBX_DS_BRANCH", "0"))
-        # DBX_SIDE_REV=1: each side batch's weight gradients in reverse queue order
-        self.side_rev = os.environ.get("DBX_SIDE_REV", "0") == "1"
         # the downsample conv's forward beside conv2 / conv3 on the side stream: +0.24 % on the headline
         # over five interleaved rounds, TinyImageNet neutral alone and +0.67 % with its block tail of one,
         # CIFAR +0.6 % (profiles/r5_side_defer/ds_fwd.txt, block_tail.txt, cifar_late.txt)
-        self.ds_fwd_side = os.environ.get("DBX_DS_FWD_SIDE", "1") == "1"
-        # (... only for downsample outputs of at most this size: DBX_DS_FWD_SIDE_MAX_HW)
-        self.ds_fwd_side_max_hw = int(os.environ.get("DBX_DS_FWD_SIDE_MAX_HW", str(1 << 30)))
-        # (DBX_DS_FWD_EARLY: fork it before conv1 when the block input is already in memory)
-        self.ds_fwd_early = os.environ.get("DBX_DS_FWD_EARLY", "0") == "1"
-        self._ds_stream = None
-        # DBX_LAZY_JOIN: no intermediate joins of the batched side stream -- every side batch reads only
+        self.ds_fwd_side = cfg.ds_fwd_side
+        # lazy_join: no intermediate joins of the batched side stream -- every side batch reads only
         # its own segment's per-block buffers (never reused within a step) and the workspaces of the main
         # stream's weight gradients are separate, so only the final join (before the optimizer) orders
         # the two; not with collectives on their own stream (they wait on the main stream at the joins)
         # (default: the CIFAR class, < 50 GFLOP of forward conv work, +1.2 %; TinyImageNet -0.3 %, the
         # headline -0.5 %: profiles/r5_side_defer/lazy_join.txt)
-        self.lazy_join = (os.environ["DBX_LAZY_JOIN"] == "1" if "DBX_LAZY_JOIN" in os.environ
-                          else self.fwd_conv_flops() < 5e10 or self.side_block)
+        self.lazy_join = cfg.lazy_join if cfg.lazy_join is not None else (pol.tiny(fl) or self.side_block)
         self._pending_side = []
         # the stem weight gradient's own slabs when it runs on the main stream (its split count depends
         # on the grid, not on the workspace capacity)
         self.ws_stem = (torch.empty(40 << 20, device=dev, dtype=torch.float32)
                         if dev.type == "cuda" and self.stem_wg_main else self.ws)
         # (not tied to the batched layout: the multi-rank trainer may switch a per-block default back to it)
-        self.ws_main = (torch.empty_like(self.ws) if ((self.tail_main > 0 or self.seg_tail_main > 0
-                                                      or self.block_tail_main > 0) and dev.type == "cuda"
+        self.ws_main = (torch.empty_like(self.ws) if ((self.tail_main > 0 or self.block_tail_main > 0)
+                                                      and dev.type == "cuda"
                                                        and self.overlap_wgrad) else self.ws)
-        # per-conv tile counters of the in-launch split-K reduction (K.conv_wgrad cnt=): zeroed once,
-        # every launch leaves them zero again; keyed by the gradient view's address
-        body = [cv for cv in self.convs if not cv.stem]
-        sizes = [K.wgrad_tiles_max(cv.OC, cv.R * cv.S * cv.IC) for cv in body]
-        self.wg_cnt = torch.zeros(max(1, sum(sizes)), device=dev, dtype=torch.int32)
-        self._wg_cnt_of, pos = {}, 0
-        for cv, n in zip(body, sizes):
-            self._wg_cnt_of[cv.grad.data_ptr()] = self.wg_cnt[pos:pos + n]
-            pos += n
         # the fused conv3 backward runs on the main stream while side-stream weight gradients use
         # self.ws: its per-workgroup slabs get their own workspace (<= 1024 slabs + 64 partials)
         fused = [b.convs[-1] for i, b in enumerate(self.blocks) if self._fuse3(b, i == len(self.blocks) - 1)]
@@ -805,7 +773,7 @@ class ResNetProgram:
         K.maxpool_fwd(self.y0, self.p0, self.parg, K=self.pool_k, stride=self.pool_s, pad=self.pool_p,
                       scale=sbn.scale, shift=sbn.shift, relu=True, ymax=self.pymax if tr else None, fin=sfin)
         x = self.p0
-        # DBX_DS_FWD_SIDE: a downsample conv reads only the block input (written by the block's conv1
+        # ds_fwd_side: a downsample conv reads only the block input (written by the block's conv1
         # tail prologue): it runs on the side stream beside conv2 / conv3, launched like a deferred side
         # batch after the main stream's next kernel, joined at the block's end
         ds_launch = {} if (self.ds_fwd_side and tr and self.dev.type == "cuda" and self.overlap_wgrad) else None
@@ -814,12 +782,6 @@ class ResNetProgram:
         for bi, b in enumerate(self.blocks):
             prev_bn = None
             deferred = None  # BN of conv i-1 whose finalize conv i's prologue performs (fin_in)
-            # (a block input already in memory -- the stem's pooled output -- forks its downsample conv
-            # before conv1; otherwise conv1's tail prologue writes it and the fork follows conv1)
-            early_ds = (self.ds_fwd_early and pending is None and ds_launch is not None and b.ds_conv is not None
-                        and b.ds_conv.OH <= self.ds_fwd_side_max_hw)
-            if early_ds:
-                ds_launch[bi] = self._ds_fwd_on_side(b, x, N)
             for i, cv in enumerate(b.convs):
                 if i == 0 and pending is not None:
                     pb, res, rsc, rsh, pfin, prfin = pending
@@ -841,8 +803,9 @@ class ResNetProgram:
                                in_shift=prev_bn.shift if prev_bn else None, relu_in=True,
                                fin=self._ff(b.bns[i]), fin_in=deferred.fin_f if deferred is not None else None)
                 deferred = None
-                if (i == 0 and not early_ds and ds_launch is not None and b.ds_conv is not None
-                        and b.ds_conv.OH <= self.ds_fwd_side_max_hw):
+                # (the fork follows conv1, whose tail prologue writes the block input; forking before
+                # conv1 where the input is already in memory measured neutral in round 5)
+                if i == 0 and ds_launch is not None and b.ds_conv is not None:
                     ds_launch[bi] = self._ds_fwd_on_side(b, x, N)
                 nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
                 c1 = nxt.convs[0] if nxt is not None else None
@@ -935,10 +898,8 @@ class ResNetProgram:
         segs.append(("head", self._bwd_head))
         for li in (4, 3, 2, 1):
             idx = list(reversed(stages[li]))
-            per_block = li == 1 and self.last_seg_blocks
-            segs.append((f"layer{li}", (lambda idx=idx, pb=per_block, li=li: [
-                (self._bwd_block(i), self._block_flush(li == 1 and j == len(idx) - 1),
-                 self._seg_block_flush(pb and j < len(idx) - 1))
+            segs.append((f"layer{li}", (lambda idx=idx, li=li: [
+                (self._bwd_block(i), self._block_flush(li == 1 and j == len(idx) - 1))
                 for j, i in enumerate(idx)])))
         segs.append(("stem", self._bwd_stem))
         # every segment ends with its weight gradients complete on the main stream (join)
@@ -969,12 +930,8 @@ class ResNetProgram:
         self._side_pending = True
 
     def _wgrad(self, *args, **kw):
-        if self.fuse_wgrad_reduce:
-            kw["cnt"] = self._wg_cnt_of.get(args[2].data_ptr())
-        if self.wgrad_lds_pad and self.dev.type == "cuda" and self.overlap_wgrad:
-            kw["lds_pad"] = self.wgrad_lds_pad  # occupancy cap: leave room for the main stream's kernels
         if self.side_cu_reserve and self.dev.type == "cuda" and self.overlap_wgrad:
-            kw["cu_reserve"] = self.side_cu_reserve  # one round over all but N CUs (DBX_SIDE_CU_RESERVE)
+            kw["cu_reserve"] = self.side_cu_reserve  # one round over all but N CUs (side_cu_reserve)
         # (a queued weight gradient takes the batch's deferred-reduction list when it is launched)
         # (ws: the workspace override of a gradient moved to the main stream's tail, see _join_side)
         self._side(lambda batch=None, ws=None: K.conv_wgrad(*args[:3], args[3] if ws is None else ws, *args[4:],
@@ -992,7 +949,7 @@ class ResNetProgram:
         self.launch_pending()  # (at most one deferred batch)
         if self._wstream is None:
             self._wstream = torch.cuda.Stream(device=self.dev)
-        q = self._side_q[::-1] if self.side_rev else self._side_q
+        q = self._side_q
         self._side_q = []
         self._side_pending = True
         main = torch.cuda.current_stream(self.dev)
@@ -1007,8 +964,7 @@ class ResNetProgram:
             if fork is not None:
                 self._wstream.wait_event(fork)
             # (each batch of a step takes an arena region of its own)
-            batch = (K.ReduceBatch(self.wred_arena, self._wred_off, self.defer_max_bytes) if self.defer_reduce
-                     else None)
+            batch = K.ReduceBatch(self.wred_arena, self._wred_off) if self.defer_reduce else None
             with torch.cuda.stream(self._wstream):
                 for fn in q:
                     if batch is not None and getattr(fn, "__defaults__", None):
@@ -1063,7 +1019,7 @@ class ResNetProgram:
 
     def _block_flush(self, last: bool = False):
         if self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
-            # the step's last block: its last DBX_BLOCK_TAIL_MAIN weight gradients run on the main stream after
+            # the step's last block: its last block_tail_main weight gradients run on the main stream after
             # the stem's backward (their own workspace) instead of behind the rest on the side stream
             n = self.block_tail_main if last else 0
             if n > 0 and len(self._side_q) > n:
@@ -1076,11 +1032,6 @@ class ResNetProgram:
         if self._wstream is None:
             self._wstream = torch.cuda.Stream(device=self.dev)
         return self._wstream
-
-    def _seg_block_flush(self, on: bool):
-        if on and self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad:
-            self._flush_side()  # (DBX_LAST_SEG_BLOCKS: this block's weight gradients now, behind the batch)
-            self._after_evt = True
 
     def _join_side(self, final: bool = True, tail_main: bool = False):
         if self.side_batch and self.dev.type == "cuda" and self.overlap_wgrad:
@@ -1095,37 +1046,35 @@ class ResNetProgram:
                 self._main_tail = []
             self.launch_pending()
             if self._side_pending and self.lazy_join and not final:
-                pass  # (DBX_LAZY_JOIN: the final join below waits for everything)
+                pass  # (lazy_join: the final join below waits for everything)
             elif self._side_pending:
                 if self._join_evt is not None:  # the previous batch only, not the blocks flushed since
                     torch.cuda.current_stream(self.dev).wait_event(self._join_evt)
-                    self._side_pending = self._after_evt or self.event_joins  # (collectives behind it)
+                    self._side_pending = self.event_joins  # (collectives behind it)
                 else:
                     torch.cuda.current_stream(self.dev).wait_stream(self._wstream)
                     self._side_pending = False
             self._join_evt = None
             # the LAST batch (layer1) is exposed at the end of the step: only the stem's short backward
-            # runs beside it -- its last DBX_TAIL_MAIN gradients go to the main stream's end instead
-            # (their own workspace); DBX_SEG_TAIL_MAIN does the same for the middle batches (a batch the
-            # side stream cannot finish within the next segment makes the main stream wait at the join)
-            n = self.tail_main if tail_main else (0 if final else self.seg_tail_main)
+            # runs beside it -- its last tail_main gradients go to the main stream's end instead
+            # (their own workspace)
+            n = self.tail_main if tail_main else 0
             if n > 0 and len(self._side_q) > n:
                 self._main_tail = self._side_q[-n:]
                 self._side_q = self._side_q[:-n]
-            want = (self.last_seg_blocks or self.event_joins) and not final
+            want = self.event_joins and not final
             evt = torch.cuda.Event() if want else None
             if self._flush_side(join_evt=evt):
                 self._join_evt = evt
             elif want and self._side_pending:
                 self._join_evt = torch.cuda.Event()
                 self._join_evt.record(self._wstream)
-            self._after_evt = False
             if not final:
                 return
         elif self.side_block and self.dev.type == "cuda" and self.overlap_wgrad:
             self._flush_side()  # (the stem / head segments queue theirs here), joined below
             if self.lazy_join and not final:
-                return  # (DBX_LAZY_JOIN: per-block batches too, joined only at the end)
+                return  # (lazy_join: per-block batches too, joined only at the end)
             if final and self._main_tail:
                 for fn in self._main_tail:  # (see _block_flush)
                     fn(None, self.ws_main)
@@ -1147,7 +1096,7 @@ class ResNetProgram:
 
     def _cin(self, bn, count=None) -> bool:
         """Does ``bn``'s next BN-backward apply pass finalize the coefficients inside its launch
-        (DBX_COEFF_IN: no bn_bwd_coeff launch in front of it)?"""
+        (coeff_in: no bn_bwd_coeff launch in front of it)?"""
         f = bn.fin_b
         return (self.coeff_in and f is not None and f.desc is not None
                 and (self.coeff_in_maxc is None or bn.C <= self.coeff_in_maxc)
@@ -1196,7 +1145,7 @@ class ResNetProgram:
             g = self.blocks[i + 1].dx
         # backward finalizes still to run for the tail BNs (else finished by block i+1's conv1 dgrad
         # epilogue): run standalone before a consumer that reads the coefficients from memory, or
-        # handed to the apply pass that consumes them (DBX_COEFF_IN)
+        # handed to the apply pass that consumes them (coeff_in)
         todo = {} if last else ({id(lbn): (lbn, cnt_last)} if not self._fused_fin(lbn) else {})
 
         def ready(bn):  # the coefficients are in memory before the next launch
@@ -1239,45 +1188,8 @@ class ResNetProgram:
             else:
                 K.bn_bwd_apply(g, b.ys[-1], lbn.coeff, b.dys[-1], mask_mode=K.MASK_NONE, fin=fin_of(lbn))
         assert not todo, "a tail BN's backward finalize was left pending"
-        # DBX_DS_BRANCH: the downsample conv's data gradient depends only on the block-output gradient
-        # (and its BN-backward apply): run it on a branch stream beside the inner convs' data gradients,
-        # joined right before conv1's dgrad consumes it as the shortcut gradient
-        # (1: its own stream -- a third graph branch, which the runtime's queue mapping handles badly;
-        # 2: the weight-gradient side stream, launched like a deferred side batch after the main
-        # stream's next kernel)
-        ds_evt = None
-        if b.ds_conv is not None and self.ds_branch and self.dev.type == "cuda" and self.overlap_wgrad:
-            dc = b.ds_conv
-
-            def ds_dgrad():
-                if ds_fold is None:
-                    K.conv_dgrad(b.dyd, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0)
-                else:
-                    K.conv_dgrad(g, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0, **ds_fold)
-            ds_evt = torch.cuda.Event()
-            if self.ds_branch == 1:
-                if self._ds_stream is None:
-                    self._ds_stream = torch.cuda.Stream(device=self.dev)
-                self._ds_stream.wait_stream(torch.cuda.current_stream(self.dev))
-                with torch.cuda.stream(self._ds_stream):
-                    ds_dgrad()
-                ds_evt.record(self._ds_stream)
-            else:
-                side = self.side_stream()
-                fork = torch.cuda.Event()
-                fork.record(torch.cuda.current_stream(self.dev))
-
-                def launch_ds():
-                    side.wait_event(fork)
-                    with torch.cuda.stream(side):
-                        ds_dgrad()
-                    ds_evt.record(side)
-                self._side_pending = True
-                if self._pending_side:
-                    self._pending_side.append(launch_ds)
-                else:
-                    self._pending_side = [launch_ds]
-                    K.set_post_launch(self.launch_pending)
+        # (the downsample conv's data gradient on a branch / the side stream beside the inner convs'
+        # measured neutral or slower in round 5 and was removed: profiles/r5_side_defer/)
         # inner convs, last to second: dgrad epilogue masks with the previous BN's ReLU and
         # accumulates that BN's backward statistics
         for j in range(nconv - 1, 0, -1):
@@ -1330,11 +1242,7 @@ class ResNetProgram:
             self._wgrad(b.dys[0], x, c0.grad, self.ws, R=c0.R, S=c0.S, stride=c0.stride, pad=c0.pad)
         if b.ds_conv is not None:
             dc = b.ds_conv
-            if ds_evt is not None:  # (dgrad on the branch stream above: join it; the wgrad follows)
-                self.launch_pending()
-                torch.cuda.current_stream(self.dev).wait_event(ds_evt)
-                self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
-            elif ds_fold is None:
+            if ds_fold is None:
                 self._wgrad(b.dyd, x, dc.grad, self.ws, R=dc.R, S=dc.S, stride=dc.stride, pad=dc.pad)
                 # 1x1 strided downsample: its dgrad is a dense GEMM onto the stride-subsampled pixels
                 K.conv_dgrad(b.dyd, dc.wt16, b.dsbuf, R=1, S=1, stride=1, pad=0)
@@ -1366,10 +1274,10 @@ class ResNetProgram:
         return sum(2.0 * self.N * cv.OH * cv.OW * cv.OC * cv.R * cv.S * cv.IC for cv in self.convs)
 
     def _materialize(self, cv: ConvL) -> bool:
-        """Does conv ``cv`` (a block-internal 3x3, or with DBX_FAST_MAT1 a bottleneck conv3) take a
+        """Does conv ``cv`` (a block-internal 3x3) take a
         materialised BN output on the eight-wave kernel?"""
         if not (self.fast_mat and self.dev.type == "cuda" and cv.stride == 1
-                and (cv.R == 3 or (cv.R == 1 and self.fast_mat1 and cv.OH <= self.fast_mat1_max_hw))):
+                and cv.R == 3):
             return False
         t = K.pick_tile(self.N * cv.OH * cv.OW, cv.OC, "fwd0", cv.IC, cv.R, cv.stride)
         return len(t) > 2 and t[2] in (4, 5)

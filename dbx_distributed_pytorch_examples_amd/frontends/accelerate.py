@@ -9,7 +9,7 @@ tracker (``log_with="mlflow"``). bf16 autocast is enabled by ``mixed_precision="
 On a GPU, ``prepare`` puts a supported ResNet (the notebook's ``resnet50`` with a new ``fc``,
 `04_accelerate/01_cifar_accelerate.ipynb:475-503`) on the native HIP kernels by default:
 :func:`~dbx_distributed_pytorch_examples_amd.engine.native_module.native_module` compiles it for
-the first training batch's shape (``DBX_ACCELERATE_NATIVE=0`` or ``mixed_precision="no"`` keep the
+the first training batch's shape (engine field ``native_frontends=0`` or ``mixed_precision="no"`` keep the
 stock module). The Parameter objects do not change, so the optimizer the notebook built before
 ``prepare`` keeps stepping the live weights; the module all-reduces its own gradient per backward
 segment, overlapped with the backward, so it is not wrapped in DDP. A model already wrapped by
@@ -30,6 +30,7 @@ from ..parallel import dist as ddist
 from ..parallel.ddp import DistributedDataParallel, unwrap
 from ..parallel.sampler import ShardSampler
 from ..utils import mlflow_compat as mlflow
+from ..engine_config import EngineConfig
 
 
 def set_seed(seed: int) -> None:
@@ -169,7 +170,7 @@ class Accelerator:
             if isinstance(obj, NativeResNet):
                 return obj  # on the device already; gradients all-reduced by its own backward
             if (self.device.type == "cuda" and self.mixed_precision == "bf16" and supports(obj)
-                    and os.environ.get("DBX_ACCELERATE_NATIVE", "1") != "0"):
+                    and EngineConfig.current().native_frontends):
                 return native_module(obj, None, None, self.device)  # compiled for the first batch
             m = obj.to(self.device)
             if self.device.type == "cuda":

@@ -11,7 +11,7 @@ On GPUs a ``ComposerResNet50`` trains on the native HIP program at any world siz
 is wrapped by ``engine.native_module`` for the train loader's batch size and image size (CutMix's
 soft targets and label smoothing stay torch ops on the logits; other batch sizes run the torch
 module on the same parameters); at world > 1 the wrapped program averages its own gradients per
-backward segment (overlapped with the backward), so the trainer's DDP only passes them through. ``DBX_COMPOSER_NATIVE=0`` keeps the stock module (2.5x slower at the notebook's
+backward segment (overlapped with the backward), so the trainer's DDP only passes them through. The engine field ``native_frontends=0`` keeps the stock module (2.5x slower at the notebook's
 b128 CIFAR shape, ``profiles/r2s5_native_module/``).
 """
 from __future__ import annotations
@@ -24,6 +24,7 @@ import torch.nn as nn
 from ..config import parse_duration
 from ..parallel import dist as ddist
 from ..utils import mlflow_compat as mlflow
+from ..engine_config import EngineConfig
 
 
 class Algorithm:
@@ -104,7 +105,7 @@ class Trainer:
         from ..engine.native_module import native_module
         from ..engine.program import supports
         from ..models.wrappers import ComposerResNet50
-        if (os.environ.get("DBX_COMPOSER_NATIVE", "1") == "0" or self.info.device.type != "cuda"
+        if (not EngineConfig.current().native_frontends or self.info.device.type != "cuda"
                 or not isinstance(model, ComposerResNet50)):
             return model
         bs = getattr(dl, "batch_size", None)

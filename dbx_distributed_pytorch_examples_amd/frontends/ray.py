@@ -24,6 +24,7 @@ from ..launch import Launcher, LaunchError
 from ..parallel import dist as ddist
 from ..parallel.ddp import DistributedDataParallel
 from ..parallel.sampler import ShardSampler
+from ..engine_config import EngineConfig
 
 
 @dataclass
@@ -113,10 +114,10 @@ def prepare_model(model: torch.nn.Module, native_batch: Optional[int] = None, na
     supported ResNet runs the worker's own loop on the native HIP program by default
     (``engine.native_module``, compiled for the first training batch's shape unless ``native_batch``
     / ``native_hw`` fix it; its backward averages the gradients per segment, overlapped with the
-    backward; ``native_batch=0`` or ``DBX_RAY_NATIVE=0`` opt out). Otherwise the model is moved to
+    backward; ``native_batch=0`` or the engine field ``native_frontends=0`` opt out). Otherwise the model is moved to
     the device and wrapped in the flat-bucket DDP at world > 1."""
     info = ddist.init_distributed(device="cpu" if os.environ.get("DBX_FORCE_CPU") == "1" else None)
-    if (native_batch != 0 and info.device.type == "cuda" and os.environ.get("DBX_RAY_NATIVE", "1") != "0"):
+    if (native_batch != 0 and info.device.type == "cuda" and EngineConfig.current().native_frontends):
         from ..engine.native_module import native_module
         from ..engine.program import supports
         if supports(model):

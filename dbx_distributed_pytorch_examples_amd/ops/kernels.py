@@ -20,6 +20,9 @@ import torch
 from ..utils import debug as _debug
 from . import reference as _ref
 from ._ext import C, stream_ptr, use_native
+from ..engine_config import EngineConfig
+
+_E = EngineConfig.current  # kernel-selection switches (engine_config.py; DBX_ENGINE overrides)
 
 FWD, DGRAD, STEM, FWD_PATCH, DGRAD_PATCH = 0, 1, 2, 3, 4
 # addsrc, add_sub, epi, mbits, ybn, ybn2, bsc, bsh, mean1, inv1, mean2, inv2, bstats1, bstats2
@@ -176,10 +179,9 @@ def _tune_table():
     if _TUNE is None:
         import json
         import os
-        p = os.environ.get("DBX_TUNE_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                            "tune_table.json")
+        p = _E().tune_table or os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune_table.json")
         _TUNE = {}
-        modes = os.environ.get("DBX_TUNE_MODES", "all").split(",")  # e.g. "none", "fwd,dgrad2"
+        modes = _E().tune_modes.split(",")  # e.g. "none", "fwd,dgrad2"
         if os.path.exists(p):
             with open(p) as f:
                 _TUNE = {k: tuple(v) for k, v in json.load(f).items() if "all" in modes or k.split(":")[0] in modes}
@@ -201,7 +203,7 @@ def pick_tile(M: int, OC: int, mode: str = "fwd", K_in: int = 0, R: int = 0, str
             if t is not None and len(t) > 2 and t[2] in (4, 5) and mode != "fwd0":
                 t = None  # an eight-wave (plain operand) entry does not serve the prologue variants
         if t is not None and len(t) > 2 and t[2] in (4, 5) and not _fast_enabled():
-            t = None  # DBX_FAST=0: no eight-wave kernel (A/B runs)
+            t = None  # fast=0: no eight-wave kernel (A/B runs)
         if t is not None and OC % t[1] == 0:
             return t  # (bm, bn) or (bm, bn, dma): a measured operand path (tools/tune_conv.py)
     if OC % 128 == 0 and ((M + 127) // 128) * (OC // 128) >= 512:
@@ -211,35 +213,26 @@ def pick_tile(M: int, OC: int, mode: str = "fwd", K_in: int = 0, R: int = 0, str
     return 64, 64
 
 
-_DMA_ENV = None
-_FAST_ENV = None
 
 
 def _fast_enabled() -> bool:
-    """DBX_FAST (default 1): use the eight-wave kernel entries of the tune table (csrc/conv_fast.hip)."""
-    global _FAST_ENV
-    if _FAST_ENV is None:
-        import os
-        _FAST_ENV = os.environ.get("DBX_FAST", "1") != "0"
-    return _FAST_ENV
+    """``fast`` (default on): use the eight-wave kernel entries of the tune table (csrc/conv_fast.hip)."""
+    return _E().fast
 
 
 def _tile_dma(t) -> Tuple[int, int, int]:
     """(bm, bn[, dma]) -> (bm, bn, dma). ``dma`` is the conv operand path (conv_igemm_kernel.h):
     0 register-staged, 1 weights by LDS-DMA (prologue convs), 2 / 3 both operands by LDS-DMA
     through a 2- / 3-slot ring of 64-channel stages, 6 through a 4-slot ring of 32-channel stages
-    (4 / 5: the eight-wave kernel; 7: the row-tile kernel of 1x1 stride-1 BN-prologue forwards and
-    folded dgrads, csrc/conv_rowtile.hip -- bm / bn are its own). DBX_CONV_DMA overrides every choice (A/B runs)."""
-    global _DMA_ENV
-    if _DMA_ENV is None:
-        import os
-        _DMA_ENV = int(os.environ.get("DBX_CONV_DMA", "-1"))
-    if _DMA_ENV >= 0:
-        return int(t[0]), int(t[1]), _DMA_ENV
+    (4 / 5: the eight-wave kernel; 7 was a row-tile kernel of the 1x1 BN-prologue forwards, measured
+    slower in round 4 and removed in round 6). The engine's ``conv_dma`` overrides every
+    choice (A/B runs)."""
+    forced = _E().conv_dma
+    if forced >= 0:
+        return int(t[0]), int(t[1]), forced
     return int(t[0]), int(t[1]), int(t[2]) if len(t) > 2 else 0
 
 
-_PATCH3 = None
 
 
 def patch3_supported(IC: int, OC: int, R: int, S: int, stride: int, pad: int, H: int, W: int) -> bool:
@@ -251,14 +244,10 @@ def patch3_supported(IC: int, OC: int, R: int, S: int, stride: int, pad: int, H:
 def _use_patch3(tile, mode: str) -> int:
     """0 = implicit GEMM, 1 = patch kernel with resident weights (one workgroup per CU), 2 = patch
     kernel with streamed weights (two workgroups per CU). tile "patch" / "patch_r" / "patch_s"
-    forces one, an explicit (bm, bn[, dma]) the implicit GEMM; otherwise DBX_PATCH3 ("all" default,
-    "fwd", "dgrad" or "0") picks the convs and DBX_PATCH3_STREAM ("dgrad" default, "fwd", "all",
+    forces one, an explicit (bm, bn[, dma]) the implicit GEMM; otherwise the engine's ``patch3`` ("all" default,
+    "fwd", "dgrad" or "0") picks the convs and ``patch3_stream`` ("dgrad" default, "fwd", "all",
     "0") the ones on the streamed-weights variant."""
-    global _PATCH3
-    if _PATCH3 is None:
-        import os
-        _PATCH3 = (os.environ.get("DBX_PATCH3", "all"), os.environ.get("DBX_PATCH3_STREAM", "dgrad"))
-    use, stream = _PATCH3
+    use, stream = _E().patch3, _E().patch3_stream
     kind = 2 if stream in ("all", mode) else 1
     if isinstance(tile, str):
         return {"patch": kind, "patch_r": 1, "patch_s": 2}.get(tile, 0)
@@ -382,16 +371,11 @@ def tail_supported(IC: int, R: int, S: int, stride: int, pad: int) -> bool:
     return R == 1 and S == 1 and stride == 1 and pad == 0 and IC <= 1024 and IC % 64 == 0
 
 
-_PRUNE = None
 
 
 def _prune() -> bool:
-    """DBX_TAP_PRUNE (default 1): conv launches skip the filter taps that only ever see padding."""
-    global _PRUNE
-    if _PRUNE is None:
-        import os
-        _PRUNE = os.environ.get("DBX_TAP_PRUNE", "1") != "0"
-    return _PRUNE
+    """``tap_prune`` (default on): conv launches skip the filter taps that only ever see padding."""
+    return _E().tap_prune
 
 
 def fwd_taps(IH: int, OH: int, R: int, stride: int, pad: int) -> Tuple[int, int]:
@@ -617,7 +601,7 @@ def stem_patch_supported(IH: int, IW: int, OC: int, R: int, S: int, stride: int,
 @_dispatch
 def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch=None):
     """Stem conv on the NHWC4 image: w16s [OC, 256] = (8 rows x 8 pixels x 4 channels).
-    ``patch``: the patch kernel (224-wide images) -- None = DBX_STEM_PATCH (default on)."""
+    ``patch``: the patch kernel (224-wide images) -- None = the engine's ``stem_patch`` (default on)."""
     N, IH, IW, C4 = x4.shape
     if C4 != 4:
         raise ValueError("stem expects NHWC4 input")
@@ -631,8 +615,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
     if R > 8 or S > 8:
         raise ValueError("stem kernel supports R,S <= 8")
     if patch is None:
-        import os
-        patch = os.environ.get("DBX_STEM_PATCH", "1") == "1"
+        patch = _E().stem_patch
     bm = 0 if patch and stem_patch_supported(IH, IW, OC, R, S, stride, pad) else 128  # bm 0: patch kernel
     C().conv_igemm(STEM, bm, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), _nsh(stats, OC),
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
@@ -640,45 +623,21 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
     return out
 
 
-_WG_ROUNDS = None
-_STEM_WGRAD = None
 
 
 def _stem_wgrad_tile() -> bool:
-    """DBX_STEM_WGRAD: "tile" (default) = the 64 x 256-tile stem weight gradient (csrc/stem_bwd.hip),
+    """``stem_wgrad``: "tile" (default) = the 64 x 256-tile stem weight gradient (csrc/stem_bwd.hip),
     "generic" = the wgrad kernel's STEM mode (two 128-column tiles; A/B switch)."""
-    global _STEM_WGRAD
-    if _STEM_WGRAD is None:
-        import os
-        _STEM_WGRAD = os.environ.get("DBX_STEM_WGRAD", "tile") == "tile"
-    return _STEM_WGRAD
-
-
-def _patch3_reserve() -> bool:
-    """DBX_PATCH3_RESERVE (default 0): the persistent 3x3 patch weight gradient honours cu_reserve too
-    (headline 16,601-16,639 with vs 16,620-16,653 img/s without: profiles/r5_cu_reserve/)."""
-    import os
-    return os.environ.get("DBX_PATCH3_RESERVE", "0") == "1"
-
-
-def _reserve_max_rounds() -> float:
-    """DBX_RESERVE_MAX_ROUNDS (default 1): workgroup rounds over the unreserved CUs of a weight
-    gradient launched with cu_reserve."""
-    import os
-    return float(os.environ.get("DBX_RESERVE_MAX_ROUNDS", "1"))
+    return _E().stem_wgrad == "tile"
 
 
 def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int,
                  rounds: Optional[float] = None, cus: Optional[int] = None) -> Tuple[int, int]:
     """Split the pixel reduction so that ``rounds`` rounds of workgroups stream over the CUs (>= 8
     K-blocks each); the workspace holds nsplit slabs + up to 64 level-1 partial slabs of the
-    reduction. ``rounds``: the tune table's per-shape value, else DBX_WGRAD_ROUNDS (2); 0 = no split
+    reduction. ``rounds``: the tune table's per-shape value, else the engine's ``wgrad_rounds`` (2); 0 = no split
     (one workgroup per tile over all M rows, the gradient written directly)."""
-    global _WG_ROUNDS
-    if _WG_ROUNDS is None:
-        import os
-        _WG_ROUNDS = float(os.environ.get("DBX_WGRAD_ROUNDS", "2"))
-    r = _WG_ROUNDS if rounds is None else float(rounds)
+    r = _E().wgrad_rounds if rounds is None else float(rounds)
     if r <= 0:
         return 1, max(64, (M + 63) // 64 * 64)
     tiles = (OC // bm) * (KTOT // bn)
@@ -694,17 +653,12 @@ def wgrad_splits(M: int, OC: int, KTOT: int, bm: int, bn: int, max_ws_elems: int
     return nsplit, ms
 
 
-_WG_FUSE_MAX = None
 
 
 def wgrad_fuse_max() -> int:
     """Largest per-tile slab volume (nsplit x BM x BN x 4 bytes) reduced inside the weight-gradient
-    launch by the tile's last block (DBX_WGRAD_FUSE_MAX bytes; 0 = always a separate reduce)."""
-    global _WG_FUSE_MAX
-    if _WG_FUSE_MAX is None:
-        import os
-        _WG_FUSE_MAX = int(os.environ.get("DBX_WGRAD_FUSE_MAX", str(1 << 20)))
-    return _WG_FUSE_MAX
+    launch by the tile's last block (``wgrad_fuse_max`` bytes; 0 = always a separate reduce)."""
+    return _E().wgrad_fuse_max
 
 
 def wgrad_tiles_max(OC: int, KTOT: int) -> int:
@@ -721,7 +675,7 @@ class ReduceBatch:
     bit-identical to ``wgrad_reduce`` in eager execution. A gradient whose slabs do not fit the
     arena's remainder is reduced at once (``need`` records the size the arena should grow to).
 
-    The program uses it for its smallest steps (engine/program.py ``_flush_side``, DBX_DEFER_REDUCE)."""
+    The program uses it for its smallest steps (engine/program.py ``_flush_side``, ``defer_reduce``)."""
 
     def __init__(self, arena: torch.Tensor, start: int = 0, max_slab_bytes: Optional[int] = None):
         self.arena, self.off, self.need, self.jobs = arena, start, start, []
@@ -770,7 +724,7 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
                rounds=None, defer: "ReduceBatch" = None, cu_reserve: int = 0):
     """dW[OC, R*S*IC] (fp32, KRSC) = sum_pixels dY^T * im2col(X) ; ws = fp32 workspace.
     ``dma``: operand path of the prologue-free kernels -- LDS-DMA ring depth 2 / 3, 0 = register
-    staged, -1 = the tune table's choice, else DBX_WGRAD_DMA, else 3 for 256-wide tiles / 2.
+    staged, -1 = the tune table's choice, else 3 for 256-wide tiles / 2.
     ``cnt``: zeroed int32 tile counters (>= wgrad_tiles_max(OC, KTOT), owned by this call site):
     when given and the split slabs of a tile are small (wgrad_fuse_max), the split-K reduction runs
     inside the launch (the last block of each tile sums its slabs, bit-identical to wgrad_reduce)
@@ -794,7 +748,7 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
             raise ValueError("wgrad workspace too small for the patch kernel")
         nsl = C().wgrad_patch3(dy.data_ptr(), x.data_ptr(), ws.data_ptr(), ws.numel(), N, IH, IW, IC, OH, OW, OC, R,
                                S, stride, pad, stream_ptr(),
-                               num_cus() - cu_reserve if cu_reserve > 0 and _patch3_reserve() else 0)
+                               0)  # (honouring cu_reserve here measured slower: profiles/r5_cu_reserve/)
         C().wgrad_reduce(ws.data_ptr(), dw.data_ptr(), OC * KTOT, nsl, float(scale), int(accumulate), stream_ptr())
         return dw
     if isinstance(tile, str):
@@ -837,8 +791,7 @@ def conv_wgrad(dy, x, dw, ws, *, R, S, stride, pad, in_scale=None, in_shift=None
         _chk(in_shift, torch.float32, "in_shift", IC)
     M = N * OH * OW
     if cu_reserve > 0:  # one round over all but cu_reserve CUs (the main stream's small kernels keep a place)
-        cap = _reserve_max_rounds()
-        rounds = min(cap, cap if rounds is None or rounds <= 0 else float(rounds))
+        rounds = min(1.0, 1.0 if rounds is None or rounds <= 0 else float(rounds))
     nsplit, ms = wgrad_splits(M, OC, KTOT, bm, bn, ws.numel(), rounds,
                               cus=num_cus() - cu_reserve if cu_reserve > 0 else None)
     if (nsplit + (min(64, nsplit) if nsplit > 8 else 0)) * OC * KTOT > ws.numel():
@@ -897,14 +850,13 @@ def dwfused_grid(C: int, K: int) -> int:
 
 def dwfused_preferred(C: int, K: int, M: int) -> bool:
     """Schedule policy: the fused conv3 backward only when every resident workgroup walks >=
-    DBX_FUSE_DW_MIN_TILES (default 4) tiles -- with fewer, the per-workgroup weight load and slab write
+    ``fuse_dw_min_tiles`` (default 4) tiles -- with fewer, the per-workgroup weight load and slab write
     and the lost wgrad side-stream overlap outweigh the saved traffic (TinyImageNet b512 fused at 2-4
     tiles per workgroup: 86.5k vs 87.2k img/s in round 2, profiles/r2s4_dwfused/; with the round-5
     per-block side forks and the 128-CU reservation its 4-tile layer1 conv3 gains: 104.3k vs 103.7k,
     2 tiles still loses: profiles/r5_side_defer/tiny_knobs_late.txt)."""
-    import os
     grid = dwfused_grid(C, K)
-    return dwfused_supported(C, K, M) and M >= int(os.environ.get("DBX_FUSE_DW_MIN_TILES", "4")) * grid * 64
+    return dwfused_supported(C, K, M) and M >= _E().fuse_dw_min_tiles * grid * 64
 
 
 @_dispatch
@@ -1203,7 +1155,7 @@ def head_splitk(M: int, N: int, K: int, ws_elems: int) -> int:
     TinyImageNet's batch 512 / 200 classes has 32) split K so ~256 workgroups run, >= 2 k-stages each."""
     tiles = -(-M // 64) * -(-N // 64)
     kst = -(-K // 128)
-    if os.environ.get("DBX_HEAD_SPLITK", "1") == "0" or tiles >= 192 or kst < 4 or ws_elems < 2 * M * N:
+    if not _E().head_splitk or tiles >= 192 or kst < 4 or ws_elems < 2 * M * N:
         return 1
     return max(1, min(kst // 2, max(2, 256 // tiles), 64, ws_elems // (M * N)))
 

@@ -13,9 +13,7 @@ import math
 import torch
 import torch.nn.functional as F
 
-import os as _os
-
-NSHARD = int(_os.environ.get("DBX_NSHARD", "32"))  # BN-statistics shards (see kernels.NSHARD)
+NSHARD = 32  # BN-statistics shards of the large steps (see kernels.NSHARD; small steps use 4: EngineConfig.nshard)
 MASK_NONE, MASK_OUT, MASK_Y = 0, 1, 2
 
 

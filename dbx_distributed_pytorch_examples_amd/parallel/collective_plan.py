@@ -21,7 +21,7 @@ latencies from the one-GPU flag hand-off measurements in the image's CDNA4 guide
 /opt/skills/guides/MI355X_MICROARCH.md -- outside this repository); the world >= 2
 measurement that would calibrate them needs a multi-GPU node (``tools/bench_allreduce.py --path
 all`` prints the nccl-tests lines to do so). Until then the direct path is opt-in
-(``DBX_DIRECT_AR=1``) and the defaults keep RCCL for everything.
+(engine field ``direct_ar=1``) and the defaults keep RCCL for everything.
 
 :func:`two_shot_segments` / :func:`two_shot_reference` are the direct kernel's index math in Python
 (segments, per-workgroup stripes, the scalar tail), used by the CPU tests.
@@ -29,7 +29,6 @@ all`` prints the nccl-tests lines to do so). Until then the direct path is opt-i
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -91,30 +90,32 @@ class AllReducePlan:
     max_ctas: int = 0
 
 
-def direct_enabled() -> bool:
-    return os.environ.get("DBX_DIRECT_AR", "0") == "1"
+def _cfg(cfg=None):
+    from ..engine_config import EngineConfig
+    return cfg or EngineConfig.current()
 
 
-def direct_max_bytes() -> int:
-    return int(float(os.environ.get("DBX_DIRECT_AR_MAX_MB", "8")) * (1 << 20))
+def direct_enabled(cfg=None) -> bool:
+    return _cfg(cfg).direct_ar
 
 
-def rccl_channel_bounds(world: int) -> Tuple[int, int]:
-    """RCCL CTA (channel) bounds for the framework communicator: at least one channel per link, so the
-    rings of a bulk bucket cover all 7 xGMI links (``DBX_RCCL_MIN_CTAS`` / ``DBX_RCCL_MAX_CTAS``
-    override; 0 = RCCL's own tuning)."""
-    lo = os.environ.get("DBX_RCCL_MIN_CTAS")
-    hi = os.environ.get("DBX_RCCL_MAX_CTAS")
-    if lo is not None or hi is not None:
-        return int(lo or 0), int(hi or 0)
-    return 0, 0  # RCCL's tuner; the plan's bucket sizes are what the framework picks
+def direct_max_bytes(cfg=None) -> int:
+    return int(_cfg(cfg).direct_ar_max_mb * (1 << 20))
+
+
+def rccl_channel_bounds(world: int, cfg=None) -> Tuple[int, int]:
+    """RCCL CTA (channel) bounds for the framework communicator (engine fields ``rccl_min_ctas`` /
+    ``rccl_max_ctas``; 0 = RCCL's own tuning, the default: the plan's bucket sizes are what the
+    framework picks)."""
+    c = _cfg(cfg)
+    return int(c.rccl_min_ctas), int(c.rccl_max_ctas)
 
 
 def plan_allreduce(numel: int, elem_bytes: int, world: int, bucket_cap_elems: int,
                    topo: Optional[XgmiTopology] = None, allow_direct: Optional[bool] = None) -> AllReducePlan:
     """Plan one gradient range: RCCL buckets of ``bucket_cap_elems`` (few, large messages -- the
     per-bucket step latency is paid 2(n-1) times), or the direct path for the whole range when it is
-    enabled, fits ``DBX_DIRECT_AR_MAX_MB`` and the model prices it below the ring."""
+    enabled, fits ``direct_ar_max_mb`` and the model prices it below the ring."""
     topo = topo or XgmiTopology(world)
     nbytes = numel * elem_bytes
     allow = direct_enabled() if allow_direct is None else allow_direct

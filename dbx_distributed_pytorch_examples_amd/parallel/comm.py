@@ -47,13 +47,14 @@ def native_comm_available() -> bool:
         return False
 
 
-def native_comm_requested() -> bool:
+def native_comm_requested(cfg=None) -> bool:
     """The engine's multi-rank gradient collectives go through :class:`NativeComm` (one-graph step)
-    unless ``DBX_COMM=torch`` (c10d collectives between per-segment graphs). Default native: over a
+    unless the engine config says ``comm=torch`` (c10d collectives between per-segment graphs). Default native: over a
     world-1 RCCL group on one MI355X the one-graph step runs at the single-graph rate (ResNet-18 CIFAR
     230.9k vs 231.9k img/s, TinyImageNet 96.7k vs 96.5k, headline 16.29k vs 16.36k) where the c10d
     path loses 21 % / 12 % / 1.4 % (profiles/r4_s3/)."""
-    return os.environ.get("DBX_COMM", "native") == "native"
+    from ..engine_config import EngineConfig
+    return (cfg or EngineConfig.current()).comm == "native"
 
 
 def comm_init_timeout() -> float:
@@ -173,7 +174,7 @@ class NativeComm:
         self.rank = dist.get_rank(process_group)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.direct = None  # DirectAllReduce once a buffer is registered (enable_direct)
-        self.loopback = 0   # world-1 test aid: a sum all-reduce scales by this (the trainer's DBX_COMM_LOOPBACK)
+        self.loopback = 0   # world-1 test aid: a sum all-reduce scales by this (the engine's comm_loopback)
         c = _C()
         obj = [c.comm_unique_id() if self.rank == 0 else None]
         src = dist.get_global_rank(process_group, 0) if process_group is not None else 0

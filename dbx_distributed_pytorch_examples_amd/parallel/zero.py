@@ -194,7 +194,7 @@ class SegmentedZero:
         """``comm``: a :class:`~.comm.NativeComm` -- the collectives are then enqueued on the caller's
         stream through the framework's RCCL communicator (capturable into the step's one graph)
         instead of c10d. ``collectives``: take the reduce-scatter / all-gather path even at world 1
-        (default: when a process group exists and DBX_SEGMENTED_GRAPHS=1 -- the one-GPU RCCL
+        (default: when a process group exists and the engine's ``segmented_graphs`` is on -- the one-GPU RCCL
         rehearsal, where every collective is an identity but runs through RCCL)."""
         if optim.name not in ("sgd", "adam", "adamw"):
             raise ValueError(f"sharded optimizer supports sgd / adam / adamw, not {optim.name!r}")
@@ -209,7 +209,7 @@ class SegmentedZero:
         self.comm = comm
         if collectives is None:
             collectives = self.world > 1 or (dist.is_available() and dist.is_initialized()
-                                             and os.environ.get("DBX_SEGMENTED_GRAPHS", "0") == "1")
+                                             and prog.cfg.segmented_graphs)
         self.coll = bool(collectives)  # the sharded exchange path (reduce-scatter / all-gather) is taken
         W, r = self.world, self.rank
         align = 16 * W

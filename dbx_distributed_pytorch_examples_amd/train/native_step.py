@@ -19,8 +19,10 @@ def build_native_step(args, info):
         opt = OptimConfig(name="lars", lr=args.lr, momentum=0.9, weight_decay=5e-5, trust_coefficient=0.001)
     else:
         opt = OptimConfig(name="sgd", lr=args.lr, momentum=0.9, weight_decay=5e-5)
-    use_graphs = os.environ.get("DBX_GRAPHS", "1") == "1"
-    ar_dtype = torch.bfloat16 if os.environ.get("DBX_ALLREDUCE_BF16", "0") == "1" else torch.float32
+    from ..engine_config import EngineConfig
+    eng = EngineConfig.current()
+    use_graphs = eng.graphs
+    ar_dtype = torch.bfloat16 if eng.allreduce_bf16 else torch.float32
     tr = NativeTrainer(model, args.batch, (args.image_size, args.image_size), dev, optim=opt,
                        use_graphs=use_graphs, allreduce_dtype=ar_dtype, zero_stage=getattr(args, "zero", 0))
     extra = {}

@@ -7,8 +7,8 @@
   ``nan`` (returns True so the caller poisons its loss), ``comm_hang`` (keeps beating but never
   issues another collective: the peers' ``parallel.comm_guard`` watchdog must end the job), ``diverge``
   (consumed by ``bench.py``: the rank perturbs its parameters after warm-up, and the replica check
-  must refuse to report). Only fires on attempt
-  ``DBX_FAULT_ATTEMPT`` (default 0) so a restarted job can run clean.
+  must refuse to report). Only fires on the attempt given as an optional fourth field
+  (``"rank:step:kind:attempt"``, default 0) so a restarted job can run clean.
 * :func:`check_finite` — cross-rank divergence / NaN guard (one all-reduce of a flag).
 """
 from __future__ import annotations
@@ -38,8 +38,14 @@ def parse_fault(spec: Optional[str] = None):
     spec = spec if spec is not None else os.environ.get("DBX_FAULT", "")
     if not spec:
         return None
-    r, s, kind = spec.split(":")
-    return int(r), int(s), kind
+    parts = spec.split(":")
+    return int(parts[0]), int(parts[1]), parts[2]
+
+
+def fault_attempt(spec: Optional[str] = None) -> int:
+    spec = spec if spec is not None else os.environ.get("DBX_FAULT", "")
+    parts = spec.split(":")
+    return int(parts[3]) if len(parts) > 3 else 0
 
 
 def maybe_inject(step: int) -> bool:
@@ -47,7 +53,7 @@ def maybe_inject(step: int) -> bool:
     if f is None:
         return False
     r, s, kind = f
-    if int(os.environ.get("DBX_RESTART_COUNT", "0")) != int(os.environ.get("DBX_FAULT_ATTEMPT", "0")):
+    if int(os.environ.get("DBX_RESTART_COUNT", "0")) != fault_attempt():
         return False
     if r != _rank() or s != step:
         return False

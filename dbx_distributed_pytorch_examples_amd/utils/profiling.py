@@ -67,7 +67,7 @@ def roctx_available() -> bool:
 @contextlib.contextmanager
 def range(name: str):  # noqa: A001 - mirrors nvtx.range / roctx range naming
     """roctx range around a code region (visible in rocprofv3 --marker-trace)."""
-    lib = _roctx() if os.environ.get("DBX_ROCTX", "1") != "0" else None
+    lib = _roctx() if "noroctx" not in os.environ.get("DBX_PROFILE", "").split(",") else None
     if lib is not None:
         lib.roctxRangePushA(name.encode())
     try:

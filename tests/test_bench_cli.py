@@ -68,13 +68,12 @@ def test_diverged_replica_refuses_to_report():
 
 def test_stalled_rank_ends_the_bench_within_the_timeout():
     """A rank that stops in warm-up (DBX_FAULT hang) must not leave the N-GPU bench blocked until the
-    driver's timeout: the watchdog names the phase and the job exits 75 within DBX_BENCH_TIMEOUT
-    (with the fresh-rank re-run switched off, DBX_BENCH_FALLBACK=0)."""
+    driver's timeout: the watchdog names the phase and the job exits 75 within --phase-timeout
+    (with the fresh-rank re-run switched off, --comm-fallback 0)."""
     import time
     t0 = time.time()
-    r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2"],
-             {"DBX_DIST_BACKEND": "gloo", "DBX_FAULT": "1:1:hang", "DBX_BENCH_TIMEOUT": "10",
-              "DBX_BENCH_FALLBACK": "0"})
+    r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2",
+              "--phase-timeout", "10", "--comm-fallback", "0"], {"DBX_DIST_BACKEND": "gloo", "DBX_FAULT": "1:1:hang"})
     assert r.returncode == 75, r.stderr[-2000:]
     assert "[comm-watchdog]" in r.stderr and "phase 'warmup'" in r.stderr
     assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
@@ -83,10 +82,10 @@ def test_stalled_rank_ends_the_bench_within_the_timeout():
 
 def test_hung_self_launched_ranks_are_remeasured_on_fresh_ranks():
     """bench.py --gpus N (self-launched): a collective hang in warm-up ends the ranks with exit 75; the
-    GPU-free parent starts fresh ranks once on the c10d step (DBX_COMM=torch; the injected fault only
+    GPU-free parent starts fresh ranks once on the c10d step (comm=torch; the injected fault only
     fires on attempt 0) and the JSON line carries the reason in ``comm_fallback``."""
-    r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2"],
-             {"DBX_DIST_BACKEND": "gloo", "DBX_FAULT": "1:1:comm_hang", "DBX_BENCH_TIMEOUT": "10"})
+    r = _run(["--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2",
+              "--phase-timeout", "60"], {"DBX_DIST_BACKEND": "gloo", "DBX_FAULT": "1:1:comm_hang"})
     assert r.returncode == 0, r.stderr[-3000:]
     assert "[comm-watchdog]" in r.stderr and "re-running 2 fresh ranks" in r.stderr
     d = _line(r.stdout)
@@ -96,16 +95,17 @@ def test_hung_self_launched_ranks_are_remeasured_on_fresh_ranks():
 def test_hung_torchrun_ranks_are_remeasured_on_fresh_ranks():
     """The driver's form, ``torch.distributed.run ... bench.py --gpus N``: each torchrun rank supervises a
     child (GPU-free supervisor); a hang in warm-up ends the children (75), the supervisors agree through
-    torchrun's agent store and re-run every rank once on a fresh rendezvous with DBX_COMM=torch."""
+    torchrun's agent store and re-run every rank once on a fresh rendezvous with comm=torch."""
     import socket
     with socket.socket() as s_:
         s_.bind(("127.0.0.1", 0))
         port = s_.getsockname()[1]
-    env = dict(os.environ, DBX_DIST_BACKEND="gloo", DBX_FAULT="1:1:comm_hang", DBX_BENCH_TIMEOUT="10")
+    env = dict(os.environ, DBX_DIST_BACKEND="gloo", DBX_FAULT="1:1:comm_hang")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2"],
+                        "--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2",
+                        "--phase-timeout", "60"],
                        cwd="/tmp", env=env, capture_output=True, text=True, timeout=500)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "[comm-watchdog]" in r.stderr and "[supervise]" in r.stderr
@@ -126,24 +126,26 @@ def test_rccl_summary_parses_the_ring_log(tmp_path):
     assert d["rings"][0] == "0 1 2 3 4 5 6 7" and len(d["rings"]) == 2
 
 
-def test_diverged_one_graph_step_is_remeasured_on_c10d(monkeypatch, capsys):
+def test_diverged_one_graph_step_is_remeasured_on_c10d(monkeypatch, capsys, engine):
     """The one-graph multi-rank step failing its replica check (on every rank: the check gathers all
-    checksums) is rebuilt on the c10d collectives (DBX_COMM=torch) and measured again; a divergence
+    checksums) is rebuilt on the c10d collectives (comm=torch) and measured again; a divergence
     on the c10d path (or without the framework communicator) still ends the run with 4."""
     sys.path.insert(0, ROOT)
     import bench
     calls = []
 
     def fake(args, info, wd, build_step, ddist, fault):
-        calls.append(os.environ.get("DBX_COMM"))
+        from dbx_distributed_pytorch_examples_amd.engine_config import EngineConfig
+        calls.append(EngineConfig.current().comm)
         if len(calls) == 1:
             return 4, 0.0, {"_native_comm": True}
         return 0, 1.0, {"grad_collectives": "c10d"}
 
-    monkeypatch.delenv("DBX_COMM", raising=False)
+    engine(comm=None)
+    monkeypatch.setenv("DBX_ENGINE", "")  # (bench.main's fallback rewrites it: restored after the test)
     monkeypatch.setattr(bench, "_measure", fake)
     assert bench.main(["--steps", "1", "--warmup", "0", "--preset", "resnet18_cifar10"]) == 0
-    assert calls == [None, "torch"]
+    assert calls == ["native", "torch"]
     d = _line(capsys.readouterr().out)
     assert d["config"]["grad_collectives"] == "c10d" and "_native_comm" not in d["config"]
     calls.clear()

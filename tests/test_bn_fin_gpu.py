@@ -100,34 +100,8 @@ def test_fused_backward_coeff_bit_identical(mode, two, tile):
         assert torch.equal(u, v)
 
 
-@pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("cifar_resnet18", 32, 64), ("resnet18", 32, 64)])
-def test_program_fused_fin_bit_identical(arch, size, batch, monkeypatch):
-    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
-    from dbx_distributed_pytorch_examples_amd.models import build_model
-    torch.manual_seed(0)
-    m1 = build_model(arch, num_classes=10)
-    m2 = copy.deepcopy(m1)
-    monkeypatch.setenv("DBX_FUSE_BN_FIN", "1")
-    t1 = NativeTrainer(m1, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
-    monkeypatch.setenv("DBX_FUSE_BN_FIN", "0")
-    t2 = NativeTrainer(m2, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
-    assert t1.prog.fuse_fin and not t2.prog.fuse_fin
-    g = torch.Generator().manual_seed(1)
-    for i in range(5):
-        img = torch.randint(0, 256, (batch, size, size, 3), dtype=torch.uint8, generator=g).cuda()
-        lab = torch.randint(0, 10, (batch,), generator=g).cuda()
-        t1.step(img, lab)
-        t2.step(img, lab)
-        assert t1.read_metrics()[0] == t2.read_metrics()[0], i
-    assert torch.equal(t1.prog.master, t2.prog.master)
-    for b1, b2 in zip(m1.buffers(), m2.buffers()):
-        assert torch.equal(b1, b2)
-    assert all(int(bn.fin_f.cnt.abs().sum()) == 0 and int(bn.fin_b.cnt.abs().sum()) == 0
-               for bn in t1.prog.bns if bn.fin_f is not None)
-
-
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64), ("cifar_resnet18", 32, 32)])
-def test_program_consumer_fin_in_bit_identical(arch, size, batch, monkeypatch):
+def test_program_consumer_fin_in_bit_identical(arch, size, batch, monkeypatch, engine):
     """The input BN's forward finalize done in the consuming conv's prologue (every workgroup derives
     scale / shift from the shards; workgroup 0 stores saved moments and running stats) == the
     standalone finalize launch, bit for bit, over eager and graph-replayed steps."""
@@ -136,9 +110,9 @@ def test_program_consumer_fin_in_bit_identical(arch, size, batch, monkeypatch):
     torch.manual_seed(0)
     m1 = build_model(arch, num_classes=10)
     m2 = copy.deepcopy(m1)
-    monkeypatch.setenv("DBX_FIN_IN", "1")
+    engine(fin_in="1")
     t1 = NativeTrainer(m1, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
-    monkeypatch.setenv("DBX_FIN_IN", "0")
+    engine(fin_in="0")
     t2 = NativeTrainer(m2, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     assert t1.prog.fin_in and not t2.prog.fin_in  # (off by default: an A/B switch)
     g = torch.Generator().manual_seed(1)
@@ -219,17 +193,17 @@ def test_apply2_consumer_coeff_bit_identical():
 
 
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64), ("cifar_resnet18", 32, 32)])
-def test_program_consumer_coeff_bit_identical(arch, size, batch, monkeypatch):
-    """Backward finalizes done by the BN-backward apply passes (DBX_COEFF_IN=1) == the standalone
+def test_program_consumer_coeff_bit_identical(arch, size, batch, monkeypatch, engine):
+    """Backward finalizes done by the BN-backward apply passes (coeff_in=1) == the standalone
     bn_bwd_coeff launches, over eager and graph-replayed steps (weights, BN buffers, coefficients)."""
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
     torch.manual_seed(0)
     m1 = build_model(arch, num_classes=10)
     m2 = copy.deepcopy(m1)
-    monkeypatch.setenv("DBX_COEFF_IN", "1")
+    engine(coeff_in="1")
     t1 = NativeTrainer(m1, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
-    monkeypatch.setenv("DBX_COEFF_IN", "0")
+    engine(coeff_in="0")
     t2 = NativeTrainer(m2, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     assert t1.prog.coeff_in and not t2.prog.coeff_in
     g = torch.Generator().manual_seed(1)

@@ -52,22 +52,22 @@ def test_model_prefers_direct_for_small_and_ring_chunks_for_large():
     assert cp.ring_allreduce_us(1 << 20, cp.XgmiTopology(1)) == 0.0
 
 
-def test_plan_paths(monkeypatch):
-    monkeypatch.delenv("DBX_DIRECT_AR", raising=False)
+def test_plan_paths(monkeypatch, engine):
+    engine(direct_ar=None)
     p = cp.plan_allreduce(1 << 18, 4, 8, 1 << 24)
     assert p.path == "rccl" and p.buckets == [(0, 1 << 18)]  # direct is opt-in
     p = cp.plan_allreduce(1 << 18, 4, 8, 1 << 24, allow_direct=True)
     assert p.path == "direct" and p.buckets == [(0, 1 << 18)]
-    monkeypatch.setenv("DBX_DIRECT_AR_MAX_MB", "0.5")
+    engine(direct_ar_max_mb="0.5")
     assert cp.plan_allreduce(1 << 18, 4, 8, 1 << 24, allow_direct=True).path == "rccl"  # 1 MiB > cap
     big = cp.plan_allreduce(25_557_032, 4, 8, 16 << 20)
     assert big.path == "rccl" and big.buckets[0] == (0, 16 << 20) and big.buckets[-1][1] == 25_557_032
     assert cp.plan_allreduce(100, 4, 1, 64, allow_direct=True).path == "rccl"  # world 1: nothing to reduce
 
 
-def test_channel_bounds_passthrough(monkeypatch):
-    monkeypatch.delenv("DBX_RCCL_MIN_CTAS", raising=False)
-    monkeypatch.delenv("DBX_RCCL_MAX_CTAS", raising=False)
+def test_channel_bounds_passthrough(monkeypatch, engine):
+    engine(rccl_min_ctas=None)
+    engine(rccl_max_ctas=None)
     assert cp.rccl_channel_bounds(8) == (0, 0)
-    monkeypatch.setenv("DBX_RCCL_MIN_CTAS", "7")
+    engine(rccl_min_ctas="7")
     assert cp.rccl_channel_bounds(8) == (7, 0)

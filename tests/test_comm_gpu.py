@@ -1,6 +1,6 @@
 """Framework-owned RCCL communicator (csrc/runtime/comm.cpp, parallel/comm.py): collectives on a
 world-1 group on one GPU (exact results), capture inside a HIP graph, and the NativeTrainer's
-one-graph step with DBX_COMM=native bit-identical to the c10d segmented step. Multi-device RCCL
+one-graph step with comm=native bit-identical to the c10d segmented step. Multi-device RCCL
 runs only where >= 2 GPUs are visible."""
 import copy
 import os
@@ -67,16 +67,16 @@ def test_native_comm_captured_in_graph(world1):
     c.close()
 
 
-def test_trainer_native_comm_one_graph_matches_segmented(world1, monkeypatch):
+def test_trainer_native_comm_one_graph_matches_segmented(world1, monkeypatch, engine):
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
-    monkeypatch.setenv("DBX_SEGMENTED_GRAPHS", "1")
+    engine(segmented_graphs="1")
     torch.manual_seed(0)
     m1 = build_model("resnet18", num_classes=10)
     m2 = copy.deepcopy(m1)
-    monkeypatch.setenv("DBX_COMM", "native")
+    engine(comm="native")
     t1 = NativeTrainer(m1, 32, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05))
-    monkeypatch.setenv("DBX_COMM", "torch")
+    engine(comm="torch")
     t2 = NativeTrainer(m2, 32, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     assert t1.ncomm is not None and t2.ncomm is None and t1.segmented and t2.segmented
     g = torch.Generator().manual_seed(1)
@@ -138,8 +138,8 @@ def test_nonblocking_init_and_captured_check(world1):
 
 @pytest.mark.parametrize("comm_side", ["1", "0", "1+defer", "1+defer+lazy", "1+defer+dsf"])
 @pytest.mark.parametrize("model,hw,batch", [("resnet18", 32, 32), ("resnet50", 64, 16)])
-def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batch, comm_side):
-    """The one-graph multi-rank step's all-reduce ORDER, checked at world 1: with DBX_COMM_LOOPBACK=2
+def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batch, comm_side, engine):
+    """The one-graph multi-rank step's all-reduce ORDER, checked at world 1: with comm_loopback=2
     every bucket all-reduce doubles its range in place (the sum of two identical replicas) and the
     update halves it, so the trajectory equals the plain one bit for bit -- unless a bucket is reduced
     before its weight gradients are final (late posts, batched side stream), which at world 1 with a
@@ -147,19 +147,19 @@ def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batc
     weight-gradient side stream behind their batch (event-scoped joins); 0: a separate comm stream."""
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
-    monkeypatch.setenv("DBX_SEGMENTED_GRAPHS", "1")
-    monkeypatch.setenv("DBX_COMM", "native")
-    monkeypatch.setenv("DBX_COMM_SIDE", comm_side[0])
-    monkeypatch.setenv("DBX_SIDE_DEFER", "1" if "defer" in comm_side else "0")
-    monkeypatch.setenv("DBX_LAZY_JOIN", "1" if "lazy" in comm_side else "0")
-    # "dsf": the downsample forwards on the same side stream as the collectives (DBX_DS_FWD_SIDE)
-    monkeypatch.setenv("DBX_DS_FWD_SIDE", "1" if "dsf" in comm_side else "0")
+    engine(segmented_graphs="1")
+    engine(comm="native")
+    engine(comm_side=comm_side[0])
+    engine(side_defer="1" if "defer" in comm_side else "0")
+    engine(lazy_join="1" if "lazy" in comm_side else "0")
+    # "dsf": the downsample forwards on the same side stream as the collectives (ds_fwd_side)
+    engine(ds_fwd_side="1" if "dsf" in comm_side else "0")
     torch.manual_seed(0)
     m1 = build_model(model, num_classes=10)
     m2 = copy.deepcopy(m1)
-    monkeypatch.setenv("DBX_COMM_LOOPBACK", "2")
+    engine(comm_loopback="2")
     t1 = NativeTrainer(m1, batch, (hw, hw), torch.device("cuda"), optim=OptimConfig(lr=0.05))
-    monkeypatch.delenv("DBX_COMM_LOOPBACK")
+    engine(comm_loopback=None)
     t2 = NativeTrainer(m2, batch, (hw, hw), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     assert t1.ncomm is not None and t1.loopback == 2 and t2.loopback == 1 and t1.late_posts
     assert t1.comm_side == (comm_side[0] == "1") and t1.prog.event_joins == t1.comm_side

@@ -17,19 +17,9 @@ def _stats_total(st, C):
     return st.view(K.NSHARD, 2, C).sum(0)
 
 
-def _variant(stage, monkeypatch):
-    """"64" / "32": the barrier-per-stage ring (DBX_FAST_STAGE); "pp": the ping-pong kernel (DBX_FAST_PP)."""
-    monkeypatch.setenv("DBX_FAST_STAGE", "32" if stage == "32" else "64")
-    monkeypatch.setenv("DBX_FAST_PP", "1" if stage == "pp" else "0")
-
-
-@pytest.mark.parametrize("stage", ["64", "32", "pp"])
 @pytest.mark.parametrize("N,H,C,Kc,R,bn", [(20, 14, 256, 256, 3, 256), (9, 7, 512, 512, 3, 256),
                                            (12, 14, 256, 1024, 1, 256), (20, 14, 128, 128, 3, 128)])
-def test_fast_fwd_matches_four_wave_and_fp32(N, H, C, Kc, R, bn, stage, monkeypatch):
-    # stage 32: the deep ring of 32-channel stages (DBX_FAST_STAGE), pp: the ping-pong kernel -- the
-    # same K order, bit-identical
-    _variant(stage, monkeypatch)
+def test_fast_fwd_matches_four_wave_and_fp32(N, H, C, Kc, R, bn):
     torch.manual_seed(N + C)
     pad = R // 2
     x = torch.randn(N, H, H, C, device="cuda").bfloat16()
@@ -47,10 +37,8 @@ def test_fast_fwd_matches_four_wave_and_fp32(N, H, C, Kc, R, bn, stage, monkeypa
     assert torch.allclose(_stats_total(s1, Kc), tot, rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("stage", ["64", "32", "pp"])
 @pytest.mark.parametrize("epi,accum,bn", [(0, False, 256), (1, True, 256), (2, False, 128), (2, True, 128)])
-def test_fast_dgrad_epilogues_match_four_wave(epi, accum, bn, stage, monkeypatch):
-    _variant(stage, monkeypatch)
+def test_fast_dgrad_epilogues_match_four_wave(epi, accum, bn):
     torch.manual_seed(epi * 7 + accum)
     N, H, C, Kc, R = 10, 14, 256, 256, 3
     dy = torch.randn(N, H, H, Kc, device="cuda").bfloat16()

@@ -154,11 +154,11 @@ def _native_dist():
     return out
 
 
-@pytest.mark.parametrize("seg_groups", ["", "3,3", "2,4"])
-def test_native_program_bucket_allreduce(seg_groups, monkeypatch):
+@pytest.mark.parametrize("seg_groups", ["", "3:3", "2:4"])
+def test_native_program_bucket_allreduce(seg_groups, monkeypatch, engine):
     """world-2 native step (CPU reference ops): grads are summed over ranks in every segment bucket,
-    with one all-reduce cut per backward segment (default) or merged segments (DBX_SEG_GROUPS)."""
-    monkeypatch.setenv("DBX_SEG_GROUPS", seg_groups)
+    with one all-reduce cut per backward segment (default) or merged segments (seg_groups)."""
+    engine(seg_groups=seg_groups)
     g2, m2 = Launcher(2, use_gpu=False).run(_native_dist)
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
@@ -422,7 +422,7 @@ def _native_zero_vs_dp(optim, clip):
 def test_native_zero1_matches_dp(world, optim, clip):
     # world 1: a one-rank process group with the segmented multi-rank path forced (the one-GPU
     # rehearsal configuration): the reduce-scatter / all-gather exchange runs as identities
-    env = {"DBX_FORCE_PG": "1", "DBX_SEGMENTED_GRAPHS": "1"} if world == 1 else None
+    env = {"DBX_FORCE_PG": "1", "DBX_ENGINE": "segmented_graphs=1"} if world == 1 else None
     equal, rel, nbytes, shard, n, coll = Launcher(world, use_gpu=False, env=env).run(_native_zero_vs_dp, optim, clip)
     assert coll
     if world <= 2:  # a two-term fp32 sum does not depend on the collective's reduction order

@@ -117,7 +117,7 @@ def test_dwfused_cu_span(nhw, ck):
     assert ((st2 - st).abs() / (st.abs() + 1.0)).max().item() < 1e-6
 
 
-def test_native_step_fused_vs_unfused(monkeypatch):
+def test_native_step_fused_vs_unfused(monkeypatch, engine):
     """One eager ResNet-50 step at 224 (stage-1 / stage-2 conv3s take the fused kernel) == the unfused
     schedule."""
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
@@ -127,9 +127,9 @@ def test_native_step_fused_vs_unfused(monkeypatch):
     img = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8, device=dev)
     lab = torch.randint(0, 1000, (2,), device=dev)
     grads = []
-    monkeypatch.setenv("DBX_FUSE_DW_MIN_TILES", "0")  # batch 2: fuse regardless of tiles per workgroup
+    engine(fuse_dw_min_tiles="0")  # batch 2: fuse regardless of tiles per workgroup
     for flag in ("1", "0"):
-        monkeypatch.setenv("DBX_FUSE_DW", flag)
+        engine(fuse_dw=flag)
         torch.manual_seed(0)
         tr = NativeTrainer(resnet50(num_classes=1000), 2, (224, 224), torch.device(dev), optim=OptimConfig(lr=0.0),
                            use_graphs=False)

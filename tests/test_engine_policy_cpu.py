@@ -21,15 +21,15 @@ def test_fwd_conv_flops():
     assert _flops("resnet18", 32, 256) < _flops("resnet50", 64, 512) < f
 
 
-def test_side_stream_defaults(monkeypatch):
+def test_side_stream_defaults(monkeypatch, engine):
     """Default: one side fork per residual block; 2 = the batched side stream (one fork per backward
     segment); 1 = per-gradient forks; 0 = off."""
     for env, overlap, batch, block in ((None, True, False, True), ("2", True, True, False), ("1", True, False, False),
                                        ("0", False, False, False)):
         if env is None:
-            monkeypatch.delenv("DBX_OVERLAP_WGRAD", raising=False)
+            engine(overlap_wgrad=None)
         else:
-            monkeypatch.setenv("DBX_OVERLAP_WGRAD", env)
+            engine(overlap_wgrad=env)
         p = ResNetProgram(build_model("resnet18", num_classes=10), 2, (32, 32), torch.device("cpu"))
         assert (p.overlap_wgrad, p.side_batch, p.side_block) == (overlap, batch, block), env
 
@@ -71,14 +71,11 @@ def test_post_launch_hook_owner_scoped_cancel():
         K.set_post_launch(None)
 
 
-def test_side_stream_defaults_by_step_size(monkeypatch):
+def test_side_stream_defaults_by_step_size(monkeypatch, engine):
     """The default side stream forks per residual block with the deferred launch and lazy joins, the
     last block's tail and the stem weight gradient on the main stream, the downsample forwards on the
     side stream; the CU reservation from 50 GFLOP of forward conv work up; an explicit
-    DBX_OVERLAP_WGRAD wins. (The step size is patched: the real ones need GPU-sized buffers.)"""
-    for var in ("DBX_OVERLAP_WGRAD", "DBX_SIDE_DEFER", "DBX_LAZY_JOIN", "DBX_SIDE_CU_RESERVE", "DBX_DS_FWD_SIDE",
-                "DBX_BLOCK_TAIL_MAIN", "DBX_STEM_WG_MAIN"):
-        monkeypatch.delenv(var, raising=False)
+    overlap_wgrad wins. (The step size is patched: the real ones need GPU-sized buffers.)"""
     m = build_model("resnet18", num_classes=10)
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e11)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
@@ -92,6 +89,6 @@ def test_side_stream_defaults_by_step_size(monkeypatch):
     monkeypatch.setattr(ResNetProgram, "fwd_conv_flops", lambda self: 1e12)
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert p.ds_fwd_side and (p.block_tail_main, p.stem_wg_main) == (2, True)
-    monkeypatch.setenv("DBX_OVERLAP_WGRAD", "2")
+    engine(overlap_wgrad="2")
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.stem_wg_main) == (False, True, False, False, False)

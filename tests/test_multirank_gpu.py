@@ -53,9 +53,9 @@ def test_dist_check_rccl(world, comm):
     runs there."""
     if _ndev() < world:
         pytest.skip(f"RCCL world {world} needs {world} GPUs ({_ndev()} visible)")
-    env = {"DBX_COMM": comm}
+    env = {"DBX_ENGINE": f"comm={comm}"}
     if world == 1:
-        env.update({"DBX_FORCE_PG": "1", "DBX_SEGMENTED_GRAPHS": "1"})
+        env.update({"DBX_FORCE_PG": "1", "DBX_ENGINE": f"comm={comm},segmented_graphs=1"})
     r = _launch(world, "tools/dist_gpu_check.py", env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert f"dist_gpu_check OK: world={world} backend=nccl comm={comm}" in r.stdout

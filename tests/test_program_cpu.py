@@ -27,11 +27,11 @@ def _cos(a, b):
 @pytest.mark.parametrize("arch,size,batch,fold,ratio", [("resnet18", 32, 8, 0, "inf"), ("cifar_resnet18", 32, 4, 0, "inf"),
                                                         ("resnet50", 64, 8, 0, "inf"), ("resnet50", 64, 8, 1 << 40, "inf"),
                                                         ("resnet50", 64, 8, 0, "1")])
-def test_program_grads_match_autograd(arch, size, batch, fold, ratio, monkeypatch):
-    # fold: DBX_FOLD_MIN_ELEMS -- 0 folds every foldable BN-backward apply into its dgrad, 2^40 none;
-    # ratio: DBX_FOLD_MAX_RATIO -- 1 keeps the bottleneck conv1 dgrads (N = 4K) unfolded (mixed schedule)
-    monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(fold))
-    monkeypatch.setenv("DBX_FOLD_MAX_RATIO", ratio)
+def test_program_grads_match_autograd(arch, size, batch, fold, ratio, monkeypatch, engine):
+    # fold: fold_min_elems -- 0 folds every foldable BN-backward apply into its dgrad, 2^40 none;
+    # ratio: fold_max_ratio -- 1 keeps the bottleneck conv1 dgrads (N = 4K) unfolded (mixed schedule)
+    engine(fold_min_elems=str(fold))
+    engine(fold_max_ratio=ratio)
     torch.manual_seed(0)
     model = build_model(arch, num_classes=10)
     _damp(model, arch)
@@ -171,14 +171,14 @@ def test_frozen_native_head_params_changed_on_resume():
 
 
 @pytest.mark.parametrize("fold", [0, 1 << 40])
-def test_fused_conv3_backward_schedule(fold, monkeypatch):
-    """DBX_FUSE_DW: the bottleneck conv3 backward as one op (K.conv_dwfused) gives the gradients of
+def test_fused_conv3_backward_schedule(fold, monkeypatch, engine):
+    """fuse_dw: the bottleneck conv3 backward as one op (K.conv_dwfused) gives the gradients of
     the unfused schedule (BN-backward apply -> MASK_Y dgrad -> weight gradient), folded or not."""
-    monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(fold))
-    monkeypatch.setenv("DBX_FUSE_DW_MIN_TILES", "0")  # small batch: fuse regardless of tiles per workgroup
+    engine(fold_min_elems=str(fold))
+    engine(fuse_dw_min_tiles="0")  # small batch: fuse regardless of tiles per workgroup
     grads = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("DBX_FUSE_DW", flag)
+        engine(fuse_dw=flag)
         torch.manual_seed(0)
         model = build_model("resnet50", num_classes=10)
         _damp(model, "resnet50")

@@ -23,9 +23,9 @@ def _cos(a, b):
 
 @pytest.mark.parametrize("arch,size,batch,fold", [("resnet50", 64, 8, 0), ("resnet50", 64, 8, 1 << 40),
                                                   ("resnet18", 32, 16, 0), ("cifar_resnet18", 32, 8, 0)])
-def test_program_matches_autograd(arch, size, batch, fold, monkeypatch):
-    # fold: DBX_FOLD_MIN_ELEMS -- 0 folds every foldable BN-backward apply into its dgrad, 2^40 none
-    monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(fold))
+def test_program_matches_autograd(arch, size, batch, fold, monkeypatch, engine):
+    # fold: fold_min_elems -- 0 folds every foldable BN-backward apply into its dgrad, 2^40 none
+    engine(fold_min_elems=str(fold))
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
 
@@ -456,12 +456,11 @@ def test_composer_trainer_runs_on_native_module():
     assert 0.0 <= hist[-1]["metrics/eval/Accuracy"] <= 1.0
 
 
-@pytest.mark.parametrize("mode", ["2", "3", "2+tail2", "2+tail2+seg3", "2+l1blocks", "2+tail2+l1blocks", "2+defer",
-                                  "2+tail2+defer", "2+lazy", "2+tail2+defer+lazy", "3+defer+lazy", "3+defer+lazy+ds", "3+defer+lazy+ds2",
-                                  "3+defer+lazy+dsf", "3+btail2+defer+lazy", "3+defer+lazy+dsf+early"])
+@pytest.mark.parametrize("mode", ["2", "3", "2+tail2", "2+defer", "2+tail2+defer", "2+lazy", "2+tail2+defer+lazy",
+                                  "3+defer+lazy", "3+defer+lazy+dsf", "3+btail2+defer+lazy", "3+btail2+defer+lazy+dsf"])
 @pytest.mark.parametrize("arch,size,batch", [("resnet50", 64, 32), ("resnet18", 32, 64)])
-def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch):
-    """DBX_OVERLAP_WGRAD=2 (weight gradients forked once per backward segment, joined one segment
+def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch, engine):
+    """overlap_wgrad=2 (weight gradients forked once per backward segment, joined one segment
     later) and =3 (forked once per block, joined at the segment's end) train bit-identically to the
     in-order schedule, eager and graph-replayed."""
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
@@ -470,33 +469,26 @@ def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch)
     m1 = build_model(arch, num_classes=10)
     m2 = copy.deepcopy(m1)
     # the same BN-backward fold schedule on both sides (without the side stream it defaults to fold-all)
-    monkeypatch.setenv("DBX_FOLD_MIN_ELEMS", str(1 << 25))
-    monkeypatch.setenv("DBX_FOLD_MAX_RATIO", "1")
-    # "2+tail2": the last batch's two last weight gradients on the main stream's tail (DBX_TAIL_MAIN),
+    engine(fold_min_elems=str(1 << 25))
+    engine(fold_max_ratio="1")
+    # "2+tail2": the last batch's two last weight gradients on the main stream's tail (tail_main),
     # the stem weight gradient on the main stream (the batched default)
-    monkeypatch.setenv("DBX_OVERLAP_WGRAD", mode[0])
-    monkeypatch.setenv("DBX_TAIL_MAIN", "2" if "tail2" in mode.split("+") else "0")
-    monkeypatch.setenv("DBX_SEG_TAIL_MAIN", "3" if "seg3" in mode else "0")
-    # "l1blocks": layer1's weight gradients forked per block (DBX_LAST_SEG_BLOCKS)
-    monkeypatch.setenv("DBX_LAST_SEG_BLOCKS", "1" if "l1blocks" in mode else "0")
-    # "defer": each side batch launched after the main stream's next kernel (DBX_SIDE_DEFER)
-    monkeypatch.setenv("DBX_SIDE_DEFER", "1" if "defer" in mode else "0")
-    # "lazy": no intermediate joins of the side stream (DBX_LAZY_JOIN)
-    monkeypatch.setenv("DBX_LAZY_JOIN", "1" if "lazy" in mode else "0")
-    # "ds": the downsample conv's data gradient on a branch stream (DBX_DS_BRANCH)
+    engine(overlap_wgrad=mode[0])
+    engine(tail_main="2" if "tail2" in mode.split("+") else "0")
+    # "defer": each side batch launched after the main stream's next kernel (side_defer)
+    engine(side_defer="1" if "defer" in mode else "0")
+    # "lazy": no intermediate joins of the side stream (lazy_join)
+    engine(lazy_join="1" if "lazy" in mode else "0")
     opts = mode.split("+")
-    monkeypatch.setenv("DBX_DS_BRANCH", "2" if "ds2" in opts else ("1" if "ds" in opts else "0"))
-    # "btail2": per-block forks, the last block's last two weight gradients on the main stream (DBX_BLOCK_TAIL_MAIN)
-    monkeypatch.setenv("DBX_BLOCK_TAIL_MAIN", "2" if "btail2" in opts else "0")
-    # "dsf": the downsample conv's forward on the side stream beside conv2 / conv3 (DBX_DS_FWD_SIDE)
-    monkeypatch.setenv("DBX_DS_FWD_SIDE", "1" if "dsf" in opts else "0")
-    monkeypatch.setenv("DBX_DS_FWD_EARLY", "1" if "early" in opts else "0")
+    # "btail2": per-block forks, the last block's last two weight gradients on the main stream (block_tail_main)
+    engine(block_tail_main="2" if "btail2" in opts else "0")
+    # "dsf": the downsample conv's forward on the side stream beside conv2 / conv3 (ds_fwd_side)
+    engine(ds_fwd_side="1" if "dsf" in opts else "0")
     t1 = NativeTrainer(m1, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
-    monkeypatch.setenv("DBX_OVERLAP_WGRAD", "0")
+    engine(overlap_wgrad="0")
     t2 = NativeTrainer(m2, batch, (size, size), dev, optim=OptimConfig(lr=0.05))
     assert (t1.prog.side_batch if mode[0] == "2" else t1.prog.side_block) and t1.prog.overlap_wgrad
     assert t1.prog.tail_main == (2 if "tail2" in mode.split("+") else 0)
-    assert t1.prog.last_seg_blocks == ("l1blocks" in mode)
     assert t1.prog.side_defer == ("defer" in mode)
     assert not t2.prog.overlap_wgrad
     g = torch.Generator().manual_seed(3)

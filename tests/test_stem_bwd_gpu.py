@@ -90,8 +90,8 @@ def test_stem_bwd_fused_deterministic():
     assert torch.equal(_fused(*args), _fused(*args))
 
 
-def test_native_step_stem_fused_vs_unfused(monkeypatch):
-    """One eager ResNet-50 step at 224: fused stem backward (opt-in, DBX_FUSE_STEM_BWD=1) ==
+def test_native_step_stem_fused_vs_unfused(monkeypatch, engine):
+    """One eager ResNet-50 step at 224: fused stem backward (opt-in, fuse_stem_bwd=1) ==
     pool_bn_bwd_apply + stem wgrad."""
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import resnet50
@@ -101,7 +101,7 @@ def test_native_step_stem_fused_vs_unfused(monkeypatch):
     lab = torch.randint(0, 1000, (2,), device=dev)
     grads = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("DBX_FUSE_STEM_BWD", flag)
+        engine(fuse_stem_bwd=flag)
         torch.manual_seed(0)
         tr = NativeTrainer(resnet50(num_classes=1000), 2, (224, 224), torch.device(dev), optim=OptimConfig(lr=0.0),
                            use_graphs=False)

@@ -45,7 +45,7 @@ def test_batched_reduce_matches_per_gradient_reduce():
 
 
 @pytest.mark.parametrize("arch,size,batch", [("cifar_resnet18", 32, 64), ("resnet50", 64, 32)])
-def test_program_deferred_reduce_bit_identical(arch, size, batch, monkeypatch):
+def test_program_deferred_reduce_bit_identical(arch, size, batch, monkeypatch, engine):
     """Whole training steps (eager warm-ups, capture, replays) with the batched reduce == without,
     bit for bit, twice (a run-to-run difference would show in one of the two)."""
     import copy
@@ -56,7 +56,7 @@ def test_program_deferred_reduce_bit_identical(arch, size, batch, monkeypatch):
     ms = [copy.deepcopy(m0) for _ in range(3)]
     ts = []
     for m, flag in zip(ms, ("0", "1", "1")):
-        monkeypatch.setenv("DBX_DEFER_REDUCE", flag)
+        engine(defer_reduce=flag)
         ts.append(NativeTrainer(m, batch, (size, size), torch.device("cuda"), optim=OptimConfig(lr=0.05)))
     assert ts[1].prog.defer_reduce and not ts[0].prog.defer_reduce
     g = torch.Generator().manual_seed(1)

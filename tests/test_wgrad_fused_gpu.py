@@ -46,37 +46,3 @@ def test_fused_wgrad_reduce_bit_identical(N, H, C, Kc, R, tile, dma, accumulate,
                                       dy.float().permute(0, 3, 1, 2), padding=pad)
     ref = ref.permute(0, 2, 3, 1).reshape(Kc, -1) * scale + (base if accumulate else 0)
     assert ((d1 - ref).norm() / ref.norm()).item() < 1e-3
-
-
-def test_program_step_with_fused_reduce_matches_unfused(monkeypatch):
-    """ResNet-18 CIFAR (small maps: the fused path is taken): one step's gradients match the two-kernel
-    path to fp32 rounding (the two-kernel path sums many-split slabs in two levels: another order; the
-    training trajectory of this random-label setup is chaotic, so later steps are not compared across
-    paths -- tools/debug_fused_wgrad.py), and the graph-replayed fused step is bit-identical to the
-    eager fused step over several steps."""
-    import copy
-    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
-    from dbx_distributed_pytorch_examples_amd.models import build_model
-    torch.manual_seed(0)
-    m1 = build_model("cifar_resnet18", num_classes=10)
-    m2, m3 = copy.deepcopy(m1), copy.deepcopy(m1)
-    monkeypatch.setenv("DBX_FUSE_WGRAD_REDUCE", "1")
-    t1 = NativeTrainer(m1, 64, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05))
-    t3 = NativeTrainer(m3, 64, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05), use_graphs=False)
-    monkeypatch.setenv("DBX_FUSE_WGRAD_REDUCE", "0")
-    t2 = NativeTrainer(m2, 64, (32, 32), torch.device("cuda"), optim=OptimConfig(lr=0.05), use_graphs=False)
-    assert t1.prog.fuse_wgrad_reduce and not t2.prog.fuse_wgrad_reduce
-    g = torch.Generator().manual_seed(1)
-    for i in range(6):
-        img = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, generator=g).cuda()
-        lab = torch.randint(0, 10, (64,), generator=g).cuda()
-        for t in ((t1, t2, t3) if i == 0 else (t1, t3)):
-            t.step(img, lab)
-        torch.cuda.synchronize()
-        if i == 0:
-            for name, off, n in t1.prog.param_ranges:
-                a, b = t1.prog.grad[off:off + n], t2.prog.grad[off:off + n]
-                assert ((a - b).norm() / b.norm().clamp_min(1e-30)).item() < 1e-5, name
-        assert t1.read_metrics()[0] == t3.read_metrics()[0], i
-    assert torch.equal(t1.prog.master, t3.prog.master)
-    assert int(t1.prog.wg_cnt.abs().sum()) == 0

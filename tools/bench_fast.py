@@ -21,8 +21,7 @@ from dbx_distributed_pytorch_examples_amd.ops import kernels as K  # noqa: E402
 
 # (name, mode, C_in, C_out, R, H, epi, variants)
 # variant tuples: (bm, bn, dma) -- dma 4 = the eight-wave kernel with the full-rounds batch split;
-# (256, bn, 4, 0) = the eight-wave kernel over the whole batch (partial last round); --pp adds
-# (..., "pp") = the same on the ping-pong kernel
+# (256, bn, 4, 0) = the eight-wave kernel over the whole batch (partial last round)
 CASES = [
     ("dgrad3x3@14 256 epi2", "dgrad", 256, 256, 3, 14, 2, [(128, 128, 2), (256, 128, 4, 0), (256, 128, 4)]),
     ("dgrad3x3@28 128 epi2", "dgrad", 128, 128, 3, 28, 2, [(128, 128, 2), (256, 128, 4)]),
@@ -66,7 +65,6 @@ def build(case, N, dev):
 
             def run():
                 st.zero_()
-                os.environ["DBX_FAST_PP"] = "1" if "pp" in tile else "0"
                 K.conv_fwd(x, w, y, R=R, S=R, stride=1, pad=pad, stats=st, tile=tile[:3], _split=tile[3:4] != (0,))
             outs[tile] = (y, st)
             return run
@@ -94,7 +92,6 @@ def build(case, N, dev):
 
         def run():
             st.zero_()
-            os.environ["DBX_FAST_PP"] = "1" if "pp" in tile else "0"
             K.conv_dgrad(dy, wt, dx, R=R, S=R, stride=1, pad=pad, tile=tile[:3], epilogue=e,
                          _split=tile[3:4] != (0,))
         outs[tile] = (dx, st)
@@ -109,8 +106,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="")
-    ap.add_argument("--pp", action="store_true",
-                    help="also time every eight-wave variant as the ping-pong kernel (DBX_FAST_PP=1)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     results = []
@@ -119,8 +114,6 @@ def main():
             continue
         make, outs, flops = build(case, a.batch, dev)
         variants = list(case[7])
-        if a.pp:
-            variants += [(t + (1,) if len(t) < 4 else t) + ("pp",) for t in case[7] if t[2] == 4]
         runs = {t: make(t) for t in variants}
         for r in runs.values():
             r()

@@ -11,10 +11,10 @@ Checks (all on the segmented-graph + comm-stream path that world > 1 takes):
   3. ZeRO-1 (reduce-scatter + sharded update + bf16 all-gather) matches plain data parallel.
   python -m dbx_distributed_pytorch_examples_amd.launch --nproc-per-node 2 tools/dist_gpu_check.py
 
-World 1 (the one-GPU RCCL rehearsal): ``DBX_FORCE_PG=1 DBX_SEGMENTED_GRAPHS=1`` under the launcher
+World 1 (the one-GPU RCCL rehearsal): ``DBX_FORCE_PG=1 DBX_ENGINE=segmented_graphs=1`` under the launcher
 creates a one-rank RCCL group and forces the segmented multi-rank path, so every RCCL-only branch
 (c10d reduce_scatter_tensor / all_gather_into_tensor in parallel/zero.py, the comm-stream bucket
-all-reduces, with DBX_COMM=native the framework communicator and the one-graph step) executes;
+all-reduces, with the engine's comm=native the framework communicator and the one-graph step) executes;
 the checks hold bit-exactly (every collective is an identity).
 """
 import os
@@ -49,7 +49,7 @@ def run(use_graphs, zero=0, steps=4, bucket_mb=1.0, pg=None, optim="sgd"):
     tr = NativeTrainer(m, B, (32, 32), info.device, optim=opt, use_graphs=use_graphs,
                        bucket_cap_mb=bucket_mb, zero_stage=zero, process_group=pg)
     if COMM == "native" and pg is None and info.device.type == "cuda" and info.backend == "nccl":
-        assert tr.ncomm is not None, "DBX_COMM=native did not create the framework communicator"
+        assert tr.ncomm is not None, "comm=native did not create the framework communicator"
     if zero:
         assert tr.zero.coll, "ZeRO did not take the collective (reduce-scatter / all-gather) path"
     for img, lab in batches(steps):
@@ -67,10 +67,11 @@ def params(tr):
 
 info = ddist.init_distributed()
 W = info.world_size
-assert W >= 2 or (dist.is_initialized() and os.environ.get("DBX_SEGMENTED_GRAPHS") == "1"), \
-    f"{info}: world 1 needs DBX_FORCE_PG=1 DBX_SEGMENTED_GRAPHS=1 (under the launcher)"
+from dbx_distributed_pytorch_examples_amd.engine_config import EngineConfig  # noqa: E402
+assert W >= 2 or (dist.is_initialized() and EngineConfig.current().segmented_graphs), \
+    f"{info}: world 1 needs DBX_FORCE_PG=1 DBX_ENGINE=segmented_graphs=1 (under the launcher)"
 exact = W <= 2
-COMM = os.environ.get("DBX_COMM", "torch")
+COMM = EngineConfig.current().comm
 
 # 1. DP gradient == sum of per-rank single-process gradients (one step, eager)
 singles = [dist.new_group([r]) for r in range(W)]

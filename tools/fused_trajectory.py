@@ -33,7 +33,8 @@ torch.manual_seed(0)
 base = build_model("resnet50", num_classes=a.classes)
 MEAN = torch.tensor((0.485, 0.456, 0.406), device=dev).view(1, 3, 1, 1) * 255
 STD = torch.tensor((0.229, 0.224, 0.225), device=dev).view(1, 3, 1, 1) * 255
-VARIANTS = {"native fused": {"DBX_FUSE_DW": "1"}, "native unfused": {"DBX_FUSE_DW": "0", "DBX_STEM_WGRAD": "generic"}}
+VARIANTS = {"native fused": {"DBX_ENGINE": "fuse_dw=1"},
+            "native unfused": {"DBX_ENGINE": "fuse_dw=0,stem_wgrad=generic"}}
 curves = {}
 for name, env in VARIANTS.items():
     old = {k: os.environ.get(k) for k in env}

@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 180 --timeout-method threa
   tests/test_comm_gpu.py "tests/test_program_gpu.py::test_composer_trainer_runs_on_native_module" -W always \
   > $O/pytest.log 2>&1; rc=$?; tail -30 $O/pytest.log; [ $rc = 0 ] || exit $rc
 grep -c "layout contract" $O/pytest.log || true
-DBX_FORCE_PG=1 DBX_SEGMENTED_GRAPHS=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+DBX_FORCE_PG=1 DBX_ENGINE=segmented_graphs=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
   --master-addr 127.0.0.1 --master-port 29711 bench.py --gpus 1 --steps 15 --warmup 5 > $O/bench_rccl_world1.log 2>&1 \
   || { tail -20 $O/bench_rccl_world1.log; exit 1; }
 grep '"metric"' $O/bench_rccl_world1.log | cut -c1-200

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 B=${1:-1024}
 cd /tmp
-export DBX_GRAPHS=0 DBX_OVERLAP_WGRAD=0
+export DBX_ENGINE=graphs=0,overlap_wgrad=0
 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE -d $R/$O/a -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --batch $B > $R/$O/a.log 2>&1 || { echo "pmc a failed"; tail -5 $R/$O/a.log; exit 1; }
 echo "pass a ok"
 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE TCC_HIT_sum TCC_MISS_sum -d $R/$O/b -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --batch $B > $R/$O/b.log 2>&1 || { echo "pmc b failed"; tail -5 $R/$O/b.log; exit 1; }

@@ -15,7 +15,7 @@ grep "^| \|  \(fwd0\|dgrad\)" $O/tune.log
 for r in 1 2; do
   for tb in before new; do
     f=$O/tune_table.json; [ $tb = before ] && f=$O/tune_table.before.json
-    DBX_TUNE_TABLE=$f timeout -k 10 300 python bench.py $BENCH > $O/bench_${tb}_$r.log 2>&1 || { tail -20 $O/bench_${tb}_$r.log; exit 1; }
+    DBX_ENGINE=tune_table=$f timeout -k 10 300 python bench.py $BENCH > $O/bench_${tb}_$r.log 2>&1 || { tail -20 $O/bench_${tb}_$r.log; exit 1; }
     echo "bench $tb r$r: $(grep -o '"value": [0-9.]*' $O/bench_${tb}_$r.log)"
   done
 done

@@ -16,7 +16,7 @@ for r in 1 2; do
   for p in resnet50_tiny_imagenet resnet18_cifar10; do
     for v in new old; do
       if [ $v = new ]; then tt=$T; else tt=dbx_distributed_pytorch_examples_amd/ops/tune_table.json; fi
-      DBX_TUNE_TABLE=$tt timeout -k 10 300 python bench.py --preset $p --steps 30 --warmup 10 > $O/${p}_${v}_r$r.log 2>&1 || { tail -20 $O/${p}_${v}_r$r.log; exit 1; }
+      DBX_ENGINE=tune_table=$tt timeout -k 10 300 python bench.py --preset $p --steps 30 --warmup 10 > $O/${p}_${v}_r$r.log 2>&1 || { tail -20 $O/${p}_${v}_r$r.log; exit 1; }
       echo "$p $v r$r: $(grep -o '"value": [0-9.]*' $O/${p}_${v}_r$r.log)"
     done
   done

@@ -13,7 +13,7 @@ grep "^| " $O/tune.log | tail -n +1
 for r in 1 2; do
   for tb in before new; do
     f=$O/tune_table.json; [ $tb = before ] && f=$O/tune_table.before.json
-    DBX_TUNE_TABLE=$f timeout -k 10 300 python bench.py --preset resnet50_imagenet_zero1 --steps 20 --warmup 5 > $O/bench_${tb}_$r.log 2>&1 || { tail -20 $O/bench_${tb}_$r.log; exit 1; }
+    DBX_ENGINE=tune_table=$f timeout -k 10 300 python bench.py --preset resnet50_imagenet_zero1 --steps 20 --warmup 5 > $O/bench_${tb}_$r.log 2>&1 || { tail -20 $O/bench_${tb}_$r.log; exit 1; }
     echo "zero1 $tb r$r: $(grep -o '"value": [0-9.]*' $O/bench_${tb}_$r.log)"
   done
 done

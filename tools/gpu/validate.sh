@@ -15,7 +15,7 @@ for p in headline resnet50_imagenet_zero1 resnet50_tiny_imagenet resnet18_cifar1
   grep '"metric"' $O/bench_$p.log >> $O/bench_lines.txt
   echo "$p: $(grep -o '"value": [0-9.]*' $O/bench_$p.log)"
 done
-DBX_FORCE_PG=1 DBX_SEGMENTED_GRAPHS=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+DBX_FORCE_PG=1 DBX_ENGINE=segmented_graphs=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
   --master-addr 127.0.0.1 --master-port 29711 bench.py --gpus 1 --steps 15 --warmup 5 > $O/bench_rccl_world1.log 2>&1 \
   || { tail -20 $O/bench_rccl_world1.log; exit 1; }
 grep '"metric"' $O/bench_rccl_world1.log >> $O/bench_lines.txt

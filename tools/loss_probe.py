@@ -5,7 +5,7 @@ from dbx_distributed_pytorch_examples_amd.models import build_model
 from dbx_distributed_pytorch_examples_amd.ops import kernels as K
 dev=torch.device('cuda')
 for patch in (1, 0):
-    K._PATCH3 = ("all" if patch else "0", "dgrad"); os.environ["DBX_STEM_PATCH"]=str(patch)
+    os.environ["DBX_ENGINE"] = f"patch3={'all' if patch else '0'},stem_patch={int(patch)}"
     for lr, steps in ((0.05, 80), (0.02, 50), (0.1, 50)):
         torch.manual_seed(0)
         model=build_model('resnet50', num_classes=1000)

@@ -17,8 +17,7 @@ from dbx_distributed_pytorch_examples_amd.ops import kernels as K  # noqa: E402
 
 
 def run(model, batch, img, lab, patch: bool):
-    K._PATCH3 = ("all" if patch else "0", "dgrad")
-    os.environ["DBX_STEM_PATCH"] = "1" if patch else "0"
+    os.environ["DBX_ENGINE"] = f"patch3={'all' if patch else '0'},stem_patch={int(patch)}"
     m = copy.deepcopy(model)
     tr = NativeTrainer(m, batch, (224, 224), torch.device("cuda"),
                        optim=OptimConfig(lr=0.0, momentum=0.0, weight_decay=0.0), use_graphs=False)

@@ -1,4 +1,4 @@
-"""Per-phase device time of the native ResNet-50 step (DBX_PROFILE_PHASES=1: eager phases with
+"""Per-phase device time of the native ResNet-50 step (DBX_PROFILE=phases: eager phases with
 hipEvent timers and roctx ranges)."""
 import json
 import os

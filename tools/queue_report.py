@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-queue kernel classes of the last replayed steps of a rocprofv3 kernel trace: which hardware
-queue the comm branch (scale kernels of DBX_COMM_LOOPBACK / RCCL kernels), the weight-gradient side
+queue the comm branch (scale kernels of comm_loopback / RCCL kernels), the weight-gradient side
 stream and the main chain land on, and how often a comm kernel ran on the same queue as a weight
 gradient.   python tools/queue_report.py run_kernel_trace.csv|run_results.db [--steps 2]"""
 import argparse

@@ -61,9 +61,6 @@ def main():
     ap.add_argument("--modes", default="fwd,fwdt,dgrad0,dgrad1,dgrad2,dgrad1b,dgrad2b,wgrad")
     ap.add_argument("--dma", type=int, default=1,
                     help="also time the LDS-DMA operand paths of the fwd / dgrad kernels (tile x path)")
-    ap.add_argument("--rowtile", action="store_true",
-                    help="also time the row-tile kernel (tile dma 7) on the BN-prologue 1x1 convs "
-                         "(1.2-3x slower on every ResNet-50 b1024 shape: profiles/r4_s4/)")
     ap.add_argument("--fast", type=float, default=0.0,
                     help="eight-wave mode: time only the current table entry against the eight-wave kernel "
                          "(csrc/conv_fast.hip, tile dma 4 / 5) on the plain-operand stride-1 fwd0 / dgrad1 / "
@@ -170,8 +167,6 @@ def main():
                 pro = mode in ("fwdt", "dgrad1b", "dgrad2b") or (mode == "fwd" and psc is not None)
                 dmas = ((0, 1) if pro else (0, 2, 3, 6)) if a.dma else (0,)
                 cands = [t + (d,) for t in TILES if OCm % t[1] == 0 for d in dmas]
-                if pro and a.rowtile and Rk == 1 and sk == 1 and Kin <= 512 and OCm % 128 == 0:
-                    cands.append((128, 128, 7))  # row-tile kernel (conv_rowtile.hip): A resident, weights streamed
             res = {t: [] for t in cands}
             for _ in range(a.rounds):
                 for t in cands:
