@@ -137,9 +137,18 @@ class NativeTrainer:
         # gradients in order on the main stream, every range posted right after its own phase
         # (per-gradient forks next to the comm stream cost more than they overlapped:
         # profiles/r2s2_multirank/).
-        if self.segmented and getattr(self.prog, "side_block_default", False):
-            # the per-block default of the larger single-GPU steps posts nothing per segment: the
-            # multi-rank step keeps the batched side stream and its late posts (the validated layout)
+        # The per-block layout (the single-GPU default: one side fork per residual block, lazy joins)
+        # keeps its schedule in the one-graph step (multirank_layout "block"): every weight gradient of
+        # segment k is queued on the side stream by the end of phase k, so the segment's collective is
+        # posted on that same stream right behind its last block batch -- in order, no late post -- and
+        # only the ranges whose last gradients run on the main stream in a later phase (layer1's
+        # block_tail_main gradients, computed after the stem backward) move to the last phase's post.
+        self.block_posts = bool(self.segmented and getattr(self.prog, "side_block_default", False)
+                                and cfg.multirank_layout == "block" and self.ncomm is not None
+                                and cfg.comm_side and device.type == "cuda")
+        if self.segmented and getattr(self.prog, "side_block_default", False) and not self.block_posts:
+            # the batched side stream with late posts (round 5's multi-rank layout; the c10d
+            # per-segment graphs can carry no fork across a graph boundary)
             p, pol = self.prog, cfg.policy
             p.side_block, p.side_batch = False, True
             p.side_defer = cfg.side_defer if cfg.side_defer is not None else pol.small(p.fwd_flops)
@@ -168,13 +177,14 @@ class NativeTrainer:
         # collective in the graph (world-1 comm_loopback=2) TinyImageNet fell from 97.9k to 85.5k
         # img/s and the headline by 1.2 % (profiles/r5_comm_queue/). The joins then wait on an event
         # behind each batch, not on the collectives queued after it.
-        self.comm_side = bool(self.ncomm is not None and self.late_posts and device.type == "cuda" and cfg.comm_side)
+        self.comm_side = bool(self.ncomm is not None and (self.late_posts or self.block_posts)
+                              and device.type == "cuda" and cfg.comm_side)
         if self.comm_side:
             self.comm_stream = self.prog.side_stream()
             self.prog.event_joins = True
             if cfg.side_defer is None:
                 self.prog.side_defer = True  # (the side branch then keeps its own hardware queue)
-        if self.segmented and (self.prog.side_block or not self.comm_side):
+        if self.segmented and ((self.prog.side_block and not self.block_posts) or not self.comm_side):
             # collectives posted per segment need that segment's weight gradients joined at its end
             # (lazy joins only where the collectives ride the side stream behind the batches)
             self.prog.lazy_join = False
@@ -237,6 +247,13 @@ class NativeTrainer:
             shifted = [None] + rgs[:-1]
             shifted[-1] = [r for r in (rgs[-2], rgs[-1]) if r is not None] if len(rgs) > 1 else rgs[-1]
             phases = [(n, fn, post) for (n, fn, _), post in zip(phases, shifted)]
+        elif self.segmented and self.block_posts:
+            # per-block layout: each range at its own phase's end, layer1's with the stem's when its last
+            # block's tail gradients run on the main stream after the stem backward (see __init__)
+            if self.prog.block_tail_main > 0 and len(phases) > 1:
+                rgs = [ph[2] for ph in phases]
+                shifted = rgs[:-2] + [None, [r for r in (rgs[-2], rgs[-1]) if r is not None]]
+                phases = [(n, fn, post) for (n, fn, _), post in zip(phases, shifted)]
         elif self.segmented:
             phases = self._merge_phases(phases)
         z = self.zero

@@ -1288,7 +1288,7 @@ class ResNetProgram:
         if not self.fuse_dw or last or b.kind != "bottleneck":
             return False
         c3 = b.convs[-1]
-        return ((c3.R, c3.S, c3.stride, c3.pad) == (1, 1, 1, 0)
+        return ((c3.R, c3.S, c3.stride, c3.pad) == (1, 1, 1, 0) and c3.OH >= self.cfg.fuse_dw_min_hw
                 and K.dwfused_preferred(c3.IC, c3.OC, self.N * c3.OH * c3.OW))
 
     def _fold(self, cv, dense: bool = False) -> bool:

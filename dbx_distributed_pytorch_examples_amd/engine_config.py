@@ -76,6 +76,7 @@ class EngineConfig:
     fuse_bwd_apply: bool = True     # BN-backward apply of a 1x1 conv's output BN in its dgrad prologue
     fuse_dw: bool = True            # bottleneck conv3 backward as one kernel (r2s4_dwfused/)
     fuse_dw_min_tiles: int = 4      # ... where every resident workgroup walks at least N tiles
+    fuse_dw_min_hw: int = 0         # ... and only on maps of at least this size (56: layer1 only)
     fuse_stem_bwd: bool = False     # stem backward as one kernel (slower: r2s4_stem/)
     fast_mat: bool = True           # materialised BN output for 3x3 consumers on the eight-wave kernel
     act_writeback: bool = True      # block-internal BN outputs stored by the MASK_Y dgrad epilogue
@@ -114,6 +115,9 @@ class EngineConfig:
     seg_side: bool = True           # batched side stream with late posts in the one-graph multi-rank step
     comm: str = "native"            # native: framework RCCL communicator, one graph; torch: c10d
     comm_side: bool = True          # collectives on the side stream behind their batch (r5_comm_queue/)
+    # one-graph multi-rank step where the single-GPU step forks per block: "block" keeps that layout
+    # (posts per segment behind its last block batch), "batch" the round-5 batched layout with late posts
+    multirank_layout: str = "block"
     comm_loopback: int = 0          # world-1 test aid: all-reduce scales by W, update divides by W
     allreduce_bf16: bool = False    # bf16 gradient all-reduce
     direct_ar: bool = False         # direct two-shot xGMI all-reduce for small buckets (opt-in)

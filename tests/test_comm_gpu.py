@@ -136,7 +136,8 @@ def test_nonblocking_init_and_captured_check(world1):
     c.close()
 
 
-@pytest.mark.parametrize("comm_side", ["1", "0", "1+defer", "1+defer+lazy", "1+defer+dsf"])
+@pytest.mark.parametrize("comm_side", ["1", "0", "1+defer", "1+defer+lazy", "1+defer+dsf",
+                                       "block", "block+btail0", "block+nodefer", "block+nolazy"])
 @pytest.mark.parametrize("model,hw,batch", [("resnet18", 32, 32), ("resnet50", 64, 16)])
 def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batch, comm_side, engine):
     """The one-graph multi-rank step's all-reduce ORDER, checked at world 1: with comm_loopback=2
@@ -144,16 +145,31 @@ def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batc
     update halves it, so the trajectory equals the plain one bit for bit -- unless a bucket is reduced
     before its weight gradients are final (late posts, batched side stream), which at world 1 with a
     real all-reduce (the identity) would go unnoticed. ``comm_side`` 1: the collectives on the
-    weight-gradient side stream behind their batch (event-scoped joins); 0: a separate comm stream."""
+    weight-gradient side stream behind their batch (event-scoped joins); 0: a separate comm stream
+    (both: the batched layout, multirank_layout=batch). "block": the per-block layout of the
+    single-GPU step kept in the one-graph step (multirank_layout=block, the default): every segment's
+    collective right behind its last block batch, layer1's with the stem's (its last block's tail
+    gradients run on the main stream after the stem backward; btail0: none do)."""
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
     engine(segmented_graphs="1")
     engine(comm="native")
-    engine(comm_side=comm_side[0])
-    engine(side_defer="1" if "defer" in comm_side else "0")
-    engine(lazy_join="1" if "lazy" in comm_side else "0")
-    # "dsf": the downsample forwards on the same side stream as the collectives (ds_fwd_side)
-    engine(ds_fwd_side="1" if "dsf" in comm_side else "0")
+    block = comm_side.startswith("block")
+    if block:
+        engine(multirank_layout="block")
+        if "btail0" in comm_side:
+            engine(block_tail_main=0)
+        if "nodefer" in comm_side:
+            engine(side_defer=0)
+        if "nolazy" in comm_side:
+            engine(lazy_join=0)
+    else:
+        engine(multirank_layout="batch")
+        engine(comm_side=comm_side[0])
+        engine(side_defer="1" if "defer" in comm_side else "0")
+        engine(lazy_join="1" if "lazy" in comm_side else "0")
+        # "dsf": the downsample forwards on the same side stream as the collectives (ds_fwd_side)
+        engine(ds_fwd_side="1" if "dsf" in comm_side else "0")
     torch.manual_seed(0)
     m1 = build_model(model, num_classes=10)
     m2 = copy.deepcopy(m1)
@@ -161,9 +177,14 @@ def test_one_graph_step_post_order_loopback(world1, monkeypatch, model, hw, batc
     t1 = NativeTrainer(m1, batch, (hw, hw), torch.device("cuda"), optim=OptimConfig(lr=0.05))
     engine(comm_loopback=None)
     t2 = NativeTrainer(m2, batch, (hw, hw), torch.device("cuda"), optim=OptimConfig(lr=0.05))
-    assert t1.ncomm is not None and t1.loopback == 2 and t2.loopback == 1 and t1.late_posts
-    assert t1.comm_side == (comm_side[0] == "1") and t1.prog.event_joins == t1.comm_side
-    assert t1.prog.side_defer == ("defer" in comm_side) and t1.prog.ds_fwd_side == ("dsf" in comm_side)
+    assert t1.ncomm is not None and t1.loopback == 2 and t2.loopback == 1
+    if block:
+        assert t1.block_posts and t1.prog.side_block and not t1.late_posts and t1.comm_side
+        assert t1.prog.side_defer == ("nodefer" not in comm_side) and t1.prog.lazy_join == ("nolazy" not in comm_side)
+    else:
+        assert t1.late_posts and not t1.block_posts
+        assert t1.comm_side == (comm_side[0] == "1") and t1.prog.event_joins == t1.comm_side
+        assert t1.prog.side_defer == ("defer" in comm_side) and t1.prog.ds_fwd_side == ("dsf" in comm_side)
     g = torch.Generator().manual_seed(1)
     for i in range(6):
         img = torch.randint(0, 256, (batch, hw, hw, 3), dtype=torch.uint8, generator=g).cuda()
