@@ -25,4 +25,6 @@ DBX_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --preset resnet
   > $O/bench_gloo2.log 2>&1 || { tail -20 $O/bench_gloo2.log; exit 1; }
 grep '"metric"' $O/bench_gloo2.log >> $O/bench_lines.txt
 grep "replicas in sync" $O/bench_gloo2.log
+# a multi-rank number measured after a fallback (fresh-rank re-run or c10d rebuild) is not a pass
+if grep -q '"comm_fallback": "' $O/bench_lines.txt; then echo "a bench line fell back: $(grep -o '"comm_fallback": "[^"]*"' $O/bench_lines.txt)"; exit 1; fi
 bash tools/gpu/profile_headline.sh $O/prof
