@@ -149,6 +149,8 @@ def main():
                 print(f"  {k} {c}: rejected ({type(e).__name__}: {str(e)[:80]})", flush=True)
                 t = None
             keep = False
+            if t is not None:
+                print(f"  {k} {c}: {t:.4f} ms/step (best {best:.4f}; {time.time() - t0:.0f} s)", flush=True)
             if t is not None and t < best * (1 - a.thresh):
                 # confirm: the incumbent again, then the candidate again
                 if prev is None:
