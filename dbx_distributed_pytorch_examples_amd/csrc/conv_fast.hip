@@ -27,16 +27,10 @@ namespace dbx {
 // a 4-slot ring of 32-channel stages keeps three stages (3 x 1024 MFMA cycles per SIMD) in flight in
 // the 128 KiB two 64-channel slots took (cdna_hip_programming.md §5, the 256^2 template's half-tile
 // prefetch).
-// NW: waves per workgroup -- 8 (two per SIMD: 128 x 64 wave tiles at BN 256, 64 x 64 at BN 128) or 4
-// (one per SIMD, 2 x 2: 128 x 128 / 128 x 64 wave tiles, the accumulators in AGPRs): a bigger wave
-// tile reads fewer LDS bytes per MFMA ((1/rows + 1/cols) of the wave tile).
-#ifndef DBX_FAST_NW
-#define DBX_FAST_NW 8
-#endif
-template <int BN, int MODE, bool STATS, bool ACCUM, int EPI, int NBUF, int BK = 64, int NW = DBX_FAST_NW>
-__global__ __launch_bounds__(64 * NW, 1) void fast_igemm_kernel(const IGemmArgs a) {
-  constexpr int BM = 256, NT = 64 * NW;
-  constexpr int WM = NW == 4 ? 2 : (BN == 256 ? 2 : 4), WN = NW / WM;
+template <int BN, int MODE, bool STATS, bool ACCUM, int EPI, int NBUF, int BK = 64>
+__global__ __launch_bounds__(512, 1) void fast_igemm_kernel(const IGemmArgs a) {
+  constexpr int BM = 256, NT = 512, NW = 8;
+  constexpr int WM = BN == 256 ? 2 : 4, WN = NW / WM;
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   constexpr int CPR = BK / 8;          // 16-B chunks per tile row
   constexpr int RPP = NT / CPR;        // tile rows per DMA pass (CPR lanes x 16 B per row)
@@ -181,7 +175,7 @@ template <int BN, int MODE, bool STATS, bool ACCUM, int EPI>
 static int launch_fast(const IGemmArgs& a, hipStream_t st) {
   const int ntile = (a.OC / BN) * ((a.M + 255) / 256);
   hipLaunchKernelGGL((fast_igemm_kernel<BN, MODE, STATS, ACCUM, EPI, BN == 256 ? 2 : 3, 64>), dim3(ntile),
-                     dim3(64 * DBX_FAST_NW), 0, st, a);
+                     dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 
