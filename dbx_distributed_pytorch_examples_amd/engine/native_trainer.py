@@ -200,6 +200,7 @@ class NativeTrainer:
             self.mom2 = self.zero.v
         self.lars = self._lars_segments() if optim.name == "lars" else None
         self._build_phases()
+        self.opt_ranges = self._optimizer_ranges()
         # broadcast initial parameters from rank 0 (DDP constructor semantics, M2)
         if self.world > 1:
             src = 0 if process_group is None else dist.get_global_rank(process_group, 0)
@@ -264,6 +265,72 @@ class NativeTrainer:
         phases.append(("optimizer", self._optimizer_phase, z.gather if z is not None else None))
         self.phases = phases
 
+    def _optimizer_ranges(self):
+        """The optimizer inside the backward (engine field ``overlap_optimizer``): SGD / Adam are
+        element-wise, so each backward segment's parameters are updated as soon as that segment's
+        gradients are final (and, at world > 1, all-reduced), on the weight-gradient side stream right
+        behind the segment's last block batch (and its collective) -- the step no longer ends with a
+        serial update of every parameter. Per phase the ranges to update after it; the last phase's
+        (and layer1's, whose last block's tail weight gradients run on the main stream after the stem
+        backward) go on the main stream after the final join; element ranges no segment covers are
+        updated in the optimizer phase. Off (None) for clipping / LARS (global norms), ZeRO (its own
+        sharded update), the c10d per-segment graphs and the batched side-stream layouts."""
+        p, cfg = self.prog, self.cfg
+        if not (cfg.overlap_optimizer != 0 and self.zero is None and self.lars is None
+                and not (self.opt.grad_clip and self.opt.grad_clip > 0)
+                and p.side_block and p.overlap_wgrad and (not self.segmented or self.block_posts)):
+            return None
+        nph = len(self.seg_ranges)
+        per = [[r] if r is not None else [] for r in self.seg_ranges]
+        if nph > 1 and p.block_tail_main > 0:
+            per[-1] = per[-2] + per[-1]
+            per[-2] = []
+        if cfg.overlap_optimizer > 0:  # only the first N segments inside the backward
+            per = [rs if k < cfg.overlap_optimizer else [] for k, rs in enumerate(per)]
+        covered = sorted(r for rs in per for r in rs)
+        gaps, pos = [], 0  # (merged: the segments are contiguous in backward order, one launch each gap)
+        for lo, hi in covered:
+            if lo > pos:
+                gaps.append((pos, lo))
+            pos = max(pos, hi)
+        if pos < p.n_params:
+            gaps.append((pos, p.n_params))
+        if not covered:
+            return None
+        return {"per_phase": per, "gaps": gaps}
+
+    def _update_range(self, lo: int, hi: int):
+        p, o = self.prog, self.opt
+        gscale = 1.0 / (self.world * self.loopback)
+        if o.name == "sgd":
+            K.sgd_step(p.master[lo:hi], p.grad[lo:hi], self.mom[lo:hi], None, lr=o.lr, momentum=o.momentum,
+                       dampening=o.dampening, weight_decay=o.weight_decay, nesterov=o.nesterov, first=False,
+                       grad_scale=gscale, hyper=self.hyper)
+        else:
+            K.adam_step(p.master[lo:hi], p.grad[lo:hi], self.mom[lo:hi], self.mom2[lo:hi], None, lr=o.lr,
+                        beta1=o.betas[0], beta2=o.betas[1], eps=o.eps, weight_decay=o.weight_decay,
+                        decoupled=(o.name == "adamw"), step=1, grad_scale=gscale, hyper=self.hyper)
+
+    def _after_phase_updates(self, i: int):
+        """Issue phase i's parameter updates (see _optimizer_ranges)."""
+        if self.opt_ranges is None:
+            return
+        rs = self.opt_ranges["per_phase"][i] if i < len(self.opt_ranges["per_phase"]) else []
+        if not rs:
+            return
+        last = i == len(self.opt_ranges["per_phase"]) - 1
+        if self.dev.type != "cuda" or last:
+            for r in rs:  # (the last phase ended with the final join: on the main stream)
+                self._update_range(*r)
+            return
+        run = (lambda rs=rs: [self._update_range(*r) for r in rs])
+        if not self.prog.defer_on_side(run):  # behind the deferred batch (and collective), or now
+            side = self.prog.side_stream()
+            side.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(side):
+                run()
+            self.prog._side_pending = True  # (the next join, at the latest the final one, waits for it)
+
     def _merge_phases(self, phases):
         """Optional coarser graph segmentation of the multi-rank path: seg_groups "3:3" merges
         the six backward segments into two graphs (one all-reduce cut after layer3). Default: one
@@ -317,6 +384,10 @@ class NativeTrainer:
             if o.grad_clip and not self._zero_norm_separate:
                 self.zero.norm_phase()
             self.zero.update(hyper=self.hyper)
+            return
+        if self.opt_ranges is not None:  # updated inside the backward: only uncovered ranges remain
+            for r in self.opt_ranges["gaps"]:
+                self._update_range(*r)
             return
         gsp = None
         gdiv = self.world * self.loopback  # the reduced gradient is a sum over gdiv replicas
@@ -433,10 +504,11 @@ class NativeTrainer:
 
     def _run_phases_eager(self):
         if self.dev.type != "cuda":  # CPU (reference ops; gloo collectives, synchronous)
-            for name, fn, post in self.phases:
+            for i, (name, fn, post) in enumerate(self.phases):
                 fn()
                 if self.segmented:
                     self._post(post)
+                self._after_phase_updates(i)
             return
         cur = torch.cuda.current_stream(self.dev)
         for i, (name, fn, post) in enumerate(self.phases):
@@ -455,6 +527,7 @@ class NativeTrainer:
                     self.comm_stream.wait_stream(cur)
                     with torch.cuda.stream(self.comm_stream):
                         self._post(post)
+            self._after_phase_updates(i)
 
     def _graph_phases(self):
         return self.phases
@@ -486,8 +559,10 @@ class NativeTrainer:
             elif not self.segmented:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode=mode):
-                    for _, fn, _ in self.phases:
+                    for i, (_, fn, _) in enumerate(self.phases):
                         fn()
+                        self._after_phase_updates(i)
+                    self.prog.launch_pending()
                 self.graphs = [g]
             else:
                 for _, fn, _ in self._graph_phases():

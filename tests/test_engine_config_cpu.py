@@ -50,3 +50,31 @@ def test_explicit_config_overrides_environment(monkeypatch):
     assert p.overlap_wgrad and p.side_block and p.side_cu_reserve == 96 and p.dwf_cus == 128 and p.tail_main == 3
     q = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert not q.overlap_wgrad  # the environment's override
+
+
+@pytest.mark.parametrize("arch,size,optim,nseg", [("resnet18", 32, "sgd", -1), ("resnet50", 64, "sgd", -1),
+                                                  ("resnet50", 64, "adamw", 3), ("cifar_resnet18", 32, "sgd", 2)])
+def test_optimizer_in_backward_is_bit_identical(arch, size, optim, nseg, monkeypatch):
+    """overlap_optimizer: each backward segment's parameters are updated right after the segment (on the
+    side stream on a GPU; in program order here) -- no parameter may be read after its update within the
+    step, so three steps must give the end-of-step optimizer's parameters bit for bit."""
+    from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
+    from dbx_distributed_pytorch_examples_amd.models import build_model
+    o = OptimConfig(lr=0.05, momentum=0.9, weight_decay=5e-4) if optim == "sgd" else \
+        OptimConfig(name="adamw", lr=1e-3, weight_decay=0.01)
+    out = {}
+    for ov in (True, False):
+        monkeypatch.setenv("DBX_ENGINE", f"overlap_optimizer={nseg if ov else 0}")
+        torch.manual_seed(0)
+        m = build_model(arch, num_classes=10)
+        tr = NativeTrainer(m, 4, (size, size), torch.device("cpu"), optim=o, use_graphs=False)
+        assert (tr.opt_ranges is not None) == ov
+        if ov:  # every parameter element is covered by a segment range or a gap range
+            rs = sorted(r for ph in tr.opt_ranges["per_phase"] for r in ph) + tr.opt_ranges["gaps"]
+            assert sum(hi - lo for lo, hi in rs) >= tr.prog.n_params
+        g = torch.Generator().manual_seed(3)
+        for _ in range(3):
+            tr.step(torch.randint(0, 256, (4, size, size, 3), dtype=torch.uint8, generator=g),
+                    torch.randint(0, 10, (4,), generator=g))
+        out[ov] = (tr.prog.master.clone(), tr.mom.clone())
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
