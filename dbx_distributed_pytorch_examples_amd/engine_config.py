@@ -73,8 +73,9 @@ class EngineConfig:
     dwf_cus: Optional[int] = None
     # the optimizer inside the backward: the first N backward segments' SGD / Adam updates (head, layer4,
     # layer3, ...) on the side stream right behind each segment's last block batch (and collective); the
-    # rest in one update at the end of the step (-1: every segment, 0: off)
-    overlap_optimizer: int = 3
+    # rest in one update at the end of the step (-1: every segment, 0: off). Off: measured 1 % slower on
+    # ResNet-18 CIFAR and flat on TinyImageNet / the headline for every N (profiles/r6_optbw/)
+    overlap_optimizer: int = 0
     # ---- fusion structure ----
     fuse_tail: bool = True          # block outputs computed in the next conv1's prologue
     fuse_bwd_apply: bool = True     # BN-backward apply of a 1x1 conv's output BN in its dgrad prologue

@@ -348,6 +348,17 @@ def agent_store(timeout_s: float = 60.0):
         return None
 
 
+def _die_with_parent() -> None:
+    """preexec_fn of a supervised child: SIGKILL when the supervisor dies (Linux PR_SET_PDEATHSIG), so no
+    rank process outlives a supervisor that was killed outright."""
+    try:
+        import ctypes
+        import signal
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL)  # PR_SET_PDEATHSIG = 1
+    except Exception:  # noqa: BLE001 - best effort (non-Linux)
+        pass
+
+
 def _kill_tree(p: "subprocess.Popen", grace_s: float = 10.0) -> None:
     import signal
     for sig, wait in ((signal.SIGTERM, grace_s), (signal.SIGKILL, 30.0)):
@@ -397,7 +408,8 @@ def supervise_rank(cmd: List[str], fallback_env: Callable[[str], Dict[str, str]]
         return None
 
     def run(attempt, env):
-        p = subprocess.Popen(list(cmd), env=env, start_new_session=True)
+        p = subprocess.Popen(list(cmd), env=env, start_new_session=True, preexec_fn=_die_with_parent)
+        current[0] = p
         t_peer = None
         while True:
             try:
@@ -411,6 +423,18 @@ def supervise_rank(cmd: List[str], fallback_env: Callable[[str], Dict[str, str]]
                       f"{peer_grace_s:.0f}s; killing it", file=sys.stderr, flush=True)
                 _kill_tree(p)
                 return p.returncode if p.returncode is not None else -9
+
+    # a supervisor that is told to stop (torchrun tearing the group down, a timeout) takes its child's
+    # whole process group with it -- the child runs in a session of its own
+    current = [None]
+
+    def on_signal(signum, frame):
+        if current[0] is not None and current[0].poll() is None:
+            _kill_tree(current[0], grace_s=5.0)
+        os._exit(128 + signum)
+    import signal
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, on_signal)
 
     rc = run(0, base)
     store.set(key(0, f"rc/{rank}"), str(rc))

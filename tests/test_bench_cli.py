@@ -151,3 +151,41 @@ def test_diverged_one_graph_step_is_remeasured_on_c10d(monkeypatch, capsys, engi
     calls.clear()
     monkeypatch.setattr(bench, "_measure", lambda *a: (calls.append(1), (4, 0.0, {"_native_comm": False}))[1])
     assert bench.main(["--steps", "1", "--warmup", "0", "--preset", "resnet18_cifar10"]) == 4 and calls == [1]
+
+
+def test_torchrun_teardown_takes_the_supervised_children_along():
+    """When torchrun tears the group down (here: SIGTERM to the whole launcher), no supervised rank
+    child may survive it: the supervisors kill their children's process groups on SIGTERM and the
+    children die with their parent (PR_SET_PDEATHSIG) -- otherwise a hung rank would keep the GPU."""
+    import signal
+    import socket
+    import time
+
+    import psutil
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    env = dict(os.environ, DBX_DIST_BACKEND="gloo", DBX_FAULT="0:0:hang")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                          "--gpus", "2", "--preset", "resnet18_cifar10", "--batch", "4", "--steps", "1", "--warmup", "2",
+                          "--phase-timeout", "600"], cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL, start_new_session=True)
+    try:
+        deadline, kids = time.time() + 180, []
+        while time.time() < deadline:  # wait for both ranks' supervised children
+            kids = [c for c in psutil.Process(p.pid).children(recursive=True)
+                    if "bench.py" in " ".join(c.cmdline()) and c.environ().get("DBX_SUPERVISED_CHILD")]
+            if len(kids) >= 2:
+                break
+            time.sleep(1)
+        assert len(kids) >= 2, "supervised children did not start"
+        time.sleep(5)
+        os.killpg(p.pid, signal.SIGTERM)
+        p.wait(60)
+        gone, alive = psutil.wait_procs(kids, timeout=60)
+        assert not alive, f"children outlived the launcher: {[c.pid for c in alive]}"
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)

@@ -505,7 +505,7 @@ def test_batched_side_stream_bit_identical(arch, size, batch, mode, monkeypatch,
 @pytest.mark.parametrize("arch,size,batch,optim", [("resnet50", 64, 32, "sgd"), ("resnet18", 32, 64, "sgd"),
                                                    ("resnet50", 64, 32, "adamw")])
 def test_optimizer_in_backward_bit_identical(arch, size, batch, optim, engine):
-    """overlap_optimizer (default): each segment's update runs on the side stream behind its last block
+    """overlap_optimizer (opt-in): each segment's update runs on the side stream behind its last block
     batch, inside the captured step -- bit-identical to the end-of-step optimizer over graph replays."""
     from dbx_distributed_pytorch_examples_amd.engine.native_trainer import NativeTrainer, OptimConfig
     from dbx_distributed_pytorch_examples_amd.models import build_model
