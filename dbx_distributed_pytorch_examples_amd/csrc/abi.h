@@ -84,6 +84,14 @@ struct IGemmArgs {
   // stats) -- the separate finalize launch between producer and consumer disappears. TAIL: an array
   // of two when the shortcut has a BN (res_scale set): [0] the block's last BN, [1] the shortcut's
   const BnFin* fin_in;
+  // ---- split-K (implicit-GEMM kernel, non-persistent launches) ---------------------------------
+  // ksplit > 1: ntile x ksplit workgroups, slice s covering K blocks [s*kper, min(KB, (s+1)*kper));
+  // each stores its fp32 partial tile to skws[s][tile] and the workgroup that draws the tile's last
+  // ticket from skcnt[tile] (zero; reset by that workgroup) sums the slices in slice order and runs the
+  // epilogue -- the same bits whichever slice finishes last
+  float* skws;
+  unsigned* skcnt;
+  int ksplit, kper;
 };
 struct WgradArgs {
   const bf16* dy;        // [M][OC]

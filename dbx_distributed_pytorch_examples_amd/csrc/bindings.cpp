@@ -105,7 +105,7 @@ PYBIND11_MODULE(_C, m) {
                          uintptr_t inv2, uintptr_t bstats1, uintptr_t bstats2, uintptr_t a_out, uintptr_t res,
                          uintptr_t res_scale, uintptr_t res_shift, uintptr_t tail_out, uintptr_t tail_bits,
                          uintptr_t st, int dma, uintptr_t fin1, uintptr_t fin2, int fin_base, int fin_final,
-                         uintptr_t fin_in) {
+                         uintptr_t fin_in, int ksplit, int kper, uintptr_t skws, uintptr_t skcnt) {
     dbx::IGemmArgs a{P<const bf16*>(x), P<const bf16*>(w), P<bf16*>(y), P<const float*>(in_scale),
                      P<const float*>(in_shift), P<double*>(stats), N, IH, IW, IC, OH, OW, OC, R, S_, stride, pad,
                      N * OH * OW, nshard > 0 ? nshard : 1, relu_in, nr, ns, r0, s0, tstep, dh0, dw0, osub, oph, opw,
@@ -115,7 +115,8 @@ PYBIND11_MODULE(_C, m) {
                      P<double*>(bstats2), P<bf16*>(a_out), P<const bf16*>(res), P<const float*>(res_scale),
                      P<const float*>(res_shift), P<bf16*>(tail_out), P<unsigned char*>(tail_bits), 0ull, 0ull,
                      P<const dbx::BnFin*>(fin1), P<const dbx::BnFin*>(fin2), fin_base, fin_final,
-                     P<const dbx::BnFin*>(fin_in)};
+                     P<const dbx::BnFin*>(fin_in), P<float*>(skws), P<unsigned*>(skcnt), ksplit > 1 ? ksplit : 1,
+                     kper};
     if (fin_in && !in_scale) throw std::invalid_argument("conv_igemm: input finalize without a BN prologue");
     if ((fin1 || fin2) && !(stats || bstats1)) throw std::invalid_argument("conv_igemm: BN finalize without statistics");
     if (fin2 && !bstats2) throw std::invalid_argument("conv_igemm: second BN finalize without its statistics");

@@ -623,6 +623,10 @@ extern "C" int dbx_conv_fast(int mode, int bn, const IGemmArgs* args, int stats,
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
                               int accum, int epi, hipStream_t st, int dma) {
   const IGemmArgs& a = *args;
+  if (a.ksplit > 1) {  // split-K: the implicit-GEMM kernel only, every slice non-empty, a counter per tile
+    if ((dma != 0 && dma != 1) || mode == STEM || mode == FWD_PATCH || mode == DGRAD_PATCH) return -67;
+    if (a.kper < 1 || a.skws == nullptr || a.skcnt == nullptr) return -68;
+  }
   if (dma == 4) {  // eight-wave 256-row kernel (conv_fast.hip): plain operands, stride-1 data gradients
     if (bm != 256 || pro || mode == STEM || (mode == DGRAD && (a.osub != 1 || a.add_sub > 1))) return -65;
     return dbx_conv_fast(mode, bn, args, stats, accum, epi, st);

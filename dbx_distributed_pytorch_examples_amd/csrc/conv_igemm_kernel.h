@@ -313,6 +313,54 @@ __device__ __forceinline__ void igemm_epilogue(const IGemmArgs& a, f32x4 (&acc)[
   }
 }
 
+// Split-K combine (IGemmArgs ksplit > 1): every slice stores its fp32 accumulators write-through (sc1)
+// to its slab, drains them, and takes a ticket from the tile's counter; the workgroup that draws the
+// last ticket reads every slab with sc1 loads (L1 bypassed: the other slices ran on other CUs) and sums
+// them in slice order -- bit-identical whichever slice finished last -- then resets the counter for the
+// next launch (cdna_hip_programming.md section 5, in-launch split-K reduction; the weight gradient's
+// wgrad_store in conv_igemm.hip is the same hand-off). Returns true in the reducer (acc = the sum);
+// the LDS is free again when it returns.
+template <int TM, int TN, int NT>
+__device__ __forceinline__ bool splitk_combine(const IGemmArgs& a, f32x4 (&acc)[TM][TN], const int tile,
+                                               const int slice, const int ntile, bf16* lds) {
+  constexpr int TILE = TM * TN * NT * 4;  // fp32 elements per tile slab
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const rsrc_t ws = make_rsrc(a.skws, (unsigned long long)a.ksplit * ntile * TILE * 4);
+  auto slot = [&](int s, int i, int j) __attribute__((always_inline)) {
+    return (unsigned)((((size_t)s * ntile + tile) * TILE + ((size_t)(wid * TM + i) * TN + j) * 256 + lane * 4) * 4);
+  };
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), ws, slot(slice, i, j), 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab has reached memory
+  __syncthreads();                                   // ... every wave's; the LDS is no longer read
+  int* flag = reinterpret_cast<int*>(lds);
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add((gu32*)(a.skcnt + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = t == (unsigned)(a.ksplit - 1);
+  }
+  __syncthreads();
+  const bool last = flag[0] != 0;
+  __syncthreads();  // every wave has read the flag before the epilogue reuses the LDS
+  if (!last) return false;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      acc[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ws, slot(0, i, j), 0, 16));
+  for (int s = 1; s < a.ksplit; ++s) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ws, slot(s, i, j), 0, 16));
+  }
+  if (tid == 0) __hip_atomic_store((gu32*)(a.skcnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 // TAIL (with PRO), A = x*s + h + (res*rs + rh) computed while staging; the first N tile writes A
 // back (tail_out). FWD: the previous residual block's output relu(bn3(x) + shortcut) -- no separate
 // bn_apply pass, no re-read of the block output, ReLU mask written too. DGRAD (1x1 stride-1): the
@@ -364,6 +412,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // The "l" indices are the LOADER's tile (the one being staged), m0/n0/tm the epilogue's.
   int ltm = 0, ltn = 0, lm0 = 0, ln0 = 0;
   int lk = 0, lcb = 0, lts = 0, ltr = 0;  // next K block to load (see advance())
+  const int KTOT = (MODE == STEM) ? 256 : a.R * a.S * a.IC;  // weight row length
+  const int cpt = (MODE == STEM) ? 1 : a.IC / BK;              // K blocks per tap
+  const int KB = (MODE == STEM) ? 4 : a.nr * a.ns * cpt;
+  // split-K (a.ksplit > 1; register-staged A operand paths only, never STEM, never persistent): this
+  // workgroup's tile, slice and K-block range (the LDS-DMA ring variants compile without it: +15-60 VGPRs)
+  const bool split = MODE != STEM && DMA <= 1 && a.ksplit > 1;  // workgroup-uniform
+  int ltile = 0, slice = 0, kb_lo = 0, kb_hi = KB;
 
   // ---- per-thread A rows: decompose output pixel once per tile ---------------------
   const int ach = tid & (CPR - 1);
@@ -375,10 +430,23 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   int ahb[A_CH], awb[A_CH];  // top-left input coordinate of the row's receptive field
   unsigned apix[A_CH];       // byte offset of (n, ahb, awb, ach*8) in x (host: bytes < kOOB)
   auto set_tile = [&](int t) __attribute__((always_inline)) {
-    const int bid = xcd_remap(t, ntile);
+    int bid;
+    if (split) {  // a tile's slices are consecutive remapped ids: one XCD's L2 holds its slabs
+      const int id = xcd_remap(t, ntile * a.ksplit);
+      bid = id / a.ksplit;
+      slice = id - bid * a.ksplit;
+      kb_lo = slice * a.kper;
+      kb_hi = kb_lo + a.kper < KB ? kb_lo + a.kper : KB;
+    } else {
+      bid = xcd_remap(t, ntile);
+    }
+    ltile = bid;
     ltm = bid / ntn; ltn = bid - ltm * ntn;
     lm0 = ltm * BM; ln0 = ltn * BN;
-    lk = lcb = lts = ltr = 0;
+    lk = kb_lo;
+    lcb = kb_lo % cpt;
+    lts = (kb_lo / cpt) % a.ns;
+    ltr = (kb_lo / cpt) / a.ns;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int m = lm0 + tid / CPR + RPP * i;
@@ -399,10 +467,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   int tcur = blockIdx.x;
   set_tile(tcur);
   const rsrc_t xr = make_rsrc(a.x, 2ull * a.N * a.IH * a.IW * a.IC);
-  const int KTOT = (MODE == STEM) ? 256 : a.R * a.S * a.IC;  // weight row length
   const rsrc_t wr = make_rsrc(a.w, 2ull * a.OC * KTOT);
-  const int cpt = (MODE == STEM) ? 1 : a.IC / BK;              // K blocks per tap
-  const int KB = (MODE == STEM) ? 4 : a.nr * a.ns * cpt;
+  const int NKB = kb_hi - kb_lo;  // K blocks of this workgroup (all of them unless split)
 
   // Two register staging sets: the loads of block kb+2 are issued while block kb+1's data (set
   // issued one iteration earlier) is still landing, so each global load has two blocks of MFMA
@@ -476,11 +542,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       const int cb = lcb * BK;
       const int r = a.r0 + a.tstep * ltr, s = a.s0 + a.tstep * lts;
       if constexpr (PRO) pcb[S] = cb;
-      if constexpr (TAIL) { wlive[S] = lk < KB && ltn == 0; wtoff[S] = 2u * (unsigned)cb; }
+      if constexpr (TAIL) { wlive[S] = lk < kb_hi && ltn == 0; wtoff[S] = 2u * (unsigned)cb; }
       // tap displacement, the same for all of this thread's rows (uniform, bytes)
       const int dh = (MODE == DGRAD) ? -ltr : r, dw = (MODE == DGRAD) ? -lts : s;
       const unsigned toff = 2u * (unsigned)((dh * a.IW + dw) * a.IC + cb);
-      const bool live = lk < KB;  // wave-uniform: false for the prefetches past the last block
+      const bool live = lk < kb_hi;  // wave-uniform: false for the prefetches past the last block
       avalid[S] = 0;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
@@ -598,7 +664,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     } else {
       koff = ((a.r0 + a.tstep * ltr) * a.S + a.s0 + a.tstep * lts) * a.IC + lcb * BK + ach * 8;
     }
-    const bool live = lk < KB;
+    const bool live = lk < kb_hi;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int n = ln0 + tid / CPR + RPP * i;
@@ -628,10 +694,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   const i32x4 wsrd = make_srd(a.w, DMA == 0 ? 0ull : 2ull * a.OC * KTOT);
   // B: the DMA-ed weights run ahead of A by one block less than the register pipeline (DMA 1), so
   // they keep their own K-block position (bk: block, bcb / bts / btr: channel block, tap column, row)
-  int bk = 0, bcb = 0, bts = 0, btr = 0;
+  int bk = kb_lo, bcb = kb_lo % cpt, bts = (kb_lo / cpt) % a.ns, btr = (kb_lo / cpt) / a.ns;
   auto dma_b = [&](int buf) __attribute__((always_inline)) {
     const int koff = ((a.r0 + a.tstep * btr) * a.S + a.s0 + a.tstep * bts) * a.IC + bcb * BK + lch * 8;
-    const bool live = bk < KB;  // past the last block: out-of-range offsets (zeros, no traffic)
+    const bool live = bk < kb_hi;  // past the last block: out-of-range offsets (zeros, no traffic)
     const unsigned dst = lds0 + 2u * (unsigned)(NBUF * BM * BK + buf * BN * BK) + 1024u * (unsigned)wid;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
@@ -647,7 +713,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     const int r = a.r0 + a.tstep * ltr, s = a.s0 + a.tstep * lts;
     const int dh = (MODE == DGRAD) ? -ltr : r, dw = (MODE == DGRAD) ? -lts : s;
     const unsigned toff = 2u * (unsigned)((dh * a.IW + dw) * a.IC + cb);
-    const bool live = lk < KB;
+    const bool live = lk < kb_hi;
     const unsigned dst = lds0 + 2u * (unsigned)(buf * BM * BK) + 1024u * (unsigned)wid;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
@@ -689,7 +755,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // and the loop body is branch-free, so hipcc's waitcnt pass sees the same in-flight loads on
   // every path and waits only for the older set (counted vmcnt) instead of draining to vmcnt(0).
   auto step = [&](int kb, int S) __attribute__((always_inline)) {
-    load_a(S ^ 1);  // block min(kb + 2, KB - 1)
+    load_a(S ^ 1);  // block kb + 2 (past the slice's end: no traffic)
     load_b(S ^ 1);
     advance();
     mma(kb & 1);
@@ -719,11 +785,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   int kb = 0;
-  for (; kb + 1 < KB; kb += 2) {
+  for (; kb + 1 < NKB; kb += 2) {
     step(kb, 1);
     step(kb + 1, 0);
   }
-  if (kb < KB) {
+  if (kb < NKB) {
     mma(kb & 1);
     __syncthreads();  // the epilogue's sC staging aliases the operand buffers
   }
@@ -733,13 +799,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
     // end of step kb, oldest first: B(kb+1) DMA, A(kb+2) loads, the tail write-back stores of
     // A(kb+1): the counted wait retires B(kb+1) and leaves the rest in flight.
     // (A(0) is already in flight: issued before the loop, or before the previous tile's epilogue)
+    // TAIL: load_a issues two loads per chunk (x and the shortcut / BN operand), pro_a one (DGRAD:
+    // tail_out) or two (FWD: + mask bits) stores; the counted wait must leave exactly the A(kb+2)
+    // loads and the stores in flight -- one chunk's worth fewer would also retire half of A(kb+2)
+    constexpr int A_LD = TAIL ? 2 * A_CH : A_CH;
     constexpr int TAIL_ST = TAIL ? (MODE == DGRAD ? A_CH : 2 * A_CH) : 0;
     dma_b(0);
     load_a(1);
     advance();
     pro_a(0);
     store_a(0, 0);
-    dma_wait<A_CH + TAIL_ST>();  // A(0), B(0) (older than the A(1) loads and the tail stores)
+    dma_wait<A_LD + TAIL_ST>();  // A(0), B(0) (older than the A(1) loads and the tail stores)
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -752,15 +822,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
       mma(kb & 1);
       pro_a(S);
       store_a((kb + 1) & 1, S);
-      dma_wait<A_CH + TAIL_ST>();
+      dma_wait<A_LD + TAIL_ST>();
       __syncthreads();
     };
     int kb = 0;
-    for (; kb + 1 < KB; kb += 2) {
+    for (; kb + 1 < NKB; kb += 2) {
       stepd(kb, 1);
       stepd(kb + 1, 0);
     }
-    if (kb < KB) mma(kb & 1);
+    if (kb < NKB) mma(kb & 1);
     dma_wait<0>();    // no DMA may still write the LDS the epilogue stages through
     __syncthreads();
   } else {
@@ -778,7 +848,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     int cur = 0;
-    for (int kb = 0; kb < KB; ++kb) {
+    for (int kb = 0; kb < NKB; ++kb) {
       dma_wait<(NBUF - 2) * ND>();  // this wave's part of block kb has landed
       __syncthreads();              // ... every wave's; and the slot issued next is no longer read
       const int nxt = cur == 0 ? NBUF - 1 : cur - 1;
@@ -802,14 +872,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void igemm_kernel(const IGemmArgs 
   // C through, so only after the barrier below)
   constexpr bool PF = EPI == 0 && !ACCUM && !TAIL && !(BM == 256 && BN == 64) && DMA <= 1;  // (+: register room)
   const int m0 = lm0, n0 = ln0, tm = ltm;
+  if (split) {  // (workgroup-uniform) the slices' sum in slice order: only the last arriver continues
+    if (!splitk_combine<TM, TN, NT>(a, acc, ltile, slice, ntile, lds)) return;
+  }
   tcur += gridDim.x;
-  const bool more = PF && tcur < ntile;  // workgroup-uniform
+  const bool more = PF && !split && tcur < ntile;  // workgroup-uniform
   if (more) {  // A (activations, HBM latency) now; B (weights, L2-resident) after the epilogue
     set_tile(tcur);
     load_a(0);
     if constexpr (DMA == 1) {
       advance();
-      bk = bcb = bts = btr = 0;
+      bk = bcb = bts = btr = 0;  // (persistent launches are never split: the slice is all of K)
     }
   }
 
@@ -853,7 +926,7 @@ static int launch_igemm_t(const IGemmArgs& a, hipStream_t st) {
   // (profiles/r5_persist_dma1/)
   constexpr int kPersistDma1 = 8;
   const bool one_per_wg = DMA == 1 && ntile < (long long)kPersistDma1 * cap;
-  const int nwg = (!PF || ntile <= cap || one_per_wg) ? ntile : cap;
+  const int nwg = a.ksplit > 1 ? ntile * a.ksplit : (!PF || ntile <= cap || one_per_wg) ? ntile : cap;
   hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, MODE, PRO, STATS, ACCUM, EPI, TAIL, DMA>), dim3(nwg), dim3(64 * WM * WN), 0, st, a);
   return (int)hipGetLastError();
 }

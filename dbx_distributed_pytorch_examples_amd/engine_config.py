@@ -111,6 +111,11 @@ class EngineConfig:
     wgrad_rounds: float = 2.0       # split-K depth target of the weight gradients (workgroup rounds)
     wgrad_fuse_max: int = 1 << 20   # largest weight gradient reduced in-launch
     head_splitk: bool = True        # split-K for the few-tile classifier-head GEMMs (r5_headsplit/)
+    # split-K of the few-tile forward / data-gradient convs (the small maps of the small steps): a launch
+    # of fewer than splitk_wgs tiles splits its K blocks into slices of at least splitk_min_kb blocks,
+    # combined in-launch (0: off)
+    splitk_wgs: int = 512
+    splitk_min_kb: int = 4
     tune_table: str = ""            # per-shape tile table (default: ops/tune_table.json)
     tune_modes: str = "all"         # which tune-table sections apply ("none", "fwd,dgrad2", ...)
     # ---- graphs / communication (train/native_step.py, engine/native_trainer.py, parallel/) ----

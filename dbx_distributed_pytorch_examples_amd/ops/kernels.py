@@ -341,13 +341,54 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
     s0, ns = fwd_taps(IW, OW, S, stride, pad)
     if nr == 0 or ns == 0:
         raise ValueError("conv_fwd: no filter tap touches the input")
+    sk = (conv_splitk(N * OH * OW, OC, bm, bn, dma, nr * ns * (IC // (32 if dma == 6 else 64)))
+          if mode == FWD else (1, 0, 0, 0))
     C().conv_igemm(mode, bm, bn, x.data_ptr(), w16.data_ptr(), out.data_ptr(), _p(in_scale), _p(in_shift),
                    int(relu_in), _p(stats), _nsh(stats, OC), N, IH, IW, IC, OH, OW, OC, R, S, stride, pad, 0,
                    nr, ns, r0, s0, 1, 0, 0, 1, 0, 0, OH, OW, *_NO_EPI, 0, _p(tail_res), _p(tail_res_scale),
-                   _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma, f1, 0, _fin[0], _fin[1], fi)
+                   _p(tail_res_shift), _p(tail_out), _p(tail_bits), stream_ptr(), dma, f1, 0, _fin[0], _fin[1], fi,
+                   *sk)
     if fin is not None and not f1 and _fin[1]:
         fin.run()
     return out
+
+
+_SK_BUFS = {}   # stream -> [fp32 slab workspace, tile counters] of the split-K conv launches
+_SK_KEEP = []   # every buffer ever handed out (a captured graph keeps using its pointers)
+
+
+def conv_splitk(M: int, OC: int, bm: int, bn: int, dma: int, KB: int) -> Tuple[int, int, int, int]:
+    """Split-K plan of one implicit-GEMM launch: (ksplit, kper, slab ptr, counter ptr); (1, 0, 0, 0) =
+    no split. Few-tile launches (fewer than the engine's ``splitk_wgs`` tiles: the 4x4 / 2x2 maps of
+    the TinyImageNet step) walk their K blocks as one chain of HBM / L2 latencies per workgroup;
+    slices of >= ``splitk_min_kb`` blocks run those chains side by side and the tile's last slice sums
+    the fp32 partials in slice order (csrc/conv_igemm_kernel.h splitk_combine: bit-identical whichever
+    slice finishes last). The slab / counter buffers are per stream (launches on one stream are
+    ordered; the side stream's downsample forward runs beside the main stream's convs). The plan never
+    depends on the buffers: a graph capture on a fresh stream allocates its own (from the graph's pool,
+    kept alive here), so captured and eager steps split alike and agree bit for bit."""
+    cfg = _E()
+    ntile = -(-M // bm) * (OC // bn)
+    if cfg.splitk_wgs <= 0 or dma not in (0, 1) or ntile >= cfg.splitk_wgs:
+        return 1, 0, 0, 0
+    s = min(cfg.splitk_wgs // ntile, KB // max(1, cfg.splitk_min_kb))
+    if s < 2:
+        return 1, 0, 0, 0
+    kper = -(-KB // s)
+    s = -(-KB // kper)  # every slice non-empty
+    if s < 2:
+        return 1, 0, 0, 0
+    need_ws, need_cnt = s * ntile * bm * bn, ntile
+    key = stream_ptr()
+    bufs = _SK_BUFS.get(key)
+    if bufs is None or bufs[0].numel() < need_ws or bufs[1].numel() < need_cnt:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        nws = max(need_ws, bufs[0].numel() if bufs else 0)
+        ncnt = max(need_cnt, bufs[1].numel() if bufs else 0, 4096)
+        bufs = [torch.empty(nws, device=dev, dtype=torch.float32), torch.zeros(ncnt, device=dev, dtype=torch.int32)]
+        _SK_BUFS[key] = bufs
+        _SK_KEEP.append(bufs)
+    return s, kper, bufs[0].data_ptr(), bufs[1].data_ptr()
 
 
 def fast_split(N: int, per_img: int, OC: int, bn: int) -> int:
@@ -530,7 +571,7 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
     if kind:
         C().conv_igemm(DGRAD_PATCH, 0, 0, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, nsh,
                        N, P, Q, K, H, W, Cc, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, H, W,
-                       0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), kind - 1, *fins, 0, 1, 0)
+                       0, 1, *epi, act_ptr, 0, 0, 0, 0, 0, stream_ptr(), kind - 1, *fins, 0, 1, 0, 1, 0, 0, 0)
         _fin_rest(epilogue, fins)
         return dx
     if isinstance(tile, str):
@@ -572,11 +613,12 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
             continue
         bm, bn, dma = _tile_dma(tile or pick_tile(N * ohs * ows, Cc, f"dgrad{epilogue.mode if epilogue else 0}"
                                                   + ("b" if bwd_y is not None else ""), K, R, stride))
+        sk = conv_splitk(N * ohs * ows, Cc, bm, bn, dma, nr * ns * (K // (32 if dma == 6 else 64)))
         C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), bwd[0], bwd[1], 0, 0, nsh,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,
                        _p(addsrc), add_sub, *epi, act_ptr, bwd[2], bwd[3], bwd[4], bwd[5], 0, stream_ptr(), dma,
-                       *fins, _fin[0], _fin[1], 0)
+                       *fins, _fin[0], _fin[1], 0, *sk)
     if _fin[1]:
         _fin_rest(epilogue, fins)
     return dx
@@ -619,7 +661,7 @@ def conv_stem_fwd(x4, w16s, out, *, R=7, S=7, stride=2, pad=3, stats=None, patch
     bm = 0 if patch and stem_patch_supported(IH, IW, OC, R, S, stride, pad) else 128  # bm 0: patch kernel
     C().conv_igemm(STEM, bm, 64, x4.data_ptr(), w16s.data_ptr(), out.data_ptr(), 0, 0, 0, _p(stats), _nsh(stats, OC),
                    N, IH, IW, 4, OH, OW, OC, R, S, stride, pad, 0, R, S, 0, 0, 1, 0, 0, 1, 0, 0, OH, OW,
-                   *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr(), 0, 0, 0, 0, 1, 0)
+                   *_NO_EPI, 0, 0, 0, 0, 0, 0, stream_ptr(), 0, 0, 0, 0, 1, 0, 1, 0, 0, 0)
     return out
 
 
