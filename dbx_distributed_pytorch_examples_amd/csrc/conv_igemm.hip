@@ -619,6 +619,7 @@ static int dispatch_fwd(const IGemmArgs& a, bool pro, bool stats, int dma, hipSt
 
 
 extern "C" int dbx_conv_fast(int mode, int bn, const IGemmArgs* args, int stats, int accum, int epi, hipStream_t st);
+extern "C" int dbx_conv_sweep(int mode, const IGemmArgs* args, int pro, int stats, int accum, int epi, hipStream_t st);
 
 extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, int pro, int stats,
                               int accum, int epi, hipStream_t st, int dma) {
@@ -627,6 +628,7 @@ extern "C" int dbx_conv_igemm(int mode, int bm, int bn, const IGemmArgs* args, i
     if ((dma != 0 && dma != 1) || mode == STEM || mode == FWD_PATCH || mode == DGRAD_PATCH) return -67;
     if (a.kper < 1 || a.skws == nullptr || a.skcnt == nullptr) return -68;
   }
+  if (dma == 8) return dbx_conv_sweep(mode, args, pro, stats, accum, epi, st);  // conv_sweep.hip
   if (dma == 4) {  // eight-wave 256-row kernel (conv_fast.hip): plain operands, stride-1 data gradients
     if (bm != 256 || pro || mode == STEM || (mode == DGRAD && (a.osub != 1 || a.add_sub > 1))) return -65;
     return dbx_conv_fast(mode, bn, args, stats, accum, epi, st);

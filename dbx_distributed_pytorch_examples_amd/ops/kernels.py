@@ -307,6 +307,9 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
         plain = in_scale is None and tail_res is None
         bm, bn, dma = _tile_dma(tile or pick_tile(N * OH * OW, OC, "fwd0" if plain else
                                                   ("fwd" if tail_res is None else "fwdt"), IC, R, stride))
+    if (tile is None and not kind and sweep_fwd_ok(N * OH * OW, IC, OC, R, S, stride, pad, in_scale is not None,
+                                                    tail_res is None, relu_in)):
+        bm, bn, dma = 128, 256, 8
     if dma in (4, 5) and (in_scale is not None or tail_res is not None):
         if tile is not None:
             raise ValueError("the eight-wave kernel (tile dma 4 / 5) takes plain operands (no BN prologue / tail)")
@@ -355,6 +358,17 @@ def conv_fwd(x, w16, out, *, R, S, stride, pad, stats=None, in_scale=None, in_sh
 
 _SK_BUFS = {}   # stream -> [fp32 slab workspace, tile counters] of the split-K conv launches
 _SK_KEEP = []   # every buffer ever handed out (a captured graph keeps using its pointers)
+
+
+def sweep_fwd_ok(M: int, IC: int, OC: int, R: int, S: int, stride: int, pad: int, pro: bool, no_tail: bool,
+                 relu_in: bool) -> bool:
+    """Does the N-sweep kernel (csrc/conv_sweep.hip, tile code dma 8) take this forward? 1x1 stride-1
+    BN-prologue (+ReLU) convs with K <= 256 input channels, >= 2 sub-tiles of 256 output channels, and
+    enough 128-row blocks to keep every CU on several of them (the engine's ``sweep_fwd``)."""
+    cfg = _E()
+    return (cfg.sweep_fwd and pro and no_tail and relu_in and (R, S, stride, pad) == (1, 1, 1, 0)
+            and IC % 64 == 0 and IC <= 256 and OC % 256 == 0 and OC >= 512
+            and -(-M // 128) >= cfg.sweep_min_tiles_per_cu * num_cus())
 
 
 def conv_splitk(M: int, OC: int, bm: int, bn: int, dma: int, KB: int) -> Tuple[int, int, int, int]:

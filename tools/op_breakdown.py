@@ -14,7 +14,7 @@ import collections
 import os
 import sys
 
-os.environ["DBX_ENGINE"] = "overlap_wgrad=0"
+os.environ["DBX_ENGINE"] = ",".join(x for x in (os.environ.get("DBX_ENGINE", ""), "overlap_wgrad=0") if x)
 import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
