@@ -114,9 +114,12 @@ class EngineConfig:
     # split-K of the few-tile forward / data-gradient convs (the small maps of the small steps): a launch
     # of fewer than splitk_wgs tiles splits its K blocks into slices of at least splitk_min_kb blocks,
     # combined in-launch (0: off)
-    # N-sweep kernel (csrc/conv_sweep.hip) for the 1x1 BN-prologue forwards with K <= 256 and
-    # >= 2 sub-tiles of 256 channels, on maps with at least sweep_min_tiles_per_cu 128-row blocks per CU
+    # N-sweep kernel (csrc/conv_sweep.hip) for the 1x1 BN-prologue forwards and the folded conv1 data
+    # gradients with K <= 256 and OC % 256 == 0, on maps with at least sweep_min_tiles_per_cu 128-row
+    # blocks per CU (profiles/r6_sweep/)
     sweep_fwd: bool = True
+    sweep_dgrad: bool = True
+    sweep_dgrad_wgs: int = 0        # its persistent grid: 0 one workgroup per CU, N a cap, -1 one per row block
     sweep_min_tiles_per_cu: float = 4.0
     splitk_wgs: int = 512
     splitk_min_kb: int = 4

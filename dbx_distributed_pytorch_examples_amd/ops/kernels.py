@@ -363,11 +363,22 @@ _SK_KEEP = []   # every buffer ever handed out (a captured graph keeps using its
 def sweep_fwd_ok(M: int, IC: int, OC: int, R: int, S: int, stride: int, pad: int, pro: bool, no_tail: bool,
                  relu_in: bool) -> bool:
     """Does the N-sweep kernel (csrc/conv_sweep.hip, tile code dma 8) take this forward? 1x1 stride-1
-    BN-prologue (+ReLU) convs with K <= 256 input channels, >= 2 sub-tiles of 256 output channels, and
+    BN-prologue (+ReLU) convs with K <= 256 input channels, a multiple of 256 output channels, and
     enough 128-row blocks to keep every CU on several of them (the engine's ``sweep_fwd``)."""
     cfg = _E()
     return (cfg.sweep_fwd and pro and no_tail and relu_in and (R, S, stride, pad) == (1, 1, 1, 0)
-            and IC % 64 == 0 and IC <= 256 and OC % 256 == 0 and OC >= 512
+            and IC % 64 == 0 and IC <= 256 and OC % 256 == 0
+            and -(-M // 128) >= cfg.sweep_min_tiles_per_cu * num_cus())
+
+
+def sweep_dgrad_ok(M: int, K: int, Cc: int, R: int, S: int, stride: int, pad: int, fold: bool, add_sub: int,
+                   epi_mode: int) -> bool:
+    """Does the N-sweep kernel take this data gradient? The folded 1x1 stride-1 dgrads (BN-backward apply
+    in the operand staging) of <= 256 channels onto a multiple of 256, with an addend at full resolution
+    and no or the MASK_OUT epilogue (the engine's ``sweep_dgrad``)."""
+    cfg = _E()
+    return (cfg.sweep_dgrad and fold and (R, S, stride, pad) == (1, 1, 1, 0) and add_sub == 1
+            and epi_mode in (0, MASK_OUT) and K % 64 == 0 and K <= 256 and Cc % 256 == 0
             and -(-M // 128) >= cfg.sweep_min_tiles_per_cu * num_cus())
 
 
@@ -590,6 +601,9 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         return dx
     if isinstance(tile, str):
         raise ValueError("tile='patch' needs a 64->64 3x3 stride-1 dgrad at width 56 (no addend / fold)")
+    if tile is None and sweep_dgrad_ok(N * H * W, K, Cc, R, S, stride, pad, bwd_y is not None, add_sub,
+                                       epilogue.mode if epilogue is not None else 0):
+        tile = (128, 256, 8)
     t_sel = tile
     if t_sel is None:
         t_sel = pick_tile(N * H * W, Cc, f"dgrad{epilogue.mode if epilogue else 0}" + ("b" if bwd_y is not None else ""),
@@ -628,6 +642,8 @@ def conv_dgrad(dy, wt16, dx, *, R, S, stride, pad, accumulate=False, tile=None, 
         bm, bn, dma = _tile_dma(tile or pick_tile(N * ohs * ows, Cc, f"dgrad{epilogue.mode if epilogue else 0}"
                                                   + ("b" if bwd_y is not None else ""), K, R, stride))
         sk = conv_splitk(N * ohs * ows, Cc, bm, bn, dma, nr * ns * (K // (32 if dma == 6 else 64)))
+        if dma == 8:  # the N-sweep kernel takes its grid cap in the (unused) split-K slice field
+            sk = (1, _E().sweep_dgrad_wgs, 0, 0)
         C().conv_igemm(DGRAD, bm, bn, dy.data_ptr(), wt16.data_ptr(), dx.data_ptr(), bwd[0], bwd[1], 0, 0, nsh,
                        N, P, Q, K, ohs, ows, Cc, R, S, stride, pad, int(accumulate),
                        nr, ns, r0, s0, stride, dh0, dw0, stride, ph, pw, H, W,

@@ -1,4 +1,4 @@
-"""N-sweep 1x1 BN-prologue forward (csrc/conv_sweep.hip, tile code dma 8): against the fp32 PyTorch
+"""N-sweep 1x1 convs (csrc/conv_sweep.hip, tile code dma 8). The BN-prologue forward: against the fp32 PyTorch
 reference of relu(x*scale + shift) conv 1x1, and bit-identical (outputs and BN statistics) to the
 128 x 256 implicit-GEMM tile it replaces -- same MFMA order, same per-tile statistics partials --
 including rows past M, the in-launch BN finalize and graph replays."""
@@ -70,7 +70,8 @@ def test_sweep_selected_for_headline_shapes(engine):
     cus = k.num_cus()
     assert k.sweep_fwd_ok(1024 * 14 * 14, 256, 1024, 1, 1, 1, 0, True, True, True)
     assert k.sweep_fwd_ok(1024 * 28 * 28, 128, 512, 1, 1, 1, 0, True, True, True)
-    assert not k.sweep_fwd_ok(1024 * 56 * 56, 64, 256, 1, 1, 1, 0, True, True, True)     # one sub-tile
+    assert k.sweep_fwd_ok(1024 * 56 * 56, 64, 256, 1, 1, 1, 0, True, True, True)         # one sub-tile
+    assert not k.sweep_fwd_ok(1024 * 56 * 56, 64, 64, 1, 1, 1, 0, True, True, True)      # OC < 256
     assert not k.sweep_fwd_ok(1024 * 7 * 7, 512, 2048, 1, 1, 1, 0, True, True, True)     # K > 256
     assert not k.sweep_fwd_ok(1024 * 14 * 14, 256, 1024, 1, 1, 1, 0, True, False, True)  # tail prologue
     assert not k.sweep_fwd_ok(512 * 4 * 4, 256, 1024, 1, 1, 1, 0, True, True, True)      # few blocks
@@ -122,3 +123,66 @@ def test_sweep_in_launch_finalize_and_graph_replay():
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(out, o1) and torch.equal(stg, s1)
+
+
+# N, H, K (conv1 output channels = the dgrad's staged channels), Cc (its input channels): the
+# bottleneck conv1 data gradients (rows past M in the last block for the odd sizes)
+DCASES = [(6, 14, 256, 1024), (5, 28, 128, 512), (3, 56, 64, 256), (7, 14, 192, 512)]
+
+
+@pytest.mark.parametrize("case", DCASES)
+@pytest.mark.parametrize("variant", ["epi1", "epi1_ds", "accum_only"])
+def test_sweep_dgrad_matches_igemm(case, variant):
+    """Folded BN1-backward dgrad + block-input addend + the previous block's MASK_OUT epilogue (and its
+    downsample BN's second statistic): dx, the stored dy and both statistics bit-identical to the
+    128 x 256 implicit-GEMM tile; dx against the fp32 reference."""
+    k = K()
+    N, H, Kc, Cc = case
+    torch.manual_seed(2)
+    g = torch.randn(N, H, H, Kc, device=dev).bfloat16()
+    yb = torch.randn(N, H, H, Kc, device=dev).bfloat16()
+    coeff = torch.randn(3, Kc, device=dev) * 0.5
+    wt = (torch.randn(Cc, Kc, device=dev) / math.sqrt(Kc)).bfloat16()
+    add = torch.randn(N, H, H, Cc, device=dev).bfloat16()
+    ybn = torch.randn(N, H, H, Cc, device=dev).bfloat16()
+    ybn2 = torch.randn(N, H, H, Cc, device=dev).bfloat16()
+    mask = torch.randn(N, H, H, Cc, device=dev) > 0
+    mb = k.pack_mask_bits(mask)
+    m1, i1 = torch.randn(Cc, device=dev) * 0.1, torch.rand(Cc, device=dev) + 0.5
+    m2, i2 = torch.randn(Cc, device=dev) * 0.1, torch.rand(Cc, device=dev) + 0.5
+    outs = []
+    for tile in ((128, 256, 1), (128, 256, 8)):
+        dx = torch.empty(N, H, H, Cc, device=dev, dtype=torch.bfloat16)
+        dyo = torch.empty_like(g)
+        s1, s2 = k.new_stats(Cc, dev), k.new_stats(Cc, dev)
+        epi = None
+        if variant != "accum_only":
+            epi = k.BNBwdEpilogue(k.MASK_OUT, ybn, m1, i1, s1, mbits=mb,
+                                  **(dict(ybn2=ybn2, mean2=m2, inv2=i2, stats2=s2) if variant == "epi1_ds" else {}))
+        k.conv_dgrad(g, wt, dx, R=1, S=1, stride=1, pad=0, tile=tile, addsrc=add, epilogue=epi, bwd_y=yb,
+                     bwd_coeff=coeff, dy_out=dyo)
+        torch.cuda.synchronize()
+        outs.append((dx, dyo, s1, s2))
+    (a0, b0, c0, d0), (a1, b1, c1, d1) = outs
+    assert torch.equal(b1, b0), "stored BN-backward operand"
+    assert torch.equal(a1, a0), "data gradient"
+    assert torch.equal(c1, c0) and torch.equal(d1, d0), "statistics"
+    # fp32 reference of the data gradient
+    dyr = (g.float() * coeff[0] + yb.float() * coeff[1] + coeff[2]).bfloat16().float()
+    assert relerr(b1, dyr) < 1e-2
+    ref = (dyr.view(-1, Kc) @ wt.float().t()).view(N, H, H, Cc) + add.float()
+    if variant != "accum_only":
+        ref = ref * mask
+    assert relerr(a1, ref) < 1e-2
+
+
+def test_sweep_dgrad_selected(engine):
+    k = K()
+    engine(sweep_dgrad=True)
+    assert k.sweep_dgrad_ok(1024 * 14 * 14, 256, 1024, 1, 1, 1, 0, True, 1, k.MASK_OUT)
+    assert k.sweep_dgrad_ok(1024 * 56 * 56, 64, 256, 1, 1, 1, 0, True, 1, 0)
+    assert not k.sweep_dgrad_ok(1024 * 14 * 14, 1024, 256, 1, 1, 1, 0, True, 1, k.MASK_Y)  # K > 256, MASK_Y
+    assert not k.sweep_dgrad_ok(1024 * 28 * 28, 256, 512, 1, 1, 1, 0, True, 2, k.MASK_OUT)  # subsampled addend
+    assert not k.sweep_dgrad_ok(1024 * 14 * 14, 256, 1024, 1, 1, 1, 0, False, 1, k.MASK_OUT)  # not folded
+    engine(sweep_dgrad=False)
+    assert not k.sweep_dgrad_ok(1024 * 14 * 14, 256, 1024, 1, 1, 1, 0, True, 1, k.MASK_OUT)

@@ -75,6 +75,13 @@ def main():
             by = N * H * H * (IC + OC) * 2
             print(f"fwd {IC:4d}->{OC:5d} @{H:2d}: igemm {t0 * 1e3:7.1f} us ({by / t0 / 1e9:4.2f} TB/s)  "
                   f"sweep {t1 * 1e3:7.1f} us ({by / t1 / 1e9:4.2f} TB/s)  {t0 / t1:5.2f}x", flush=True)
+        print("# folded conv1 data gradients + addend + MASK_OUT epilogue", flush=True)
+        for H, Kc, Cc in ((14, 256, 1024), (28, 128, 512), (56, 64, 256)):
+            t0 = min(dgrad_case(N, H, Kc, Cc, (128, 256, 1), a.iters) for _ in range(3))
+            t1 = min(dgrad_case(N, H, Kc, Cc, (128, 256, 8), a.iters) for _ in range(3))
+            by = N * H * H * (3 * Kc + 3 * Cc) * 2
+            print(f"dgrad {Kc:4d}->{Cc:5d} @{H:2d}: igemm {t0 * 1e3:7.1f} us ({by / t0 / 1e9:4.2f} TB/s)  "
+                  f"sweep {t1 * 1e3:7.1f} us ({by / t1 / 1e9:4.2f} TB/s)  {t0 / t1:5.2f}x", flush=True)
         return
     tile = (128, 256, 1)
     print(f"# batch {N}, tile {tile}: per-tile us = time / (M/128 * N/256)", flush=True)
