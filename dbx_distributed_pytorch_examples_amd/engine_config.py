@@ -118,7 +118,7 @@ class EngineConfig:
     # gradients with K <= 256 and OC % 256 == 0, on maps with at least sweep_min_tiles_per_cu 128-row
     # blocks per CU (profiles/r6_sweep/)
     sweep_fwd: bool = True
-    sweep_dgrad: bool = True
+    sweep_dgrad: bool = False       # (1.08-1.23x per launch, neutral inside the step: off)
     sweep_dgrad_wgs: int = 0        # its persistent grid: 0 one workgroup per CU, N a cap, -1 one per row block
     sweep_min_tiles_per_cu: float = 4.0
     splitk_wgs: int = 512
