@@ -21,6 +21,13 @@ def K():
     return kernels
 
 
+@pytest.fixture(autouse=True)
+def _no_splitk(engine):
+    """The register path splits the K loop of few-tile launches (splitk_wgs) and the ring paths never
+    do: compare the operand paths on unsplit launches (split-K has its own tests, test_splitk_gpu.py)."""
+    engine(splitk_wgs=0)
+
+
 def _same(outs0, outs1, what):
     for a, b in zip(outs0, outs1):
         assert torch.equal(a, b), what

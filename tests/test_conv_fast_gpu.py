@@ -13,6 +13,13 @@ from dbx_distributed_pytorch_examples_amd.ops import kernels as K
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _no_splitk(engine):
+    """These compare kernels bit for bit against the four-wave implicit-GEMM launch, which splits the K
+    loop of few-tile launches (splitk_wgs; its own tests: test_splitk_gpu.py): compare unsplit launches."""
+    engine(splitk_wgs=0)
+
+
 def _stats_total(st, C):
     return st.view(K.NSHARD, 2, C).sum(0)
 

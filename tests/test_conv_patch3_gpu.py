@@ -21,6 +21,13 @@ def K():
     return kernels
 
 
+@pytest.fixture(autouse=True)
+def _no_splitk(engine):
+    """These compare kernels bit for bit against the four-wave implicit-GEMM launch, which splits the K
+    loop of few-tile launches (splitk_wgs; its own tests: test_splitk_gpu.py): compare unsplit launches."""
+    engine(splitk_wgs=0)
+
+
 def _close_stats(a, b, count):
     a, b = a.view(-1, 2, 64).sum(0), b.view(-1, 2, 64).sum(0)
     return ((a - b).abs() / (b.abs() + count * 1e-3)).max().item()
