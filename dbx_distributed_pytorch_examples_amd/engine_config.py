@@ -120,7 +120,7 @@ class EngineConfig:
     sweep_fwd: bool = True
     sweep_dgrad: bool = False       # (1.08-1.23x per launch, neutral inside the step: off)
     sweep_dgrad_wgs: int = 0        # its persistent grid: 0 one workgroup per CU, N a cap, -1 one per row block
-    sweep_min_tiles_per_cu: float = 4.0
+    sweep_min_tiles_per_cu: float = 1.0   # (4: ZeRO-1 -0.6 %; 0.25: TinyImageNet -1.8 %, r6_sweep/ab_threshold.txt)
     splitk_wgs: int = 512
     splitk_min_kb: int = 4
     tune_table: str = ""            # per-shape tile table (default: ops/tune_table.json)
