@@ -17,8 +17,10 @@
 // LDS: [KB][128][64] resident A | a region shared by the weight ring [2][256][64] and the epilogue's
 // C staging [128][264] | the prologue affine [2][256] fp32  -> 132 KiB at K = 256: one workgroup per
 // CU (8 waves), persistent over the 128-row blocks (grid = CUs, a multiple of 8: block b on XCD b % 8).
-// The next block's A loads are issued during the last sub-tile's K loop (after its last weight DMA,
-// so the counted ring waits never wait on them) and land while that sub-tile's epilogue runs.
+// The next block's A loads are issued at the last K step of the last sub-tile (after its last weight
+// DMA: no ring wait of this block waits on them) and land while that sub-tile's epilogue runs.
+// Measured and rejected variants: deferred epilogue stores (r6_defer/), a 4-slot ring of 32-channel
+// weight stages (r6_ring4/).
 #include "conv_igemm_kernel.h"
 
 namespace dbx {
@@ -26,7 +28,9 @@ namespace dbx {
 // MODE FWD: A = relu(x*scale + shift) (BN + ReLU prologue), STATS: this layer's BN statistics.
 // MODE DGRAD (TAIL): the bottleneck conv1 data gradient with the BN1-backward apply folded in --
 // A = g*k1 + k3 + y*k2 (x = g, res = y; no ReLU), stored once per row block to tail_out (the weight
-// gradient's dy); ACCUM: + the block-input addend; EPI 1 / 2: the previous BN's backward epilogue.
+// gradient's dy); ACCUM: + the block-input addend; EPI 1: the previous block's MASK_OUT epilogue (the
+// data-gradient mode is 1.08-1.23x per launch but neutral inside the step: engine default off,
+// profiles/r6_sweep/).
 // APF: the next row block's A loads are issued under the last sub-tile (register room permitting).
 template <int KB, int MODE, bool STATS, bool ACCUM, int EPI, bool TAIL>
 __global__ __launch_bounds__(512, 1) void sweep_kernel(const IGemmArgs a) {
