@@ -249,7 +249,10 @@ class ResNetProgram:
         # explicitly win.
         self.small_step = pol.small(fl)
         self.nshard = cfg.nshard if cfg.nshard is not None else (4 if self.small_step else K.NSHARD)
-        if self.small_step and cfg.fin_in is None:
+        # (round 6: only the launch-bound CIFAR class keeps it; the TinyImageNet class runs the finalize
+        # launches again after the round-5/6 schedule changes: 105,548 / 105,605 vs 105,038 / 104,844
+        # img/s, profiles/r6_tiny_fin/)
+        if pol.tiny(fl) and cfg.fin_in is None:
             self.fin_in = True
         # consumer-side backward finalize: a BN-backward apply pass computes its coefficients from the
         # moment shards itself (K.bn_bwd_apply fin=) instead of a bn_bwd_coeff launch in front of it

@@ -92,7 +92,8 @@ class EngineConfig:
     fold_max_ratio: Optional[float] = None
     fold_ratio_min_hw: int = 56
     # BN finalize in the consumer (forward: consuming conv's prologue; backward: the apply pass) and
-    # statistics shards per BN; None: on with 4 shards for small steps, off with 32 shards above
+    # statistics shards per BN; None: fin_in on for the CIFAR class only (r6_tiny_fin/), coeff_in on and
+    # 4 shards for small steps, off with 32 shards above
     # (r4_s6/, r4_s7/, r4_s18/)
     fin_in: Optional[bool] = None
     coeff_in: Optional[bool] = None
