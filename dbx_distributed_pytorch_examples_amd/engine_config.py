@@ -123,7 +123,7 @@ class EngineConfig:
     sweep_dgrad_wgs: int = 0        # its persistent grid: 0 one workgroup per CU, N a cap, -1 one per row block
     sweep_min_tiles_per_cu: float = 1.0   # (4: ZeRO-1 -0.6 %; 0.25: TinyImageNet -1.8 %, r6_sweep/ab_threshold.txt)
     splitk_wgs: int = 512
-    splitk_min_kb: int = 4
+    splitk_min_kb: int = 8           # (4: CIFAR -2.0 %, TinyImageNet -0.3 %; r6_tiny_knobs/confirm.txt)
     tune_table: str = ""            # per-shape tile table (default: ops/tune_table.json)
     tune_modes: str = "all"         # which tune-table sections apply ("none", "fwd,dgrad2", ...)
     # ---- graphs / communication (train/native_step.py, engine/native_trainer.py, parallel/) ----
