@@ -92,3 +92,29 @@ def test_side_stream_defaults_by_step_size(monkeypatch, engine):
     engine(overlap_wgrad="2")
     p = ResNetProgram(m, 2, (32, 32), torch.device("cpu"))
     assert (p.side_block, p.side_batch, p.side_defer, p.lazy_join, p.stem_wg_main) == (False, True, False, False, False)
+
+
+@pytest.mark.parametrize("flops,fin_in,coeff_in,nshard", [
+    (2.0e10, True, True, 4),     # CIFAR class: consumer-side forward finalize kept
+    (3.5e11, False, True, 4),    # TinyImageNet class: standalone finalize launches (profiles/r6_tiny_fin/)
+    (8.4e12, False, False, None),  # headline class: NSHARD shards, standalone finalizes
+])
+def test_small_step_finalize_policy(monkeypatch, engine, flops, fin_in, coeff_in, nshard):
+    """Round-6 policy: the consumer-side forward BN finalize only for the launch-bound CIFAR class;
+    4 statistics shards and the in-apply backward finalize for both small classes."""
+    from dbx_distributed_pytorch_examples_amd.engine import program as P
+    from dbx_distributed_pytorch_examples_amd.ops import kernels as K
+    engine(fin_in=None, coeff_in=None, nshard=None)
+    monkeypatch.setattr(P.ResNetProgram, "fwd_conv_flops", lambda self: flops)
+    p = ResNetProgram(build_model("resnet18", num_classes=10), 2, (32, 32), torch.device("cpu"))
+    assert (p.fin_in, p.coeff_in) == (fin_in, coeff_in)
+    assert p.nshard == (nshard if nshard is not None else K.NSHARD)
+
+
+def test_splitk_and_sweep_defaults():
+    """Defaults measured in round 6: split-K slices of >= 8 K blocks (profiles/r6_tiny_knobs/), the
+    sweep forward from one 128-row block per CU, the dgrad sweep off (profiles/r6_sweep/)."""
+    from dbx_distributed_pytorch_examples_amd.engine_config import EngineConfig
+    c = EngineConfig()
+    assert (c.splitk_wgs, c.splitk_min_kb) == (512, 8)
+    assert c.sweep_fwd and not c.sweep_dgrad and c.sweep_min_tiles_per_cu == 1.0
