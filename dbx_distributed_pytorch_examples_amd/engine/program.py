@@ -185,7 +185,8 @@ class ResNetProgram:
         # (profiles/r3s2_batched/)
         self.overlap_wgrad = ow != 0
         # (the in-launch split-K reduce and the producer-side BN finalize (K.BnFin) measured slower than
-        # the launches they remove on all three presets and were removed in round 6: profiles/r3s2_fuse_ab/)
+        # the launches they remove on all three presets and were removed in round 6: profiles/r3s2_fuse_ab/;
+        # the finalize re-measured after the round-6 changes: -4 % to -8 %, profiles/r6_fuse_fin/)
         self.fuse_fin = False
 
         # store block-internal BN outputs from the MASK_Y dgrad epilogue for the wgrads
